@@ -1,0 +1,241 @@
+"""ctypes binding of liblincheck.so (include/lincheck.h, include/lincheck_synth.h).
+
+This is the build's own library, loaded in-process.  It exposes the GPU
+checker (lc_*) and the seeded synthetic-history generator (lc_synth_*).
+Loading fails loudly when the HIP library is missing: there is no fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblincheck.so")
+
+LC_F_READ, LC_F_WRITE, LC_F_CAS = 0, 1, 2
+LC_NIL = -1
+LC_INF = (1 << 63) - 1
+LC_VALID, LC_INVALID, LC_UNKNOWN = 1, 0, -1
+
+REASONS = {
+    0: "none",
+    1: "nonlinearizable",
+    2: "config-budget",
+    3: "window-overflow",
+    4: "malformed",
+    5: "unknown-f",
+    6: "frontier-lds",
+}
+LC_REASON_NONLINEARIZABLE = 1
+LC_REASON_CONFIG_BUDGET = 2
+LC_REASON_WINDOW_OVERFLOW = 3
+LC_REASON_MALFORMED = 4
+LC_REASON_UNKNOWN_F = 5
+LC_FLAG_NO_HBM_RETRY = 1
+
+# lc_op: 6 x int64 (f, value, expected, version, call, ret); arrays are (n, 6).
+OP_FIELDS = ("f", "value", "expected", "version", "call", "ret")
+RESULT_DTYPE = np.dtype([
+    ("verdict", "<i4"), ("reason", "<i4"), ("fail_op", "<i8"),
+    ("fail_prefix_end", "<i8"), ("configs_explored", "<i8"),
+    ("max_frontier", "<i8"),
+])
+assert RESULT_DTYPE.itemsize == 40
+
+
+class LcOpts(ctypes.Structure):
+    _fields_ = [("init_version", ctypes.c_int64), ("init_value", ctypes.c_int64),
+                ("max_configs_per_key", ctypes.c_int64),
+                ("time_budget_ms", ctypes.c_int64), ("flags", ctypes.c_int64)]
+
+
+class LcStats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_double), ("hbm_kernel_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double), ("n_keys", ctypes.c_int64),
+                ("n_ops", ctypes.c_int64), ("n_hbm_keys", ctypes.c_int64),
+                ("n_devices", ctypes.c_int64)]
+
+
+class LcSynthParams(ctypes.Structure):
+    _fields_ = [("n_keys", ctypes.c_int64), ("ops_per_key", ctypes.c_int64),
+                ("concurrency", ctypes.c_int32), ("n_values", ctypes.c_int32),
+                ("p_info", ctypes.c_double), ("p_anomaly", ctypes.c_double),
+                ("seed", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def lib():
+    """Load liblincheck.so once; raise if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                "liblincheck.so not built (%s); run `python -c 'import "
+                "__graft_entry__ as g; g.build()'` — there is no CPU fallback" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        p, i64, i32, u32, vp = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                ctypes.c_uint32, ctypes.c_void_p)
+        L.lc_open.argtypes = [u32, ctypes.POINTER(vp)]
+        L.lc_open.restype = ctypes.c_int
+        L.lc_check.argtypes = [vp, p, p, i64, ctypes.POINTER(LcOpts), p]
+        L.lc_check.restype = ctypes.c_int
+        L.lc_check_device.argtypes = [vp, vp, vp, i64, ctypes.POINTER(LcOpts), vp, vp]
+        L.lc_check_device.restype = ctypes.c_int
+        L.lc_last_stats.argtypes = [vp, ctypes.POINTER(LcStats)]
+        L.lc_last_stats.restype = ctypes.c_int
+        L.lc_last_error.argtypes = [vp]
+        L.lc_last_error.restype = ctypes.c_char_p
+        L.lc_close.argtypes = [vp]
+        L.lc_close.restype = None
+        L.lc_default_opts.argtypes = [ctypes.POINTER(LcOpts)]
+        L.lc_default_opts.restype = None
+        L.lc_plan_partition.argtypes = [p, p, i64, i32, p]
+        L.lc_plan_partition.restype = ctypes.c_int
+        L.lc_abi_version.argtypes = []
+        L.lc_abi_version.restype = ctypes.c_int
+        L.lc_synth_register.argtypes = [ctypes.POINTER(LcSynthParams), p, p, p,
+                                        ctypes.POINTER(i64), ctypes.c_int]
+        L.lc_synth_register.restype = ctypes.c_int
+        L.lc_synth_key.argtypes = [ctypes.POINTER(LcSynthParams), i64, p, p, p, i64,
+                                   ctypes.POINTER(i64), ctypes.POINTER(i32)]
+        L.lc_synth_key.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def default_opts(max_configs_per_key=0, init_version=0, init_value=LC_NIL, flags=0):
+    o = LcOpts()
+    lib().lc_default_opts(ctypes.byref(o))
+    o.max_configs_per_key = max_configs_per_key
+    o.init_version = init_version
+    o.init_value = init_value
+    o.flags = flags
+    return o
+
+
+def as_ops(ops):
+    a = np.ascontiguousarray(ops, dtype=np.int64)
+    if a.ndim != 2 or a.shape[1] != 6:
+        a = a.reshape(-1, 6)
+    return a
+
+
+class LcError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("lincheck error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Context:
+    """An lc_ctx on the GPUs of device_mask (0 = all)."""
+
+    def __init__(self, device_mask=0):
+        h = ctypes.c_void_p()
+        rc = lib().lc_open(device_mask, ctypes.byref(h))
+        if rc != 0:
+            raise LcError(rc, "lc_open failed (no usable GPU; there is no CPU fallback)")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().lc_close(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def last_error(self):
+        return lib().lc_last_error(self._h).decode()
+
+    def stats(self):
+        s = LcStats()
+        lib().lc_last_stats(self._h, ctypes.byref(s))
+        return {f: getattr(s, f) for f, _ in LcStats._fields_}
+
+    def check(self, ops, key_off, opts=None, raise_on_error=True):
+        """Host-buffer check. Returns (rc, results structured array)."""
+        ops = as_ops(ops)
+        key_off = np.ascontiguousarray(key_off, dtype=np.int64)
+        n_keys = len(key_off) - 1
+        out = np.zeros(max(n_keys, 0), dtype=RESULT_DTYPE)
+        o = opts if opts is not None else default_opts()
+        rc = lib().lc_check(self._h, _ptr(ops), _ptr(key_off), n_keys,
+                            ctypes.byref(o), _ptr(out))
+        if rc != 0 and raise_on_error:
+            raise LcError(rc, self.last_error())
+        return rc, out
+
+    def check_device(self, d_ops, d_key_off, n_keys, d_out, stream=None, opts=None):
+        """Device-pointer check (ints), e.g. from torch tensors' data_ptr()."""
+        o = opts if opts is not None else default_opts()
+        rc = lib().lc_check_device(self._h, ctypes.c_void_p(d_ops),
+                                   ctypes.c_void_p(d_key_off), n_keys,
+                                   ctypes.byref(o), ctypes.c_void_p(d_out),
+                                   ctypes.c_void_p(stream) if stream else None)
+        if rc != 0:
+            raise LcError(rc, self.last_error())
+        return rc
+
+
+def plan_partition(key_off, n_parts):
+    key_off = np.ascontiguousarray(key_off, dtype=np.int64)
+    bounds = np.zeros(n_parts + 1, dtype=np.int64)
+    rc = lib().lc_plan_partition(None, _ptr(key_off), len(key_off) - 1, n_parts,
+                                 _ptr(bounds))
+    if rc != 0:
+        raise LcError(rc, "lc_plan_partition")
+    return bounds
+
+
+def synth_params(n_keys, ops_per_key, concurrency=10, n_values=5, p_info=0.0,
+                 p_anomaly=0.0, seed=0x5EED0000):
+    return LcSynthParams(n_keys, ops_per_key, concurrency, n_values, p_info,
+                         p_anomaly, seed)
+
+
+def synth(n_keys, ops_per_key, concurrency=10, n_values=5, p_info=0.0,
+          p_anomaly=0.0, seed=0x5EED0000, n_threads=None):
+    """Packed synthetic histories: (ops (n,6) int64, key_off, labels, n_invocations)."""
+    prm = synth_params(n_keys, ops_per_key, concurrency, n_values, p_info,
+                       p_anomaly, seed)
+    ops = np.zeros((n_keys * ops_per_key, 6), dtype=np.int64)
+    key_off = np.zeros(n_keys + 1, dtype=np.int64)
+    labels = np.zeros(n_keys, dtype=np.int32)
+    ninv = ctypes.c_int64(0)
+    if n_threads is None:
+        n_threads = min(16, os.cpu_count() or 1)
+    rc = lib().lc_synth_register(ctypes.byref(prm), _ptr(ops), _ptr(key_off),
+                                 _ptr(labels), ctypes.byref(ninv), n_threads)
+    if rc != 0:
+        raise LcError(rc, "lc_synth_register")
+    return ops, key_off, labels, ninv.value
+
+
+def synth_key(key, ops_per_key, concurrency=10, n_values=5, p_info=0.0,
+              p_anomaly=0.0, seed=0x5EED0000):
+    """One key's full op stream incl. :fail: (ops, proc, status, label)."""
+    prm = synth_params(1, ops_per_key, concurrency, n_values, p_info, p_anomaly, seed)
+    n = ctypes.c_int64(0)
+    lab = ctypes.c_int32(0)
+    cap = 4 * ops_per_key + 64
+    while True:
+        ops = np.zeros((cap, 6), dtype=np.int64)
+        proc = np.zeros(cap, dtype=np.int32)
+        st = np.zeros(cap, dtype=np.int32)
+        rc = lib().lc_synth_key(ctypes.byref(prm), key, _ptr(ops), _ptr(proc), _ptr(st),
+                                cap, ctypes.byref(n), ctypes.byref(lab))
+        if rc == 0:
+            k = n.value
+            return ops[:k], proc[:k], st[:k], lab.value
+        cap = n.value

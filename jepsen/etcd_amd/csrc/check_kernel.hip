@@ -1,0 +1,512 @@
+// check_kernel.hip — batched per-key linearizability search for the
+// VersionedRegister model on CDNA4 (gfx950).
+//
+// Reference semantics: the model step is
+//   /root/reference/src/jepsen/etcd/register.clj:59-96
+// and the search replaces knossos's JIT-linear analyzer invoked through
+// (checker/linearizable {:model (->VersionedRegister 0 nil)}) at
+// register.clj:110-111, once per independent key (register.clj:108).
+//
+// Mapping to the hardware:
+//  * one wavefront owns one key; a 256-thread workgroup runs 4 independent keys;
+//  * LANE t = WINDOW SLOT t: the record of the t-th open call (called, not yet
+//    returned, or crashed) lives in lane t's VGPRs, so "which pending ops may
+//    the model step next from state s" is ONE vector compare + __ballot over
+//    all 64 open calls (wave-level candidate compaction);
+//  * a configuration (linearized-slot bitmask, (version, value)) is 16 bytes and
+//    wave-uniform; the frontier lives in LDS, 3 regions x 128 configs per wave;
+//  * the key's records are streamed from HBM 64 at a time (one 48-byte record
+//    per lane, double-buffered), and read out by v_readlane as calls happen;
+//  * the next event is min(next call, min over open slots of ret): a 64-lane
+//    min reduction, so no per-key event sort is ever built.
+//
+// Search (Lowe's just-in-time linearization, as knossos.linear) with one exact,
+// model-specific reduction — EAGER READ CLOSURE: a read (a no-op on the state,
+// register.clj:84-96) that is pending and legal in a configuration is
+// linearized immediately.  (s, L+{r}) dominates (s, L): any continuation of the
+// latter linearizes r at some state where it is legal, and deleting that step
+// leaves every other step unchanged.  So the frontier is empty at exactly the
+// same returns as knossos's, verdicts and counterexample prefixes are
+// unchanged, and the 2^k subsets of concurrent reads never materialise.
+#include "kernels.h"
+
+namespace lcdev {
+namespace {
+
+constexpr int64_t kInf = INT64_MAX;
+constexpr int64_t kFieldMax = 0x7FFFFFFE;  // int32 range for value/expected/version
+
+struct Cfg {
+  uint64_t mask;  // bit t: the op in window slot t is linearized
+  uint64_t sv;    // (uint32 version << 32) | uint32 value-id (NIL = 0xFFFFFFFF)
+};
+
+__device__ __forceinline__ uint64_t pack_sv(int32_t ver, int32_t val) {
+  return ((uint64_t)(uint32_t)ver << 32) | (uint32_t)val;
+}
+__device__ __forceinline__ int32_t sv_ver(uint64_t sv) { return (int32_t)(sv >> 32); }
+__device__ __forceinline__ int32_t sv_val(uint64_t sv) { return (int32_t)(uint32_t)sv; }
+
+__device__ __forceinline__ int rl32(int v, int l) {
+  return __builtin_amdgcn_readlane(v, l);
+}
+__device__ __forceinline__ int64_t rl64(int64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+// Number of set bits of m in lanes below this one (prefix-sum compaction).
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ int64_t wave_min64(int64_t v) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int64_t w = (int64_t)__shfl_xor((long long)v, o);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+// VersionedRegister.step legality (register.clj:60-96); NIL = -1.
+//   write :64-68  version' = version+1 must equal op-version unless nil
+//   cas   :70-82  same, and the current value must equal the expected value
+//   read  :84-96  op-version (if non-nil) == version, op-value (if non-nil) == value
+// A mutation's next state is (version+1, op value).
+__device__ __forceinline__ bool legal(int f, int opver, int opval, int opexp,
+                                      int ver, int val) {
+  if (f == LC_F_READ)
+    return (opver == -1 || opver == ver) && (opval == -1 || opval == val);
+  return (opver == -1 || opver == ver + 1) && (f != LC_F_CAS || val == opexp);
+}
+
+// One record, decoded by one lane.
+struct Rec {
+  int f, val, exp, ver, bad;
+  int64_t call, ret;
+};
+
+__device__ __forceinline__ Rec load_rec(const lc_op *__restrict__ o, int64_t i,
+                                        int64_t n) {
+  Rec r;
+  if (i < n) {
+    const longlong2 *p = reinterpret_cast<const longlong2 *>(o + i);
+    const longlong2 a = p[0], b = p[1], c = p[2];
+    const int64_t f = a.x, value = a.y, expected = b.x, version = b.y;
+    r.call = c.x;
+    r.ret = c.y;
+    r.bad = (value < -1) | (value > kFieldMax) | (expected < -1) |
+            (expected > kFieldMax) | (version < -1) | (version > kFieldMax) |
+            (r.call < 0) | (r.ret <= r.call);
+    r.f = (f >= 0 && f <= 2) ? (int)f : 3;
+    r.val = (int)value;
+    r.exp = (int)expected;
+    r.ver = (int)version;
+  } else {
+    r.f = 0;
+    r.val = r.exp = r.ver = -1;
+    r.bad = 0;
+    r.call = kInf;
+    r.ret = kInf;
+  }
+  return r;
+}
+
+struct KeyOut {
+  int verdict, reason;
+  int64_t fail_op, fail_end, explored, max_frontier;
+};
+
+// ---------------------------------------------------------------- stores
+// A Store holds three configuration regions (roles rotate: frontier F,
+// results R, worklist/visited W) and deduplicating insertion into the R and W
+// roles.  All member functions are called by the whole wave with uniform
+// arguments unless named *_lane.
+
+enum { ROLE_R = 0, ROLE_W = 1 };
+
+struct LdsStore {
+  Cfg *base;  // 3 regions of cap configurations, contiguous
+  static constexpr int cap = kLdsCap;
+  __device__ __forceinline__ Cfg *reg(int r) const { return base + r * cap; }
+  __device__ __forceinline__ Cfg get(int r, int j) const { return reg(r)[j]; }
+  __device__ __forceinline__ void set_mask_lane(int r, int j, uint64_t m) {
+    reg(r)[j].mask = m;
+  }
+  __device__ __forceinline__ void begin_return() {}
+  // Lane-parallel insertion of configurations known to be distinct.
+  __device__ __forceinline__ void add_unique_lane(int, int r, int j, const Cfg &c) {
+    reg(r)[j] = c;
+  }
+  // Returns 1 inserted, 0 duplicate, -1 full.
+  __device__ __forceinline__ int insert(int, int r, int &n, uint64_t m,
+                                        uint64_t sv, int lane) {
+    const Cfg *R = reg(r);
+    for (int j0 = 0; j0 < n; j0 += kWave) {
+      const int j = j0 + lane;
+      bool eq = false;
+      if (j < n) {
+        const Cfg c = R[j];
+        eq = (c.mask == m) & (c.sv == sv);
+      }
+      if (__ballot(eq)) return 0;
+    }
+    if (n >= cap) return -1;
+    if (lane == 0) reg(r)[n] = Cfg{m, sv};
+    n++;
+    return 1;
+  }
+};
+
+// HBM store: regions are global arrays of `cap` configurations; R and W each
+// have an open-addressed table of 2*cap entries in 8-entry (128-byte) buckets,
+// valid when their epoch tag equals the current return's epoch, so a table is
+// "cleared" by bumping the epoch.  One wave owns one workspace: no atomics.
+struct HbmStore {
+  Cfg *base;      // 3 regions of cap configurations, contiguous
+  Cfg *tabs;      // 2 tables (roles R, W) of 2*cap entries
+  uint32_t *tags; // 2 tag arrays of 2*cap
+  int cap;         // configurations per region
+  uint32_t tmask;  // table entries - 1 (power of two)
+  uint32_t epoch;
+  __device__ __forceinline__ Cfg *reg(int r) const { return base + (size_t)r * cap; }
+  __device__ __forceinline__ Cfg *tab(int role) const { return tabs + (size_t)role * (tmask + 1); }
+  __device__ __forceinline__ uint32_t *tag(int role) const { return tags + (size_t)role * (tmask + 1); }
+  __device__ __forceinline__ Cfg get(int r, int j) const { return reg(r)[j]; }
+  __device__ __forceinline__ void set_mask_lane(int r, int j, uint64_t m) {
+    reg(r)[j].mask = m;
+  }
+  __device__ __forceinline__ void begin_return() { epoch++; }
+  __device__ __forceinline__ static uint32_t hash(uint64_t m, uint64_t sv) {
+    uint64_t h = m * 0x9E3779B97F4A7C15ULL ^ (sv + 0x632BE59BD9B4E019ULL);
+    h ^= h >> 29;
+    h *= 0xBF58476D1CE4E5B9ULL;
+    h ^= h >> 32;
+    return (uint32_t)h;
+  }
+  // Lane-parallel: each active lane inserts its own distinct config into the
+  // role's table (claiming a tag with atomicCAS: lanes of one wave may race on
+  // one bucket) and stores it at region index j.
+  __device__ __forceinline__ void add_unique_lane(int role, int r, int j,
+                                                  const Cfg &c) {
+    reg(r)[j] = c;
+    uint32_t h = hash(c.mask, c.sv) & tmask;
+    for (;;) {
+      const uint32_t old = tag(role)[h];
+      if (old != epoch) {
+        if (atomicCAS(&tag(role)[h], old, epoch) == old) {
+          tab(role)[h] = c;
+          return;
+        }
+        continue;
+      }
+      h = (h + 1) & tmask;
+    }
+  }
+  // Wave-uniform dedup insert: probe one 128-byte bucket (8 lanes x 16 B)
+  // per step, linear over buckets.
+  __device__ __forceinline__ int insert(int role, int r, int &n, uint64_t m,
+                                        uint64_t sv, int lane) {
+    uint32_t b = (hash(m, sv) & tmask) & ~7u;
+    const int sub = lane & 7;
+    for (uint32_t probes = 0; probes <= tmask; probes += 8) {
+      bool live = false, eq = false;
+      if (lane < 8) {
+        live = tag(role)[b + sub] == epoch;
+        if (live) {
+          const Cfg c = tab(role)[b + sub];
+          eq = (c.mask == m) & (c.sv == sv);
+        }
+      }
+      if (__ballot(eq)) return 0;
+      const uint64_t free_m = __ballot(lane < 8 && !live);
+      if (free_m) {
+        if (n >= cap) return -1;
+        const int slot = __builtin_ctzll(free_m);
+        if (lane == slot) {
+          tag(role)[b + slot] = epoch;
+          tab(role)[b + slot] = Cfg{m, sv};
+        }
+        if (lane == 0) reg(r)[n] = Cfg{m, sv};
+        n++;
+        return 1;
+      }
+      b = (b + 8) & tmask;
+    }
+    return -1;
+  }
+};
+
+// ------------------------------------------------------------ the search
+
+template <class Store>
+__device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
+                          const KParams &p, Store &st, KeyOut &o,
+                          const int lane) {
+  o.verdict = LC_VALID;
+  o.reason = LC_REASON_NONE;
+  o.fail_op = -1;
+  o.fail_end = -1;
+  o.explored = 1;
+  o.max_frontier = 1;
+
+  int rF = 0, rR = 1, rW = 2;
+  int nF = 0;
+  st.begin_return();
+  st.insert(ROLE_R, rF, nF, 0ull, pack_sv(p.init_ver, p.init_val), lane);
+
+  // Window slot held by this lane.
+  int s_f = 0, s_val = -1, s_exp = -1, s_ver = -1, s_idx = -1;
+  int64_t s_ret = kInf;
+  uint64_t occ = 0;  // occupied slots (uniform)
+
+  Rec cur = load_rec(kops, lane, n);
+  Rec nxt = load_rec(kops, kWave + lane, n);
+  int64_t base = 0, i = 0, prev_call = -1;
+
+  for (;;) {
+    const int64_t ncall = (i < n) ? rl64(cur.call, (int)(i - base)) : kInf;
+    const bool mine = (occ >> lane) & 1;
+    const int64_t nret = wave_min64(mine ? s_ret : kInf);
+    if (i >= n && nret == kInf) break;  // only crashed ops remain open
+
+    if (nret < ncall) {
+      // ----------------------------------------------------- return of x
+      const uint64_t hit = __ballot(mine && s_ret == nret);
+      const int s = __builtin_ctzll(hit);
+      const uint64_t bs = 1ull << s;
+      const int x_idx = rl32(s_idx, s);
+      st.begin_return();
+      int nR = 0, nW = 0;
+      // Split F: configs that already linearized x go to R (x's bit dropped),
+      // the others to the worklist W.  Ballot + lanes_below compaction.
+      for (int j0 = 0; j0 < nF; j0 += kWave) {
+        const int j = j0 + lane;
+        const bool v = j < nF;
+        Cfg c{0, 0};
+        if (v) c = st.get(rF, j);
+        const bool has = v && (c.mask & bs);
+        const bool lacks = v && !(c.mask & bs);
+        const uint64_t mh = __ballot(has), ml = __ballot(lacks);
+        if (has) st.add_unique_lane(ROLE_R, rR, nR + lanes_below(mh), Cfg{c.mask & ~bs, c.sv});
+        if (lacks) st.add_unique_lane(ROLE_W, rW, nW + lanes_below(ml), c);
+        nR += __popcll(mh);
+        nW += __popcll(ml);
+      }
+      // Expand W breadth-first until x is linearized in each branch.
+      bool overflow = false, over_budget = false;
+      for (int head = 0; head < nW && !overflow && !over_budget; head++) {
+        const Cfg c = st.get(rW, head);
+        const uint64_t cm = rfl64(c.mask), csv = rfl64(c.sv);
+        const int cver = sv_ver(csv), cval = sv_val(csv);
+        const bool pend = ((occ & ~cm) >> lane) & 1;
+        uint64_t cand = __ballot(pend && s_f != LC_F_READ &&
+                                 legal(s_f, s_ver, s_val, s_exp, cver, cval));
+        while (cand) {
+          const int t = __builtin_ctzll(cand);
+          cand &= cand - 1;
+          const int nver = cver + 1;
+          const int nval = rl32(s_val, t);
+          uint64_t nm = cm | (1ull << t);
+          // eager read closure at the new state
+          nm |= __ballot((((occ & ~nm) >> lane) & 1) && s_f == LC_F_READ &&
+                         legal(LC_F_READ, s_ver, s_val, s_exp, nver, nval));
+          o.explored++;
+          const uint64_t nsv = pack_sv(nver, nval);
+          const int r = (nm & bs) ? st.insert(ROLE_R, rR, nR, nm & ~bs, nsv, lane)
+                                  : st.insert(ROLE_W, rW, nW, nm, nsv, lane);
+          if (r < 0) {
+            overflow = true;
+            break;
+          }
+          if (o.explored > p.budget) {
+            over_budget = true;
+            break;
+          }
+        }
+      }
+      if (overflow || over_budget) {
+        o.verdict = LC_UNKNOWN;
+        o.reason = overflow ? LC_REASON_FRONTIER_LDS : LC_REASON_CONFIG_BUDGET;
+        return;
+      }
+      const int t = rF;
+      rF = rR;
+      rR = t;
+      nF = nR;
+      occ &= ~bs;
+      if (nF > o.max_frontier) o.max_frontier = nF;
+      if (nF == 0) {
+        o.verdict = LC_INVALID;
+        o.reason = LC_REASON_NONLINEARIZABLE;
+        o.fail_op = x_idx;
+        o.fail_end = nret;
+        return;
+      }
+    } else {
+      // ------------------------------------------------------- call of op i
+      const int li = (int)(i - base);
+      const int f = rl32(cur.f, li), val = rl32(cur.val, li);
+      const int ex = rl32(cur.exp, li), ver = rl32(cur.ver, li);
+      const int bad = rl32(cur.bad, li);
+      const int64_t ret = rl64(cur.ret, li);
+      if (bad || ncall <= prev_call) {
+        o.verdict = LC_UNKNOWN;
+        o.reason = LC_REASON_MALFORMED;
+        return;
+      }
+      if (f > LC_F_CAS) {  // register.clj:63: condp without default throws
+        o.verdict = LC_UNKNOWN;
+        o.reason = LC_REASON_UNKNOWN_F;
+        return;
+      }
+      prev_call = ncall;
+      // A read that never returned, or read [nil nil], is legal in every
+      // state and changes nothing: it never constrains the search.
+      const bool trivial =
+          (f == LC_F_READ) && (ret == kInf || (ver == -1 && val == -1));
+      if (!trivial) {
+        if (occ == ~0ull) {
+          o.verdict = LC_UNKNOWN;
+          o.reason = LC_REASON_WINDOW_OVERFLOW;
+          return;
+        }
+        const int s = __builtin_ctzll(~occ);
+        if (lane == s) {
+          s_f = f;
+          s_val = val;
+          s_exp = ex;
+          s_ver = ver;
+          s_ret = ret;
+          s_idx = (int)i;
+        }
+        occ |= 1ull << s;
+        if (f == LC_F_READ) {  // eager read closure at the call
+          for (int j0 = 0; j0 < nF; j0 += kWave) {
+            const int j = j0 + lane;
+            if (j < nF) {
+              const Cfg c = st.get(rF, j);
+              if (legal(LC_F_READ, ver, val, ex, sv_ver(c.sv), sv_val(c.sv)))
+                st.set_mask_lane(rF, j, c.mask | (1ull << s));
+            }
+          }
+        }
+      }
+      i++;
+      if (i - base == kWave) {
+        base += kWave;
+        cur = nxt;
+        nxt = load_rec(kops, base + kWave + lane, n);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void write_result(lc_key_result *r, const KeyOut &o) {
+  r->verdict = o.verdict;
+  r->reason = o.reason;
+  r->fail_op = o.fail_op;
+  r->fail_prefix_end = o.fail_end;
+  r->configs_explored = o.explored;
+  r->max_frontier = o.max_frontier;
+}
+
+__global__ __launch_bounds__(kWave *kWavesPerWG) void lds_tier_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
+    const int64_t key_base, const int64_t n_keys, const KParams p,
+    lc_key_result *__restrict__ out, int32_t *__restrict__ ovf_keys,
+    KStatus *__restrict__ status) {
+  __shared__ Cfg lds[kWavesPerWG][3][kLdsCap];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  const int64_t key = (int64_t)blockIdx.x * kWavesPerWG + wid;
+  if (key >= n_keys) return;
+  const int64_t beg = key_off[key], end = key_off[key + 1];
+  KeyOut o;
+  if (end < beg) {
+    o = KeyOut{LC_UNKNOWN, LC_REASON_MALFORMED, -1, -1, 0, 0};
+  } else {
+    LdsStore st{&lds[wid][0][0]};
+    check_key(ops + (beg - key_base), end - beg, p, st, o, lane);
+  }
+  if (lane == 0) {
+    write_result(&out[key], o);
+    if (o.reason == LC_REASON_MALFORMED) atomicAdd(&status->malformed, 1);
+    if (o.reason == LC_REASON_FRONTIER_LDS) {
+      const int pos = atomicAdd(&status->n_overflow, 1);
+      ovf_keys[pos] = (int32_t)key;
+    }
+  }
+}
+
+// Workspace layout per wave: 3 regions of cap Cfg, 2 tables of 2*cap Cfg,
+// 2 tag arrays of 2*cap uint32.
+__host__ __device__ inline size_t hbm_wave_bytes(int64_t cap) {
+  return (size_t)cap * 16 * 3 + (size_t)cap * 2 * 16 * 2 + (size_t)cap * 2 * 4 * 2;
+}
+
+__global__ __launch_bounds__(kWave) void hbm_tier_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
+    const int64_t key_base, const int32_t *__restrict__ keys, const int32_t n_list,
+    const KParams p, lc_key_result *__restrict__ out, char *__restrict__ ws,
+    const int64_t cap, KStatus *__restrict__ status) {
+  const int lane = threadIdx.x;
+  char *w = ws + (size_t)blockIdx.x * hbm_wave_bytes(cap);
+  HbmStore st;
+  st.base = reinterpret_cast<Cfg *>(w);
+  st.tabs = st.base + 3 * cap;
+  st.tags = reinterpret_cast<uint32_t *>(st.tabs + 4 * cap);
+  st.cap = (int)cap;
+  st.tmask = (uint32_t)(2 * cap - 1);
+  // Tags are zeroed by the host before the launch; epochs start at 1.
+  st.epoch = 0;
+  for (int li = blockIdx.x; li < n_list; li += gridDim.x) {
+    const int64_t key = keys[li];
+    const int64_t beg = key_off[key], end = key_off[key + 1];
+    KeyOut o;
+    check_key(ops + (beg - key_base), end - beg, p, st, o, lane);
+    if (o.reason == LC_REASON_FRONTIER_LDS) {
+      o.reason = LC_REASON_CONFIG_BUDGET;  // HBM sets full: budget exhausted
+    }
+    if (lane == 0) write_result(&out[key], o);
+  }
+  (void)status;
+}
+
+}  // namespace
+
+hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
+                           int64_t key_base, int64_t n_keys, const KParams &p,
+                           lc_key_result *d_out, int32_t *d_ovf_keys,
+                           KStatus *d_status, hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  const int64_t blocks = (n_keys + kWavesPerWG - 1) / kWavesPerWG;
+  hipLaunchKernelGGL(lds_tier_kernel, dim3((unsigned)blocks),
+                     dim3(kWave * kWavesPerWG), 0, stream, d_ops, d_key_off,
+                     key_base, n_keys, p, d_out, d_ovf_keys, d_status);
+  return hipGetLastError();
+}
+
+size_t hbm_tier_ws_bytes(int n_waves, int64_t cap) {
+  return hbm_wave_bytes(cap) * (size_t)n_waves;
+}
+
+hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
+                           int64_t key_base, const int32_t *d_keys,
+                           int32_t n_list, const KParams &p, lc_key_result *d_out,
+                           void *d_ws, int n_waves, int64_t cap,
+                           KStatus *d_status, hipStream_t stream) {
+  if (n_list <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hbm_tier_kernel, dim3((unsigned)n_waves), dim3(kWave), 0,
+                     stream, d_ops, d_key_off, key_base, d_keys, n_list, p,
+                     d_out, static_cast<char *>(d_ws), cap, d_status);
+  return hipGetLastError();
+}
+
+}  // namespace lcdev

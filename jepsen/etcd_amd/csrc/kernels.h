@@ -1,0 +1,49 @@
+// kernels.h — internal interface between the host runtime (lincheck.cpp) and
+// the device code (check_kernel.hip).  Not part of the public C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../../include/lincheck.h"
+
+namespace lcdev {
+
+// Launch parameters shared by both tiers.
+struct KParams {
+  int32_t init_ver;
+  int32_t init_val;
+  int64_t budget;  // max configurations generated per key
+};
+
+// Device-side status words, zeroed before every call.
+struct KStatus {
+  int32_t malformed;  // keys with LC_REASON_MALFORMED
+  int32_t n_overflow; // keys appended to the overflow list (LDS tier full)
+  int32_t pad[2];
+};
+
+constexpr int kWave = 64;
+constexpr int kWavesPerWG = 4;   // independent keys per 256-thread workgroup
+constexpr int kLdsCap = 128;     // configurations per LDS region (3 regions/wave)
+
+// LDS tier: one wavefront per key.  key_off is indexed by local key id; the
+// record pointer is rebased by key_base (= key_off[0] of the slice).
+// Keys whose frontier outgrows the LDS regions are appended to ovf_keys
+// (count in status->n_overflow) with reason LC_REASON_FRONTIER_LDS.
+hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
+                           int64_t key_base, int64_t n_keys, const KParams &p,
+                           lc_key_result *d_out, int32_t *d_ovf_keys,
+                           KStatus *d_status, hipStream_t stream);
+
+// HBM tier: re-runs the listed keys with configuration sets in global memory
+// (open-addressed hash tables, 128-byte buckets).  ws is a workspace of
+// hbm_tier_ws_bytes(n_waves, cap) bytes; cap = configurations per set.
+size_t hbm_tier_ws_bytes(int n_waves, int64_t cap);
+hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
+                           int64_t key_base, const int32_t *d_keys,
+                           int32_t n_list, const KParams &p, lc_key_result *d_out,
+                           void *d_ws, int n_waves, int64_t cap,
+                           KStatus *d_status, hipStream_t stream);
+
+}  // namespace lcdev

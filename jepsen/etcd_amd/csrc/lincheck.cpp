@@ -1,0 +1,397 @@
+// lincheck.cpp — host runtime behind include/lincheck.h.
+//
+// Replaces, as one unit, the checker built at
+//   /root/reference/src/jepsen/etcd/register.clj:108-112
+// (independent/checker over checker/linearizable with VersionedRegister).
+// jepsen.independent checks keys concurrently on a bounded JVM thread pool;
+// here all keys of a call go to the GPUs in one batch: contiguous,
+// cost-balanced key ranges per device (one host thread + one HIP stream per
+// device), an LDS-tier kernel over every key, then an HBM-tier re-run of the
+// few keys whose frontier outgrew LDS.  No collective is needed: keys are
+// independent and results land in the caller's array.  There is no CPU
+// fallback: without a usable GPU lc_open fails with -ENODEV.
+#include <errno.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../../include/lincheck.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int64_t kDefaultBudget = 1 << 22;   // configurations per key
+constexpr int64_t kHbmCap = 1 << 16;          // configurations per HBM set
+constexpr int kHbmWaves = 512;                // concurrent HBM-tier keys
+
+struct Dev {
+  int id = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+  void *d_ops = nullptr;
+  size_t ops_cap = 0;
+  int64_t *d_off = nullptr;
+  size_t off_cap = 0;
+  lc_key_result *d_out = nullptr;
+  size_t out_cap = 0;
+  int32_t *d_ovf = nullptr;
+  size_t ovf_cap = 0;
+  lcdev::KStatus *d_status = nullptr;
+  lcdev::KStatus *h_status = nullptr;  // pinned
+  void *d_ws = nullptr;
+  size_t ws_cap = 0;
+  double kernel_ms = 0, hbm_ms = 0;
+  int64_t n_hbm = 0;
+  int malformed = 0;
+};
+
+}  // namespace
+
+struct lc_ctx {
+  std::vector<Dev> devs;
+  std::string err;
+  std::mutex err_mu;
+  lc_stats stats{};
+};
+
+namespace {
+
+void set_err(lc_ctx *c, const std::string &s) {
+  std::lock_guard<std::mutex> g(c->err_mu);
+  c->err = s;
+}
+
+#define HIP_TRY(ctx, expr)                                                   \
+  do {                                                                       \
+    hipError_t e_ = (expr);                                                  \
+    if (e_ != hipSuccess) {                                                  \
+      set_err(ctx, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+      return -EIO;                                                           \
+    }                                                                        \
+  } while (0)
+
+template <class T>
+int ensure(lc_ctx *c, T **p, size_t *cap, size_t need) {
+  if (*cap >= need && *p) return 0;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  size_t n = std::max<size_t>(need, 256);
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(p), n);
+  if (e != hipSuccess) {
+    set_err(c, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return -ENOMEM;
+  }
+  *cap = n;
+  return 0;
+}
+
+int opts_to_params(lc_ctx *c, const lc_opts *o, lcdev::KParams *p) {
+  lc_opts d;
+  lc_default_opts(&d);
+  if (!o) o = &d;
+  if (o->init_version < 0 || o->init_version > 0x7FFFFFFE ||
+      o->init_value < -1 || o->init_value > 0x7FFFFFFE) {
+    set_err(c, "lc_opts: init_version/init_value out of int32 range");
+    return -EINVAL;
+  }
+  p->init_ver = (int32_t)o->init_version;
+  p->init_val = (int32_t)o->init_value;
+  p->budget = o->max_configs_per_key > 0 ? o->max_configs_per_key : kDefaultBudget;
+  return 0;
+}
+
+// Run both tiers for n_keys keys whose device arrays are in place.
+int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
+               int64_t key_base, int64_t n_keys, const lcdev::KParams &p,
+               lc_key_result *d_out, hipStream_t st, int64_t flags) {
+  d.kernel_ms = d.hbm_ms = 0;
+  d.n_hbm = 0;
+  d.malformed = 0;
+  if (n_keys <= 0) return 0;
+  if (n_keys > INT32_MAX) {
+    set_err(c, "lc_check: more than 2^31-1 keys in one call");
+    return -EINVAL;
+  }
+  int rc = ensure(c, &d.d_ovf, &d.ovf_cap, sizeof(int32_t) * (size_t)n_keys);
+  if (rc) return rc;
+  HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
+  HIP_TRY(c, hipEventRecord(d.e0, st));
+  HIP_TRY(c, lcdev::launch_lds_tier(d_ops, d_off, key_base, n_keys, p, d_out,
+                                    d.d_ovf, d.d_status, st));
+  HIP_TRY(c, hipEventRecord(d.e1, st));
+  HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
+                            hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  float ms = 0;
+  HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.e1));
+  d.kernel_ms = ms;
+  d.malformed = d.h_status->malformed;
+  const int32_t n_ovf = d.h_status->n_overflow;
+  d.n_hbm = n_ovf;
+  if (n_ovf > 0 && !(flags & LC_FLAG_NO_HBM_RETRY)) {
+    const int waves = std::min<int>(kHbmWaves, n_ovf);
+    const size_t ws = lcdev::hbm_tier_ws_bytes(waves, kHbmCap);
+    rc = ensure(c, reinterpret_cast<char **>(&d.d_ws), &d.ws_cap, ws);
+    if (rc) return rc;
+    HIP_TRY(c, hipMemsetAsync(d.d_ws, 0, ws, st));
+    HIP_TRY(c, hipEventRecord(d.e1, st));
+    HIP_TRY(c, lcdev::launch_hbm_tier(d_ops, d_off, key_base, d.d_ovf, n_ovf, p,
+                                      d_out, d.d_ws, waves, kHbmCap,
+                                      d.d_status, st));
+    HIP_TRY(c, hipEventRecord(d.e2, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    HIP_TRY(c, hipEventElapsedTime(&ms, d.e1, d.e2));
+    d.hbm_ms = ms;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lc_abi_version(void) { return LC_ABI_VERSION; }
+
+void lc_default_opts(lc_opts *o) {
+  if (!o) return;
+  o->init_version = 0;
+  o->init_value = LC_NIL;
+  o->max_configs_per_key = 0;
+  o->time_budget_ms = 0;
+  o->flags = 0;
+}
+
+int lc_open(uint32_t device_mask, lc_ctx **out) {
+  if (!out) return -EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -ENODEV;
+  lc_ctx *c = new lc_ctx();
+  for (int i = 0; i < n && i < 32; i++) {
+    if (device_mask && !(device_mask & (1u << i))) continue;
+    Dev d;
+    d.id = i;
+    if (hipSetDevice(i) != hipSuccess ||
+        hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&d.e0) != hipSuccess || hipEventCreate(&d.e1) != hipSuccess ||
+        hipEventCreate(&d.e2) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&d.d_status), sizeof(lcdev::KStatus)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess) {
+      lc_close(c);
+      return -ENODEV;
+    }
+    c->devs.push_back(d);
+  }
+  if (c->devs.empty()) {
+    delete c;
+    return -ENODEV;
+  }
+  *out = c;
+  return 0;
+}
+
+void lc_close(lc_ctx *c) {
+  if (!c) return;
+  for (Dev &d : c->devs) {
+    (void)hipSetDevice(d.id);
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+    if (d.d_ops) (void)hipFree(d.d_ops);
+    if (d.d_off) (void)hipFree(d.d_off);
+    if (d.d_out) (void)hipFree(d.d_out);
+    if (d.d_ovf) (void)hipFree(d.d_ovf);
+    if (d.d_ws) (void)hipFree(d.d_ws);
+    if (d.d_status) (void)hipFree(d.d_status);
+    if (d.h_status) (void)hipHostFree(d.h_status);
+    if (d.e0) (void)hipEventDestroy(d.e0);
+    if (d.e1) (void)hipEventDestroy(d.e1);
+    if (d.e2) (void)hipEventDestroy(d.e2);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+  }
+  delete c;
+}
+
+const char *lc_last_error(lc_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int lc_last_stats(lc_ctx *c, lc_stats *out) {
+  if (!c || !out) return -EINVAL;
+  *out = c->stats;
+  return 0;
+}
+
+// Contiguous split: key k's cost is its record count plus a fixed per-key
+// overhead (one wave launch + result write); boundaries at equal cost.
+int lc_plan_partition(const lc_op *ops, const int64_t *key_off, int64_t n_keys,
+                      int32_t n_parts, int64_t *bounds) {
+  (void)ops;
+  if (!key_off || !bounds || n_parts < 1 || n_keys < 0) return -EINVAL;
+  const int64_t kOverhead = 64;
+  const int64_t total = (key_off[n_keys] - key_off[0]) + kOverhead * n_keys;
+  bounds[0] = 0;
+  int64_t k = 0;
+  for (int32_t p = 1; p < n_parts; p++) {
+    const long double goal = (long double)total * p / n_parts;
+    while (k < n_keys &&
+           (long double)((key_off[k] - key_off[0]) + kOverhead * k) < goal)
+      k++;
+    bounds[p] = k;
+  }
+  bounds[n_parts] = n_keys;
+  return 0;
+}
+
+int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
+             int64_t n_keys, const lc_opts *opts, lc_key_result *out) {
+  if (!c) return -EINVAL;
+  const auto t0 = std::chrono::steady_clock::now();
+  c->stats = lc_stats{};
+  if (n_keys < 0 || (n_keys > 0 && (!ops || !key_off || !out))) {
+    set_err(c, "lc_check: null buffer or negative n_keys");
+    return -EINVAL;
+  }
+  if (n_keys == 0) return 0;
+  if (key_off[0] < 0) {
+    set_err(c, "lc_check: key_off[0] < 0");
+    return -EINVAL;
+  }
+  for (int64_t k = 0; k < n_keys; k++)
+    if (key_off[k + 1] < key_off[k]) {
+      set_err(c, "lc_check: key_off not monotone at key " + std::to_string(k));
+      return -EINVAL;
+    }
+  lcdev::KParams p;
+  int rc = opts_to_params(c, opts, &p);
+  if (rc) return rc;
+  const int64_t flags = opts ? opts->flags : 0;
+  const int nd = (int)c->devs.size();
+  std::vector<int64_t> bounds(nd + 1);
+  lc_plan_partition(ops, key_off, n_keys, nd, bounds.data());
+
+  std::vector<int> rcs(nd, 0);
+  auto work = [&](int di) {
+    Dev &d = c->devs[di];
+    const int64_t a = bounds[di], b = bounds[di + 1];
+    const int64_t nk = b - a;
+    if (nk <= 0) return;
+    if (hipSetDevice(d.id) != hipSuccess) {
+      rcs[di] = -EIO;
+      return;
+    }
+    const int64_t r0 = key_off[a], r1 = key_off[b];
+    const size_t ops_bytes = sizeof(lc_op) * (size_t)(r1 - r0);
+    int r = ensure(c, reinterpret_cast<char **>(&d.d_ops), &d.ops_cap, ops_bytes);
+    if (!r) r = ensure(c, &d.d_off, &d.off_cap, sizeof(int64_t) * (size_t)(nk + 1));
+    if (!r) r = ensure(c, &d.d_out, &d.out_cap, sizeof(lc_key_result) * (size_t)nk);
+    if (r) {
+      rcs[di] = r;
+      return;
+    }
+    hipError_t e = hipSuccess;
+    if (ops_bytes)
+      e = hipMemcpyAsync(d.d_ops, ops + r0, ops_bytes, hipMemcpyHostToDevice, d.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d.d_off, key_off + a, sizeof(int64_t) * (size_t)(nk + 1),
+                         hipMemcpyHostToDevice, d.stream);
+    if (e != hipSuccess) {
+      set_err(c, std::string("hipMemcpyAsync H2D: ") + hipGetErrorString(e));
+      rcs[di] = -EIO;
+      return;
+    }
+    r = run_device(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, r0, nk, p,
+                   d.d_out, d.stream, flags);
+    if (r) {
+      rcs[di] = r;
+      return;
+    }
+    e = hipMemcpyAsync(out + a, d.d_out, sizeof(lc_key_result) * (size_t)nk,
+                       hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
+    if (e != hipSuccess) {
+      set_err(c, std::string("hipMemcpyAsync D2H: ") + hipGetErrorString(e));
+      rcs[di] = -EIO;
+    }
+  };
+  if (nd == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int di = 0; di < nd; di++) th.emplace_back(work, di);
+    for (auto &t : th) t.join();
+  }
+  int malformed = 0;
+  for (int di = 0; di < nd; di++) {
+    if (rcs[di] && !rc) rc = rcs[di];
+    c->stats.kernel_ms += c->devs[di].kernel_ms;
+    c->stats.hbm_kernel_ms += c->devs[di].hbm_ms;
+    c->stats.n_hbm_keys += c->devs[di].n_hbm;
+    malformed += c->devs[di].malformed;
+  }
+  c->stats.n_keys = n_keys;
+  c->stats.n_ops = key_off[n_keys] - key_off[0];
+  c->stats.n_devices = nd;
+  c->stats.total_ms = std::chrono::duration<double, std::milli>(
+                          std::chrono::steady_clock::now() - t0).count();
+  if (rc) return rc;
+  if (malformed) {
+    set_err(c, std::to_string(malformed) + " key(s) hold malformed records");
+    return -EINVAL;
+  }
+  return 0;
+}
+
+int lc_check_device(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
+                    int64_t n_keys, const lc_opts *opts, lc_key_result *d_out,
+                    void *stream) {
+  if (!c) return -EINVAL;
+  const auto t0 = std::chrono::steady_clock::now();
+  c->stats = lc_stats{};
+  if (n_keys < 0 || (n_keys > 0 && (!d_ops || !d_key_off || !d_out))) {
+    set_err(c, "lc_check_device: null buffer or negative n_keys");
+    return -EINVAL;
+  }
+  if (reinterpret_cast<uintptr_t>(d_ops) % 16) {
+    set_err(c, "lc_check_device: ops must be 16-byte aligned");
+    return -EINVAL;
+  }
+  lcdev::KParams p;
+  int rc = opts_to_params(c, opts, &p);
+  if (rc) return rc;
+  Dev &d = c->devs[0];
+  HIP_TRY(c, hipSetDevice(d.id));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d.stream;
+  // key_off[0] is the record base of ops; read it (8 bytes) so a caller may
+  // pass a key_off slice of a larger array.
+  int64_t base = 0, last = 0;
+  if (n_keys > 0) {
+    HIP_TRY(c, hipMemcpyAsync(&base, d_key_off, sizeof(int64_t),
+                              hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipMemcpyAsync(&last, d_key_off + n_keys, sizeof(int64_t),
+                              hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+  }
+  rc = run_device(c, d, d_ops, d_key_off, base, n_keys, p, d_out, st,
+                  opts ? opts->flags : 0);
+  c->stats.kernel_ms = d.kernel_ms;
+  c->stats.hbm_kernel_ms = d.hbm_ms;
+  c->stats.n_hbm_keys = d.n_hbm;
+  c->stats.n_keys = n_keys;
+  c->stats.n_ops = last - base;
+  c->stats.n_devices = 1;
+  c->stats.total_ms = std::chrono::duration<double, std::milli>(
+                          std::chrono::steady_clock::now() - t0).count();
+  if (rc) return rc;
+  if (d.malformed) {
+    set_err(c, std::to_string(d.malformed) + " key(s) hold malformed records");
+    return -EINVAL;
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+"""CPU oracle for the register linearizability check — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this package; the product path (jepsen/etcd_amd) never does.  PARITY UNPINNED
+against outputs of the reference itself (Clojure/Knossos; no JVM here and no
+reference fixtures exist for this path): see oracle.h and DESIGN.md.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+JIT, WGL = 0, 1
+
+RESULT_DTYPE = np.dtype([
+    ("verdict", "<i4"), ("reason", "<i4"), ("fail_op", "<i8"),
+    ("fail_prefix_end", "<i8"), ("configs_explored", "<i8"),
+    ("max_frontier", "<i8"),
+])
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [("init_version", ctypes.c_int64), ("init_value", ctypes.c_int64),
+                ("max_configs_per_key", ctypes.c_int64),
+                ("time_budget_ms", ctypes.c_int64), ("flags", ctypes.c_int64)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp = ctypes.c_void_p
+        L.oracle_check.argtypes = [vp, vp, ctypes.c_int64, ctypes.POINTER(_Opts), vp,
+                                   ctypes.c_int, ctypes.c_int]
+        L.oracle_check.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def check(ops, key_off, algo=JIT, n_threads=1, max_configs=0, init_version=0,
+          init_value=-1):
+    """Returns (rc, results) with the same layout as the GPU library."""
+    ops = np.ascontiguousarray(ops, dtype=np.int64).reshape(-1, 6)
+    key_off = np.ascontiguousarray(key_off, dtype=np.int64)
+    n = len(key_off) - 1
+    out = np.zeros(max(n, 0), dtype=RESULT_DTYPE)
+    o = _Opts(init_version, init_value, max_configs, 0, 0)
+    rc = lib().oracle_check(ops.ctypes.data_as(ctypes.c_void_p),
+                            key_off.ctypes.data_as(ctypes.c_void_p), n,
+                            ctypes.byref(o), out.ctypes.data_as(ctypes.c_void_p),
+                            algo, n_threads)
+    return rc, out
