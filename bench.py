@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Benchmark: history ops linearizability-checked per second (BASELINE.json).
+
+One step = one lc_check_device() call over one batch of resident synthetic
+register histories: by default the C2 workload of BASELINE.json configs[1],
+10k keys x 1k ops (packed records), concurrency 20, valid CAS-register+version
+histories, on one MI355X.  For N GPUs (torchrun, one rank per GPU) every rank
+checks its own 10k-key batch (distinct seeds): per-GPU work is fixed
+("scaling": "weak") and keys are independent, so the data path has no
+collective; the only cross-rank traffic is the timing barrier/max.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with the
+roofline of the dominant kernel (lds_tier_kernel, HIP events on its stream)
+and a CPU baseline: the oracle's C restatement of knossos (faster of its JIT
+and WGL analyzers) on a bounded sample of the same workload, on host threads.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = ("history ops linearizability-checked/sec (1/2/4/8 GPU) + per-key "
+          "verdict parity")
+ALGO_BYTES_PER_OP = 176   # 48-B record + one 128-B probe line
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--keys", type=int, default=10000)
+    ap.add_argument("--ops-per-key", type=int, default=1000)
+    ap.add_argument("--concurrency", type=int, default=20)
+    ap.add_argument("--p-info", type=float, default=0.0)
+    ap.add_argument("--cpu-sample-keys", type=int, default=2000)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from jepsen.etcd_amd import abi
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    # ---- workload (seeded per rank: configs[1] = C2, seed 0x5EED0002)
+    seed = 0x5EED0002 + 0x1000 * rank
+    ops, key_off, _, n_inv = abi.synth(args.keys, args.ops_per_key,
+                                       concurrency=args.concurrency,
+                                       p_info=args.p_info, seed=seed)
+    n_ops = int(key_off[-1])
+    d_ops = torch.from_numpy(ops).to(dev)
+    d_off = torch.from_numpy(key_off).to(dev)
+    d_out = torch.zeros(args.keys * abi.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ctx = abi.Context(device_mask=1 << local)
+
+    def step():
+        ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), args.keys,
+                         d_out.data_ptr(), stream=stream.cuda_stream)
+        return ctx.stats()
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms, hms = [], []
+    for _ in range(args.steps):
+        s = step()
+        kms.append(s["kernel_ms"])
+        hms.append(s["hbm_kernel_ms"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    res = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
+    counts = torch.tensor([n_ops, int((res["verdict"] == 1).sum()),
+                           int((res["verdict"] == 0).sum()),
+                           int((res["verdict"] == -1).sum())],
+                          dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(counts)
+    total_ops, n_valid, n_invalid, n_unknown = [int(v) for v in counts.tolist()]
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = total_ops * args.steps / elapsed
+    kernel_ms = float(np.mean(kms))
+    achieved = ALGO_BYTES_PER_OP * n_ops / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("n_ops") == n_ops:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
+
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "ops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (seeded register+version histories, lc_synth_register)",
+        "config": {
+            "workload": "C2: %d keys x %d ops/key (packed records), concurrency %d, "
+                        "valid CAS-register+version histories, per GPU"
+                        % (args.keys, args.ops_per_key, args.concurrency),
+            "keys_per_gpu": args.keys,
+            "ops_per_key": args.ops_per_key,
+            "invocations_per_gpu_incl_fail": int(n_inv),
+            "concurrency": args.concurrency,
+            "p_info": args.p_info,
+            "parallelism": "keys sharded, 1 rank per GPU, no data-path collective",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "lds_tier_kernel",
+            "kernel_ms": kernel_ms,
+            "algorithmic_bytes_per_op": ALGO_BYTES_PER_OP,
+        },
+        "verdicts": {"valid": n_valid, "invalid": n_invalid, "unknown": n_unknown},
+        "hbm_tier_ms": float(np.mean(hms)),
+        "cpu_baseline": None,
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args, ops, key_off, res)
+
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, ops, key_off, gpu_res):
+    """The oracle (C restatement of knossos.linear / knossos.wgl; no JVM on
+    the box, so not Knossos itself) on the first --cpu-sample-keys keys of the
+    same workload, on --cpu-threads host threads.  Knossos races both
+    analyzers per key; the faster analyzer's whole-sample rate is reported.
+    Also checks the sample's verdicts against the GPU's."""
+    import oracle
+    k = min(args.cpu_sample_keys, len(key_off) - 1)
+    sub_ops = ops[: key_off[k]]
+    sub_off = key_off[: k + 1]
+    best = None
+    mism = 0
+    for name, algo in (("jit", oracle.JIT), ("wgl", oracle.WGL)):
+        t0 = time.perf_counter()
+        _, r = oracle.check(sub_ops, sub_off, algo=algo, n_threads=args.cpu_threads)
+        dt = time.perf_counter() - t0
+        mism += int((r["verdict"] != gpu_res["verdict"][:k]).sum())
+        rate = len(sub_ops) / dt
+        if best is None or rate > best[0]:
+            best = (rate, name, dt)
+    return {
+        "value": best[0],
+        "unit": "ops/s",
+        "cores": args.cpu_threads,
+        "kind": "port",
+        "sample": "%d keys x %d ops of the same C2 workload (%d records), "
+                  "oracle/%s restatement of knossos (faster of jit/wgl), %.1f s"
+                  % (k, args.ops_per_key, len(sub_ops), best[1], best[2]),
+        "verdict_mismatches_vs_gpu": mism,
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -14,11 +14,15 @@
 //    the model step next from state s" is ONE vector compare + __ballot over
 //    all 64 open calls (wave-level candidate compaction);
 //  * a configuration (linearized-slot bitmask, (version, value)) is 16 bytes and
-//    wave-uniform; the frontier lives in LDS, 3 regions x 128 configs per wave;
+//    wave-uniform.  While the frontier holds ONE configuration (the common case:
+//    :ok mutations are pinned by version, register.clj:64-75) it lives in SGPRs
+//    and a return's expansion is a chain walk of ballots; a larger frontier
+//    lives in LDS (3 regions x kLdsCap configs per wave), and a key that
+//    outgrows LDS is re-run from HBM hash tables (hbm_tier_kernel);
 //  * the key's records are streamed from HBM 64 at a time (one 48-byte record
 //    per lane, double-buffered), and read out by v_readlane as calls happen;
 //  * the next event is min(next call, min over open slots of ret): a 64-lane
-//    min reduction, so no per-key event sort is ever built.
+//    DPP min to an SGPR, so no per-key event sort is ever built.
 //
 // Search (Lowe's just-in-time linearization, as knossos.linear) with one exact,
 // model-specific reduction — EAGER READ CLOSURE: a read (a no-op on the state,
@@ -35,6 +39,7 @@ namespace {
 
 constexpr int64_t kInf = INT64_MAX;
 constexpr int64_t kFieldMax = 0x7FFFFFFE;  // int32 range for value/expected/version
+constexpr uint32_t kNever = 0xFFFFFFFFu;   // key-relative index of "no return"
 
 struct Cfg {
   uint64_t mask;  // bit t: the op in window slot t is linearized
@@ -50,11 +55,6 @@ __device__ __forceinline__ int32_t sv_val(uint64_t sv) { return (int32_t)(uint32
 __device__ __forceinline__ int rl32(int v, int l) {
   return __builtin_amdgcn_readlane(v, l);
 }
-__device__ __forceinline__ int64_t rl64(int64_t v, int l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
 __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
@@ -65,13 +65,21 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-__device__ __forceinline__ int64_t wave_min64(int64_t v) {
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int64_t w = (int64_t)__shfl_xor((long long)v, o);
-    v = w < v ? w : v;
-  }
-  return v;
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+// Minimum of v over the 64 lanes as a wave-uniform (SGPR) value: four DPP
+// min steps inside each 16-lane row (quad_perm [1,0,3,2], quad_perm
+// [2,3,0,1], row_half_mirror, row_mirror), then the four row minima are read
+// with v_readlane and combined on the scalar unit.  No LDS round trip.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  v = umin(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
+  v = umin(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
+  v = umin(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));
+  v = umin(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+  const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+  const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  return umin(umin(r0, r1), umin(r2, r3));
 }
 
 // VersionedRegister.step legality (register.clj:60-96); NIL = -1.
@@ -86,34 +94,40 @@ __device__ __forceinline__ bool legal(int f, int opver, int opval, int opexp,
   return (opver == -1 || opver == ver + 1) && (f != LC_F_CAS || val == opexp);
 }
 
-// One record, decoded by one lane.
+// One record, decoded by one lane.  Event indices become key-relative 32-bit
+// (index - first call of the key; LC_INF -> kNever) so event selection is a
+// 32-bit min.  A key whose indices span >= 2^32-1 is rejected as malformed
+// (documented limit).
 struct Rec {
   int f, val, exp, ver, bad;
-  int64_t call, ret;
+  uint32_t call, ret;
 };
 
 __device__ __forceinline__ Rec load_rec(const lc_op *__restrict__ o, int64_t i,
-                                        int64_t n) {
+                                        int64_t n, int64_t base_idx) {
   Rec r;
   if (i < n) {
     const longlong2 *p = reinterpret_cast<const longlong2 *>(o + i);
     const longlong2 a = p[0], b = p[1], c = p[2];
     const int64_t f = a.x, value = a.y, expected = b.x, version = b.y;
-    r.call = c.x;
-    r.ret = c.y;
+    const int64_t call = c.x, ret = c.y;
+    const int64_t rc = call - base_idx, rr = ret - base_idx;
     r.bad = (value < -1) | (value > kFieldMax) | (expected < -1) |
             (expected > kFieldMax) | (version < -1) | (version > kFieldMax) |
-            (r.call < 0) | (r.ret <= r.call);
+            (call < 0) | (ret <= call) | (rc < 0) | (rc >= (int64_t)kNever) |
+            ((ret != kInf) & (rr >= (int64_t)kNever));
     r.f = (f >= 0 && f <= 2) ? (int)f : 3;
     r.val = (int)value;
     r.exp = (int)expected;
     r.ver = (int)version;
+    r.call = (uint32_t)rc;
+    r.ret = ret == kInf ? kNever : (uint32_t)rr;
   } else {
     r.f = 0;
     r.val = r.exp = r.ver = -1;
     r.bad = 0;
-    r.call = kInf;
-    r.ret = kInf;
+    r.call = kNever;
+    r.ret = kNever;
   }
   return r;
 }
@@ -167,13 +181,14 @@ struct LdsStore {
 // HBM store: regions are global arrays of `cap` configurations; R and W each
 // have an open-addressed table of 2*cap entries in 8-entry (128-byte) buckets,
 // valid when their epoch tag equals the current return's epoch, so a table is
-// "cleared" by bumping the epoch.  One wave owns one workspace: no atomics.
+// "cleared" by bumping the epoch.  One wave owns one workspace.  Probing is
+// linear from the start of the hashed bucket, whole buckets at a time.
 struct HbmStore {
   Cfg *base;      // 3 regions of cap configurations, contiguous
   Cfg *tabs;      // 2 tables (roles R, W) of 2*cap entries
   uint32_t *tags; // 2 tag arrays of 2*cap
   int cap;         // configurations per region
-  uint32_t tmask;  // table entries - 1 (power of two)
+  uint32_t tmask;  // table entries - 1 (power of two, >= 7)
   uint32_t epoch;
   __device__ __forceinline__ Cfg *reg(int r) const { return base + (size_t)r * cap; }
   __device__ __forceinline__ Cfg *tab(int role) const { return tabs + (size_t)role * (tmask + 1); }
@@ -191,12 +206,13 @@ struct HbmStore {
     return (uint32_t)h;
   }
   // Lane-parallel: each active lane inserts its own distinct config into the
-  // role's table (claiming a tag with atomicCAS: lanes of one wave may race on
-  // one bucket) and stores it at region index j.
+  // role's table, claiming the first free entry at or after its bucket start
+  // with atomicCAS (lanes of one wave may race for one bucket), and stores it
+  // at region index j.
   __device__ __forceinline__ void add_unique_lane(int role, int r, int j,
                                                   const Cfg &c) {
     reg(r)[j] = c;
-    uint32_t h = hash(c.mask, c.sv) & tmask;
+    uint32_t h = (hash(c.mask, c.sv) & tmask) & ~7u;
     for (;;) {
       const uint32_t old = tag(role)[h];
       if (old != epoch) {
@@ -210,9 +226,10 @@ struct HbmStore {
     }
   }
   // Wave-uniform dedup insert: probe one 128-byte bucket (8 lanes x 16 B)
-  // per step, linear over buckets.
+  // per step.
   __device__ __forceinline__ int insert(int role, int r, int &n, uint64_t m,
                                         uint64_t sv, int lane) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     uint32_t b = (hash(m, sv) & tmask) & ~7u;
     const int sub = lane & 7;
     for (uint32_t probes = 0; probes <= tmask; probes += 8) {
@@ -234,6 +251,7 @@ struct HbmStore {
           tab(role)[b + slot] = Cfg{m, sv};
         }
         if (lane == 0) reg(r)[n] = Cfg{m, sv};
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         n++;
         return 1;
       }
@@ -245,6 +263,77 @@ struct HbmStore {
 
 // ------------------------------------------------------------ the search
 
+// Per-lane record of the window slot this lane holds.
+struct Slot {
+  int f, val, exp, ver, idx;
+  uint32_t ret;  // kNever: free or crashed (never returns)
+};
+
+// Candidate mutations from configuration (cm, state) and the eager read
+// closure of a successor: ballots over the 64 window slots.
+__device__ __forceinline__ uint64_t mutation_candidates(const Slot &sl, uint64_t occ,
+                                                        uint64_t cm, int ver, int val,
+                                                        int lane) {
+  const bool pend = ((occ & ~cm) >> lane) & 1;
+  return __ballot(pend && sl.f != LC_F_READ && legal(sl.f, sl.ver, sl.val, sl.exp, ver, val));
+}
+__device__ __forceinline__ uint64_t read_closure(const Slot &sl, uint64_t occ,
+                                                 uint64_t nm, int ver, int val,
+                                                 int lane) {
+  const bool pend = ((occ & ~nm) >> lane) & 1;
+  return __ballot(pend && sl.f == LC_F_READ &&
+                  legal(LC_F_READ, sl.ver, sl.val, sl.exp, ver, val));
+}
+
+// Expand the frontier held in region rF (nF configurations) for the return
+// of the op in slot s.  Returns the new frontier size (in region rR), or -1
+// (LDS/HBM sets full) / -2 (configuration budget).
+template <class Store>
+__device__ __forceinline__ int general_return(Store &st, const Slot &sl, uint64_t occ,
+                                              int s, int rF, int rR, int rW, int nF,
+                                              const KParams &p, KeyOut &o, int lane) {
+  const uint64_t bs = 1ull << s;
+  st.begin_return();
+  int nR = 0, nW = 0;
+  // Split F: configs that already linearized x go to R (x's bit dropped),
+  // the others to the worklist W.  Ballot + lanes_below compaction.
+  for (int j0 = 0; j0 < nF; j0 += kWave) {
+    const int j = j0 + lane;
+    const bool v = j < nF;
+    Cfg c{0, 0};
+    if (v) c = st.get(rF, j);
+    const bool has = v && (c.mask & bs);
+    const bool lacks = v && !(c.mask & bs);
+    const uint64_t mh = __ballot(has), ml = __ballot(lacks);
+    if (has) st.add_unique_lane(ROLE_R, rR, nR + lanes_below(mh), Cfg{c.mask & ~bs, c.sv});
+    if (lacks) st.add_unique_lane(ROLE_W, rW, nW + lanes_below(ml), c);
+    nR += __popcll(mh);
+    nW += __popcll(ml);
+  }
+  // Expand W breadth-first until x is linearized in each branch.
+  for (int head = 0; head < nW; head++) {
+    const Cfg c = st.get(rW, head);
+    const uint64_t cm = rfl64(c.mask), csv = rfl64(c.sv);
+    const int cver = sv_ver(csv), cval = sv_val(csv);
+    uint64_t cand = mutation_candidates(sl, occ, cm, cver, cval, lane);
+    while (cand) {
+      const int t = __builtin_ctzll(cand);
+      cand &= cand - 1;
+      const int nver = cver + 1;
+      const int nval = rl32(sl.val, t);
+      uint64_t nm = cm | (1ull << t);
+      nm |= read_closure(sl, occ, nm, nver, nval, lane);
+      o.explored++;
+      const uint64_t nsv = pack_sv(nver, nval);
+      const int r = (nm & bs) ? st.insert(ROLE_R, rR, nR, nm & ~bs, nsv, lane)
+                              : st.insert(ROLE_W, rW, nW, nm, nsv, lane);
+      if (r < 0) return -1;
+      if (o.explored > p.budget) return -2;
+    }
+  }
+  return nR;
+}
+
 template <class Store>
 __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
                           const KParams &p, Store &st, KeyOut &o,
@@ -255,98 +344,113 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
   o.fail_end = -1;
   o.explored = 1;
   o.max_frontier = 1;
+  if (n <= 0) return;
 
-  int rF = 0, rR = 1, rW = 2;
-  int nF = 0;
-  st.begin_return();
-  st.insert(ROLE_R, rF, nF, 0ull, pack_sv(p.init_ver, p.init_val), lane);
+  // Frontier: one configuration in SGPRs (single) or nF of them in region rF.
+  bool single = true;
+  uint64_t fm = 0, fsv = pack_sv(p.init_ver, p.init_val);
+  int rF = 0, rR = 1, rW = 2, nF = 1;
 
-  // Window slot held by this lane.
-  int s_f = 0, s_val = -1, s_exp = -1, s_ver = -1, s_idx = -1;
-  int64_t s_ret = kInf;
-  uint64_t occ = 0;  // occupied slots (uniform)
+  Slot sl{0, -1, -1, -1, -1, kNever};
+  uint64_t occ = 0;  // occupied window slots (uniform)
 
-  Rec cur = load_rec(kops, lane, n);
-  Rec nxt = load_rec(kops, kWave + lane, n);
-  int64_t base = 0, i = 0, prev_call = -1;
+  const int64_t base_idx = kops[0].call;
+  Rec cur = load_rec(kops, lane, n, base_idx);
+  Rec nxt = load_rec(kops, kWave + lane, n, base_idx);
+  int64_t base = 0, i = 0;
+  uint32_t prev_call = 0;
 
   for (;;) {
-    const int64_t ncall = (i < n) ? rl64(cur.call, (int)(i - base)) : kInf;
-    const bool mine = (occ >> lane) & 1;
-    const int64_t nret = wave_min64(mine ? s_ret : kInf);
-    if (i >= n && nret == kInf) break;  // only crashed ops remain open
+    const uint32_t ncall = (i < n) ? (uint32_t)rl32((int)cur.call, (int)(i - base)) : kNever;
+    const uint32_t nret = wave_min_u32(sl.ret);
+    if (i >= n && nret == kNever) break;  // only crashed ops remain open
 
     if (nret < ncall) {
       // ----------------------------------------------------- return of x
-      const uint64_t hit = __ballot(mine && s_ret == nret);
+      const uint64_t hit = __ballot(sl.ret == nret);
       const int s = __builtin_ctzll(hit);
       const uint64_t bs = 1ull << s;
-      const int x_idx = rl32(s_idx, s);
-      st.begin_return();
-      int nR = 0, nW = 0;
-      // Split F: configs that already linearized x go to R (x's bit dropped),
-      // the others to the worklist W.  Ballot + lanes_below compaction.
-      for (int j0 = 0; j0 < nF; j0 += kWave) {
-        const int j = j0 + lane;
-        const bool v = j < nF;
-        Cfg c{0, 0};
-        if (v) c = st.get(rF, j);
-        const bool has = v && (c.mask & bs);
-        const bool lacks = v && !(c.mask & bs);
-        const uint64_t mh = __ballot(has), ml = __ballot(lacks);
-        if (has) st.add_unique_lane(ROLE_R, rR, nR + lanes_below(mh), Cfg{c.mask & ~bs, c.sv});
-        if (lacks) st.add_unique_lane(ROLE_W, rW, nW + lanes_below(ml), c);
-        nR += __popcll(mh);
-        nW += __popcll(ml);
-      }
-      // Expand W breadth-first until x is linearized in each branch.
-      bool overflow = false, over_budget = false;
-      for (int head = 0; head < nW && !overflow && !over_budget; head++) {
-        const Cfg c = st.get(rW, head);
-        const uint64_t cm = rfl64(c.mask), csv = rfl64(c.sv);
-        const int cver = sv_ver(csv), cval = sv_val(csv);
-        const bool pend = ((occ & ~cm) >> lane) & 1;
-        uint64_t cand = __ballot(pend && s_f != LC_F_READ &&
-                                 legal(s_f, s_ver, s_val, s_exp, cver, cval));
-        while (cand) {
-          const int t = __builtin_ctzll(cand);
-          cand &= cand - 1;
-          const int nver = cver + 1;
-          const int nval = rl32(s_val, t);
-          uint64_t nm = cm | (1ull << t);
-          // eager read closure at the new state
-          nm |= __ballot((((occ & ~nm) >> lane) & 1) && s_f == LC_F_READ &&
-                         legal(LC_F_READ, s_ver, s_val, s_exp, nver, nval));
-          o.explored++;
-          const uint64_t nsv = pack_sv(nver, nval);
-          const int r = (nm & bs) ? st.insert(ROLE_R, rR, nR, nm & ~bs, nsv, lane)
-                                  : st.insert(ROLE_W, rW, nW, nm, nsv, lane);
-          if (r < 0) {
-            overflow = true;
-            break;
+      const int x_idx = rl32(sl.idx, s);
+      bool empty = false;
+      if (single) {
+        if (!(fm & bs)) {
+          // Chain walk: while exactly one mutation can step the lone
+          // configuration, the JIT expansion is a path (versions strictly
+          // increase, so no configuration repeats) and stays in SGPRs.
+          const int64_t explored0 = o.explored;
+          uint64_t cm = fm, csv = fsv;
+          bool branch = false;
+          for (;;) {
+            const int cver = sv_ver(csv), cval = sv_val(csv);
+            const uint64_t cand = mutation_candidates(sl, occ, cm, cver, cval, lane);
+            if (cand == 0) {
+              empty = true;
+              break;
+            }
+            if (cand & (cand - 1)) {
+              branch = true;
+              break;
+            }
+            const int t = __builtin_ctzll(cand);
+            const int nver = cver + 1;
+            const int nval = rl32(sl.val, t);
+            uint64_t nm = cm | (1ull << t);
+            nm |= read_closure(sl, occ, nm, nver, nval, lane);
+            o.explored++;
+            if (o.explored > p.budget) {
+              o.verdict = LC_UNKNOWN;
+              o.reason = LC_REASON_CONFIG_BUDGET;
+              return;
+            }
+            cm = nm;
+            csv = pack_sv(nver, nval);
+            if (nm & bs) break;
           }
-          if (o.explored > p.budget) {
-            over_budget = true;
-            break;
+          if (branch) {
+            // Several successors: redo this return on the general path from
+            // the lone configuration.
+            o.explored = explored0;
+            empty = false;
+            single = false;
+            rF = 0;
+            if (lane == 0) st.reg(rF)[0] = Cfg{fm, fsv};
+            rR = 1;
+            rW = 2;
+            nF = 1;
+          } else if (!empty) {
+            fm = cm;
+            fsv = csv;
           }
         }
+        if (single && !empty) fm &= ~bs;
       }
-      if (overflow || over_budget) {
-        o.verdict = LC_UNKNOWN;
-        o.reason = overflow ? LC_REASON_FRONTIER_LDS : LC_REASON_CONFIG_BUDGET;
-        return;
+      if (!single) {
+        const int r = general_return(st, sl, occ, s, rF, rR, rW, nF, p, o, lane);
+        if (r < 0) {
+          o.verdict = LC_UNKNOWN;
+          o.reason = r == -1 ? LC_REASON_FRONTIER_LDS : LC_REASON_CONFIG_BUDGET;
+          return;
+        }
+        const int t = rF;
+        rF = rR;
+        rR = t;
+        nF = r;
+        if (nF > o.max_frontier) o.max_frontier = nF;
+        empty = nF == 0;
+        if (nF == 1) {  // back to the register-resident frontier
+          const Cfg c = st.get(rF, 0);
+          fm = rfl64(c.mask);
+          fsv = rfl64(c.sv);
+          single = true;
+        }
       }
-      const int t = rF;
-      rF = rR;
-      rR = t;
-      nF = nR;
       occ &= ~bs;
-      if (nF > o.max_frontier) o.max_frontier = nF;
-      if (nF == 0) {
+      if (lane == s) sl.ret = kNever;
+      if (empty) {
         o.verdict = LC_INVALID;
         o.reason = LC_REASON_NONLINEARIZABLE;
         o.fail_op = x_idx;
-        o.fail_end = nret;
+        o.fail_end = base_idx + (int64_t)nret;
         return;
       }
     } else {
@@ -355,8 +459,8 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
       const int f = rl32(cur.f, li), val = rl32(cur.val, li);
       const int ex = rl32(cur.exp, li), ver = rl32(cur.ver, li);
       const int bad = rl32(cur.bad, li);
-      const int64_t ret = rl64(cur.ret, li);
-      if (bad || ncall <= prev_call) {
+      const uint32_t ret = (uint32_t)rl32((int)cur.ret, li);
+      if (bad || (i > 0 && ncall <= prev_call)) {
         o.verdict = LC_UNKNOWN;
         o.reason = LC_REASON_MALFORMED;
         return;
@@ -370,7 +474,7 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
       // A read that never returned, or read [nil nil], is legal in every
       // state and changes nothing: it never constrains the search.
       const bool trivial =
-          (f == LC_F_READ) && (ret == kInf || (ver == -1 && val == -1));
+          (f == LC_F_READ) && (ret == kNever || (ver == -1 && val == -1));
       if (!trivial) {
         if (occ == ~0ull) {
           o.verdict = LC_UNKNOWN;
@@ -379,21 +483,25 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
         }
         const int s = __builtin_ctzll(~occ);
         if (lane == s) {
-          s_f = f;
-          s_val = val;
-          s_exp = ex;
-          s_ver = ver;
-          s_ret = ret;
-          s_idx = (int)i;
+          sl.f = f;
+          sl.val = val;
+          sl.exp = ex;
+          sl.ver = ver;
+          sl.ret = ret;
+          sl.idx = (int)i;
         }
         occ |= 1ull << s;
         if (f == LC_F_READ) {  // eager read closure at the call
-          for (int j0 = 0; j0 < nF; j0 += kWave) {
-            const int j = j0 + lane;
-            if (j < nF) {
-              const Cfg c = st.get(rF, j);
-              if (legal(LC_F_READ, ver, val, ex, sv_ver(c.sv), sv_val(c.sv)))
-                st.set_mask_lane(rF, j, c.mask | (1ull << s));
+          if (single) {
+            if (legal(LC_F_READ, ver, val, ex, sv_ver(fsv), sv_val(fsv))) fm |= 1ull << s;
+          } else {
+            for (int j0 = 0; j0 < nF; j0 += kWave) {
+              const int j = j0 + lane;
+              if (j < nF) {
+                const Cfg c = st.get(rF, j);
+                if (legal(LC_F_READ, ver, val, ex, sv_ver(c.sv), sv_val(c.sv)))
+                  st.set_mask_lane(rF, j, c.mask | (1ull << s));
+              }
             }
           }
         }
@@ -402,7 +510,7 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
       if (i - base == kWave) {
         base += kWave;
         cur = nxt;
-        nxt = load_rec(kops, base + kWave + lane, n);
+        nxt = load_rec(kops, base + kWave + lane, n, base_idx);
       }
     }
   }

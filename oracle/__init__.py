@@ -15,6 +15,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liboracle.so")
 
 JIT, WGL = 0, 1
+# OR into JIT: eager read closure (exact reduction; checked against plain JIT)
+READ_CLOSURE = 0x100
+JITC = JIT | READ_CLOSURE
 
 RESULT_DTYPE = np.dtype([
     ("verdict", "<i4"), ("reason", "<i4"), ("fail_op", "<i8"),

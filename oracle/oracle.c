@@ -226,8 +226,35 @@ static event *build_events(const lc_op *o, int64_t n, int64_t *ne) {
  * the history prefix up to that return has no linearization: x is the
  * canonical counterexample.  Slots index the open calls; crashed ops keep
  * their slot forever. */
+/* closure != 0 enables the eager read closure (ORACLE_FLAG_READ_CLOSURE):
+ * a pending read legal in a configuration is linearized at once, and reads
+ * that can never constrain (crashed, or [nil nil]) get no slot.  This is an
+ * exact reduction (the linearized read dominates the pending one because a
+ * read never changes the state, register.clj:84-96); the faithful mode
+ * (closure == 0) is what tests/ check it against. */
+static int is_trivial_read(const lc_op *op) {
+  return op->f == LC_F_READ &&
+         (op->ret == LC_INF || (op->version == LC_NIL && op->value == LC_NIL));
+}
+
+static void close_reads(const lc_op *o, const int32_t *slot_op, const uint64_t *occ,
+                        int bw, uint64_t *cfg) {
+  for (int w = 0; w < bw; w++) {
+    uint64_t pend = occ[w] & ~cfg[w];
+    while (pend) {
+      const int b = __builtin_ctzll(pend);
+      pend &= pend - 1;
+      const lc_op *op = &o[slot_op[w * 64 + b]];
+      int64_t nv, nval;
+      if (op->f == LC_F_READ &&
+          oracle_step((int64_t)cfg[bw], (int64_t)cfg[bw + 1], op, &nv, &nval) == 1)
+        cfg[w] |= 1ULL << b;
+    }
+  }
+}
+
 static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
-                          int64_t budget, lc_key_result *res) {
+                          int64_t budget, int closure, lc_key_result *res) {
   result_init(res);
   if (n == 0) return;
   int64_t ne = 0;
@@ -270,13 +297,30 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
   for (int64_t e = 0; e < ne; e++) {
     const int32_t x = ev[e].op;
     if (!ev[e].is_ret) {
+      if (closure && is_trivial_read(&o[x])) {
+        slot_of[x] = -1;
+        continue;
+      }
       int s = 0;
       while (occ[s >> 6] >> (s & 63) & 1) s++;
       occ[s >> 6] |= 1ULL << (s & 63);
       slot_of[x] = s;
       slot_op[s] = x;
+      if (closure && o[x].f == LC_F_READ) {
+        /* linearize the new read in every configuration where it is legal;
+         * configurations stay distinct (equal states decide alike) */
+        for (size_t i = 0; i < F.n; i++) {
+          uint64_t *c = F.arena + i * (size_t)nw;
+          int64_t nv, nval;
+          if (oracle_step((int64_t)c[bw], (int64_t)c[bw + 1], &o[x], &nv, &nval) == 1)
+            c[s >> 6] |= 1ULL << (s & 63);
+        }
+        /* masks changed in place: rebuild F's hash index */
+        cset_rehash(&F, F.tcap);
+      }
       continue;
     }
+    if (slot_of[x] < 0) continue; /* trivial read: nothing to do */
     const int sx = slot_of[x];
     const int wx = sx >> 6;
     const uint64_t bx = 1ULL << (sx & 63);
@@ -313,9 +357,17 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
           tmp[w] |= 1ULL << b;
           tmp[bw] = (uint64_t)nv;
           tmp[bw + 1] = (uint64_t)nval;
+          if (closure) {
+            if (o[slot_op[t]].f == LC_F_READ) continue; /* closed already */
+            close_reads(o, slot_op, occ, bw, tmp);
+          }
           explored++;
           int r;
           if (t == sx) {
+            tmp[wx] &= ~bx;
+            r = cset_add(&R, tmp);
+          } else if (closure && (tmp[wx] & bx)) {
+            /* x (a read) was linearized by the closure */
             tmp[wx] &= ~bx;
             r = cset_add(&R, tmp);
           } else {
@@ -512,6 +564,7 @@ typedef struct {
   const lc_opts *opts;
   lc_key_result *out;
   int algo;
+  int closure;
   int64_t budget;
   _Atomic int64_t next;
   _Atomic int malformed;
@@ -543,7 +596,7 @@ static void *worker(void *arg) {
     if (j->algo == ORACLE_WGL)
       check_key_wgl(o, n, j->opts, j->budget, r);
     else
-      check_key_jit(o, n, j->opts, j->budget, r);
+      check_key_jit(o, n, j->opts, j->budget, j->closure, r);
   }
   return NULL;
 }
@@ -567,7 +620,8 @@ int oracle_check(const lc_op *ops, const int64_t *key_off, int64_t n_keys,
   j.n_keys = n_keys;
   j.opts = opts;
   j.out = out;
-  j.algo = algo;
+  j.algo = algo & 0xff;
+  j.closure = (algo & ORACLE_FLAG_READ_CLOSURE) != 0;
   j.budget = opts->max_configs_per_key > 0 ? opts->max_configs_per_key
                                            : (int64_t)4000000;
   atomic_init(&j.next, 0);
