@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--ops-per-key", type=int, default=1000)
     ap.add_argument("--concurrency", type=int, default=20)
     ap.add_argument("--p-info", type=float, default=0.0)
-    ap.add_argument("--cpu-sample-keys", type=int, default=2000)
+    ap.add_argument("--cpu-sample-keys", type=int, default=5000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
@@ -95,19 +95,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-
     res = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
-    counts = torch.tensor([n_ops, int((res["verdict"] == 1).sum()),
-                           int((res["verdict"] == 0).sum()),
-                           int((res["verdict"] == -1).sum())],
-                          dtype=torch.int64, device=dev)
-    if world > 1:
-        dist.all_reduce(counts)
-    total_ops, n_valid, n_invalid, n_unknown = [int(v) for v in counts.tolist()]
+    elapsed, (total_ops, n_valid, n_invalid, n_unknown) = reduce_run(
+        elapsed, n_ops, res, world, dev)
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = total_ops * args.steps / elapsed
@@ -170,6 +160,23 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def reduce_run(elapsed, n_ops, res, world, dev):
+    """Whole-job numbers: the MAX of the ranks' timed-region wall times and
+    the SUM of their checked ops and verdict counts (weak scaling: every rank
+    checks its own batch)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    counts = torch.tensor([n_ops, int((res["verdict"] == 1).sum()),
+                           int((res["verdict"] == 0).sum()),
+                           int((res["verdict"] == -1).sum())],
+                          dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(counts)
+    return float(t.item()), [int(v) for v in counts.tolist()]
 
 
 def cpu_baseline(args, ops, key_off, gpu_res):

@@ -1,0 +1,109 @@
+"""Checker mirror of the reference's plugin boundary for the register workload.
+
+The reference builds, at /root/reference/src/jepsen/etcd/register.clj:108-112,
+
+    (independent/checker
+      (checker/compose {:linear   (checker/linearizable {:model (->VersionedRegister 0 nil)})
+                        :timeline (timeline/html)}))
+
+and jepsen calls it through the jepsen.checker/Checker protocol,
+(check [this test history opts]) -> {:valid? ...}.  `register_checker()` is
+the drop-in for that whole expression: one object whose check() splits the
+history by key, completes and packs it on the host, and decides every key in
+one batched GPU call (include/lincheck.h).  The result has
+jepsen.independent/checker's shape:
+
+    {"valid?": merged, "results": {k: {...}}, "failures": [k ...]}
+
+with merged = false > "unknown" > true, and "failures" the keys whose
+:valid? is false (jepsen.independent keeps :unknown keys out of :failures,
+since :unknown is truthy in Clojure).  The timeline renderer is out of scope.
+Errors: a malformed history raises LcError (-EINVAL); jepsen's check-safe
+would turn an exception into {:valid? :unknown :error ...}, which
+`check_safe` reproduces.
+"""
+from . import abi, history as H
+
+UNKNOWN = "unknown"
+
+
+class VersionedRegister:
+    """The model of register.clj:55-96 as data: its initial state.  The step
+    function itself runs on the GPU (check_kernel.hip, `legal`)."""
+
+    def __init__(self, version=0, value=None):
+        self.version = version
+        self.value = value
+
+    def __repr__(self):  # register.clj:57
+        return "v%s: %s" % (self.version, self.value)
+
+
+def _merge_valid(vs):
+    vs = list(vs)
+    if any(v is False for v in vs):
+        return False
+    if any(v == UNKNOWN for v in vs):
+        return UNKNOWN
+    return True
+
+
+class RegisterChecker:
+    """Drop-in for independent/checker + checker/linearizable(VersionedRegister)."""
+
+    def __init__(self, model=None, device_mask=0, max_configs_per_key=0):
+        self.model = model or VersionedRegister(0, None)
+        self.device_mask = device_mask
+        self.max_configs_per_key = max_configs_per_key
+        self._ctx = None
+
+    def _context(self):
+        if self._ctx is None:
+            self._ctx = abi.Context(self.device_mask)
+        return self._ctx
+
+    def check(self, test, history, opts=None):
+        keys, ops, key_off, done = H.pack(history)
+        if not keys:
+            return {"valid?": True, "results": {}, "failures": []}
+        interned_init = H.LC_NIL
+        if self.model.value is not None:
+            # the initial value must share the per-key id space; only nil
+            # (the reference's model, register.clj:111) is supported here.
+            raise ValueError("only (->VersionedRegister v nil) initial states are supported")
+        o = abi.default_opts(self.max_configs_per_key, self.model.version, interned_init)
+        _, res = self._context().check(ops, key_off, o)
+        results = {}
+        for i, k in enumerate(keys):
+            r = res[i]
+            v = {1: True, 0: False}.get(int(r["verdict"]), UNKNOWN)
+            out = {"valid?": v, "analyzer": "mi355x",
+                   "configs-explored": int(r["configs_explored"]),
+                   "max-frontier": int(r["max_frontier"])}
+            if v is False:
+                d = done[i][int(r["fail_op"])]
+                out["op"] = d["completion"] or d["invoke"]
+                out["fail-prefix-end"] = int(r["fail_prefix_end"])
+            elif v == UNKNOWN:
+                out["cause"] = abi.REASONS.get(int(r["reason"]), "?")
+            results[k] = out
+        return {"valid?": _merge_valid(r["valid?"] for r in results.values()),
+                "results": results,
+                "failures": [k for k, r in results.items() if r["valid?"] is False]}
+
+    def close(self):
+        if self._ctx is not None:
+            self._ctx.close()
+            self._ctx = None
+
+
+def register_checker(**kw):
+    return RegisterChecker(**kw)
+
+
+def check_safe(checker, test, history, opts=None):
+    """jepsen.checker/check-safe: exceptions become {:valid? :unknown :error}."""
+    try:
+        return checker.check(test, history, opts)
+    except Exception as e:  # noqa: BLE001 — mirrors check-safe's catch-all
+        return {"valid?": UNKNOWN, "error": repr(e)}

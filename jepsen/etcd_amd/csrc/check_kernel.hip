@@ -82,6 +82,21 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return umin(umin(r0, r1), umin(r2, r3));
 }
 
+// Bitwise AND of a 64-bit value over the 64 lanes (wave-uniform result).
+__device__ __forceinline__ uint32_t wave_and_u32(uint32_t v) {
+  v &= (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false);
+  v &= (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false);
+  v &= (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false);
+  v &= (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) &
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 16) &
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) &
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+__device__ __forceinline__ uint64_t wave_and_u64(uint64_t v) {
+  return ((uint64_t)wave_and_u32((uint32_t)(v >> 32)) << 32) | wave_and_u32((uint32_t)v);
+}
+
 // VersionedRegister.step legality (register.clj:60-96); NIL = -1.
 //   write :64-68  version' = version+1 must equal op-version unless nil
 //   cas   :70-82  same, and the current value must equal the expected value
@@ -264,8 +279,15 @@ struct HbmStore {
 // ------------------------------------------------------------ the search
 
 // Per-lane record of the window slot this lane holds.
+//   pred   for a crashed write/CAS: the slot of the previously called crashed
+//          op of the same class (f, value, expected), or -1.  Such ops are
+//          interchangeable (their version is nil: the completion never came),
+//          so only the earliest-called unlinearized member of a class is a
+//          candidate: an exact symmetry reduction (checked against the oracle's
+//          faithful search in tests/).
+//   latest this slot is the most recently called crashed op of its class.
 struct Slot {
-  int f, val, exp, ver, idx;
+  int f, val, exp, ver, idx, pred, latest;
   uint32_t ret;  // kNever: free or crashed (never returns)
 };
 
@@ -275,7 +297,9 @@ __device__ __forceinline__ uint64_t mutation_candidates(const Slot &sl, uint64_t
                                                         uint64_t cm, int ver, int val,
                                                         int lane) {
   const bool pend = ((occ & ~cm) >> lane) & 1;
-  return __ballot(pend && sl.f != LC_F_READ && legal(sl.f, sl.ver, sl.val, sl.exp, ver, val));
+  const bool turn = sl.pred < 0 || ((cm >> sl.pred) & 1);
+  return __ballot(pend && turn && sl.f != LC_F_READ &&
+                  legal(sl.f, sl.ver, sl.val, sl.exp, ver, val));
 }
 __device__ __forceinline__ uint64_t read_closure(const Slot &sl, uint64_t occ,
                                                  uint64_t nm, int ver, int val,
@@ -351,8 +375,9 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
   uint64_t fm = 0, fsv = pack_sv(p.init_ver, p.init_val);
   int rF = 0, rR = 1, rW = 2, nF = 1;
 
-  Slot sl{0, -1, -1, -1, -1, kNever};
-  uint64_t occ = 0;  // occupied window slots (uniform)
+  Slot sl{0, -1, -1, -1, -1, -1, 0, kNever};
+  uint64_t occ = 0;      // occupied window slots (uniform)
+  uint64_t crashed = 0;  // slots holding crashed writes/CAS (uniform)
 
   const int64_t base_idx = kops[0].call;
   Rec cur = load_rec(kops, lane, n, base_idx);
@@ -453,6 +478,28 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
         o.fail_end = base_idx + (int64_t)nret;
         return;
       }
+      // Retirement: a crashed op linearized in EVERY configuration is done for
+      // good (no return to wait for); free its slot everywhere.
+      uint64_t rb = crashed;
+      if (single) {
+        rb &= fm;
+      } else {
+        uint64_t acc = ~0ull;
+        for (int j = lane; j < nF; j += kWave) acc &= st.get(rF, j).mask;
+        rb &= wave_and_u64(acc);
+      }
+      if (rb) {
+        occ &= ~rb;
+        crashed &= ~rb;
+        if (single) {
+          fm &= ~rb;
+        } else {
+          for (int j = lane; j < nF; j += kWave)
+            st.set_mask_lane(rF, j, st.get(rF, j).mask & ~rb);
+        }
+        if ((rb >> lane) & 1) sl.latest = 0;
+        if (sl.pred >= 0 && ((rb >> sl.pred) & 1)) sl.pred = -1;
+      }
     } else {
       // ------------------------------------------------------- call of op i
       const int li = (int)(i - base);
@@ -482,6 +529,18 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
           return;
         }
         const int s = __builtin_ctzll(~occ);
+        int pred = -1;
+        const bool crash = ret == kNever;  // (crashed reads are trivial)
+        if (crash) {
+          const uint64_t m = __ballot(((crashed >> lane) & 1) && sl.latest &&
+                                      sl.f == f && sl.val == val && sl.exp == ex &&
+                                      sl.ver == ver);
+          if (m) {
+            pred = __builtin_ctzll(m);
+            if (lane == pred) sl.latest = 0;
+          }
+          crashed |= 1ull << s;
+        }
         if (lane == s) {
           sl.f = f;
           sl.val = val;
@@ -489,6 +548,8 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
           sl.ver = ver;
           sl.ret = ret;
           sl.idx = (int)i;
+          sl.pred = pred;
+          sl.latest = crash ? 1 : 0;
         }
         occ |= 1ull << s;
         if (f == LC_F_READ) {  // eager read closure at the call
@@ -563,7 +624,8 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
     const int64_t key_base, const int32_t *__restrict__ keys, const int32_t n_list,
     const KParams p, lc_key_result *__restrict__ out, char *__restrict__ ws,
-    const int64_t cap, KStatus *__restrict__ status) {
+    const int64_t cap, int32_t *__restrict__ ovf_out, int32_t *__restrict__ n_ovf_out,
+    const int last_tier) {
   const int lane = threadIdx.x;
   char *w = ws + (size_t)blockIdx.x * hbm_wave_bytes(cap);
   HbmStore st;
@@ -580,11 +642,14 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
     KeyOut o;
     check_key(ops + (beg - key_base), end - beg, p, st, o, lane);
     if (o.reason == LC_REASON_FRONTIER_LDS) {
-      o.reason = LC_REASON_CONFIG_BUDGET;  // HBM sets full: budget exhausted
+      if (last_tier) {
+        o.reason = LC_REASON_CONFIG_BUDGET;  // largest sets full: give up
+      } else if (lane == 0) {
+        ovf_out[atomicAdd(n_ovf_out, 1)] = (int32_t)key;  // next, larger tier
+      }
     }
     if (lane == 0) write_result(&out[key], o);
   }
-  (void)status;
 }
 
 }  // namespace
@@ -609,11 +674,13 @@ hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
                            int64_t key_base, const int32_t *d_keys,
                            int32_t n_list, const KParams &p, lc_key_result *d_out,
                            void *d_ws, int n_waves, int64_t cap,
-                           KStatus *d_status, hipStream_t stream) {
+                           int32_t *d_ovf_out, int32_t *d_n_ovf_out, int last_tier,
+                           hipStream_t stream) {
   if (n_list <= 0) return hipSuccess;
   hipLaunchKernelGGL(hbm_tier_kernel, dim3((unsigned)n_waves), dim3(kWave), 0,
                      stream, d_ops, d_key_off, key_base, d_keys, n_list, p,
-                     d_out, static_cast<char *>(d_ws), cap, d_status);
+                     d_out, static_cast<char *>(d_ws), cap, d_ovf_out, d_n_ovf_out,
+                     last_tier);
   return hipGetLastError();
 }
 

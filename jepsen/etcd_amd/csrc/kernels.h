@@ -18,9 +18,10 @@ struct KParams {
 
 // Device-side status words, zeroed before every call.
 struct KStatus {
-  int32_t malformed;  // keys with LC_REASON_MALFORMED
-  int32_t n_overflow; // keys appended to the overflow list (LDS tier full)
-  int32_t pad[2];
+  int32_t malformed;    // keys with LC_REASON_MALFORMED
+  int32_t n_overflow;   // keys appended to the overflow list (LDS tier full)
+  int32_t n_overflow2;  // keys that also overflowed the first HBM tier
+  int32_t pad;
 };
 
 constexpr int kWave = 64;
@@ -38,12 +39,16 @@ hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
 
 // HBM tier: re-runs the listed keys with configuration sets in global memory
 // (open-addressed hash tables, 128-byte buckets).  ws is a workspace of
-// hbm_tier_ws_bytes(n_waves, cap) bytes; cap = configurations per set.
+// hbm_tier_ws_bytes(n_waves, cap) bytes (zeroed by the caller); cap =
+// configurations per set.  Keys that overflow again are appended to
+// d_ovf_out (count *d_n_ovf_out) unless last_tier, where they become
+// LC_REASON_CONFIG_BUDGET (:unknown).
 size_t hbm_tier_ws_bytes(int n_waves, int64_t cap);
 hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
                            int64_t key_base, const int32_t *d_keys,
                            int32_t n_list, const KParams &p, lc_key_result *d_out,
                            void *d_ws, int n_waves, int64_t cap,
-                           KStatus *d_status, hipStream_t stream);
+                           int32_t *d_ovf_out, int32_t *d_n_ovf_out, int last_tier,
+                           hipStream_t stream);
 
 }  // namespace lcdev

@@ -27,9 +27,11 @@
 
 namespace {
 
-constexpr int64_t kDefaultBudget = 1 << 22;   // configurations per key
-constexpr int64_t kHbmCap = 1 << 16;          // configurations per HBM set
-constexpr int kHbmWaves = 512;                // concurrent HBM-tier keys
+constexpr int64_t kDefaultBudget = 1 << 24;   // configurations per key
+// HBM tiers: (configurations per set, concurrent keys).  Workspace per key
+// is ~128 B per configuration of capacity (3 regions + 2 hash tables).
+constexpr int64_t kHbmCap[2] = {1 << 16, 1 << 21};
+constexpr int kHbmWaves[2] = {512, 16};
 
 struct Dev {
   int id = -1;
@@ -43,6 +45,8 @@ struct Dev {
   size_t out_cap = 0;
   int32_t *d_ovf = nullptr;
   size_t ovf_cap = 0;
+  int32_t *d_ovf2 = nullptr;
+  size_t ovf2_cap = 0;
   lcdev::KStatus *d_status = nullptr;
   lcdev::KStatus *h_status = nullptr;  // pinned
   void *d_ws = nullptr;
@@ -121,6 +125,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     return -EINVAL;
   }
   int rc = ensure(c, &d.d_ovf, &d.ovf_cap, sizeof(int32_t) * (size_t)n_keys);
+  if (!rc) rc = ensure(c, &d.d_ovf2, &d.ovf2_cap, sizeof(int32_t) * (size_t)n_keys);
   if (rc) return rc;
   HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
   HIP_TRY(c, hipEventRecord(d.e0, st));
@@ -137,15 +142,25 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   const int32_t n_ovf = d.h_status->n_overflow;
   d.n_hbm = n_ovf;
   if (n_ovf > 0 && !(flags & LC_FLAG_NO_HBM_RETRY)) {
-    const int waves = std::min<int>(kHbmWaves, n_ovf);
-    const size_t ws = lcdev::hbm_tier_ws_bytes(waves, kHbmCap);
-    rc = ensure(c, reinterpret_cast<char **>(&d.d_ws), &d.ws_cap, ws);
-    if (rc) return rc;
-    HIP_TRY(c, hipMemsetAsync(d.d_ws, 0, ws, st));
+    int32_t n_list = n_ovf;
+    int32_t *list = d.d_ovf, *next = d.d_ovf2;
     HIP_TRY(c, hipEventRecord(d.e1, st));
-    HIP_TRY(c, lcdev::launch_hbm_tier(d_ops, d_off, key_base, d.d_ovf, n_ovf, p,
-                                      d_out, d.d_ws, waves, kHbmCap,
-                                      d.d_status, st));
+    for (int tier = 0; tier < 2 && n_list > 0; tier++) {
+      const int waves = std::min<int>(kHbmWaves[tier], n_list);
+      const size_t ws = lcdev::hbm_tier_ws_bytes(waves, kHbmCap[tier]);
+      rc = ensure(c, reinterpret_cast<char **>(&d.d_ws), &d.ws_cap, ws);
+      if (rc) return rc;
+      HIP_TRY(c, hipMemsetAsync(d.d_ws, 0, ws, st));
+      HIP_TRY(c, hipMemsetAsync(&d.d_status->n_overflow2, 0, sizeof(int32_t), st));
+      HIP_TRY(c, lcdev::launch_hbm_tier(d_ops, d_off, key_base, list, n_list, p,
+                                        d_out, d.d_ws, waves, kHbmCap[tier], next,
+                                        &d.d_status->n_overflow2, tier == 1, st));
+      HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
+                                hipMemcpyDeviceToHost, st));
+      HIP_TRY(c, hipStreamSynchronize(st));
+      n_list = tier == 0 ? d.h_status->n_overflow2 : 0;
+      std::swap(list, next);
+    }
     HIP_TRY(c, hipEventRecord(d.e2, st));
     HIP_TRY(c, hipStreamSynchronize(st));
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e1, d.e2));
@@ -207,6 +222,7 @@ void lc_close(lc_ctx *c) {
     if (d.d_off) (void)hipFree(d.d_off);
     if (d.d_out) (void)hipFree(d.d_out);
     if (d.d_ovf) (void)hipFree(d.d_ovf);
+    if (d.d_ovf2) (void)hipFree(d.d_ovf2);
     if (d.d_ws) (void)hipFree(d.d_ws);
     if (d.d_status) (void)hipFree(d.d_status);
     if (d.h_status) (void)hipHostFree(d.h_status);

@@ -15,9 +15,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liboracle.so")
 
 JIT, WGL = 0, 1
-# OR into JIT: eager read closure (exact reduction; checked against plain JIT)
+# OR into JIT: exact reductions, each checked against plain JIT in tests/
 READ_CLOSURE = 0x100
-JITC = JIT | READ_CLOSURE
+CRASH_SYMMETRY = 0x200
+RETIRE = 0x400
+JITC = JIT | READ_CLOSURE | CRASH_SYMMETRY | RETIRE
 
 RESULT_DTYPE = np.dtype([
     ("verdict", "<i4"), ("reason", "<i4"), ("fail_op", "<i8"),

@@ -225,16 +225,32 @@ static event *build_events(const lc_op *o, int64_t n, int64_t *ne) {
  * is linearized; expansion stops at x.  An empty frontier at x's return means
  * the history prefix up to that return has no linearization: x is the
  * canonical counterexample.  Slots index the open calls; crashed ops keep
- * their slot forever. */
-/* closure != 0 enables the eager read closure (ORACLE_FLAG_READ_CLOSURE):
- * a pending read legal in a configuration is linearized at once, and reads
- * that can never constrain (crashed, or [nil nil]) get no slot.  This is an
- * exact reduction (the linearized read dominates the pending one because a
- * read never changes the state, register.clj:84-96); the faithful mode
- * (closure == 0) is what tests/ check it against. */
+ * their slot (until retired, below).
+ *
+ * `reduce` (ORACLE_FLAG_*) enables exact reductions, each checked by tests/
+ * against the faithful mode (reduce == 0), which is knossos.linear's search:
+ *  READ_CLOSURE   a pending read legal in a configuration is linearized at
+ *                 once, and reads that can never constrain (crashed, or
+ *                 [nil nil]) get no slot.  A read never changes the state
+ *                 (register.clj:84-96), so (s, L+{r}) dominates (s, L).
+ *  CRASH_SYMMETRY crashed writes/CAS with equal (f, value, expected) are
+ *                 interchangeable once called (their version is always nil:
+ *                 the completion never arrived), so only the earliest-called
+ *                 unlinearized member of such a class may be linearized next.
+ *  RETIRE         a crashed op linearized in every configuration is done for
+ *                 good (it has no return to wait for): its slot is freed. */
 static int is_trivial_read(const lc_op *op) {
   return op->f == LC_F_READ &&
          (op->ret == LC_INF || (op->version == LC_NIL && op->value == LC_NIL));
+}
+
+static int is_crashed_mutation(const lc_op *op) {
+  return op->ret == LC_INF && op->f != LC_F_READ;
+}
+
+static int same_class(const lc_op *a, const lc_op *b) {
+  return a->f == b->f && a->value == b->value && a->expected == b->expected &&
+         a->version == b->version;
 }
 
 static void close_reads(const lc_op *o, const int32_t *slot_op, const uint64_t *occ,
@@ -253,8 +269,13 @@ static void close_reads(const lc_op *o, const int32_t *slot_op, const uint64_t *
   }
 }
 
+#define BIT(a, s) (((a)[(s) >> 6] >> ((s) & 63)) & 1)
+
 static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
-                          int64_t budget, int closure, lc_key_result *res) {
+                          int64_t budget, int reduce, lc_key_result *res) {
+  const int closure = (reduce & ORACLE_FLAG_READ_CLOSURE) != 0;
+  const int symmetry = (reduce & ORACLE_FLAG_CRASH_SYMMETRY) != 0;
+  const int retire = (reduce & ORACLE_FLAG_RETIRE) != 0;
   result_init(res);
   if (n == 0) return;
   int64_t ne = 0;
@@ -263,7 +284,7 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
     result_unknown(res, LC_REASON_CONFIG_BUDGET);
     return;
   }
-  /* Window size bound: simulate open-slot count. */
+  /* Window size bound: simulate open-slot count (retirement only lowers it). */
   int64_t open = 0, maxopen = 0;
   for (int64_t e = 0; e < ne; e++) {
     if (!ev[e].is_ret) {
@@ -277,16 +298,21 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
   const int nw = bw + 2;
   int32_t *slot_of = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
   int32_t *slot_op = (int32_t *)malloc(sizeof(int32_t) * (size_t)(bw * 64));
+  int32_t *pred = (int32_t *)malloc(sizeof(int32_t) * (size_t)(bw * 64));
+  uint8_t *latest = (uint8_t *)calloc((size_t)(bw * 64), 1);
   uint64_t *occ = (uint64_t *)calloc((size_t)bw, sizeof(uint64_t));
+  uint64_t *crashed = (uint64_t *)calloc((size_t)bw, sizeof(uint64_t));
+  uint64_t *all = (uint64_t *)calloc((size_t)bw, sizeof(uint64_t));
   uint64_t *tmp = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)nw);
   cset F, R, V;
-  int ok = slot_of && slot_op && occ && tmp;
+  int ok = slot_of && slot_op && pred && latest && occ && crashed && all && tmp;
   ok = ok && cset_init(&F, nw) == 0 && cset_init(&R, nw) == 0 &&
        cset_init(&V, nw) == 0;
   if (!ok) {
     result_unknown(res, LC_REASON_CONFIG_BUDGET);
     goto done;
   }
+  for (int u = 0; u < bw * 64; u++) pred[u] = -1;
   memset(tmp, 0, sizeof(uint64_t) * (size_t)nw);
   tmp[bw] = (uint64_t)opts->init_version;
   tmp[bw + 1] = (uint64_t)opts->init_value;
@@ -302,10 +328,25 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
         continue;
       }
       int s = 0;
-      while (occ[s >> 6] >> (s & 63) & 1) s++;
+      while (BIT(occ, s)) s++;
       occ[s >> 6] |= 1ULL << (s & 63);
       slot_of[x] = s;
       slot_op[s] = x;
+      pred[s] = -1;
+      latest[s] = 0;
+      if (is_crashed_mutation(&o[x])) {
+        crashed[s >> 6] |= 1ULL << (s & 63);
+        if (symmetry) {
+          for (int u = 0; u < bw * 64; u++)
+            if (u != s && BIT(crashed, u) && latest[u] &&
+                same_class(&o[slot_op[u]], &o[x])) {
+              pred[s] = u;
+              latest[u] = 0;
+              break;
+            }
+          latest[s] = 1;
+        }
+      }
       if (closure && o[x].f == LC_F_READ) {
         /* linearize the new read in every configuration where it is legal;
          * configurations stay distinct (equal states decide alike) */
@@ -345,6 +386,7 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
           pend &= pend - 1;
           const int t = w * 64 + b;
           c = cset_get(&V, h);
+          if (symmetry && pred[t] >= 0 && !BIT(c, pred[t])) continue;
           int64_t nv, nval;
           const int st = oracle_step((int64_t)c[bw], (int64_t)c[bw + 1],
                                      &o[slot_op[t]], &nv, &nval);
@@ -363,11 +405,7 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
           }
           explored++;
           int r;
-          if (t == sx) {
-            tmp[wx] &= ~bx;
-            r = cset_add(&R, tmp);
-          } else if (closure && (tmp[wx] & bx)) {
-            /* x (a read) was linearized by the closure */
+          if (tmp[wx] & bx) { /* x linearized (directly, or by the closure) */
             tmp[wx] &= ~bx;
             r = cset_add(&R, tmp);
           } else {
@@ -394,6 +432,32 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
       res->fail_prefix_end = o[x].ret;
       break;
     }
+    if (retire) {
+      int any = 0;
+      for (int w = 0; w < bw; w++) {
+        all[w] = crashed[w];
+        for (size_t i = 0; i < F.n; i++) all[w] &= cset_get(&F, i)[w];
+        any |= all[w] != 0;
+      }
+      if (any) {
+        for (size_t i = 0; i < F.n; i++) {
+          uint64_t *c = F.arena + i * (size_t)nw;
+          for (int w = 0; w < bw; w++) c[w] &= ~all[w];
+        }
+        cset_rehash(&F, F.tcap);
+        for (int w = 0; w < bw; w++) {
+          occ[w] &= ~all[w];
+          crashed[w] &= ~all[w];
+        }
+        for (int u = 0; u < bw * 64; u++) {
+          if (BIT(all, u)) {
+            latest[u] = 0;
+            pred[u] = -1;
+          }
+          if (BIT(occ, u) && pred[u] >= 0 && BIT(all, pred[u])) pred[u] = -1;
+        }
+      }
+    }
   }
   res->configs_explored = explored;
 done:
@@ -402,7 +466,11 @@ done:
   cset_free(&V);
   free(slot_of);
   free(slot_op);
+  free(pred);
+  free(latest);
   free(occ);
+  free(crashed);
+  free(all);
   free(tmp);
   free(ev);
 }
@@ -564,7 +632,7 @@ typedef struct {
   const lc_opts *opts;
   lc_key_result *out;
   int algo;
-  int closure;
+  int reduce;
   int64_t budget;
   _Atomic int64_t next;
   _Atomic int malformed;
@@ -596,7 +664,7 @@ static void *worker(void *arg) {
     if (j->algo == ORACLE_WGL)
       check_key_wgl(o, n, j->opts, j->budget, r);
     else
-      check_key_jit(o, n, j->opts, j->budget, j->closure, r);
+      check_key_jit(o, n, j->opts, j->budget, j->reduce, r);
   }
   return NULL;
 }
@@ -621,7 +689,7 @@ int oracle_check(const lc_op *ops, const int64_t *key_off, int64_t n_keys,
   j.opts = opts;
   j.out = out;
   j.algo = algo & 0xff;
-  j.closure = (algo & ORACLE_FLAG_READ_CLOSURE) != 0;
+  j.reduce = algo & ~0xff;
   j.budget = opts->max_configs_per_key > 0 ? opts->max_configs_per_key
                                            : (int64_t)4000000;
   atomic_init(&j.next, 0);

@@ -25,9 +25,11 @@ extern "C" {
 
 #define ORACLE_JIT 0  /* knossos.linear (Lowe's just-in-time linearization) */
 #define ORACLE_WGL 1  /* knossos.wgl (Wing-Gong with Lowe's cache)          */
-/* OR into algo with ORACLE_JIT: eager read closure (exact reduction, see
- * oracle.c); tests check it against the faithful mode. */
-#define ORACLE_FLAG_READ_CLOSURE 0x100
+/* OR into algo with ORACLE_JIT: exact reductions (see oracle.c); tests/
+ * check each against the faithful mode. */
+#define ORACLE_FLAG_READ_CLOSURE   0x100
+#define ORACLE_FLAG_CRASH_SYMMETRY 0x200
+#define ORACLE_FLAG_RETIRE         0x400
 
 /* Check every key with the chosen algorithm on n_threads host threads.
  * Same record format, options and result struct as lc_check().

@@ -1,0 +1,107 @@
+"""Shared test helpers: tiny random register histories, fixture loading."""
+import json
+import os
+import random
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+INF = (1 << 63) - 1
+R, W, C, N = 0, 1, 2, -1
+
+
+def load_kats():
+    with open(os.path.join(GOLDEN, "kat.json")) as fh:
+        return json.load(fh)
+
+
+def pack_keys(list_of_ops):
+    """[[record...] per key] -> (ops (n,6) int64, key_off)."""
+    key_off = np.zeros(len(list_of_ops) + 1, dtype=np.int64)
+    rows = []
+    for i, ops in enumerate(list_of_ops):
+        key_off[i + 1] = key_off[i] + len(ops)
+        rows.extend(ops)
+    ops = np.array(rows, dtype=np.int64).reshape(-1, 6)
+    return ops, key_off
+
+
+def _step(state, f, value, expected, version):
+    ver, val = state
+    if f == W:
+        return (ver + 1, value)
+    if f == C:
+        return (ver + 1, value) if val == expected else None
+    return state
+
+
+def random_tiny(rng, n_ops, p_info=0.2, p_perturb=0.35, n_values=3):
+    """A small history: a random sequential execution whose ops get random
+    overlapping intervals around their linearization points, then (with
+    p_perturb) one field perturbed.  Mix of valid and invalid keys, nil
+    versions/values, crashed ops (some never take effect)."""
+    # linearization order = op order; intervals from random event positions
+    state = (0, N)
+    recs = []
+    for _ in range(n_ops):
+        f = rng.choice([R, R, W, C])
+        info = f != R and rng.random() < p_info
+        if f == R:
+            ver, val = state
+            rec = [R, val if ver > 0 else N, N, ver if ver > 0 else N]
+            if rng.random() < 0.15:
+                rec[1] = N  # version-only read
+        elif f == W:
+            v = rng.randrange(n_values)
+            took = not info or rng.random() < 0.5
+            if took:
+                state = (state[0] + 1, v)
+            rec = [W, v, N, N if info else state[0]]
+        else:
+            old = rng.choice([state[1], rng.randrange(n_values)])
+            new = rng.randrange(n_values)
+            ok = state[1] == old
+            if not ok and not info:
+                continue  # a failed CAS is dropped by history completion
+            took = ok and (not info or rng.random() < 0.5)
+            if took:
+                state = (state[0] + 1, new)
+            rec = [C, new, old, N if info else state[0]]
+        recs.append((rec, info))
+    n = len(recs)
+    # lin point of op i at time 2i+1; call uniformly before, ret after
+    ops = []
+    times = []
+    for i, (rec, info) in enumerate(recs):
+        lin = 10 * i + 5
+        call = lin - rng.randrange(1, 25)
+        ret = INF if info else lin + rng.randrange(1, 25)
+        times.append((call, ret))
+        ops.append(rec)
+    # rank event times into distinct indices (calls before rets at ties)
+    ev = []
+    for i, (c, r) in enumerate(times):
+        ev.append((c, 0, i))
+        if r != INF:
+            ev.append((r, 1, i))
+    ev.sort()
+    cidx, ridx = {}, {}
+    for k, (_, kind, i) in enumerate(ev):
+        (ridx if kind else cidx)[i] = k
+    out = []
+    for i, rec in enumerate(ops):
+        out.append(rec + [cidx[i], ridx.get(i, INF)])
+    out.sort(key=lambda r: r[4])
+    if out and rng.random() < p_perturb:
+        j = rng.randrange(len(out))
+        fld = rng.choice([1, 3])
+        out[j][fld] = rng.choice([N, 0, 1, 2, 3])
+        if out[j][0] != C and fld == 2:
+            out[j][2] = N
+    return out
+
+
+def tiny_batch(seed, n_keys, max_ops=6):
+    rng = random.Random(seed)
+    return [random_tiny(rng, rng.randrange(0, max_ops + 1)) for _ in range(n_keys)]

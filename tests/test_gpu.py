@@ -1,0 +1,218 @@
+"""GPU parity tests: the HIP path through the C ABI against the oracle and the
+hand-derived known answers.  Integer work: bit-exact verdicts and fail ops."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from helpers import GOLDEN, INF, load_kats, pack_keys, tiny_batch
+from jepsen.etcd_amd import abi
+
+pytestmark = pytest.mark.gpu
+
+KATS = load_kats()
+
+
+def test_kats(ctx):
+    ops, off = pack_keys([k["ops"] for k in KATS])
+    rc, r = ctx.check(ops, off)
+    assert rc == 0
+    for i, k in enumerate(KATS):
+        assert r["verdict"][i] == (1 if k["valid"] else 0), k["name"]
+        assert r["fail_op"][i] == k["fail_op"], k["name"]
+        assert r["fail_prefix_end"][i] == k["fail_prefix_end"], k["name"]
+
+
+@pytest.mark.parametrize("name", ["c1", "c5", "info", "tiny"])
+def test_golden_fixtures(ctx, name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    _, r = ctx.check(z["ops"], z["key_off"])
+    assert (r["verdict"] == z["verdict"]).all()
+    assert (r["fail_op"] == z["fail_op"]).all()
+
+
+def test_tiny_random_vs_oracle(ctx):
+    ops, off = pack_keys(tiny_batch(777, 20000, max_ops=8))
+    _, g = ctx.check(ops, off)
+    _, j = oracle.check(ops, off, algo=oracle.JIT, n_threads=8)
+    assert (g["verdict"] == j["verdict"]).all()
+    assert (g["fail_op"] == j["fail_op"]).all()
+    assert (g["fail_prefix_end"] == j["fail_prefix_end"]).all()
+
+
+@pytest.mark.parametrize("conc,p_info,p_anom,seed", [
+    (10, 0.0, 0.1, 0x5EED0005),   # C5-shaped
+    (20, 0.0, 0.2, 11),
+    (30, 0.02, 0.2, 12),
+    (8, 0.1, 0.1, 13),
+])
+def test_synthetic_vs_oracle(ctx, conc, p_info, p_anom, seed):
+    ops, off, lab, _ = abi.synth(400, 200, concurrency=conc, p_info=p_info,
+                                 p_anomaly=p_anom, seed=seed)
+    _, g = ctx.check(ops, off)
+    _, j = oracle.check(ops, off, algo=oracle.JITC, n_threads=8, max_configs=1 << 21)
+    known = j["verdict"] != -1
+    assert known.mean() > 0.95
+    assert (g["verdict"][known] == j["verdict"][known]).all()
+    assert (g["fail_op"][known] == j["fail_op"][known]).all()
+    assert (g["verdict"][lab == 1] == 0).all()   # stale reads are always visible
+
+
+def _prefix(recs, end):
+    """History truncated at index `end`: ops called after it dropped, ops
+    still open at it made pending (completed fields kept)."""
+    out = []
+    for r in recs:
+        if r[4] > end:
+            continue
+        r = list(r)
+        if r[5] > end:
+            r[5] = INF
+        out.append(r)
+    return out
+
+
+def test_counterexamples_are_minimal_nonlinearizable_prefixes(ctx):
+    ops, off, lab, _ = abi.synth(500, 200, concurrency=10, p_anomaly=0.5, seed=21)
+    _, g = ctx.check(ops, off)
+    bad = np.nonzero(g["verdict"] == 0)[0]
+    assert len(bad) > 100
+    pre, prev = [], []
+    for k in bad:
+        recs = ops[off[k]:off[k + 1]].tolist()
+        end = int(g["fail_prefix_end"][k])
+        assert recs[g["fail_op"][k]][5] == end
+        pre.append(_prefix(recs, end))
+        # the prefix ending just before the failing return is linearizable
+        rets = sorted(r[5] for r in recs if r[5] < end)
+        prev.append(_prefix(recs, rets[-1]) if rets else [])
+    p_ops, p_off = pack_keys(pre)
+    _, a = oracle.check(p_ops, p_off, algo=oracle.WGL, n_threads=8)
+    assert (a["verdict"] == 0).all()
+    q_ops, q_off = pack_keys(prev)
+    _, b = oracle.check(q_ops, q_off, algo=oracle.WGL, n_threads=8)
+    assert (b["verdict"] == 1).all()
+
+
+def test_c2_full_size_properties(ctx):
+    """BASELINE configs[1] at full size: 10k keys x 1k ops, concurrency 20.
+    Valid by construction; a 300-key sample matches the oracle."""
+    ops, off, _, _ = abi.synth(10000, 1000, concurrency=20, seed=0x5EED0002)
+    _, g = ctx.check(ops, off)
+    assert (g["verdict"] == 1).all()
+    assert ctx.stats()["n_ops"] == 10_000_000
+    _, j = oracle.check(ops[:off[300]], off[:301], algo=oracle.JITC, n_threads=8)
+    assert (g["verdict"][:300] == j["verdict"]).all()
+
+
+def test_long_key(ctx):
+    ops, off, _, _ = abi.synth(2, 200_000, concurrency=40, p_anomaly=0.0, seed=3)
+    _, g = ctx.check(ops, off)
+    assert (g["verdict"] == 1).all()
+
+
+def test_hbm_tier_resolves_lds_overflow(ctx):
+    z = np.load(os.path.join(GOLDEN, "info.npz"))
+    o = abi.default_opts(flags=abi.LC_FLAG_NO_HBM_RETRY)
+    _, lds_only = ctx.check(z["ops"], z["key_off"], o)
+    spilled = lds_only["reason"] == 6
+    assert spilled.any()
+    _, full = ctx.check(z["ops"], z["key_off"])
+    assert ctx.stats()["n_hbm_keys"] == spilled.sum()
+    assert (full["verdict"] == z["verdict"]).all()
+    assert (full["fail_op"] == z["fail_op"]).all()
+
+
+def test_edge_cases(ctx):
+    W, R_ = 1, 0
+    keys = [
+        [],                                               # empty key
+        [[R_, -1, -1, -1, 0, 1]],                         # lone [nil nil] read
+        [[W, 1, -1, 1, 10, 11]],                          # one write
+        [[R_, -1, -1, -1, i, 100 + i] for i in range(80)],  # 80 open trivial reads
+        [],
+    ]
+    ops, off = pack_keys(keys)
+    rc, r = ctx.check(ops, off)
+    assert rc == 0 and (r["verdict"] == 1).all()
+    rc, r = ctx.check(np.zeros((0, 6), np.int64), np.zeros(1, np.int64))
+    assert rc == 0 and len(r) == 0
+
+
+def test_window_overflow_is_unknown(ctx):
+    recs = [[1, i % 4, -1, -1, i, INF] for i in range(65)]  # 65 crashed writes
+    ops, off = pack_keys([recs, [[1, 1, -1, 1, 0, 1]]])
+    _, r = ctx.check(ops, off)
+    assert r["verdict"][0] == -1 and r["reason"][0] == abi.LC_REASON_WINDOW_OVERFLOW
+    assert r["verdict"][1] == 1
+
+
+def test_budget_is_unknown(ctx):
+    recs = [[1, i % 3, -1, -1, i, INF] for i in range(20)]
+    recs.append([0, 2, -1, 21, 30, 31])
+    ops, off = pack_keys([recs])
+    _, r = ctx.check(ops, off, abi.default_opts(max_configs_per_key=500))
+    assert r["verdict"][0] == -1 and r["reason"][0] == abi.LC_REASON_CONFIG_BUDGET
+
+
+def test_malformed_and_unknown_f(ctx):
+    bad_order = [[1, 1, -1, 1, 5, 6], [1, 2, -1, 2, 3, 4]]
+    bad_ret = [[1, 1, -1, 1, 5, 5]]
+    bad_range = [[1, 1 << 40, -1, 1, 0, 1]]
+    unknown_f = [[7, 1, -1, 1, 0, 1]]
+    good = [[1, 1, -1, 1, 0, 1]]
+    ops, off = pack_keys([bad_order, bad_ret, bad_range, unknown_f, good])
+    rc, r = ctx.check(ops, off, raise_on_error=False)
+    assert rc == -22  # -EINVAL
+    assert list(r["reason"]) == [4, 4, 4, 5, 0]
+    assert list(r["verdict"]) == [-1, -1, -1, -1, 1]
+    bad_off = np.array([0, 2, 1], dtype=np.int64)
+    rc, _ = ctx.check(ops, bad_off, raise_on_error=False)
+    assert rc == -22
+
+
+def test_initial_state_option(ctx):
+    # (->VersionedRegister 5 nil): the first write must report version 6
+    ops, off = pack_keys([[[1, 1, -1, 6, 0, 1]], [[1, 1, -1, 1, 0, 1]]])
+    _, r = ctx.check(ops, off, abi.default_opts(init_version=5))
+    assert list(r["verdict"]) == [1, 0]
+
+
+def test_check_device_path_with_torch(ctx):
+    import torch
+    z = np.load(os.path.join(GOLDEN, "c5.npz"))
+    dev = torch.device("cuda", 0)
+    # a slice of keys whose key_off does not start at 0
+    a, b = 50, 250
+    d_ops = torch.from_numpy(np.ascontiguousarray(z["ops"][z["key_off"][a]:])).to(dev)
+    d_off = torch.from_numpy(np.ascontiguousarray(z["key_off"][a:b + 1])).to(dev)
+    d_out = torch.zeros((b - a) * 40, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream(dev)
+    ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), b - a, d_out.data_ptr(),
+                     stream=s.cuda_stream)
+    r = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
+    assert (r["verdict"] == z["verdict"][a:b]).all()
+    assert (r["fail_op"] == z["fail_op"][a:b]).all()
+    assert ctx.stats()["kernel_ms"] > 0
+
+
+def test_register_checker_end_to_end():
+    from jepsen.etcd_amd import checker as C, synth
+    hist, labels = synth.jepsen_history(60, 120, concurrency=10, p_info=0.03,
+                                        p_anomaly=0.3, seed=5)
+    chk = C.register_checker(device_mask=1)
+    res = chk.check({"name": "etcd register"}, hist, {})
+    chk.close()
+    from jepsen.etcd_amd import history as H
+    _, ops, off, _ = H.pack(hist)
+    _, ref = oracle.check(ops, off, algo=oracle.JITC)
+    bad = sorted(int(k) for k in np.nonzero(ref["verdict"] == 0)[0])
+    assert set(k for k, l in enumerate(labels) if l == 1) <= set(bad)
+    assert res["valid?"] is False
+    assert sorted(res["failures"]) == bad
+    for k in bad:
+        r = res["results"][k]
+        assert r["valid?"] is False and r["op"]["type"] == "ok"
+    assert C.check_safe(chk, {}, [{"type": "invoke", "process": 0, "value": None}]) == \
+        {"valid?": True, "results": {}, "failures": []}

@@ -1,0 +1,154 @@
+"""Host logic without a GPU: generator, Jepsen history preprocessing,
+partitioning, and the C ABI's exported symbols."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+from helpers import load_kats, pack_keys
+from jepsen.etcd_amd import abi, history as H, synth
+from jepsen.etcd_amd.history import Tuple
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(abi.LIB_PATH)
+    names = []
+    for h in ("lincheck.h", "lincheck_synth.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        names += re.findall(r"^\s*(?:const\s+)?\w+\s+\**(lc_\w+)\s*\(", src, re.M)
+    assert set(names) == {
+        "lc_open", "lc_check", "lc_check_device", "lc_last_stats", "lc_last_error",
+        "lc_close", "lc_default_opts", "lc_plan_partition", "lc_abi_version",
+        "lc_synth_register", "lc_synth_key"}
+    for n in names:
+        assert hasattr(lib, n), n
+    assert abi.lib().lc_abi_version() == 1
+
+
+def test_struct_sizes():
+    assert abi.RESULT_DTYPE.itemsize == 40
+    assert ctypes.sizeof(abi.LcOpts) == 40
+    assert ctypes.sizeof(abi.LcSynthParams) == 48
+
+
+def test_open_without_gpu_fails_loudly():
+    from conftest import gpu_available
+    if gpu_available():
+        pytest.skip("GPU present")
+    with pytest.raises(abi.LcError):
+        abi.Context(0)
+
+
+def test_synth_deterministic_and_exact():
+    a = abi.synth(50, 300, concurrency=20, seed=42, n_threads=1)
+    b = abi.synth(50, 300, concurrency=20, seed=42, n_threads=8)
+    assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
+    ops, off = a[0], a[1]
+    assert off[-1] == 50 * 300 and (np.diff(off) == 300).all()
+    # per key: calls strictly increasing, ret > call, fields in range
+    for k in range(50):
+        r = ops[off[k]:off[k + 1]]
+        assert (np.diff(r[:, 4]) > 0).all() and (r[:, 5] > r[:, 4]).all()
+        assert set(np.unique(r[:, 0])) <= {0, 1, 2}
+    c = abi.synth(50, 300, concurrency=20, seed=43)
+    assert not (a[0] == c[0]).all()
+
+
+def test_synth_clean_keys_valid_anomalies_invalid():
+    ops, off, lab, ninv = abi.synth(300, 200, concurrency=10, p_anomaly=0.3, seed=5)
+    assert ninv > len(ops)  # failed CAS invocations were dropped
+    _, r = oracle.check(ops, off, algo=oracle.JITC, n_threads=4)
+    assert (r["verdict"][lab == 0] == 1).all()
+    assert (r["verdict"][lab == 1] == 0).all()          # stale read: always visible
+    assert (r["verdict"][lab == 2] == 0).mean() > 0.8   # lost CAS: unless nothing follows it
+    assert (lab > 0).sum() > 30
+
+
+def test_history_pairing_kat8_fail_dropped():
+    # KAT8 as a Jepsen history: a :fail CAS between the write and the read.
+    h = [
+        {"type": "invoke", "f": "write", "process": 0, "value": Tuple("k", [None, 1])},
+        {"type": "ok", "f": "write", "process": 0, "value": Tuple("k", [1, 1])},
+        {"type": "invoke", "f": "cas", "process": 1, "value": Tuple("k", [None, [3, 4]])},
+        {"type": "fail", "f": "cas", "process": 1, "value": Tuple("k", [None, [3, 4]])},
+        {"type": "invoke", "f": "read", "process": 0, "value": Tuple("k", [None, None])},
+        {"type": "ok", "f": "read", "process": 0, "value": Tuple("k", [1, 1])},
+    ]
+    keys, ops, off, done = H.pack(h)
+    assert keys == ["k"] and len(ops) == 2
+    assert ops[0].tolist() == [1, 0, -1, 1, 0, 1]       # value 1 interned as id 0
+    assert ops[1].tolist() == [0, 0, -1, 1, 4, 5]
+
+
+def test_history_info_nemesis_and_nontuple():
+    h = [
+        {"type": "invoke", "f": "write", "process": 0, "value": Tuple(1, [None, 7])},
+        {"type": "info", "f": "start", "process": "nemesis", "value": None},
+        {"type": "info", "f": "write", "process": 0, "value": Tuple(1, [None, 7])},
+        {"type": "invoke", "f": "cas", "process": 5, "value": Tuple(2, [None, [None, 3]])},
+        {"type": "ok", "f": "cas", "process": 5, "value": Tuple(2, [1, [None, 3]])},
+        {"type": "invoke", "f": "read", "process": 6, "value": Tuple(1, [None, None])},
+    ]
+    keys, ops, off, done = H.pack(h)
+    assert keys == [1, 2]
+    k1 = ops[off[0]:off[1]].tolist()
+    assert k1[0] == [1, 0, -1, -1, 0, abi.LC_INF]       # crashed write
+    assert k1[1] == [0, -1, -1, -1, 5, abi.LC_INF]      # unterminated read
+    k2 = ops[off[1]:off[2]].tolist()
+    assert k2 == [[2, 0, -1, 1, 3, 4]]                  # cas nil->3, version 1
+
+
+def test_history_unknown_f_and_bad_value():
+    h = [
+        {"type": "invoke", "f": "frob", "process": 0, "value": Tuple("a", [None, 1])},
+        {"type": "ok", "f": "frob", "process": 0, "value": Tuple("a", [1, 1])},
+        {"type": "invoke", "f": "cas", "process": 1, "value": Tuple("b", [None, 3])},
+        {"type": "ok", "f": "cas", "process": 1, "value": Tuple("b", [1, 3])},
+    ]
+    _, ops, off, _ = H.pack(h)
+    assert ops[0, 0] == H.F_UNKNOWN and ops[1, 0] == H.F_UNKNOWN
+
+
+def test_interning_distinguishes_types():
+    it = H.Interner()
+    assert it(1) == it(1) and it(1) != it(1.0) and it(True) != it(1)
+    assert it(None) == abi.LC_NIL
+
+
+def test_jepsen_history_roundtrip_matches_packed_generator():
+    """Rendering generator keys as one Jepsen history (fails, nemesis ops,
+    interleaving) and re-packing gives the same verdicts as the packed
+    generator output."""
+    hist, labels = synth.jepsen_history(40, 150, concurrency=10, p_info=0.05,
+                                        p_anomaly=0.3, seed=77)
+    keys, ops, off, done = H.pack(hist)
+    assert keys == list(range(40))
+    ref_ops = []
+    for k in range(40):
+        o, p, st, _ = abi.synth_key(k, 150, 10, 5, 0.05, 0.3, 77)
+        ref_ops.append(o[st != 0])
+    ref, ref_off = pack_keys([r.tolist() for r in ref_ops])
+    _, a = oracle.check(ops, off, algo=oracle.JITC)
+    _, b = oracle.check(ref, ref_off, algo=oracle.JITC)
+    assert (a["verdict"] == b["verdict"]).all() and (a["fail_op"] == b["fail_op"]).all()
+    assert (a["verdict"][np.array(labels) == 0] == 1).all()
+    assert (a["verdict"][np.array(labels) == 1] == 0).all()
+
+
+def test_plan_partition_balanced_and_contiguous():
+    off = np.concatenate([[0], np.cumsum(np.random.RandomState(0).randint(0, 500, 1000))])
+    for parts in (1, 2, 3, 8):
+        b = abi.plan_partition(off, parts)
+        assert b[0] == 0 and b[-1] == 1000 and (np.diff(b) >= 0).all()
+        cost = [(off[b[i + 1]] - off[b[i]]) + 64 * (b[i + 1] - b[i]) for i in range(parts)]
+        assert max(cost) - min(cost) <= 2 * (500 + 64)  # one key per boundary
+
+
+def test_kat_file_consistent():
+    for k in load_kats():
+        assert k["fail_prefix_end"] == (k["ops"][k["fail_op"]][5] if k["fail_op"] >= 0 else -1)

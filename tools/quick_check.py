@@ -16,7 +16,7 @@ for (name, nk, n, conc, pi, pa, seed) in cases:
     ops, off, lab, _ = abi.synth(nk, n, concurrency=conc, p_info=pi, p_anomaly=pa, seed=seed)
     t = time.time(); rc, g = ctx.check(ops, off, raise_on_error=False); tg = time.time() - t
     st = ctx.stats()
-    _, r = oracle.check(ops, off, algo=oracle.JITC, n_threads=16, max_configs=300000)
+    _, r = oracle.check(ops, off, algo=oracle.JITC, n_threads=16, max_configs=2000000)
     known = r['verdict'] != -1
     mism = np.nonzero(known & ((g['verdict'] != r['verdict']) | (g['fail_op'] != r['fail_op'])))[0]
     print(name, "rc", rc, "kernel_ms %.3f hbm_ms %.3f hbm_keys %d" % (st['kernel_ms'], st['hbm_kernel_ms'], st['n_hbm_keys']),
