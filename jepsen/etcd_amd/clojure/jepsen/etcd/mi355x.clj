@@ -1,0 +1,184 @@
+(ns jepsen.etcd.mi355x
+  "Drop-in jepsen.checker/Checker for the register workload's hot path.
+
+  Replaces, as one unit, the checker built at
+  src/jepsen/etcd/register.clj:108-112:
+
+    (independent/checker
+      (checker/compose
+        {:linear   (checker/linearizable {:model (->VersionedRegister 0 nil)})
+         :timeline (timeline/html)}))
+
+  The JVM side does the host preprocessing (client ops only, the independent
+  per-key split, knossos-style invoke/completion pairing with :fail pairs
+  dropped and :info ops pending forever, per-key value interning by Clojure
+  =) and packs one 48-byte lc_op record per operation into off-heap memory.
+  One lc_check call (JNA, liblincheck.so; C ABI in include/lincheck.h) then
+  decides every key on the MI355X GPUs of the control node.  The result has
+  jepsen.independent/checker's shape.  The timeline renderer is not
+  reproduced (out of scope); compose it separately if wanted.
+
+  Usage, in register.clj's workload:
+
+    :checker (jepsen.etcd.mi355x/checker)
+
+  Untested in the build container (no JVM there); the same contract is
+  exercised from Python by tests/test_gpu.py::test_register_checker_end_to_end."
+  (:require [jepsen.checker :as checker]
+            [jepsen.independent :as independent])
+  (:import (com.sun.jna Function Memory NativeLibrary Pointer)
+           (com.sun.jna.ptr PointerByReference)))
+
+(def ^:const LC_NIL -1)
+(def ^:const LC_INF Long/MAX_VALUE)
+(def ^:const op-bytes 48)
+(def ^:const result-bytes 40)
+
+(defonce ^:private lib
+  (delay (NativeLibrary/getInstance
+           (or (System/getenv "LINCHECK_LIB") "lincheck"))))
+
+(defn- fun ^Function [name] (.getFunction ^NativeLibrary @lib name))
+
+(defonce ^:private ctx
+  (delay
+    (let [out (PointerByReference.)
+          rc  (.invokeInt (fun "lc_open") (object-array [(int 0) out]))]
+      (when-not (zero? rc)
+        (throw (ex-info "lc_open failed: no usable GPU (no CPU fallback)"
+                        {:rc rc})))
+      (.getValue out))))
+
+(defn- client-op? [op] (integer? (:process op)))
+
+(defn- subhistories
+  "{k [op ...]}: jepsen.independent's split of the client ops; tuple values
+  are unwrapped, non-tuple ops go to every key."
+  [history]
+  (let [ops  (filter client-op? history)
+        keys (->> ops (keep (fn [op] (let [v (:value op)]
+                                       (when (independent/tuple? v) (key v)))))
+                  distinct)]
+    (into (array-map)
+          (for [k keys]
+            [k (->> ops
+                    (keep (fn [op]
+                            (let [v (:value op)]
+                              (cond (not (independent/tuple? v)) op
+                                    (= k (key v)) (assoc op :value (val v))))))
+                    vec)]))))
+
+(defn- complete
+  "knossos-style completion of one key: [{:op invoke-with-completed-value
+  :call i :ret j-or-INF :completion c}] in invoke order, :fail pairs dropped."
+  [ops]
+  (loop [ops ops, pending {}, out []]
+    (if-let [op (first ops)]
+      (let [p (:process op)]
+        (case (:type op)
+          :invoke (recur (rest ops) (assoc pending p (count out))
+                         (conj out {:op op :call (:index op) :ret LC_INF}))
+          (:ok :fail :info)
+          (if-let [i (pending p)]
+            (recur (rest ops) (dissoc pending p)
+                   (update out i
+                           (fn [r]
+                             (case (:type op)
+                               :ok   (assoc r :op (assoc (:op r) :value (:value op))
+                                              :ret (:index op) :completion op)
+                               :fail (assoc r :fail? true)
+                               :info (assoc r :completion op)))))
+            (recur (rest ops) pending out))
+          (recur (rest ops) pending out)))
+      (vec (remove :fail? out)))))
+
+(defn- interner []
+  (let [ids (volatile! {})]
+    (fn [v]
+      (if (nil? v)
+        LC_NIL
+        (or (@ids v)
+            (let [i (count @ids)] (vswap! ids assoc v i) i))))))
+
+(defn- record
+  "[f value expected version call ret] for one completed op
+  (register.clj:22-44, 98-100); f 3 (unknown) if the shape does not match,
+  which the GPU reports as :unknown like the model's throwing step (:63)."
+  [intern {:keys [op call ret]}]
+  (let [[version v] (:value op)
+        f (case (:f op) :read 0 :write 1 :cas 2 3)]
+    (if (or (= f 3) (and (some? version) (not (integer? version)))
+            (and (= f 2) (not (sequential? v))))
+      [3 LC_NIL LC_NIL LC_NIL call ret]
+      (let [ver (if (nil? version) LC_NIL (long version))]
+        (if (= f 2)
+          [2 (intern (second v)) (intern (first v)) ver call ret]
+          [f (intern v) LC_NIL ver call ret])))))
+
+(defn- pack
+  "Packs all keys: returns [keys completed-per-key ^Memory ops ^Memory key-off]."
+  [subs]
+  (let [keys  (vec (keys subs))
+        done  (mapv (fn [k] (complete (get subs k))) keys)
+        n     (reduce + (map count done))
+        ops   (Memory. (max 1 (* op-bytes n)))
+        off   (Memory. (* 8 (inc (count keys))))]
+    (loop [ki 0, i 0]
+      (.setLong off (* 8 ki) i)
+      (when (< ki (count keys))
+        (let [intern (interner)
+              recs   (map (partial record intern) (nth done ki))
+              i'     (reduce (fn [i r]
+                               (dotimes [j 6]
+                                 (.setLong ops (+ (* i op-bytes) (* 8 j)) (long (nth r j))))
+                               (inc i))
+                             i recs)]
+          (recur (inc ki) i'))))
+    [keys done ops off]))
+
+(defn- merge-valid [vs]
+  (cond (some false? vs)          false
+        (some #{:unknown} vs)     :unknown
+        :else                     true))
+
+(defn checker
+  "The drop-in (see ns doc).  opts: :max-configs-per-key (0 = default)."
+  ([] (checker {}))
+  ([{:keys [max-configs-per-key] :or {max-configs-per-key 0}}]
+   (reify checker/Checker
+     (check [_ test history _opts]
+       (let [subs (subhistories history)]
+         (if (empty? subs)
+           {:valid? true :results {} :failures []}
+           (let [[keys done ops off] (pack subs)
+                 nk   (count keys)
+                 out  (Memory. (* result-bytes nk))
+                 o    (doto (Memory. 40)
+                        (.setLong 0 0) (.setLong 8 LC_NIL)
+                        (.setLong 16 max-configs-per-key)
+                        (.setLong 24 0) (.setLong 32 0))
+                 rc   (locking ctx
+                        (.invokeInt (fun "lc_check")
+                                    (object-array [@ctx ops off (long nk) o out])))]
+             (when-not (zero? rc)
+               (throw (ex-info "lc_check failed"
+                               {:rc rc :error (.invoke (fun "lc_last_error")
+                                                       String (object-array [@ctx]))})))
+             (let [results
+                   (into (array-map)
+                         (for [ki (range nk)]
+                           (let [b       (* ki result-bytes)
+                                 verdict (.getInt out b)
+                                 reason  (.getInt out (+ b 4))
+                                 fail-op (.getLong out (+ b 8))
+                                 v       (case verdict 1 true 0 false :unknown)]
+                             [(nth keys ki)
+                              (cond-> {:valid?   v
+                                       :analyzer :mi355x
+                                       :configs  (.getLong out (+ b 24))}
+                                (false? v)   (assoc :op (let [r (nth (nth done ki) fail-op)]
+                                                          (or (:completion r) (:op r))))
+                                (= v :unknown) (assoc :error [:lincheck-reason reason]))])))]
+               {:valid?   (merge-valid (map :valid? (vals results)))
+                :results  results
+                :failures (vec (for [[k r] results :when (false? (:valid? r))] k))}))))))))
