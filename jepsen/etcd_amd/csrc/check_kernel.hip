@@ -358,6 +358,22 @@ __device__ __forceinline__ int general_return(Store &st, const Slot &sl, uint64_
   return nR;
 }
 
+// Retire slots rb: ops linearized in every configuration are finished (a
+// crashed op has no return; an :ok op's return would keep every configuration
+// unchanged), so their slots are freed and their returns never become events.
+// Exact (oracle ORACLE_FLAG_RETIRE, checked against the faithful search).
+__device__ __forceinline__ void retire(Slot &sl, uint64_t &occ, uint64_t &crashed,
+                                       uint64_t rb, int lane) {
+  occ &= ~rb;
+  crashed &= ~rb;
+  if ((rb >> lane) & 1) {
+    sl.ret = kNever;
+    sl.latest = 0;
+    sl.pred = -1;
+  }
+  if (sl.pred >= 0 && ((rb >> sl.pred) & 1)) sl.pred = -1;
+}
+
 template <class Store>
 __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
                           const KParams &p, Store &st, KeyOut &o,
@@ -370,9 +386,11 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
   o.max_frontier = 1;
   if (n <= 0) return;
 
-  // Frontier: one configuration in SGPRs (single) or nF of them in region rF.
+  // Frontier: either ONE configuration in SGPRs (single; after retirement its
+  // linearized set is always empty, so it is just the state fsv and every
+  // occupied slot is pending in it), or nF configurations in region rF.
   bool single = true;
-  uint64_t fm = 0, fsv = pack_sv(p.init_ver, p.init_val);
+  uint64_t fsv = pack_sv(p.init_ver, p.init_val);
   int rF = 0, rR = 1, rW = 2, nF = 1;
 
   Slot sl{0, -1, -1, -1, -1, -1, 0, kNever};
@@ -387,120 +405,11 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
 
   for (;;) {
     const uint32_t ncall = (i < n) ? (uint32_t)rl32((int)cur.call, (int)(i - base)) : kNever;
-    const uint32_t nret = wave_min_u32(sl.ret);
-    if (i >= n && nret == kNever) break;  // only crashed ops remain open
-
-    if (nret < ncall) {
-      // ----------------------------------------------------- return of x
-      const uint64_t hit = __ballot(sl.ret == nret);
-      const int s = __builtin_ctzll(hit);
-      const uint64_t bs = 1ull << s;
-      const int x_idx = rl32(sl.idx, s);
-      bool empty = false;
-      if (single) {
-        if (!(fm & bs)) {
-          // Chain walk: while exactly one mutation can step the lone
-          // configuration, the JIT expansion is a path (versions strictly
-          // increase, so no configuration repeats) and stays in SGPRs.
-          const int64_t explored0 = o.explored;
-          uint64_t cm = fm, csv = fsv;
-          bool branch = false;
-          for (;;) {
-            const int cver = sv_ver(csv), cval = sv_val(csv);
-            const uint64_t cand = mutation_candidates(sl, occ, cm, cver, cval, lane);
-            if (cand == 0) {
-              empty = true;
-              break;
-            }
-            if (cand & (cand - 1)) {
-              branch = true;
-              break;
-            }
-            const int t = __builtin_ctzll(cand);
-            const int nver = cver + 1;
-            const int nval = rl32(sl.val, t);
-            uint64_t nm = cm | (1ull << t);
-            nm |= read_closure(sl, occ, nm, nver, nval, lane);
-            o.explored++;
-            if (o.explored > p.budget) {
-              o.verdict = LC_UNKNOWN;
-              o.reason = LC_REASON_CONFIG_BUDGET;
-              return;
-            }
-            cm = nm;
-            csv = pack_sv(nver, nval);
-            if (nm & bs) break;
-          }
-          if (branch) {
-            // Several successors: redo this return on the general path from
-            // the lone configuration.
-            o.explored = explored0;
-            empty = false;
-            single = false;
-            rF = 0;
-            if (lane == 0) st.reg(rF)[0] = Cfg{fm, fsv};
-            rR = 1;
-            rW = 2;
-            nF = 1;
-          } else if (!empty) {
-            fm = cm;
-            fsv = csv;
-          }
-        }
-        if (single && !empty) fm &= ~bs;
-      }
-      if (!single) {
-        const int r = general_return(st, sl, occ, s, rF, rR, rW, nF, p, o, lane);
-        if (r < 0) {
-          o.verdict = LC_UNKNOWN;
-          o.reason = r == -1 ? LC_REASON_FRONTIER_LDS : LC_REASON_CONFIG_BUDGET;
-          return;
-        }
-        const int t = rF;
-        rF = rR;
-        rR = t;
-        nF = r;
-        if (nF > o.max_frontier) o.max_frontier = nF;
-        empty = nF == 0;
-        if (nF == 1) {  // back to the register-resident frontier
-          const Cfg c = st.get(rF, 0);
-          fm = rfl64(c.mask);
-          fsv = rfl64(c.sv);
-          single = true;
-        }
-      }
-      occ &= ~bs;
-      if (lane == s) sl.ret = kNever;
-      if (empty) {
-        o.verdict = LC_INVALID;
-        o.reason = LC_REASON_NONLINEARIZABLE;
-        o.fail_op = x_idx;
-        o.fail_end = base_idx + (int64_t)nret;
-        return;
-      }
-      // Retirement: a crashed op linearized in EVERY configuration is done for
-      // good (no return to wait for); free its slot everywhere.
-      uint64_t rb = crashed;
-      if (single) {
-        rb &= fm;
-      } else {
-        uint64_t acc = ~0ull;
-        for (int j = lane; j < nF; j += kWave) acc &= st.get(rF, j).mask;
-        rb &= wave_and_u64(acc);
-      }
-      if (rb) {
-        occ &= ~rb;
-        crashed &= ~rb;
-        if (single) {
-          fm &= ~rb;
-        } else {
-          for (int j = lane; j < nF; j += kWave)
-            st.set_mask_lane(rF, j, st.get(rF, j).mask & ~rb);
-        }
-        if ((rb >> lane) & 1) sl.latest = 0;
-        if (sl.pred >= 0 && ((rb >> sl.pred) & 1)) sl.pred = -1;
-      }
-    } else {
+    // Returns due before the next call: one ballot; the DPP min only when
+    // several are due at once.
+    const uint64_t due = __ballot(sl.ret < ncall);
+    if (due == 0) {
+      if (i >= n) break;  // no calls left, no pending returns
       // ------------------------------------------------------- call of op i
       const int li = (int)(i - base);
       const int f = rl32(cur.f, li), val = rl32(cur.val, li);
@@ -518,11 +427,13 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
         return;
       }
       prev_call = ncall;
-      // A read that never returned, or read [nil nil], is legal in every
-      // state and changes nothing: it never constrains the search.
-      const bool trivial =
-          (f == LC_F_READ) && (ret == kNever || (ver == -1 && val == -1));
-      if (!trivial) {
+      // Reads that never constrain (crashed, or [nil nil]) and, with a lone
+      // configuration, reads legal right now (eager closure + retirement)
+      // need no slot at all.
+      bool done = (f == LC_F_READ) && (ret == kNever || (ver == -1 && val == -1));
+      if (!done && single && f == LC_F_READ)
+        done = legal(LC_F_READ, ver, val, ex, sv_ver(fsv), sv_val(fsv));
+      if (!done) {
         if (occ == ~0ull) {
           o.verdict = LC_UNKNOWN;
           o.reason = LC_REASON_WINDOW_OVERFLOW;
@@ -530,7 +441,7 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
         }
         const int s = __builtin_ctzll(~occ);
         int pred = -1;
-        const bool crash = ret == kNever;  // (crashed reads are trivial)
+        const bool crash = ret == kNever;  // (crashed reads never get here)
         if (crash) {
           const uint64_t m = __ballot(((crashed >> lane) & 1) && sl.latest &&
                                       sl.f == f && sl.val == val && sl.exp == ex &&
@@ -552,18 +463,11 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
           sl.latest = crash ? 1 : 0;
         }
         occ |= 1ull << s;
-        if (f == LC_F_READ) {  // eager read closure at the call
-          if (single) {
-            if (legal(LC_F_READ, ver, val, ex, sv_ver(fsv), sv_val(fsv))) fm |= 1ull << s;
-          } else {
-            for (int j0 = 0; j0 < nF; j0 += kWave) {
-              const int j = j0 + lane;
-              if (j < nF) {
-                const Cfg c = st.get(rF, j);
-                if (legal(LC_F_READ, ver, val, ex, sv_ver(c.sv), sv_val(c.sv)))
-                  st.set_mask_lane(rF, j, c.mask | (1ull << s));
-              }
-            }
+        if (f == LC_F_READ && !single) {  // eager read closure at the call
+          for (int j = lane; j < nF; j += kWave) {
+            const Cfg c = st.get(rF, j);
+            if (legal(LC_F_READ, ver, val, ex, sv_ver(c.sv), sv_val(c.sv)))
+              st.set_mask_lane(rF, j, c.mask | (1ull << s));
           }
         }
       }
@@ -573,6 +477,106 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
         cur = nxt;
         nxt = load_rec(kops, base + kWave + lane, n, base_idx);
       }
+      continue;
+    }
+
+    // ----------------------------------------------------- return of x
+    int s;
+    if ((due & (due - 1)) == 0) {
+      s = __builtin_ctzll(due);
+    } else {
+      const bool mine = (due >> lane) & 1;
+      const uint32_t m = wave_min_u32(mine ? sl.ret : kNever);
+      s = __builtin_ctzll(__ballot(mine && sl.ret == m));
+    }
+    const uint64_t bs = 1ull << s;
+    const int x_idx = rl32(sl.idx, s);
+    const uint32_t nret = (uint32_t)rl32((int)sl.ret, s);
+    bool empty = false;
+    if (single) {
+      // x is pending (a linearized op would have been retired).  Chain walk:
+      // while exactly one mutation can step the lone configuration, the JIT
+      // expansion is a path (versions strictly increase, so no configuration
+      // repeats) and stays in SGPRs.
+      const int64_t explored0 = o.explored;
+      uint64_t cm = 0, csv = fsv;
+      bool branch = false;
+      for (;;) {
+        const int cver = sv_ver(csv), cval = sv_val(csv);
+        const uint64_t cand = mutation_candidates(sl, occ, cm, cver, cval, lane);
+        if (cand == 0) {
+          empty = true;
+          break;
+        }
+        if (cand & (cand - 1)) {
+          branch = true;
+          break;
+        }
+        const int t = __builtin_ctzll(cand);
+        const int nver = cver + 1;
+        const int nval = rl32(sl.val, t);
+        uint64_t nm = cm | (1ull << t);
+        nm |= read_closure(sl, occ, nm, nver, nval, lane);
+        o.explored++;
+        if (o.explored > p.budget) {
+          o.verdict = LC_UNKNOWN;
+          o.reason = LC_REASON_CONFIG_BUDGET;
+          return;
+        }
+        cm = nm;
+        csv = pack_sv(nver, nval);
+        if (nm & bs) break;
+      }
+      if (branch) {
+        // Several successors: redo this return on the general path from the
+        // lone configuration.
+        o.explored = explored0;
+        single = false;
+        rF = 0;
+        rR = 1;
+        rW = 2;
+        nF = 1;
+        if (lane == 0) st.reg(rF)[0] = Cfg{0ull, fsv};
+      } else if (!empty) {
+        fsv = csv;
+        retire(sl, occ, crashed, cm, lane);  // x included
+      }
+    }
+    if (!single) {
+      const int r = general_return(st, sl, occ, s, rF, rR, rW, nF, p, o, lane);
+      if (r < 0) {
+        o.verdict = LC_UNKNOWN;
+        o.reason = r == -1 ? LC_REASON_FRONTIER_LDS : LC_REASON_CONFIG_BUDGET;
+        return;
+      }
+      const int t = rF;
+      rF = rR;
+      rR = t;
+      nF = r;
+      if (nF > o.max_frontier) o.max_frontier = nF;
+      empty = nF == 0;
+      if (!empty) {
+        retire(sl, occ, crashed, bs, lane);  // x returned
+        uint64_t acc = ~0ull;
+        for (int j = lane; j < nF; j += kWave) acc &= st.get(rF, j).mask;
+        const uint64_t rb = occ & wave_and_u64(acc);
+        if (rb) {
+          retire(sl, occ, crashed, rb, lane);
+          for (int j = lane; j < nF; j += kWave)
+            st.set_mask_lane(rF, j, st.get(rF, j).mask & ~rb);
+        }
+        if (nF == 1) {  // back to the register-resident frontier (mask now empty)
+          fsv = rfl64(st.get(rF, 0).sv);
+          single = true;
+        }
+      }
+    }
+    if (empty) {
+      o.verdict = LC_INVALID;
+      o.reason = LC_REASON_NONLINEARIZABLE;
+      o.fail_op = x_idx;
+      o.fail_end = base_idx + (int64_t)nret;
+      return;
     }
   }
 }

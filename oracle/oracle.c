@@ -237,8 +237,12 @@ static event *build_events(const lc_op *o, int64_t n, int64_t *ne) {
  *                 interchangeable once called (their version is always nil:
  *                 the completion never arrived), so only the earliest-called
  *                 unlinearized member of such a class may be linearized next.
- *  RETIRE         a crashed op linearized in every configuration is done for
- *                 good (it has no return to wait for): its slot is freed. */
+ *  RETIRE         an op linearized in every configuration is done for good:
+ *                 a crashed op has no return, and an :ok op's return would
+ *                 keep every configuration unchanged (JIT keeps the configs
+ *                 that already linearized it), so its slot is freed and its
+ *                 return skipped.  Real time stays respected: anything
+ *                 called later is linearized after it in every config. */
 static int is_trivial_read(const lc_op *op) {
   return op->f == LC_F_READ &&
          (op->ret == LC_INF || (op->version == LC_NIL && op->value == LC_NIL));
@@ -433,9 +437,12 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
       break;
     }
     if (retire) {
+      /* an op linearized in every configuration is finished: a crashed op has
+       * no return to wait for, and an :ok op's return would keep every
+       * configuration as it is (all of them already linearized it) */
       int any = 0;
       for (int w = 0; w < bw; w++) {
-        all[w] = crashed[w];
+        all[w] = occ[w];
         for (size_t i = 0; i < F.n; i++) all[w] &= cset_get(&F, i)[w];
         any |= all[w] != 0;
       }
@@ -445,16 +452,17 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
           for (int w = 0; w < bw; w++) c[w] &= ~all[w];
         }
         cset_rehash(&F, F.tcap);
-        for (int w = 0; w < bw; w++) {
-          occ[w] &= ~all[w];
-          crashed[w] &= ~all[w];
-        }
         for (int u = 0; u < bw * 64; u++) {
           if (BIT(all, u)) {
             latest[u] = 0;
             pred[u] = -1;
+            slot_of[slot_op[u]] = -1; /* its return (if any) is now a no-op */
           }
           if (BIT(occ, u) && pred[u] >= 0 && BIT(all, pred[u])) pred[u] = -1;
+        }
+        for (int w = 0; w < bw; w++) {
+          occ[w] &= ~all[w];
+          crashed[w] &= ~all[w];
         }
       }
     }
