@@ -97,54 +97,87 @@ __device__ __forceinline__ uint64_t wave_and_u64(uint64_t v) {
   return ((uint64_t)wave_and_u32((uint32_t)(v >> 32)) << 32) | wave_and_u32((uint32_t)v);
 }
 
-// VersionedRegister.step legality (register.clj:60-96); NIL = -1.
-//   write :64-68  version' = version+1 must equal op-version unless nil
-//   cas   :70-82  same, and the current value must equal the expected value
-//   read  :84-96  op-version (if non-nil) == version, op-value (if non-nil) == value
-// A mutation's next state is (version+1, op value).
-__device__ __forceinline__ bool legal(int f, int opver, int opval, int opexp,
-                                      int ver, int val) {
-  if (f == LC_F_READ)
-    return (opver == -1 || opver == ver) && (opval == -1 || opval == val);
-  return (opver == -1 || opver == ver + 1) && (f != LC_F_CAS || val == opexp);
-}
-
 // One record, decoded by one lane.  Event indices become key-relative 32-bit
 // (index - first call of the key; LC_INF -> kNever) so event selection is a
-// 32-bit min.  A key whose indices span >= 2^32-1 is rejected as malformed
-// (documented limit).
+// 32-bit compare.  A key whose indices span >= 2^32-1 is rejected as
+// malformed (documented limit).  The op's precondition on the state it is
+// stepped from is precomputed as (nv, nvm, nl, nlm):
+//     legal(ver, val)  <=>  (((ver ^ nv) & nvm) | ((val ^ nl) & nlm)) == 0
+// (register.clj:60-96: read needs version == op-version and value ==
+// op-value where non-nil; write needs version+1 == op-version where non-nil;
+// cas additionally needs value == expected), so legality over all 64 window
+// slots is a handful of VALU ops and one compare — no per-lane boolean
+// logic on lane masks.
 struct Rec {
-  int f, val, exp, ver, bad;
-  uint32_t call, ret;
+  int f, val, exp, ver;  // raw fields (int32; f = 3 for an unknown :f)
+  int nv, nvm, nl, nlm;  // precondition
+  uint32_t call, ret;    // key-relative; kNever = none
+  int bad;
 };
 
-__device__ __forceinline__ Rec load_rec(const lc_op *__restrict__ o, int64_t i,
-                                        int64_t n, int64_t base_idx) {
-  Rec r;
+// Raw 48-byte record as loaded (three 16-byte loads per lane).  Decoding is
+// deferred to the chunk switch so the prefetch of the next 64 records stays
+// in flight while the current chunk is processed.
+struct Raw {
+  longlong2 a, b, c;
+};
+
+__device__ __forceinline__ Raw load_raw(const lc_op *__restrict__ o, int i, int n) {
+  Raw r;
   if (i < n) {
     const longlong2 *p = reinterpret_cast<const longlong2 *>(o + i);
-    const longlong2 a = p[0], b = p[1], c = p[2];
-    const int64_t f = a.x, value = a.y, expected = b.x, version = b.y;
-    const int64_t call = c.x, ret = c.y;
-    const int64_t rc = call - base_idx, rr = ret - base_idx;
-    r.bad = (value < -1) | (value > kFieldMax) | (expected < -1) |
-            (expected > kFieldMax) | (version < -1) | (version > kFieldMax) |
-            (call < 0) | (ret <= call) | (rc < 0) | (rc >= (int64_t)kNever) |
-            ((ret != kInf) & (rr >= (int64_t)kNever));
-    r.f = (f >= 0 && f <= 2) ? (int)f : 3;
-    r.val = (int)value;
-    r.exp = (int)expected;
-    r.ver = (int)version;
-    r.call = (uint32_t)rc;
-    r.ret = ret == kInf ? kNever : (uint32_t)rr;
+    r.a = p[0];
+    r.b = p[1];
+    r.c = p[2];
   } else {
+    r.a = make_longlong2(0, -1);
+    r.b = make_longlong2(-1, -1);
+    r.c = make_longlong2(-1, -1);  // call = ret = -1 marks "past the end"
+  }
+  return r;
+}
+
+__device__ __forceinline__ Rec decode(const Raw &w, int64_t base_idx) {
+  Rec r;
+  const int64_t f = w.a.x, value = w.a.y, expected = w.b.x, version = w.b.y;
+  const int64_t call = w.c.x, ret = w.c.y;
+  if (call == -1 && ret == -1) {  // past the end of the key
     r.f = 0;
     r.val = r.exp = r.ver = -1;
+    r.nv = r.nvm = r.nl = r.nlm = 0;
     r.bad = 0;
     r.call = kNever;
     r.ret = kNever;
+    return r;
+  }
+  const int64_t rc = call - base_idx, rr = ret - base_idx;
+  r.bad = (value < -1) | (value > kFieldMax) | (expected < -1) |
+          (expected > kFieldMax) | (version < -1) | (version > kFieldMax) |
+          (call < 0) | (ret <= call) | (rc < 0) | (rc >= (int64_t)kNever) |
+          ((ret != kInf) & (rr >= (int64_t)kNever));
+  r.f = (f >= 0 && f <= 2) ? (int)f : 3;
+  r.val = (int)value;
+  r.exp = (int)expected;
+  r.ver = (int)version;
+  r.call = (uint32_t)rc;
+  r.ret = ret == kInf ? kNever : (uint32_t)rr;
+  const int vchk = r.ver != -1 ? -1 : 0;
+  if (r.f == LC_F_READ) {
+    r.nv = r.ver;
+    r.nvm = vchk;
+    r.nl = r.val;
+    r.nlm = r.val != -1 ? -1 : 0;
+  } else {
+    r.nv = r.ver - 1;
+    r.nvm = vchk;
+    r.nl = r.exp;
+    r.nlm = r.f == LC_F_CAS ? -1 : 0;
   }
   return r;
+}
+
+__device__ __forceinline__ bool pre_ok(int nv, int nvm, int nl, int nlm, int ver, int val) {
+  return (((ver ^ nv) & nvm) | ((val ^ nl) & nlm)) == 0;
 }
 
 struct KeyOut {
@@ -278,42 +311,69 @@ struct HbmStore {
 
 // ------------------------------------------------------------ the search
 
-// Per-lane record of the window slot this lane holds.
-//   pred   for a crashed write/CAS: the slot of the previously called crashed
-//          op of the same class (f, value, expected), or -1.  Such ops are
-//          interchangeable (their version is nil: the completion never came),
-//          so only the earliest-called unlinearized member of a class is a
-//          candidate: an exact symmetry reduction (checked against the oracle's
-//          faithful search in tests/).
-//   latest this slot is the most recently called crashed op of its class.
+// Per-lane record of the window slot this lane holds (valid when the lane's
+// bit is set in `occ`).  Slot kinds are uniform 64-bit masks (occ, rdm =
+// reads, crashed, latest); the per-lane fields are the precondition, the
+// value a mutation writes, the class fields for crashed-op symmetry, the
+// return index and the op index.
+//   pbit  for a crashed write/CAS: one-hot slot of the previously called
+//         crashed op of the same class (f, value, expected, version), or 0.
+//         Such ops are interchangeable (the completion never came), so only
+//         the earliest-called unlinearized member of a class is a candidate:
+//         an exact symmetry reduction (oracle ORACLE_FLAG_CRASH_SYMMETRY,
+//         checked against the faithful search in tests/).
 struct Slot {
-  int f, val, exp, ver, idx, pred, latest;
-  uint32_t ret;  // kNever: free or crashed (never returns)
+  int nv, nvm, nl, nlm;   // precondition
+  int val;                // value written (mutations)
+  int f, exp, ver;        // class fields (crashed ops)
+  int idx;                // op index within the key
+  uint32_t ret;           // kNever: free or crashed (never returns)
+  uint64_t pbit;
 };
 
-// Candidate mutations from configuration (cm, state) and the eager read
-// closure of a successor: ballots over the 64 window slots.
-__device__ __forceinline__ uint64_t mutation_candidates(const Slot &sl, uint64_t occ,
-                                                        uint64_t cm, int ver, int val,
-                                                        int lane) {
-  const bool pend = ((occ & ~cm) >> lane) & 1;
-  const bool turn = sl.pred < 0 || ((cm >> sl.pred) & 1);
-  return __ballot(pend && turn && sl.f != LC_F_READ &&
-                  legal(sl.f, sl.ver, sl.val, sl.exp, ver, val));
+struct Masks {
+  uint64_t occ;      // occupied slots
+  uint64_t rdm;      // slots holding reads
+  uint64_t crashed;  // slots holding crashed writes/CAS
+  uint64_t latest;   // crashed slots that are the latest of their class
+};
+
+__device__ __forceinline__ uint64_t legal_ballot(const Slot &sl, int ver, int val) {
+  return __ballot(pre_ok(sl.nv, sl.nvm, sl.nl, sl.nlm, ver, val));
 }
-__device__ __forceinline__ uint64_t read_closure(const Slot &sl, uint64_t occ,
-                                                 uint64_t nm, int ver, int val,
-                                                 int lane) {
-  const bool pend = ((occ & ~nm) >> lane) & 1;
-  return __ballot(pend && sl.f == LC_F_READ &&
-                  legal(LC_F_READ, sl.ver, sl.val, sl.exp, ver, val));
+
+// Mutations that may step configuration (cm, state): legal, pending, and — for
+// crashed ops — first of their class among the unlinearized ones.
+__device__ __forceinline__ uint64_t mutation_candidates(const Slot &sl, const Masks &mk,
+                                                        uint64_t cm, int ver, int val) {
+  uint64_t cand = legal_ballot(sl, ver, val) & mk.occ & ~mk.rdm & ~cm;
+  if (cand & mk.crashed) cand &= __ballot((sl.pbit & ~cm) == 0);
+  return cand;
+}
+// Eager read closure at a successor state: pending reads legal there.
+__device__ __forceinline__ uint64_t read_closure(const Slot &sl, const Masks &mk,
+                                                 uint64_t nm, int ver, int val) {
+  return legal_ballot(sl, ver, val) & mk.occ & mk.rdm & ~nm;
+}
+
+// Retire slots rb: ops linearized in every configuration are finished (a
+// crashed op has no return; an :ok op's return would keep every configuration
+// unchanged), so their slots are freed and their returns never become events.
+// Exact (oracle ORACLE_FLAG_RETIRE, checked against the faithful search).
+__device__ __forceinline__ void retire(Slot &sl, Masks &mk, uint64_t rb, int lane) {
+  mk.occ &= ~rb;
+  mk.rdm &= ~rb;
+  mk.crashed &= ~rb;
+  mk.latest &= ~rb;
+  if ((rb >> lane) & 1) sl.ret = kNever;
+  sl.pbit &= ~rb;
 }
 
 // Expand the frontier held in region rF (nF configurations) for the return
 // of the op in slot s.  Returns the new frontier size (in region rR), or -1
 // (LDS/HBM sets full) / -2 (configuration budget).
 template <class Store>
-__device__ __forceinline__ int general_return(Store &st, const Slot &sl, uint64_t occ,
+__device__ __forceinline__ int general_return(Store &st, const Slot &sl, const Masks &mk,
                                               int s, int rF, int rR, int rW, int nF,
                                               const KParams &p, KeyOut &o, int lane) {
   const uint64_t bs = 1ull << s;
@@ -339,14 +399,14 @@ __device__ __forceinline__ int general_return(Store &st, const Slot &sl, uint64_
     const Cfg c = st.get(rW, head);
     const uint64_t cm = rfl64(c.mask), csv = rfl64(c.sv);
     const int cver = sv_ver(csv), cval = sv_val(csv);
-    uint64_t cand = mutation_candidates(sl, occ, cm, cver, cval, lane);
+    uint64_t cand = mutation_candidates(sl, mk, cm, cver, cval);
     while (cand) {
       const int t = __builtin_ctzll(cand);
       cand &= cand - 1;
       const int nver = cver + 1;
       const int nval = rl32(sl.val, t);
       uint64_t nm = cm | (1ull << t);
-      nm |= read_closure(sl, occ, nm, nver, nval, lane);
+      nm |= read_closure(sl, mk, nm, nver, nval);
       o.explored++;
       const uint64_t nsv = pack_sv(nver, nval);
       const int r = (nm & bs) ? st.insert(ROLE_R, rR, nR, nm & ~bs, nsv, lane)
@@ -358,24 +418,36 @@ __device__ __forceinline__ int general_return(Store &st, const Slot &sl, uint64_
   return nR;
 }
 
-// Retire slots rb: ops linearized in every configuration are finished (a
-// crashed op has no return; an :ok op's return would keep every configuration
-// unchanged), so their slots are freed and their returns never become events.
-// Exact (oracle ORACLE_FLAG_RETIRE, checked against the faithful search).
-__device__ __forceinline__ void retire(Slot &sl, uint64_t &occ, uint64_t &crashed,
-                                       uint64_t rb, int lane) {
-  occ &= ~rb;
-  crashed &= ~rb;
-  if ((rb >> lane) & 1) {
-    sl.ret = kNever;
-    sl.latest = 0;
-    sl.pred = -1;
-  }
-  if (sl.pred >= 0 && ((rb >> sl.pred) & 1)) sl.pred = -1;
+// Per-chunk uniform masks over the 64 records of the current chunk.
+struct ChunkMasks {
+  uint64_t special;    // malformed or unknown :f
+  uint64_t isread;     // reads
+  uint64_t skip;       // reads that never constrain: crashed, or [nil nil]
+  uint64_t legal_now;  // reads legal in the lone configuration (single mode)
+};
+
+__device__ __forceinline__ ChunkMasks chunk_masks(const Rec &r, uint64_t fsv) {
+  ChunkMasks m;
+  m.special = __ballot(r.bad || r.f > LC_F_CAS);
+  m.isread = __ballot(r.f == LC_F_READ);
+  m.skip = __ballot(r.f == LC_F_READ && (r.ret == kNever || (r.ver == -1 && r.val == -1)));
+  m.legal_now = m.isread & __ballot(pre_ok(r.nv, r.nvm, r.nl, r.nlm, sv_ver(fsv), sv_val(fsv)));
+  return m;
+}
+
+// Calls must strictly increase within a key: compare each record with its
+// predecessor (lane-1, or the previous chunk's last call for lane 0).
+__device__ __forceinline__ void check_order(Rec &r, uint32_t &last_call, int lane) {
+  const uint32_t prev = (uint32_t)__shfl_up((int)r.call, 1);
+  const bool first_key_rec = lane == 0 && last_call == kNever;
+  const uint32_t p = lane == 0 ? last_call : prev;
+  if (r.call != kNever && !first_key_rec && r.call <= p) r.bad = 1;
+  const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)r.call, kWave - 1);
+  if (l != kNever) last_call = l;
 }
 
 template <class Store>
-__device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
+__device__ void check_key(const lc_op *__restrict__ kops, const int n,
                           const KParams &p, Store &st, KeyOut &o,
                           const int lane) {
   o.verdict = LC_VALID;
@@ -393,89 +465,89 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
   uint64_t fsv = pack_sv(p.init_ver, p.init_val);
   int rF = 0, rR = 1, rW = 2, nF = 1;
 
-  Slot sl{0, -1, -1, -1, -1, -1, 0, kNever};
-  uint64_t occ = 0;      // occupied window slots (uniform)
-  uint64_t crashed = 0;  // slots holding crashed writes/CAS (uniform)
+  Slot sl{0, 0, 0, 0, -1, 0, -1, -1, -1, kNever, 0ull};
+  Masks mk{0, 0, 0, 0};
 
-  const int64_t base_idx = kops[0].call;
-  Rec cur = load_rec(kops, lane, n, base_idx);
-  Rec nxt = load_rec(kops, kWave + lane, n, base_idx);
-  int64_t base = 0, i = 0;
-  uint32_t prev_call = 0;
+  const int64_t base_idx = kops[0].call;  // scalar load (key is wave-uniform)
+  uint32_t last_call = kNever;
+  Rec cur = decode(load_raw(kops, lane, n), base_idx);
+  check_order(cur, last_call, lane);
+  ChunkMasks cmk = chunk_masks(cur, fsv);
+  Raw nxt = load_raw(kops, kWave + lane, n);
+  int base = 0, i = 0;
 
   for (;;) {
-    const uint32_t ncall = (i < n) ? (uint32_t)rl32((int)cur.call, (int)(i - base)) : kNever;
+    const uint32_t ncall = (i < n) ? (uint32_t)rl32((int)cur.call, i - base) : kNever;
     // Returns due before the next call: one ballot; the DPP min only when
     // several are due at once.
     const uint64_t due = __ballot(sl.ret < ncall);
     if (due == 0) {
       if (i >= n) break;  // no calls left, no pending returns
       // ------------------------------------------------------- call of op i
-      const int li = (int)(i - base);
-      const int f = rl32(cur.f, li), val = rl32(cur.val, li);
-      const int ex = rl32(cur.exp, li), ver = rl32(cur.ver, li);
-      const int bad = rl32(cur.bad, li);
-      const uint32_t ret = (uint32_t)rl32((int)cur.ret, li);
-      if (bad || (i > 0 && ncall <= prev_call)) {
+      const int li = i - base;
+      const uint64_t bit = 1ull << li;
+      if (cmk.special & bit) {
         o.verdict = LC_UNKNOWN;
-        o.reason = LC_REASON_MALFORMED;
+        // register.clj:63: condp without a default clause throws
+        o.reason = rl32(cur.bad, li) ? LC_REASON_MALFORMED : LC_REASON_UNKNOWN_F;
         return;
       }
-      if (f > LC_F_CAS) {  // register.clj:63: condp without default throws
-        o.verdict = LC_UNKNOWN;
-        o.reason = LC_REASON_UNKNOWN_F;
-        return;
-      }
-      prev_call = ncall;
-      // Reads that never constrain (crashed, or [nil nil]) and, with a lone
-      // configuration, reads legal right now (eager closure + retirement)
-      // need no slot at all.
-      bool done = (f == LC_F_READ) && (ret == kNever || (ver == -1 && val == -1));
-      if (!done && single && f == LC_F_READ)
-        done = legal(LC_F_READ, ver, val, ex, sv_ver(fsv), sv_val(fsv));
+      // Reads that never constrain, and (lone configuration) reads legal
+      // right now — eager closure + retirement — take no slot at all.
+      const bool done = (cmk.isread & bit) &&
+                        ((cmk.skip & bit) || (single && (cmk.legal_now & bit)));
       if (!done) {
-        if (occ == ~0ull) {
+        if (mk.occ == ~0ull) {
           o.verdict = LC_UNKNOWN;
           o.reason = LC_REASON_WINDOW_OVERFLOW;
           return;
         }
-        const int s = __builtin_ctzll(~occ);
-        int pred = -1;
-        const bool crash = ret == kNever;  // (crashed reads never get here)
-        if (crash) {
-          const uint64_t m = __ballot(((crashed >> lane) & 1) && sl.latest &&
-                                      sl.f == f && sl.val == val && sl.exp == ex &&
-                                      sl.ver == ver);
-          if (m) {
-            pred = __builtin_ctzll(m);
-            if (lane == pred) sl.latest = 0;
-          }
-          crashed |= 1ull << s;
+        const int s = __builtin_ctzll(~mk.occ);
+        const uint64_t bs = 1ull << s;
+        const int f = rl32(cur.f, li), val = rl32(cur.val, li);
+        const int ex = rl32(cur.exp, li), ver = rl32(cur.ver, li);
+        const int nv = rl32(cur.nv, li), nvm = rl32(cur.nvm, li);
+        const int nl = rl32(cur.nl, li), nlm = rl32(cur.nlm, li);
+        const uint32_t ret = (uint32_t)rl32((int)cur.ret, li);
+        uint64_t pbit = 0;
+        if (ret == kNever) {  // crashed write/CAS (crashed reads were skipped)
+          pbit = __ballot(sl.f == f && sl.val == val && sl.exp == ex && sl.ver == ver) &
+                 mk.crashed & mk.latest;
+          mk.latest = (mk.latest & ~pbit) | bs;
+          mk.crashed |= bs;
         }
         if (lane == s) {
-          sl.f = f;
+          sl.nv = nv;
+          sl.nvm = nvm;
+          sl.nl = nl;
+          sl.nlm = nlm;
           sl.val = val;
+          sl.f = f;
           sl.exp = ex;
           sl.ver = ver;
+          sl.idx = i;
           sl.ret = ret;
-          sl.idx = (int)i;
-          sl.pred = pred;
-          sl.latest = crash ? 1 : 0;
+          sl.pbit = pbit;
         }
-        occ |= 1ull << s;
-        if (f == LC_F_READ && !single) {  // eager read closure at the call
-          for (int j = lane; j < nF; j += kWave) {
-            const Cfg c = st.get(rF, j);
-            if (legal(LC_F_READ, ver, val, ex, sv_ver(c.sv), sv_val(c.sv)))
-              st.set_mask_lane(rF, j, c.mask | (1ull << s));
+        mk.occ |= bs;
+        if (f == LC_F_READ) {
+          mk.rdm |= bs;
+          if (!single) {  // eager read closure at the call, per configuration
+            for (int j = lane; j < nF; j += kWave) {
+              const Cfg c = st.get(rF, j);
+              if (pre_ok(nv, nvm, nl, nlm, sv_ver(c.sv), sv_val(c.sv)))
+                st.set_mask_lane(rF, j, c.mask | bs);
+            }
           }
         }
       }
       i++;
       if (i - base == kWave) {
         base += kWave;
-        cur = nxt;
-        nxt = load_rec(kops, base + kWave + lane, n, base_idx);
+        cur = decode(nxt, base_idx);
+        check_order(cur, last_call, lane);
+        cmk = chunk_masks(cur, fsv);
+        nxt = load_raw(kops, base + kWave + lane, n);
       }
       continue;
     }
@@ -503,7 +575,7 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
       bool branch = false;
       for (;;) {
         const int cver = sv_ver(csv), cval = sv_val(csv);
-        const uint64_t cand = mutation_candidates(sl, occ, cm, cver, cval, lane);
+        const uint64_t cand = mutation_candidates(sl, mk, cm, cver, cval);
         if (cand == 0) {
           empty = true;
           break;
@@ -516,7 +588,7 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
         const int nver = cver + 1;
         const int nval = rl32(sl.val, t);
         uint64_t nm = cm | (1ull << t);
-        nm |= read_closure(sl, occ, nm, nver, nval, lane);
+        nm |= read_closure(sl, mk, nm, nver, nval);
         o.explored++;
         if (o.explored > p.budget) {
           o.verdict = LC_UNKNOWN;
@@ -539,11 +611,13 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
         if (lane == 0) st.reg(rF)[0] = Cfg{0ull, fsv};
       } else if (!empty) {
         fsv = csv;
-        retire(sl, occ, crashed, cm, lane);  // x included
+        retire(sl, mk, cm, lane);  // x included
+        cmk.legal_now = cmk.isread &
+                        __ballot(pre_ok(cur.nv, cur.nvm, cur.nl, cur.nlm, sv_ver(fsv), sv_val(fsv)));
       }
     }
     if (!single) {
-      const int r = general_return(st, sl, occ, s, rF, rR, rW, nF, p, o, lane);
+      const int r = general_return(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
       if (r < 0) {
         o.verdict = LC_UNKNOWN;
         o.reason = r == -1 ? LC_REASON_FRONTIER_LDS : LC_REASON_CONFIG_BUDGET;
@@ -556,18 +630,20 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int64_t n,
       if (nF > o.max_frontier) o.max_frontier = nF;
       empty = nF == 0;
       if (!empty) {
-        retire(sl, occ, crashed, bs, lane);  // x returned
+        retire(sl, mk, bs, lane);  // x returned
         uint64_t acc = ~0ull;
         for (int j = lane; j < nF; j += kWave) acc &= st.get(rF, j).mask;
-        const uint64_t rb = occ & wave_and_u64(acc);
+        const uint64_t rb = mk.occ & wave_and_u64(acc);
         if (rb) {
-          retire(sl, occ, crashed, rb, lane);
+          retire(sl, mk, rb, lane);
           for (int j = lane; j < nF; j += kWave)
             st.set_mask_lane(rF, j, st.get(rF, j).mask & ~rb);
         }
         if (nF == 1) {  // back to the register-resident frontier (mask now empty)
           fsv = rfl64(st.get(rF, 0).sv);
           single = true;
+          cmk.legal_now = cmk.isread &
+                          __ballot(pre_ok(cur.nv, cur.nvm, cur.nl, cur.nlm, sv_ver(fsv), sv_val(fsv)));
         }
       }
     }
@@ -597,16 +673,18 @@ __global__ __launch_bounds__(kWave *kWavesPerWG) void lds_tier_kernel(
     KStatus *__restrict__ status) {
   __shared__ Cfg lds[kWavesPerWG][3][kLdsCap];
   const int lane = threadIdx.x & (kWave - 1);
-  const int wid = threadIdx.x / kWave;
+  // wave-uniform by construction; readfirstlane lets the compiler use scalar
+  // loads for key_off and keeps vector-memory waits off the event loop
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t key = (int64_t)blockIdx.x * kWavesPerWG + wid;
   if (key >= n_keys) return;
   const int64_t beg = key_off[key], end = key_off[key + 1];
   KeyOut o;
-  if (end < beg) {
+  if (end < beg || end - beg > 0x7FFFFFFF) {
     o = KeyOut{LC_UNKNOWN, LC_REASON_MALFORMED, -1, -1, 0, 0};
   } else {
     LdsStore st{&lds[wid][0][0]};
-    check_key(ops + (beg - key_base), end - beg, p, st, o, lane);
+    check_key(ops + (beg - key_base), (int)(end - beg), p, st, o, lane);
   }
   if (lane == 0) {
     write_result(&out[key], o);
@@ -644,7 +722,7 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
     const int64_t key = keys[li];
     const int64_t beg = key_off[key], end = key_off[key + 1];
     KeyOut o;
-    check_key(ops + (beg - key_base), end - beg, p, st, o, lane);
+    check_key(ops + (beg - key_base), (int)(end - beg), p, st, o, lane);
     if (o.reason == LC_REASON_FRONTIER_LDS) {
       if (last_tier) {
         o.reason = LC_REASON_CONFIG_BUDGET;  // largest sets full: give up
