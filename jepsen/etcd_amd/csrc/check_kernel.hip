@@ -32,6 +32,8 @@
 // leaves every other step unchanged.  So the frontier is empty at exactly the
 // same returns as knossos's, verdicts and counterexample prefixes are
 // unchanged, and the 2^k subsets of concurrent reads never materialise.
+#include <climits>
+
 #include "kernels.h"
 
 namespace lcdev {
@@ -668,16 +670,17 @@ __device__ __forceinline__ void write_result(lc_key_result *r, const KeyOut &o) 
 
 __global__ __launch_bounds__(kWave *kWavesPerWG) void lds_tier_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
-    const int64_t key_base, const int64_t n_keys, const KParams p,
-    lc_key_result *__restrict__ out, int32_t *__restrict__ ovf_keys,
+    const int64_t key_base, const int32_t *__restrict__ keys, const int64_t n_keys,
+    const KParams p, lc_key_result *__restrict__ out, int32_t *__restrict__ ovf_keys,
     KStatus *__restrict__ status) {
   __shared__ Cfg lds[kWavesPerWG][3][kLdsCap];
   const int lane = threadIdx.x & (kWave - 1);
   // wave-uniform by construction; readfirstlane lets the compiler use scalar
   // loads for key_off and keeps vector-memory waits off the event loop
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int64_t key = (int64_t)blockIdx.x * kWavesPerWG + wid;
-  if (key >= n_keys) return;
+  const int64_t item = (int64_t)blockIdx.x * kWavesPerWG + wid;
+  if (item >= n_keys) return;
+  const int64_t key = keys ? keys[item] : item;
   const int64_t beg = key_off[key], end = key_off[key + 1];
   KeyOut o;
   if (end < beg || end - beg > 0x7FFFFFFF) {
@@ -693,6 +696,187 @@ __global__ __launch_bounds__(kWave *kWavesPerWG) void lds_tier_kernel(
       const int pos = atomicAdd(&status->n_overflow, 1);
       ovf_keys[pos] = (int32_t)key;
     }
+  }
+}
+
+// ==================================================================
+// Version-order fast tier (every key first).
+//
+// For a key whose :ok writes/CAS all carry a version and which has no crashed
+// writes/CAS, the model pins the mutation order: the op with version v is the
+// (v - init_version)-th mutation (register.clj:64-75).  Linearizability then
+// reduces to (SURVEY.md §7 "version pinning"; exact, checked against the
+// oracle's searches in tests/):
+//   * versions init+1 .. init+M each held by exactly one mutation;
+//   * each CAS's expected value equals the value before it (register.clj:77);
+//   * each read [v x] sees version v and, when x is non-nil, the value at v;
+//   * increasing linearization points t_1 < ... < t_M exist with
+//       L_k < t_k < U_k,  L_k = max(call(m_k), calls of reads of version k-1),
+//                         U_k = min(ret(m_k),  rets of reads of version k),
+//     i.e. max(L_1..L_k) < U_k for every k (a prefix-max scan).
+// Reads place themselves between t_v and t_{v+1}; crashed or [nil nil] reads
+// never constrain.  One 256-thread workgroup decides one key from LDS tables
+// filled by LDS atomics; keys it cannot decide (crashed mutations, nil
+// versions, a read [nil x], more than kFastMax records, malformed records) or
+// finds invalid are handed to the JIT search, which also names the canonical
+// counterexample.
+constexpr int kFastThreads = 256;
+constexpr int kFastMax = 1024;
+constexpr int kNone = INT_MIN;  // "no CAS expectation" / "no value claimed"
+
+__device__ __forceinline__ uint32_t block_max_scan_excl(uint32_t v, uint32_t *wtot) {
+  // exclusive max-scan of v over the workgroup (0 identity)
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  uint32_t incl = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+    if (lane >= o) incl = incl > y ? incl : y;
+  }
+  if (lane == kWave - 1) wtot[w] = incl;
+  __syncthreads();
+  uint32_t pre = 0;
+  for (int j = 0; j < w; j++) pre = pre > wtot[j] ? pre : wtot[j];
+  uint32_t excl = (uint32_t)__shfl_up((int)incl, 1);
+  if (lane == 0) excl = 0;
+  return pre > excl ? pre : excl;
+}
+
+__global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
+    const int64_t key_base, const KParams p, lc_key_result *__restrict__ out,
+    int32_t *__restrict__ jit_keys, KStatus *__restrict__ status) {
+  __shared__ uint32_t Lm[kFastMax], Um[kFastMax];
+  __shared__ int Val[kFastMax], Exp[kFastMax];
+  __shared__ uint32_t RL[kFastMax + 1], RU[kFastMax + 1];
+  __shared__ int Claim[kFastMax + 1];
+  __shared__ uint32_t wtot[kFastThreads / kWave];
+  __shared__ int s_inel, s_bad, s_maxpos, s_nmut;
+  const int tid = threadIdx.x;
+  const int64_t key = blockIdx.x;
+  const int64_t beg = key_off[key], end = key_off[key + 1];
+  const int64_t n64 = end - beg;
+  if (n64 <= 0 || n64 > kFastMax) {
+    if (tid == 0) {
+      if (n64 == 0) {
+        out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 0};
+      } else {
+        jit_keys[atomicAdd(&status->n_jit, 1)] = (int32_t)key;
+      }
+    }
+    return;
+  }
+  const int n = (int)n64;
+  const lc_op *kops = ops + (beg - key_base);
+  for (int k = tid; k <= n; k += kFastThreads) {
+    if (k < n) {
+      Lm[k] = kNever;
+      Exp[k] = kNone;
+    }
+    RL[k] = 0;  // call + 1; 0 = no read constrains t_{k+1}
+    RU[k] = kNever;
+    Claim[k] = kNone;
+  }
+  if (tid == 0) {
+    s_inel = 0;
+    s_bad = 0;
+    s_maxpos = -1;
+    s_nmut = 0;
+  }
+  __syncthreads();
+  const int64_t base_idx = kops[0].call;
+  const int V0 = p.init_ver;
+  int inel = 0, bad = 0;
+  for (int r = tid; r < n; r += kFastThreads) {
+    Raw w;
+    const longlong2 *q = reinterpret_cast<const longlong2 *>(kops + r);
+    w.a = q[0];
+    w.b = q[1];
+    w.c = q[2];
+    const Rec d = decode(w, base_idx);
+    const bool unsorted = r > 0 && kops[r - 1].call >= w.c.x;
+    if (d.bad || d.f > LC_F_CAS || unsorted) {
+      inel = 1;  // the JIT tier reports malformed / unknown :f
+      continue;
+    }
+    if (d.f == LC_F_READ) {
+      if (d.ret == kNever || (d.ver == -1 && d.val == -1)) continue;  // never constrains
+      if (d.ver == -1) {
+        inel = 1;  // read [nil x]: its version is free
+        continue;
+      }
+      const int k = d.ver - V0;
+      if (k < 0 || k > n) {
+        bad = 1;
+        continue;
+      }
+      atomicMax(&RL[k], d.call + 1);
+      atomicMin(&RU[k], d.ret);
+      if (d.val != -1) {
+        const int prev = atomicCAS(&Claim[k], kNone, d.val);
+        if (prev != kNone && prev != d.val) bad = 1;
+      }
+    } else {
+      if (d.ret == kNever || d.ver == -1) {
+        inel = 1;  // crashed, or no version: order not pinned
+        continue;
+      }
+      const int pos = d.ver - V0 - 1;
+      if (pos < 0 || pos >= n) {
+        bad = 1;
+        continue;
+      }
+      if (atomicCAS(&Lm[pos], kNever, d.call) != kNever) {
+        bad = 1;  // two mutations claim one version
+        continue;
+      }
+      Um[pos] = d.ret;
+      Val[pos] = d.val;
+      Exp[pos] = d.f == LC_F_CAS ? d.exp : kNone;
+      atomicMax(&s_maxpos, pos);
+      atomicAdd(&s_nmut, 1);
+    }
+  }
+  if (inel) atomicOr(&s_inel, 1);
+  if (bad) atomicOr(&s_bad, 1);
+  __syncthreads();
+  const int M = s_maxpos + 1;
+  bool decided = !s_inel && !s_bad && s_nmut == M;
+  if (decided) {
+    // feasibility: prefix max of L below U; CAS expectations
+    const int per = (M + kFastThreads - 1) / kFastThreads;
+    const int k0 = tid * per, k1 = min(k0 + per, M);
+    uint32_t loc = 0;
+    for (int k = k0; k < k1; k++) {
+      const uint32_t L = max(Lm[k] + 1, RL[k]);  // +1: compare in call+1 units
+      loc = max(loc, L);
+    }
+    uint32_t pm = block_max_scan_excl(loc, wtot);
+    for (int k = k0; k < k1; k++) {
+      pm = max(pm, max(Lm[k] + 1, RL[k]));
+      const uint32_t U = min(Um[k], RU[k + 1]);
+      if (pm - 1 >= U) bad = 1;  // need max call < U
+      const int before = k == 0 ? p.init_val : Val[k - 1];
+      if (Exp[k] != kNone && Exp[k] != before) bad = 1;
+    }
+    // reads: claimed values, and no read beyond the last version
+    for (int k = tid; k <= n; k += kFastThreads) {
+      if (k > M) {
+        if (RL[k] != 0 || RU[k] != kNever) bad = 1;
+      } else if (Claim[k] != kNone) {
+        const int actual = k == 0 ? p.init_val : Val[k - 1];
+        if (Claim[k] != actual) bad = 1;
+      }
+    }
+    if (bad) atomicOr(&s_bad, 1);
+    __syncthreads();
+    decided = !s_bad;
+  }
+  if (tid == 0) {
+    if (decided)
+      out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
+    else
+      jit_keys[atomicAdd(&status->n_jit, 1)] = (int32_t)key;
   }
 }
 
@@ -736,15 +920,25 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
 
 }  // namespace
 
+hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
+                            int64_t key_base, int64_t n_keys, const KParams &p,
+                            lc_key_result *d_out, int32_t *d_jit_keys,
+                            KStatus *d_status, hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fast_tier_kernel, dim3((unsigned)n_keys), dim3(kFastThreads), 0,
+                     stream, d_ops, d_key_off, key_base, p, d_out, d_jit_keys, d_status);
+  return hipGetLastError();
+}
+
 hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
-                           int64_t key_base, int64_t n_keys, const KParams &p,
-                           lc_key_result *d_out, int32_t *d_ovf_keys,
+                           int64_t key_base, const int32_t *d_keys, int64_t n_keys,
+                           const KParams &p, lc_key_result *d_out, int32_t *d_ovf_keys,
                            KStatus *d_status, hipStream_t stream) {
   if (n_keys <= 0) return hipSuccess;
   const int64_t blocks = (n_keys + kWavesPerWG - 1) / kWavesPerWG;
   hipLaunchKernelGGL(lds_tier_kernel, dim3((unsigned)blocks),
                      dim3(kWave * kWavesPerWG), 0, stream, d_ops, d_key_off,
-                     key_base, n_keys, p, d_out, d_ovf_keys, d_status);
+                     key_base, d_keys, n_keys, p, d_out, d_ovf_keys, d_status);
   return hipGetLastError();
 }
 

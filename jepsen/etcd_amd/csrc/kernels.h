@@ -21,20 +21,30 @@ struct KStatus {
   int32_t malformed;    // keys with LC_REASON_MALFORMED
   int32_t n_overflow;   // keys appended to the overflow list (LDS tier full)
   int32_t n_overflow2;  // keys that also overflowed the first HBM tier
-  int32_t pad;
+  int32_t n_jit;        // keys handed from the fast tier to the JIT search
 };
 
 constexpr int kWave = 64;
 constexpr int kWavesPerWG = 4;   // independent keys per 256-thread workgroup
 constexpr int kLdsCap = 128;     // configurations per LDS region (3 regions/wave)
 
-// LDS tier: one wavefront per key.  key_off is indexed by local key id; the
-// record pointer is rebased by key_base (= key_off[0] of the slice).
+// Fast tier: one 256-thread workgroup per key decides version-pinned keys
+// (check_kernel.hip, "Version-order fast tier"); the others are appended to
+// d_jit_keys (count in status->n_jit) for the JIT search.
+hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
+                            int64_t key_base, int64_t n_keys, const KParams &p,
+                            lc_key_result *d_out, int32_t *d_jit_keys,
+                            KStatus *d_status, hipStream_t stream);
+
+// LDS tier (JIT search): one wavefront per key, for the keys in d_keys
+// (n_keys of them), or for keys 0..n_keys-1 when d_keys is null.  key_off is
+// indexed by local key id; the record pointer is rebased by key_base
+// (= key_off[0] of the slice).
 // Keys whose frontier outgrows the LDS regions are appended to ovf_keys
 // (count in status->n_overflow) with reason LC_REASON_FRONTIER_LDS.
 hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
-                           int64_t key_base, int64_t n_keys, const KParams &p,
-                           lc_key_result *d_out, int32_t *d_ovf_keys,
+                           int64_t key_base, const int32_t *d_keys, int64_t n_keys,
+                           const KParams &p, lc_key_result *d_out, int32_t *d_ovf_keys,
                            KStatus *d_status, hipStream_t stream);
 
 // HBM tier: re-runs the listed keys with configuration sets in global memory

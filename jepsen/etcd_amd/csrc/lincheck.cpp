@@ -47,6 +47,11 @@ struct Dev {
   size_t ovf_cap = 0;
   int32_t *d_ovf2 = nullptr;
   size_t ovf2_cap = 0;
+  int32_t *d_jit = nullptr;
+  size_t jit_cap = 0;
+  hipEvent_t ef = nullptr;
+  double fast_ms = 0, jit_ms = 0;
+  int64_t n_jit = 0;
   lcdev::KStatus *d_status = nullptr;
   lcdev::KStatus *h_status = nullptr;  // pinned
   void *d_ws = nullptr;
@@ -116,8 +121,8 @@ int opts_to_params(lc_ctx *c, const lc_opts *o, lcdev::KParams *p) {
 int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                int64_t key_base, int64_t n_keys, const lcdev::KParams &p,
                lc_key_result *d_out, hipStream_t st, int64_t flags) {
-  d.kernel_ms = d.hbm_ms = 0;
-  d.n_hbm = 0;
+  d.kernel_ms = d.hbm_ms = d.fast_ms = d.jit_ms = 0;
+  d.n_hbm = d.n_jit = 0;
   d.malformed = 0;
   if (n_keys <= 0) return 0;
   if (n_keys > INT32_MAX) {
@@ -126,16 +131,38 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   }
   int rc = ensure(c, &d.d_ovf, &d.ovf_cap, sizeof(int32_t) * (size_t)n_keys);
   if (!rc) rc = ensure(c, &d.d_ovf2, &d.ovf2_cap, sizeof(int32_t) * (size_t)n_keys);
+  if (!rc) rc = ensure(c, &d.d_jit, &d.jit_cap, sizeof(int32_t) * (size_t)n_keys);
   if (rc) return rc;
   HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
+  float ms = 0;
+  int64_t n_jit = n_keys;
+  const int32_t *jit_list = nullptr;
   HIP_TRY(c, hipEventRecord(d.e0, st));
-  HIP_TRY(c, lcdev::launch_lds_tier(d_ops, d_off, key_base, n_keys, p, d_out,
+  if (!(flags & LC_FLAG_NO_FAST_PATH)) {
+    // tier 0: version-order decision for every key; the rest go to the JIT
+    HIP_TRY(c, lcdev::launch_fast_tier(d_ops, d_off, key_base, n_keys, p, d_out,
+                                       d.d_jit, d.d_status, st));
+    HIP_TRY(c, hipEventRecord(d.ef, st));
+    HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
+                              hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.ef));
+    d.fast_ms = ms;
+    n_jit = d.h_status->n_jit;
+    jit_list = d.d_jit;
+  } else {
+    HIP_TRY(c, hipEventRecord(d.ef, st));
+  }
+  d.n_jit = n_jit;
+  // tier 1: JIT search with the frontier in SGPRs / LDS
+  HIP_TRY(c, lcdev::launch_lds_tier(d_ops, d_off, key_base, jit_list, n_jit, p, d_out,
                                     d.d_ovf, d.d_status, st));
   HIP_TRY(c, hipEventRecord(d.e1, st));
   HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                             hipMemcpyDeviceToHost, st));
   HIP_TRY(c, hipStreamSynchronize(st));
-  float ms = 0;
+  HIP_TRY(c, hipEventElapsedTime(&ms, d.ef, d.e1));
+  d.jit_ms = ms;
   HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.e1));
   d.kernel_ms = ms;
   d.malformed = d.h_status->malformed;
@@ -197,7 +224,7 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
     if (hipSetDevice(i) != hipSuccess ||
         hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&d.e0) != hipSuccess || hipEventCreate(&d.e1) != hipSuccess ||
-        hipEventCreate(&d.e2) != hipSuccess ||
+        hipEventCreate(&d.e2) != hipSuccess || hipEventCreate(&d.ef) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&d.d_status), sizeof(lcdev::KStatus)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess) {
       lc_close(c);
@@ -229,6 +256,8 @@ void lc_close(lc_ctx *c) {
     if (d.e0) (void)hipEventDestroy(d.e0);
     if (d.e1) (void)hipEventDestroy(d.e1);
     if (d.e2) (void)hipEventDestroy(d.e2);
+    if (d.ef) (void)hipEventDestroy(d.ef);
+    if (d.d_jit) (void)hipFree(d.d_jit);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
   delete c;
@@ -345,6 +374,9 @@ int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
   for (int di = 0; di < nd; di++) {
     if (rcs[di] && !rc) rc = rcs[di];
     c->stats.kernel_ms += c->devs[di].kernel_ms;
+    c->stats.fast_kernel_ms += c->devs[di].fast_ms;
+    c->stats.jit_kernel_ms += c->devs[di].jit_ms;
+    c->stats.n_jit_keys += c->devs[di].n_jit;
     c->stats.hbm_kernel_ms += c->devs[di].hbm_ms;
     c->stats.n_hbm_keys += c->devs[di].n_hbm;
     malformed += c->devs[di].malformed;
@@ -395,6 +427,9 @@ int lc_check_device(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
   rc = run_device(c, d, d_ops, d_key_off, base, n_keys, p, d_out, st,
                   opts ? opts->flags : 0);
   c->stats.kernel_ms = d.kernel_ms;
+  c->stats.fast_kernel_ms = d.fast_ms;
+  c->stats.jit_kernel_ms = d.jit_ms;
+  c->stats.n_jit_keys = d.n_jit;
   c->stats.hbm_kernel_ms = d.hbm_ms;
   c->stats.n_hbm_keys = d.n_hbm;
   c->stats.n_keys = n_keys;

@@ -32,6 +32,20 @@ def test_golden_fixtures(ctx, name):
     assert (r["fail_op"] == z["fail_op"]).all()
 
 
+@pytest.mark.parametrize("name", ["c1", "c5", "info", "tiny"])
+def test_fast_tier_and_search_agree(ctx, name):
+    """Version-order tier + JIT vs the JIT search alone: identical verdicts and
+    fail ops (the fast tier hands invalid keys to the JIT for the fail op)."""
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    _, a = ctx.check(z["ops"], z["key_off"])
+    fast_decided = len(a) - ctx.stats()["n_jit_keys"]
+    _, b = ctx.check(z["ops"], z["key_off"], abi.default_opts(flags=abi.LC_FLAG_NO_FAST_PATH))
+    assert ctx.stats()["n_jit_keys"] == len(b)
+    assert (a["verdict"] == b["verdict"]).all() and (a["fail_op"] == b["fail_op"]).all()
+    if name in ("c1", "c5"):
+        assert fast_decided >= 0.85 * len(a)
+
+
 def test_tiny_random_vs_oracle(ctx):
     ops, off = pack_keys(tiny_batch(777, 20000, max_ops=8))
     _, g = ctx.check(ops, off)

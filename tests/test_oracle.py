@@ -128,3 +128,28 @@ def test_budget_gives_unknown():
     ops, off = pack_keys([recs])
     _, r = oracle.check(ops, off, algo=oracle.JIT, max_configs=1000)
     assert r["verdict"][0] == -1 and r["reason"][0] == 2
+
+
+def test_version_order_decision_matches_search():
+    """The GPU fast tier's decision procedure (restated in fastpath_ref.py)
+    agrees with the searches on every key it decides."""
+    import fastpath_ref
+    keys = tiny_batch(4242, 3000, max_ops=8)
+    sets = [keys]
+    for (nk, n, conc, pi, pa, seed) in [(200, 200, 10, 0, 0.5, 1), (100, 300, 20, 0.02, 0.5, 2)]:
+        ops, off, _, _ = abi.synth(nk, n, concurrency=conc, p_info=pi, p_anomaly=pa, seed=seed)
+        sets.append([ops[off[k]:off[k + 1]].tolist() for k in range(nk)])
+    decided = 0
+    for ks in sets:
+        ops, off = pack_keys(ks)
+        _, j = oracle.check(ops, off, algo=oracle.JITC, n_threads=4)
+        for i, recs in enumerate(ks):
+            d = fastpath_ref.decide([tuple(r) for r in recs])
+            if d is None:
+                continue
+            decided += 1
+            assert d == j["verdict"][i], recs
+    assert decided > 2000
+    for k in KATS:
+        d = fastpath_ref.decide([tuple(r) for r in k["ops"]])
+        assert d is None or d == (1 if k["valid"] else 0), k["name"]
