@@ -670,9 +670,10 @@ __device__ __forceinline__ void write_result(lc_key_result *r, const KeyOut &o) 
 
 __global__ __launch_bounds__(kWave *kWavesPerWG) void lds_tier_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
-    const int64_t key_base, const int32_t *__restrict__ keys, const int64_t n_keys,
-    const KParams p, lc_key_result *__restrict__ out, int32_t *__restrict__ ovf_keys,
+    const int32_t *__restrict__ keys, const int64_t n_keys, const KParams p,
+    lc_key_result *__restrict__ out, int32_t *__restrict__ ovf_keys,
     KStatus *__restrict__ status) {
+  const int64_t key_base = key_off[0];  // ops points at key_off[0]'s record
   __shared__ Cfg lds[kWavesPerWG][3][kLdsCap];
   const int lane = threadIdx.x & (kWave - 1);
   // wave-uniform by construction; readfirstlane lets the compiler use scalar
@@ -744,7 +745,7 @@ __device__ __forceinline__ uint32_t block_max_scan_excl(uint32_t v, uint32_t *wt
 
 __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
-    const int64_t key_base, const KParams p, lc_key_result *__restrict__ out,
+    const KParams p, lc_key_result *__restrict__ out,
     int32_t *__restrict__ jit_keys, KStatus *__restrict__ status) {
   __shared__ uint32_t Lm[kFastMax], Um[kFastMax];
   __shared__ int Val[kFastMax], Exp[kFastMax];
@@ -767,7 +768,7 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
     return;
   }
   const int n = (int)n64;
-  const lc_op *kops = ops + (beg - key_base);
+  const lc_op *kops = ops + (beg - key_off[0]);
   for (int k = tid; k <= n; k += kFastThreads) {
     if (k < n) {
       Lm[k] = kNever;
@@ -888,7 +889,7 @@ __host__ __device__ inline size_t hbm_wave_bytes(int64_t cap) {
 
 __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
-    const int64_t key_base, const int32_t *__restrict__ keys, const int32_t n_list,
+    const int32_t *__restrict__ keys, const int32_t n_list,
     const KParams p, lc_key_result *__restrict__ out, char *__restrict__ ws,
     const int64_t cap, int32_t *__restrict__ ovf_out, int32_t *__restrict__ n_ovf_out,
     const int last_tier) {
@@ -902,6 +903,7 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
   st.tmask = (uint32_t)(2 * cap - 1);
   // Tags are zeroed by the host before the launch; epochs start at 1.
   st.epoch = 0;
+  const int64_t key_base = key_off[0];
   for (int li = blockIdx.x; li < n_list; li += gridDim.x) {
     const int64_t key = keys[li];
     const int64_t beg = key_off[key], end = key_off[key + 1];
@@ -921,24 +923,24 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
 }  // namespace
 
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
-                            int64_t key_base, int64_t n_keys, const KParams &p,
+                            int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_jit_keys,
                             KStatus *d_status, hipStream_t stream) {
   if (n_keys <= 0) return hipSuccess;
   hipLaunchKernelGGL(fast_tier_kernel, dim3((unsigned)n_keys), dim3(kFastThreads), 0,
-                     stream, d_ops, d_key_off, key_base, p, d_out, d_jit_keys, d_status);
+                     stream, d_ops, d_key_off, p, d_out, d_jit_keys, d_status);
   return hipGetLastError();
 }
 
 hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
-                           int64_t key_base, const int32_t *d_keys, int64_t n_keys,
+                           const int32_t *d_keys, int64_t n_keys,
                            const KParams &p, lc_key_result *d_out, int32_t *d_ovf_keys,
                            KStatus *d_status, hipStream_t stream) {
   if (n_keys <= 0) return hipSuccess;
   const int64_t blocks = (n_keys + kWavesPerWG - 1) / kWavesPerWG;
   hipLaunchKernelGGL(lds_tier_kernel, dim3((unsigned)blocks),
                      dim3(kWave * kWavesPerWG), 0, stream, d_ops, d_key_off,
-                     key_base, d_keys, n_keys, p, d_out, d_ovf_keys, d_status);
+                     d_keys, n_keys, p, d_out, d_ovf_keys, d_status);
   return hipGetLastError();
 }
 
@@ -947,14 +949,14 @@ size_t hbm_tier_ws_bytes(int n_waves, int64_t cap) {
 }
 
 hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
-                           int64_t key_base, const int32_t *d_keys,
+                           const int32_t *d_keys,
                            int32_t n_list, const KParams &p, lc_key_result *d_out,
                            void *d_ws, int n_waves, int64_t cap,
                            int32_t *d_ovf_out, int32_t *d_n_ovf_out, int last_tier,
                            hipStream_t stream) {
   if (n_list <= 0) return hipSuccess;
   hipLaunchKernelGGL(hbm_tier_kernel, dim3((unsigned)n_waves), dim3(kWave), 0,
-                     stream, d_ops, d_key_off, key_base, d_keys, n_list, p,
+                     stream, d_ops, d_key_off, d_keys, n_list, p,
                      d_out, static_cast<char *>(d_ws), cap, d_ovf_out, d_n_ovf_out,
                      last_tier);
   return hipGetLastError();

@@ -32,18 +32,19 @@ constexpr int kLdsCap = 128;     // configurations per LDS region (3 regions/wav
 // (check_kernel.hip, "Version-order fast tier"); the others are appended to
 // d_jit_keys (count in status->n_jit) for the JIT search.
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
-                            int64_t key_base, int64_t n_keys, const KParams &p,
+                            int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_jit_keys,
                             KStatus *d_status, hipStream_t stream);
 
 // LDS tier (JIT search): one wavefront per key, for the keys in d_keys
-// (n_keys of them), or for keys 0..n_keys-1 when d_keys is null.  key_off is
-// indexed by local key id; the record pointer is rebased by key_base
-// (= key_off[0] of the slice).
+// (n_keys of them), or for keys 0..n_keys-1 when d_keys is null.  In every
+// tier key_off is indexed by local key id and d_ops points at the record of
+// index key_off[0] (a slice of a larger array may be passed); kernels read
+// key_off[0] themselves.
 // Keys whose frontier outgrows the LDS regions are appended to ovf_keys
 // (count in status->n_overflow) with reason LC_REASON_FRONTIER_LDS.
 hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
-                           int64_t key_base, const int32_t *d_keys, int64_t n_keys,
+                           const int32_t *d_keys, int64_t n_keys,
                            const KParams &p, lc_key_result *d_out, int32_t *d_ovf_keys,
                            KStatus *d_status, hipStream_t stream);
 
@@ -55,7 +56,7 @@ hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
 // LC_REASON_CONFIG_BUDGET (:unknown).
 size_t hbm_tier_ws_bytes(int n_waves, int64_t cap);
 hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
-                           int64_t key_base, const int32_t *d_keys,
+                           const int32_t *d_keys,
                            int32_t n_list, const KParams &p, lc_key_result *d_out,
                            void *d_ws, int n_waves, int64_t cap,
                            int32_t *d_ovf_out, int32_t *d_n_ovf_out, int last_tier,

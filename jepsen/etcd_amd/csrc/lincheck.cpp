@@ -119,7 +119,7 @@ int opts_to_params(lc_ctx *c, const lc_opts *o, lcdev::KParams *p) {
 
 // Run both tiers for n_keys keys whose device arrays are in place.
 int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
-               int64_t key_base, int64_t n_keys, const lcdev::KParams &p,
+               int64_t n_keys, const lcdev::KParams &p,
                lc_key_result *d_out, hipStream_t st, int64_t flags) {
   d.kernel_ms = d.hbm_ms = d.fast_ms = d.jit_ms = 0;
   d.n_hbm = d.n_jit = 0;
@@ -140,7 +140,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   HIP_TRY(c, hipEventRecord(d.e0, st));
   if (!(flags & LC_FLAG_NO_FAST_PATH)) {
     // tier 0: version-order decision for every key; the rest go to the JIT
-    HIP_TRY(c, lcdev::launch_fast_tier(d_ops, d_off, key_base, n_keys, p, d_out,
+    HIP_TRY(c, lcdev::launch_fast_tier(d_ops, d_off, n_keys, p, d_out,
                                        d.d_jit, d.d_status, st));
     HIP_TRY(c, hipEventRecord(d.ef, st));
     HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
@@ -154,17 +154,21 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     HIP_TRY(c, hipEventRecord(d.ef, st));
   }
   d.n_jit = n_jit;
-  // tier 1: JIT search with the frontier in SGPRs / LDS
-  HIP_TRY(c, lcdev::launch_lds_tier(d_ops, d_off, key_base, jit_list, n_jit, p, d_out,
-                                    d.d_ovf, d.d_status, st));
-  HIP_TRY(c, hipEventRecord(d.e1, st));
-  HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
-                            hipMemcpyDeviceToHost, st));
-  HIP_TRY(c, hipStreamSynchronize(st));
-  HIP_TRY(c, hipEventElapsedTime(&ms, d.ef, d.e1));
-  d.jit_ms = ms;
-  HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.e1));
-  d.kernel_ms = ms;
+  if (n_jit > 0) {
+    // tier 1: JIT search with the frontier in SGPRs / LDS
+    HIP_TRY(c, lcdev::launch_lds_tier(d_ops, d_off, jit_list, n_jit, p, d_out,
+                                      d.d_ovf, d.d_status, st));
+    HIP_TRY(c, hipEventRecord(d.e1, st));
+    HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
+                              hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    HIP_TRY(c, hipEventElapsedTime(&ms, d.ef, d.e1));
+    d.jit_ms = ms;
+    HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.e1));
+    d.kernel_ms = ms;
+  } else {
+    d.kernel_ms = d.fast_ms;
+  }
   d.malformed = d.h_status->malformed;
   const int32_t n_ovf = d.h_status->n_overflow;
   d.n_hbm = n_ovf;
@@ -179,7 +183,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       if (rc) return rc;
       HIP_TRY(c, hipMemsetAsync(d.d_ws, 0, ws, st));
       HIP_TRY(c, hipMemsetAsync(&d.d_status->n_overflow2, 0, sizeof(int32_t), st));
-      HIP_TRY(c, lcdev::launch_hbm_tier(d_ops, d_off, key_base, list, n_list, p,
+      HIP_TRY(c, lcdev::launch_hbm_tier(d_ops, d_off, list, n_list, p,
                                         d_out, d.d_ws, waves, kHbmCap[tier], next,
                                         &d.d_status->n_overflow2, tier == 1, st));
       HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
@@ -349,7 +353,7 @@ int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
       rcs[di] = -EIO;
       return;
     }
-    r = run_device(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, r0, nk, p,
+    r = run_device(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, nk, p,
                    d.d_out, d.stream, flags);
     if (r) {
       rcs[di] = r;
@@ -414,17 +418,9 @@ int lc_check_device(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
   Dev &d = c->devs[0];
   HIP_TRY(c, hipSetDevice(d.id));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d.stream;
-  // key_off[0] is the record base of ops; read it (8 bytes) so a caller may
-  // pass a key_off slice of a larger array.
-  int64_t base = 0, last = 0;
-  if (n_keys > 0) {
-    HIP_TRY(c, hipMemcpyAsync(&base, d_key_off, sizeof(int64_t),
-                              hipMemcpyDeviceToHost, st));
-    HIP_TRY(c, hipMemcpyAsync(&last, d_key_off + n_keys, sizeof(int64_t),
-                              hipMemcpyDeviceToHost, st));
-    HIP_TRY(c, hipStreamSynchronize(st));
-  }
-  rc = run_device(c, d, d_ops, d_key_off, base, n_keys, p, d_out, st,
+  // d_ops points at the record of index d_key_off[0]; the kernels read that
+  // base themselves, so a key_off slice of a larger array may be passed.
+  rc = run_device(c, d, d_ops, d_key_off, n_keys, p, d_out, st,
                   opts ? opts->flags : 0);
   c->stats.kernel_ms = d.kernel_ms;
   c->stats.fast_kernel_ms = d.fast_ms;
@@ -433,7 +429,7 @@ int lc_check_device(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
   c->stats.hbm_kernel_ms = d.hbm_ms;
   c->stats.n_hbm_keys = d.n_hbm;
   c->stats.n_keys = n_keys;
-  c->stats.n_ops = last - base;
+  c->stats.n_ops = -1;  // not read back from device memory
   c->stats.n_devices = 1;
   c->stats.total_ms = std::chrono::duration<double, std::milli>(
                           std::chrono::steady_clock::now() - t0).count();

@@ -6,7 +6,7 @@ do not fit one pass; both are in KiB; on gfx950 FETCH_SIZE reports half the
 bytes of a wide coalesced read (16 B/lane) — our record loads are 16-B
 dwordx4 per lane, so the read side is doubled).
 
-usage: python tools/pmc_traffic.py gpurun_out/prof_r01 profiles r01 N_OPS
+usage: python tools/pmc_traffic.py gpurun_out/prof_r01 profiles r01 N_OPS [KERNEL]
 """
 import csv
 import json
@@ -15,7 +15,7 @@ import shutil
 import statistics
 import sys
 
-KERNEL = "lds_tier_kernel"
+KERNEL = sys.argv[5] if len(sys.argv) > 5 else "fast_tier_kernel"
 
 
 def counter(path, name):
@@ -29,7 +29,7 @@ def main():
     os.makedirs(os.path.join(dst, tag), exist_ok=True)
     fetch_kib, nf = counter(os.path.join(src, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
     write_kib, nw = counter(os.path.join(src, "write", "write_counter_collection.csv"), "WRITE_SIZE")
-    read_b = fetch_kib * 1024 * 2      # gfx950 correction for 16-B/lane streaming reads
+    read_b = fetch_kib * 1024 * 2      # gfx950 correction for 16-B/lane reads
     write_b = write_kib * 1024
     stats = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))))
     k = [r for r in stats if KERNEL in r["Name"]][0]
