@@ -769,6 +769,23 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
   }
   const int n = (int)n64;
   const lc_op *kops = ops + (beg - key_off[0]);
+  // Issue every load of this thread's records (and of each predecessor's
+  // call, for the order check) before touching LDS: up to 4 x 56 B in flight
+  // per thread, ~56 KB per workgroup.
+  constexpr int kPer = kFastMax / kFastThreads;
+  Raw w[kPer];
+  int64_t prevcall[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int r = tid + u * kFastThreads;
+    if (r < n) {
+      const longlong2 *q = reinterpret_cast<const longlong2 *>(kops + r);
+      w[u].a = q[0];
+      w[u].b = q[1];
+      w[u].c = q[2];
+      prevcall[u] = r > 0 ? kops[r - 1].call : INT64_MIN;
+    }
+  }
   for (int k = tid; k <= n; k += kFastThreads) {
     if (k < n) {
       Lm[k] = kNever;
@@ -788,14 +805,12 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
   const int64_t base_idx = kops[0].call;
   const int V0 = p.init_ver;
   int inel = 0, bad = 0;
-  for (int r = tid; r < n; r += kFastThreads) {
-    Raw w;
-    const longlong2 *q = reinterpret_cast<const longlong2 *>(kops + r);
-    w.a = q[0];
-    w.b = q[1];
-    w.c = q[2];
-    const Rec d = decode(w, base_idx);
-    const bool unsorted = r > 0 && kops[r - 1].call >= w.c.x;
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int r = tid + u * kFastThreads;
+    if (r >= n) continue;
+    const Rec d = decode(w[u], base_idx);
+    const bool unsorted = prevcall[u] >= w[u].c.x;
     if (d.bad || d.f > LC_F_CAS || unsorted) {
       inel = 1;  // the JIT tier reports malformed / unknown :f
       continue;
