@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblincheck.so")
+# LINCHECK_LIB: dev-only override (A/B builds of the same ABI in tools/)
+LIB_PATH = os.environ.get("LINCHECK_LIB") or os.path.join(_HERE, "liblincheck.so")
 
 LC_F_READ, LC_F_WRITE, LC_F_CAS = 0, 1, 2
 LC_NIL = -1
