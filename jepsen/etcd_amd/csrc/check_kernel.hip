@@ -743,10 +743,18 @@ __device__ __forceinline__ uint32_t block_max_scan_excl(uint32_t v, uint32_t *wt
   return pre > excl ? pre : excl;
 }
 
+// Hand key over to the JIT tier (thread 0 only); tell the host there is work.
+__device__ __forceinline__ void fast_tier_handoff(int64_t key, int32_t *jit_keys,
+                                                  KStatus *status, int32_t *h_handoff) {
+  jit_keys[atomicAdd(&status->n_jit, 1)] = (int32_t)key;
+  __hip_atomic_store(h_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
     const KParams p, lc_key_result *__restrict__ out,
-    int32_t *__restrict__ jit_keys, KStatus *__restrict__ status) {
+    int32_t *__restrict__ jit_keys, KStatus *__restrict__ status,
+    int32_t *__restrict__ h_handoff) {
   __shared__ uint32_t Lm[kFastMax], Um[kFastMax];
   __shared__ int Val[kFastMax], Exp[kFastMax];
   __shared__ uint32_t RL[kFastMax + 1], RU[kFastMax + 1];
@@ -762,7 +770,7 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
       if (n64 == 0) {
         out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 0};
       } else {
-        jit_keys[atomicAdd(&status->n_jit, 1)] = (int32_t)key;
+        fast_tier_handoff(key, jit_keys, status, h_handoff);
       }
     }
     return;
@@ -892,7 +900,7 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
     if (decided)
       out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
     else
-      jit_keys[atomicAdd(&status->n_jit, 1)] = (int32_t)key;
+      fast_tier_handoff(key, jit_keys, status, h_handoff);
   }
 }
 
@@ -940,10 +948,12 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_jit_keys,
-                            KStatus *d_status, hipStream_t stream) {
+                            KStatus *d_status, int32_t *h_handoff,
+                            hipStream_t stream) {
   if (n_keys <= 0) return hipSuccess;
   hipLaunchKernelGGL(fast_tier_kernel, dim3((unsigned)n_keys), dim3(kFastThreads), 0,
-                     stream, d_ops, d_key_off, p, d_out, d_jit_keys, d_status);
+                     stream, d_ops, d_key_off, p, d_out, d_jit_keys, d_status,
+                     h_handoff);
   return hipGetLastError();
 }
 

@@ -6,10 +6,12 @@
 // jepsen.independent checks keys concurrently on a bounded JVM thread pool;
 // here all keys of a call go to the GPUs in one batch: contiguous,
 // cost-balanced key ranges per device (one host thread + one HIP stream per
-// device), an LDS-tier kernel over every key, then an HBM-tier re-run of the
-// few keys whose frontier outgrew LDS.  No collective is needed: keys are
-// independent and results land in the caller's array.  There is no CPU
-// fallback: without a usable GPU lc_open fails with -ENODEV.
+// device).  Per device: the version-order tier over every key (one launch,
+// one sync when it decides them all), then the JIT-search tier over the keys
+// it hands over, then HBM-tier re-runs of the few keys whose frontier outgrew
+// LDS.  No collective is needed: keys are independent and results land in
+// the caller's array.  There is no CPU fallback: without a usable GPU lc_open
+// fails with -ENODEV.
 #include <errno.h>
 #include <hip/hip_runtime.h>
 
@@ -52,8 +54,11 @@ struct Dev {
   hipEvent_t ef = nullptr;
   double fast_ms = 0, jit_ms = 0;
   int64_t n_jit = 0;
-  lcdev::KStatus *d_status = nullptr;
-  lcdev::KStatus *h_status = nullptr;  // pinned
+  lcdev::KStatus *d_status = nullptr;   // all-zero between calls
+  lcdev::KStatus *h_status = nullptr;   // pinned: D2H copies of d_status
+  int32_t *h_handoff = nullptr;         // host-coherent flag: fast tier handed keys over
+  int32_t *h_handoff_dev = nullptr;     // its device address
+  bool status_dirty = true;             // d_status may be non-zero
   void *d_ws = nullptr;
   size_t ws_cap = 0;
   double kernel_ms = 0, hbm_ms = 0;
@@ -133,28 +138,43 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   if (!rc) rc = ensure(c, &d.d_ovf2, &d.ovf2_cap, sizeof(int32_t) * (size_t)n_keys);
   if (!rc) rc = ensure(c, &d.d_jit, &d.jit_cap, sizeof(int32_t) * (size_t)n_keys);
   if (rc) return rc;
-  HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
+  // d_status is zero on entry (the fast tier re-zeroes it; later tiers are
+  // followed by a memset).  Until this call ends cleanly, assume it is not.
+  if (d.status_dirty)
+    HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
+  d.status_dirty = true;
   float ms = 0;
   int64_t n_jit = n_keys;
   const int32_t *jit_list = nullptr;
   HIP_TRY(c, hipEventRecord(d.e0, st));
   if (!(flags & LC_FLAG_NO_FAST_PATH)) {
-    // tier 0: version-order decision for every key; the rest go to the JIT
-    HIP_TRY(c, lcdev::launch_fast_tier(d_ops, d_off, n_keys, p, d_out,
-                                       d.d_jit, d.d_status, st));
+    // tier 0: version-order decision for every key; the rest go to the JIT.
+    // Only when some workgroup raised h_handoff is the count copied back.
+    __atomic_store_n(d.h_handoff, 0, __ATOMIC_RELEASE);
+    HIP_TRY(c, lcdev::launch_fast_tier(d_ops, d_off, n_keys, p, d_out, d.d_jit,
+                                       d.d_status, d.h_handoff_dev, st));
     HIP_TRY(c, hipEventRecord(d.ef, st));
-    HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
-                              hipMemcpyDeviceToHost, st));
-    HIP_TRY(c, hipStreamSynchronize(st));
+    HIP_TRY(c, hipEventSynchronize(d.ef));
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.ef));
     d.fast_ms = ms;
-    n_jit = d.h_status->n_jit;
+    n_jit = 0;
+    if (__atomic_load_n(d.h_handoff, __ATOMIC_ACQUIRE)) {
+      HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
+                                hipMemcpyDeviceToHost, st));
+      HIP_TRY(c, hipStreamSynchronize(st));
+      n_jit = d.h_status->n_jit;
+    }
     jit_list = d.d_jit;
   } else {
     HIP_TRY(c, hipEventRecord(d.ef, st));
   }
   d.n_jit = n_jit;
-  if (n_jit > 0) {
+  if (n_jit == 0) {
+    d.kernel_ms = d.fast_ms;
+    d.status_dirty = false;
+    return 0;
+  }
+  {
     // tier 1: JIT search with the frontier in SGPRs / LDS
     HIP_TRY(c, lcdev::launch_lds_tier(d_ops, d_off, jit_list, n_jit, p, d_out,
                                       d.d_ovf, d.d_status, st));
@@ -166,8 +186,6 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     d.jit_ms = ms;
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.e1));
     d.kernel_ms = ms;
-  } else {
-    d.kernel_ms = d.fast_ms;
   }
   d.malformed = d.h_status->malformed;
   const int32_t n_ovf = d.h_status->n_overflow;
@@ -197,6 +215,9 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e1, d.e2));
     d.hbm_ms = ms;
   }
+  HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  d.status_dirty = false;
   return 0;
 }
 
@@ -230,7 +251,10 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
         hipEventCreate(&d.e0) != hipSuccess || hipEventCreate(&d.e1) != hipSuccess ||
         hipEventCreate(&d.e2) != hipSuccess || hipEventCreate(&d.ef) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&d.d_status), sizeof(lcdev::KStatus)) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess) {
+        hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&d.h_handoff), sizeof(int32_t),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&d.h_handoff_dev), d.h_handoff, 0) != hipSuccess) {
       lc_close(c);
       return -ENODEV;
     }
@@ -257,6 +281,7 @@ void lc_close(lc_ctx *c) {
     if (d.d_ws) (void)hipFree(d.d_ws);
     if (d.d_status) (void)hipFree(d.d_status);
     if (d.h_status) (void)hipHostFree(d.h_status);
+    if (d.h_handoff) (void)hipHostFree(d.h_handoff);
     if (d.e0) (void)hipEventDestroy(d.e0);
     if (d.e1) (void)hipEventDestroy(d.e1);
     if (d.e2) (void)hipEventDestroy(d.e2);
