@@ -32,6 +32,7 @@
 // leaves every other step unchanged.  So the frontier is empty at exactly the
 // same returns as knossos's, verdicts and counterexample prefixes are
 // unchanged, and the 2^k subsets of concurrent reads never materialise.
+#include <algorithm>
 #include <climits>
 
 #include "kernels.h"
@@ -723,7 +724,6 @@ __global__ __launch_bounds__(kWave *kWavesPerWG) void lds_tier_kernel(
 // counterexample.
 constexpr int kFastThreads = 256;
 constexpr int kFastMax = 1024;
-constexpr int kNone = INT_MIN;  // "no CAS expectation" / "no value claimed"
 
 __device__ __forceinline__ uint32_t block_max_scan_excl(uint32_t v, uint32_t *wtot) {
   // exclusive max-scan of v over the workgroup (0 identity)
@@ -750,76 +750,98 @@ __device__ __forceinline__ void fast_tier_handoff(int64_t key, int32_t *jit_keys
   __hip_atomic_store(h_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
-    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
-    const KParams p, lc_key_result *__restrict__ out,
-    int32_t *__restrict__ jit_keys, KStatus *__restrict__ status,
-    int32_t *__restrict__ h_handoff) {
-  __shared__ uint32_t Lm[kFastMax], Um[kFastMax];
-  __shared__ int Val[kFastMax], Exp[kFastMax];
-  __shared__ uint32_t RL[kFastMax + 1], RU[kFastMax + 1];
-  __shared__ int Claim[kFastMax + 1];
-  __shared__ uint32_t wtot[kFastThreads / kWave];
-  __shared__ int s_inel, s_bad, s_maxpos, s_nmut;
-  const int tid = threadIdx.x;
-  const int64_t key = blockIdx.x;
-  const int64_t beg = key_off[key], end = key_off[key + 1];
-  const int64_t n64 = end - beg;
-  if (n64 <= 0 || n64 > kFastMax) {
-    if (tid == 0) {
-      if (n64 == 0) {
-        out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 0};
-      } else {
-        fast_tier_handoff(key, jit_keys, status, h_handoff);
-      }
-    }
-    return;
-  }
-  const int n = (int)n64;
-  const lc_op *kops = ops + (beg - key_off[0]);
-  // Issue every load of this thread's records (and of each predecessor's
-  // call, for the order check) before touching LDS: up to 4 x 56 B in flight
-  // per thread, ~56 KB per workgroup.
-  constexpr int kPer = kFastMax / kFastThreads;
+constexpr int kPer = kFastMax / kFastThreads;  // records per thread
+
+// 12.4 KB of LDS per workgroup, so 8 workgroups (32 waves) fit on a CU: the
+// residency, i.e. the bytes in flight per CU, is what bounds this kernel.
+// Index k of A/B is mutation position k (version V0+k+1):
+//   A[k] = max(call(m_k), calls of reads of version V0+k) + 1     (= L_k + 1)
+//   B[k] = min(ret(m_k),  rets of reads of version V0+k+1)        (= U_k)
+// Both are single LDS atomics per record; value claims and CAS expectations
+// are checked in a second pass against Val once every mutation is placed.
+struct FastLds {
+  uint32_t A[kFastMax + 1], B[kFastMax];
+  int Val[kFastMax];
+  uint32_t held[kFastMax / 32];  // positions taken (duplicate versions)
+  uint32_t wtot[kFastThreads / kWave];
+  int inel, bad, maxpos, nmut, maxread;
+};
+
+// One thread's records of one key, as loaded (decoded only once they land).
+struct FastRecs {
   Raw w[kPer];
-  int64_t prevcall[kPer];
+  int64_t pc[kPer];  // wave-uniform (SGPRs): call of the record before lane 0's
+};
+
+// Issue every load of this thread's records without waiting: up to 4 x 48 B
+// per thread, 48 KB per workgroup in flight.  The order check takes the
+// previous record's call from the neighbouring lane; only lane 0 of a wave
+// loads it from memory.
+__device__ __forceinline__ void fast_issue(const lc_op *__restrict__ kops, int n, int tid,
+                                           FastRecs &b) {
 #pragma unroll
   for (int u = 0; u < kPer; u++) {
     const int r = tid + u * kFastThreads;
     if (r < n) {
       const longlong2 *q = reinterpret_cast<const longlong2 *>(kops + r);
-      w[u].a = q[0];
-      w[u].b = q[1];
-      w[u].c = q[2];
-      prevcall[u] = r > 0 ? kops[r - 1].call : INT64_MIN;
+      b.w[u].a = q[0];
+      b.w[u].b = q[1];
+      b.w[u].c = q[2];
     }
   }
+  const int w0 = __builtin_amdgcn_readfirstlane(tid & ~(kWave - 1));
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int r0 = w0 + u * kFastThreads;  // lane 0's record: a scalar load
+    b.pc[u] = (r0 > 0 && r0 < n) ? kops[r0 - 1].call : INT64_MIN;
+  }
+}
+
+// Decide one key (records in b when 0 < n64 <= kFastMax) or hand it over.
+__device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *__restrict__ kops,
+                                         const FastRecs &b, const KParams &p, FastLds &s,
+                                         lc_key_result *__restrict__ out,
+                                         int32_t *__restrict__ jit_keys,
+                                         KStatus *__restrict__ status,
+                                         int32_t *__restrict__ h_handoff) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  if (n64 <= 0 || n64 > kFastMax) {
+    if (tid == 0) {
+      if (n64 == 0)
+        out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 0};
+      else
+        fast_tier_handoff(key, jit_keys, status, h_handoff);
+    }
+    return;
+  }
+  const int n = (int)n64;
   for (int k = tid; k <= n; k += kFastThreads) {
-    if (k < n) {
-      Lm[k] = kNever;
-      Exp[k] = kNone;
-    }
-    RL[k] = 0;  // call + 1; 0 = no read constrains t_{k+1}
-    RU[k] = kNever;
-    Claim[k] = kNone;
+    s.A[k] = 0;  // 0 = nothing constrains t_k from below
+    if (k < n) s.B[k] = kNever;
   }
+  for (int k = tid; k < (n + 31) / 32; k += kFastThreads) s.held[k] = 0;
   if (tid == 0) {
-    s_inel = 0;
-    s_bad = 0;
-    s_maxpos = -1;
-    s_nmut = 0;
+    s.inel = 0;
+    s.bad = 0;
+    s.maxpos = -1;
+    s.nmut = 0;
+    s.maxread = -1;
   }
   __syncthreads();
   const int64_t base_idx = kops[0].call;
   const int V0 = p.init_ver;
-  int inel = 0, bad = 0;
+  int inel = 0, bad = 0, maxread = -1;
+  // pass 1: place mutations, fold read intervals into A / B
 #pragma unroll
   for (int u = 0; u < kPer; u++) {
     const int r = tid + u * kFastThreads;
+    // previous record's call: lane-1's record of the same u, or for lane 0
+    // the scalar-loaded one
+    int64_t prev = __shfl_up(b.w[u].c.x, 1);
+    if (lane == 0) prev = b.pc[u];
     if (r >= n) continue;
-    const Rec d = decode(w[u], base_idx);
-    const bool unsorted = prevcall[u] >= w[u].c.x;
-    if (d.bad || d.f > LC_F_CAS || unsorted) {
+    const Rec d = decode(b.w[u], base_idx);
+    if (d.bad || d.f > LC_F_CAS || (r > 0 && prev >= b.w[u].c.x)) {
       inel = 1;  // the JIT tier reports malformed / unknown :f
       continue;
     }
@@ -834,12 +856,9 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
         bad = 1;
         continue;
       }
-      atomicMax(&RL[k], d.call + 1);
-      atomicMin(&RU[k], d.ret);
-      if (d.val != -1) {
-        const int prev = atomicCAS(&Claim[k], kNone, d.val);
-        if (prev != kNone && prev != d.val) bad = 1;
-      }
+      maxread = max(maxread, k);
+      atomicMax(&s.A[k], d.call + 1);
+      if (k > 0) atomicMin(&s.B[k - 1], d.ret);
     } else {
       if (d.ret == kNever || d.ver == -1) {
         inel = 1;  // crashed, or no version: order not pinned
@@ -850,51 +869,54 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
         bad = 1;
         continue;
       }
-      if (atomicCAS(&Lm[pos], kNever, d.call) != kNever) {
+      if (atomicOr(&s.held[pos >> 5], 1u << (pos & 31)) & (1u << (pos & 31))) {
         bad = 1;  // two mutations claim one version
         continue;
       }
-      Um[pos] = d.ret;
-      Val[pos] = d.val;
-      Exp[pos] = d.f == LC_F_CAS ? d.exp : kNone;
-      atomicMax(&s_maxpos, pos);
-      atomicAdd(&s_nmut, 1);
+      atomicMax(&s.A[pos], d.call + 1);
+      atomicMin(&s.B[pos], d.ret);
+      s.Val[pos] = d.val;
+      atomicMax(&s.maxpos, pos);
+      atomicAdd(&s.nmut, 1);
     }
   }
-  if (inel) atomicOr(&s_inel, 1);
-  if (bad) atomicOr(&s_bad, 1);
+  if (inel) atomicOr(&s.inel, 1);
+  if (bad) atomicOr(&s.bad, 1);
+  if (maxread >= 0) atomicMax(&s.maxread, maxread);
   __syncthreads();
-  const int M = s_maxpos + 1;
-  bool decided = !s_inel && !s_bad && s_nmut == M;
+  const int M = s.maxpos + 1;
+  // positions 0..M-1 each held once (no duplicates, so nmut == M means no
+  // gap), and no read beyond the last version
+  bool decided = !s.inel && !s.bad && s.nmut == M && s.maxread <= M;
   if (decided) {
-    // feasibility: prefix max of L below U; CAS expectations
+    // pass 2: CAS expectations and read claims against the placed values
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const int r = tid + u * kFastThreads;
+      if (r >= n) continue;
+      const int f = (int)b.w[u].a.x, val = (int)b.w[u].a.y, exp = (int)b.w[u].b.x;
+      const int ver = (int)b.w[u].b.y;
+      if (f == LC_F_CAS) {
+        const int pos = ver - V0 - 1;
+        if (exp != (pos == 0 ? p.init_val : s.Val[pos - 1])) bad = 1;
+      } else if (f == LC_F_READ && ver != -1 && val != -1 && b.w[u].c.y != kInf) {
+        const int k = ver - V0;
+        if (val != (k == 0 ? p.init_val : s.Val[k - 1])) bad = 1;
+      }
+    }
+    // timing: prefix max of L below U
     const int per = (M + kFastThreads - 1) / kFastThreads;
     const int k0 = tid * per, k1 = min(k0 + per, M);
     uint32_t loc = 0;
+    for (int k = k0; k < k1; k++) loc = max(loc, s.A[k]);
+    uint32_t pm = block_max_scan_excl(loc, s.wtot);
     for (int k = k0; k < k1; k++) {
-      const uint32_t L = max(Lm[k] + 1, RL[k]);  // +1: compare in call+1 units
-      loc = max(loc, L);
+      pm = max(pm, s.A[k]);
+      if (pm - 1 >= s.B[k]) bad = 1;  // need max call < U (A holds call + 1)
     }
-    uint32_t pm = block_max_scan_excl(loc, wtot);
-    for (int k = k0; k < k1; k++) {
-      pm = max(pm, max(Lm[k] + 1, RL[k]));
-      const uint32_t U = min(Um[k], RU[k + 1]);
-      if (pm - 1 >= U) bad = 1;  // need max call < U
-      const int before = k == 0 ? p.init_val : Val[k - 1];
-      if (Exp[k] != kNone && Exp[k] != before) bad = 1;
-    }
-    // reads: claimed values, and no read beyond the last version
-    for (int k = tid; k <= n; k += kFastThreads) {
-      if (k > M) {
-        if (RL[k] != 0 || RU[k] != kNever) bad = 1;
-      } else if (Claim[k] != kNone) {
-        const int actual = k == 0 ? p.init_val : Val[k - 1];
-        if (Claim[k] != actual) bad = 1;
-      }
-    }
-    if (bad) atomicOr(&s_bad, 1);
+    if (bad) atomicOr(&s.bad, 1);
     __syncthreads();
-    decided = !s_bad;
+    decided = !s.bad;
   }
   if (tid == 0) {
     if (decided)
@@ -902,6 +924,24 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
     else
       fast_tier_handoff(key, jit_keys, status, h_handoff);
   }
+}
+
+// One workgroup per key.  (A persistent grid that issues key i+G's loads
+// before deciding key i measured slower, 0.113 -> 0.156 ms on C2: its two
+// register sets cut residency from 5 to 3 workgroups per CU, i.e. fewer
+// bytes in flight per CU than the hardware dispatcher keeps with 5.)
+__global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
+    const KParams p, lc_key_result *__restrict__ out,
+    int32_t *__restrict__ jit_keys, KStatus *__restrict__ status,
+    int32_t *__restrict__ h_handoff) {
+  __shared__ FastLds s;
+  const int64_t key = blockIdx.x;
+  const int64_t beg = key_off[key], end = key_off[key + 1];
+  const lc_op *kops = ops + (beg - key_off[0]);
+  FastRecs r;
+  if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
+  fast_key(key, end - beg, kops, r, p, s, out, jit_keys, status, h_handoff);
 }
 
 // Workspace layout per wave: 3 regions of cap Cfg, 2 tables of 2*cap Cfg,
@@ -948,12 +988,10 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_jit_keys,
-                            KStatus *d_status, int32_t *h_handoff,
-                            hipStream_t stream) {
+                            KStatus *d_status, int32_t *h_handoff, hipStream_t stream) {
   if (n_keys <= 0) return hipSuccess;
   hipLaunchKernelGGL(fast_tier_kernel, dim3((unsigned)n_keys), dim3(kFastThreads), 0,
-                     stream, d_ops, d_key_off, p, d_out, d_jit_keys, d_status,
-                     h_handoff);
+                     stream, d_ops, d_key_off, p, d_out, d_jit_keys, d_status, h_handoff);
   return hipGetLastError();
 }
 

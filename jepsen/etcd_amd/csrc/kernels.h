@@ -40,8 +40,7 @@ constexpr int kLdsCap = 128;     // configurations per LDS region (3 regions/wav
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_jit_keys,
-                            KStatus *d_status, int32_t *h_handoff,
-                            hipStream_t stream);
+                            KStatus *d_status, int32_t *h_handoff, hipStream_t stream);
 
 // LDS tier (JIT search): one wavefront per key, for the keys in d_keys
 // (n_keys of them), or for keys 0..n_keys-1 when d_keys is null.  In every
