@@ -34,6 +34,7 @@ LC_REASON_MALFORMED = 4
 LC_REASON_UNKNOWN_F = 5
 LC_FLAG_NO_HBM_RETRY = 1
 LC_FLAG_NO_FAST_PATH = 2
+LC_FLAG_NO_GAP_TIER = 4
 
 # lc_op: 6 x int64 (f, value, expected, version, call, ret); arrays are (n, 6).
 OP_FIELDS = ("f", "value", "expected", "version", "call", "ret")
@@ -56,7 +57,8 @@ class LcStats(ctypes.Structure):
                 ("total_ms", ctypes.c_double), ("n_keys", ctypes.c_int64),
                 ("n_ops", ctypes.c_int64), ("n_hbm_keys", ctypes.c_int64),
                 ("n_devices", ctypes.c_int64), ("fast_kernel_ms", ctypes.c_double),
-                ("jit_kernel_ms", ctypes.c_double), ("n_jit_keys", ctypes.c_int64)]
+                ("jit_kernel_ms", ctypes.c_double), ("n_jit_keys", ctypes.c_int64),
+                ("gap_kernel_ms", ctypes.c_double), ("n_gap_keys", ctypes.c_int64)]
 
 
 class LcSynthParams(ctypes.Structure):

@@ -21,7 +21,9 @@ struct KStatus {
   int32_t malformed;    // keys with LC_REASON_MALFORMED
   int32_t n_overflow;   // keys appended to the overflow list (LDS tier full)
   int32_t n_overflow2;  // keys that also overflowed the first HBM tier
-  int32_t n_jit;        // keys handed from the fast tier to the JIT search
+  int32_t n_jit;        // keys handed over by the fast tier
+  int32_t max_len;      // longest key among them (records)
+  int32_t n_jit2;       // keys the gap tier passes on to the JIT search
 };
 
 constexpr int kWave = 64;
@@ -67,5 +69,15 @@ hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
                            void *d_ws, int n_waves, int64_t cap,
                            int32_t *d_ovf_out, int32_t *d_n_ovf_out, int last_tier,
                            hipStream_t stream);
+
+// Gap tier (gap_tier.hip): one 256-thread workgroup per key of d_keys decides
+// version-pinned keys with crashed writes/CAS by matching gaps to optional
+// ops; keys it cannot decide are appended to d_pass_keys (status->n_jit2).
+// Workspace: gap_tier_ws_bytes(n_wg, cap) with cap >= longest key + 2.
+size_t gap_tier_ws_bytes(int n_wg, int64_t cap);
+hipError_t launch_gap_tier(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
+                           int32_t n_list, const KParams &p, lc_key_result *d_out,
+                           int32_t *d_ws, int n_wg, int64_t cap, int32_t *d_pass_keys,
+                           KStatus *d_status, hipStream_t stream);
 
 }  // namespace lcdev

@@ -35,6 +35,10 @@ constexpr int64_t kDefaultBudget = 1 << 24;   // configurations per key
 // is ~128 B per configuration of capacity (3 regions + 2 hash tables).
 constexpr int64_t kHbmCap[2] = {1 << 16, 1 << 21};
 constexpr int kHbmWaves[2] = {512, 16};
+// Gap tier: at most this many workgroups, and this much workspace (each
+// workgroup needs 84 B per record of the longest key handed over).
+constexpr int kGapMaxWG = 1024;
+constexpr size_t kGapWsBytes = size_t(1) << 30;
 
 struct Dev {
   int id = -1;
@@ -52,6 +56,13 @@ struct Dev {
   size_t ovf2_cap = 0;
   int32_t *d_jit = nullptr;
   size_t jit_cap = 0;
+  int32_t *d_jit2 = nullptr;           // keys the gap tier passes on
+  size_t jit2_cap = 0;
+  int32_t *d_gws = nullptr;            // gap-tier workspace
+  size_t gws_cap = 0;
+  hipEvent_t eg = nullptr;
+  double gap_ms = 0;
+  int64_t n_gap = 0;
   hipEvent_t ef = nullptr;
   double fast_ms = 0, jit_ms = 0;
   int64_t n_jit = 0;
@@ -127,8 +138,8 @@ int opts_to_params(lc_ctx *c, const lc_opts *o, lcdev::KParams *p) {
 int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                int64_t n_keys, const lcdev::KParams &p,
                lc_key_result *d_out, hipStream_t st, int64_t flags) {
-  d.kernel_ms = d.hbm_ms = d.fast_ms = d.jit_ms = 0;
-  d.n_hbm = d.n_jit = 0;
+  d.kernel_ms = d.hbm_ms = d.fast_ms = d.jit_ms = d.gap_ms = 0;
+  d.n_hbm = d.n_jit = d.n_gap = 0;
   d.malformed = 0;
   if (n_keys <= 0) return 0;
   if (n_keys > INT32_MAX) {
@@ -169,21 +180,49 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   } else {
     HIP_TRY(c, hipEventRecord(d.ef, st));
   }
-  d.n_jit = n_jit;
   if (n_jit == 0) {
     d.kernel_ms = d.fast_ms;
     d.status_dirty = false;
     return 0;
   }
-  {
-    // tier 1: JIT search with the frontier in SGPRs / LDS
+  hipEvent_t before_jit = d.ef;
+  const int64_t gap_cap = (int64_t)d.h_status->max_len + 2;
+  const size_t gap_per_wg = lcdev::gap_tier_ws_bytes(1, gap_cap);
+  if (!(flags & (LC_FLAG_NO_FAST_PATH | LC_FLAG_NO_GAP_TIER)) && gap_per_wg <= kGapWsBytes) {
+    // tier 1: gap matching for version-pinned keys (crashed writes/CAS, long
+    // keys, invalid keys); what it cannot decide goes on to the JIT search
+    const int n_wg = (int)std::min<int64_t>(
+        {n_jit, (int64_t)kGapMaxWG, std::max<int64_t>(1, (int64_t)(kGapWsBytes / gap_per_wg))});
+    rc = ensure(c, reinterpret_cast<char **>(&d.d_gws), &d.gws_cap,
+                lcdev::gap_tier_ws_bytes(n_wg, gap_cap));
+    if (!rc) rc = ensure(c, &d.d_jit2, &d.jit2_cap, sizeof(int32_t) * (size_t)n_keys);
+    if (rc) return rc;
+    HIP_TRY(c, lcdev::launch_gap_tier(d_ops, d_off, jit_list, (int32_t)n_jit, p, d_out,
+                                      d.d_gws, n_wg, gap_cap, d.d_jit2, d.d_status, st));
+    HIP_TRY(c, hipEventRecord(d.eg, st));
+    HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
+                              hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    HIP_TRY(c, hipEventElapsedTime(&ms, d.ef, d.eg));
+    d.gap_ms = ms;
+    d.n_gap = n_jit;
+    n_jit = d.h_status->n_jit2;
+    jit_list = d.d_jit2;
+    before_jit = d.eg;
+  }
+  d.n_jit = n_jit;
+  if (n_jit == 0) {
+    HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, before_jit));
+    d.kernel_ms = ms;
+  } else {
+    // tier 2: JIT search with the frontier in SGPRs / LDS
     HIP_TRY(c, lcdev::launch_lds_tier(d_ops, d_off, jit_list, n_jit, p, d_out,
                                       d.d_ovf, d.d_status, st));
     HIP_TRY(c, hipEventRecord(d.e1, st));
     HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                               hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipStreamSynchronize(st));
-    HIP_TRY(c, hipEventElapsedTime(&ms, d.ef, d.e1));
+    HIP_TRY(c, hipEventElapsedTime(&ms, before_jit, d.e1));
     d.jit_ms = ms;
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.e1));
     d.kernel_ms = ms;
@@ -251,6 +290,7 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
         hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&d.e0) != hipSuccess || hipEventCreate(&d.e1) != hipSuccess ||
         hipEventCreate(&d.e2) != hipSuccess || hipEventCreate(&d.ef) != hipSuccess ||
+        hipEventCreate(&d.eg) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&d.d_status), sizeof(lcdev::KStatus)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&d.h_handoff), sizeof(int32_t),
@@ -288,6 +328,9 @@ void lc_close(lc_ctx *c) {
     if (d.e2) (void)hipEventDestroy(d.e2);
     if (d.ef) (void)hipEventDestroy(d.ef);
     if (d.d_jit) (void)hipFree(d.d_jit);
+    if (d.d_jit2) (void)hipFree(d.d_jit2);
+    if (d.d_gws) (void)hipFree(d.d_gws);
+    if (d.eg) (void)hipEventDestroy(d.eg);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
   delete c;
@@ -407,6 +450,8 @@ int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
     c->stats.fast_kernel_ms += c->devs[di].fast_ms;
     c->stats.jit_kernel_ms += c->devs[di].jit_ms;
     c->stats.n_jit_keys += c->devs[di].n_jit;
+    c->stats.gap_kernel_ms += c->devs[di].gap_ms;
+    c->stats.n_gap_keys += c->devs[di].n_gap;
     c->stats.hbm_kernel_ms += c->devs[di].hbm_ms;
     c->stats.n_hbm_keys += c->devs[di].n_hbm;
     malformed += c->devs[di].malformed;
@@ -452,6 +497,8 @@ int lc_check_device(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
   c->stats.fast_kernel_ms = d.fast_ms;
   c->stats.jit_kernel_ms = d.jit_ms;
   c->stats.n_jit_keys = d.n_jit;
+  c->stats.gap_kernel_ms = d.gap_ms;
+  c->stats.n_gap_keys = d.n_gap;
   c->stats.hbm_kernel_ms = d.hbm_ms;
   c->stats.n_hbm_keys = d.n_hbm;
   c->stats.n_keys = n_keys;

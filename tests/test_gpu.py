@@ -128,11 +128,12 @@ def test_long_key(ctx):
 
 def test_hbm_tier_resolves_lds_overflow(ctx):
     z = np.load(os.path.join(GOLDEN, "info.npz"))
-    o = abi.default_opts(flags=abi.LC_FLAG_NO_HBM_RETRY)
+    nogap = abi.LC_FLAG_NO_GAP_TIER  # crash-heavy keys reach the JIT search
+    o = abi.default_opts(flags=abi.LC_FLAG_NO_HBM_RETRY | nogap)
     _, lds_only = ctx.check(z["ops"], z["key_off"], o)
     spilled = lds_only["reason"] == 6
     assert spilled.any()
-    _, full = ctx.check(z["ops"], z["key_off"])
+    _, full = ctx.check(z["ops"], z["key_off"], abi.default_opts(flags=nogap))
     assert ctx.stats()["n_hbm_keys"] == spilled.sum()
     assert (full["verdict"] == z["verdict"]).all()
     assert (full["fail_op"] == z["fail_op"]).all()
@@ -157,17 +158,85 @@ def test_edge_cases(ctx):
 def test_window_overflow_is_unknown(ctx):
     recs = [[1, i % 4, -1, -1, i, INF] for i in range(65)]  # 65 crashed writes
     ops, off = pack_keys([recs, [[1, 1, -1, 1, 0, 1]]])
-    _, r = ctx.check(ops, off)
+    _, r = ctx.check(ops, off, abi.default_opts(flags=abi.LC_FLAG_NO_GAP_TIER))
     assert r["verdict"][0] == -1 and r["reason"][0] == abi.LC_REASON_WINDOW_OVERFLOW
     assert r["verdict"][1] == 1
+    # the gap tier decides it: no :ok op needs any crashed write
+    _, r = ctx.check(ops, off)
+    assert list(r["verdict"]) == [1, 1]
 
 
 def test_budget_is_unknown(ctx):
     recs = [[1, i % 3, -1, -1, i, INF] for i in range(20)]
     recs.append([0, 2, -1, 21, 30, 31])
     ops, off = pack_keys([recs])
-    _, r = ctx.check(ops, off, abi.default_opts(max_configs_per_key=500))
+    o = abi.default_opts(max_configs_per_key=500, flags=abi.LC_FLAG_NO_GAP_TIER)
+    _, r = ctx.check(ops, off, o)
     assert r["verdict"][0] == -1 and r["reason"][0] == abi.LC_REASON_CONFIG_BUDGET
+    # the gap tier decides it: version 21 needs 21 mutations, 20 exist
+    _, r = ctx.check(ops, off, abi.default_opts(max_configs_per_key=500))
+    assert r["verdict"][0] == 0 and r["fail_op"][0] == 20
+
+
+def _gm_recs(ops, off, k):
+    return [tuple(r) for r in ops[off[k]:off[k + 1]].tolist()]
+
+
+@pytest.mark.parametrize("opk,conc,seed", [(60, 10, 31), (120, 16, 32), (200, 20, 33)])
+def test_gap_tier_vs_oracle(ctx, opk, conc, seed):
+    """Crash-heavy keys (20 % :info, C4-shaped but small enough for the
+    oracle's search): the gap tier decides them, bit-exact with the oracle
+    wherever the oracle finishes, and the Python restatement everywhere."""
+    import gapmatch_ref as gm
+    ops, off, lab, _ = abi.synth(200, opk, concurrency=conc, p_info=0.2,
+                                 p_anomaly=0.3, seed=seed)
+    _, g = ctx.check(ops, off)
+    st = ctx.stats()
+    assert st["n_gap_keys"] > 0 and st["n_jit_keys"] == 0
+    assert (g["verdict"] != -1).all()
+    _, j = oracle.check(ops, off, algo=oracle.JITC, n_threads=8, max_configs=1 << 20)
+    known = j["verdict"] != -1
+    assert known.sum() >= 20
+    assert (g["verdict"][known] == j["verdict"][known]).all()
+    assert (g["fail_op"][known] == j["fail_op"][known]).all()
+    assert (g["fail_prefix_end"][known] == j["fail_prefix_end"][known]).all()
+    for k in range(0, 200, 7):
+        recs = _gm_recs(ops, off, k)
+        assert g["verdict"][k] == gm.decide(recs)
+        if g["verdict"][k] == 0:
+            assert (g["fail_op"][k], g["fail_prefix_end"][k]) == gm.first_failure(recs)
+
+
+@pytest.mark.parametrize("seed,anom", [(0x5EED0004, 0.0), (1004, 0.5), (1006, 1.0)])
+def test_c4_hot_key(ctx, seed, anom):
+    """BASELINE configs[3] at full size: one key, 5k ops, concurrency 50,
+    20 % :info.  Every frontier search (knossos's, the oracle's, the JIT
+    tier's) runs out of budget here; the gap tier decides it exactly.  No
+    oracle finishes, so parity is against the restated procedure (itself
+    checked against the oracle on smaller keys above)."""
+    import gapmatch_ref as gm
+    ops, off, lab, _ = abi.synth(1, 5000, concurrency=50, p_info=0.2,
+                                 p_anomaly=anom, seed=seed)
+    _, g = ctx.check(ops, off)
+    recs = _gm_recs(ops, off, 0)
+    want = gm.decide(recs)
+    assert want is not None and g["verdict"][0] == want
+    if want == 0:
+        assert (g["fail_op"][0], g["fail_prefix_end"][0]) == gm.first_failure(recs)
+    if lab[0] == 1:
+        assert want == 0  # an injected stale read is always visible
+
+
+def test_gap_tier_and_search_agree(ctx):
+    """Where the JIT search decides crash-heavy keys, the gap tier agrees."""
+    z = np.load(os.path.join(GOLDEN, "info.npz"))
+    _, a = ctx.check(z["ops"], z["key_off"])
+    assert ctx.stats()["n_gap_keys"] > 0
+    _, b = ctx.check(z["ops"], z["key_off"], abi.default_opts(flags=abi.LC_FLAG_NO_GAP_TIER))
+    both = (a["verdict"] != -1) & (b["verdict"] != -1)
+    assert (a["verdict"][both] == b["verdict"][both]).all()
+    assert (a["fail_op"][both] == b["fail_op"][both]).all()
+    assert ((a["verdict"] != -1) | (b["verdict"] == -1)).all()
 
 
 def test_malformed_and_unknown_f(ctx):
