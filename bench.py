@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--cpu-sample-keys", type=int, default=5000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--bare", action="store_true",
+                    help="timed region only (no CPU baseline, no hot-key leg): "
+                         "for rocprofv3 runs whose per-kernel averages must "
+                         "match the bench line")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return ap.parse_args()
 
@@ -174,10 +178,10 @@ def main():
         "cpu_baseline": None,
         "hot_key": None,
     }
-    if rank == 0:
+    if rank == 0 and not args.bare:
         line["hot_key"] = hot_key(ctx, abi)
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not (args.no_cpu_baseline or args.bare):
         line["cpu_baseline"] = cpu_baseline(args, ops, key_off, res)
 
     if rank == 0:

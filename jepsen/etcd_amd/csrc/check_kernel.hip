@@ -640,25 +640,37 @@ __global__ __launch_bounds__(kWave *kWavesPerWG) void lds_tier_kernel(
 // versions, a read [nil x], more than kFastMax records, malformed records) or
 // finds invalid are handed to the JIT search, which also names the canonical
 // counterexample.
+#ifndef LC_FAST_DEV
+#define LC_FAST_DEV 0  // dev timing switches (tools/build_variants.sh); 0 in the product
+#endif
 constexpr int kFastThreads = 256;
+constexpr int kFastWaves = kFastThreads / kWave;
 constexpr int kFastMax = 1024;
+constexpr int kPer = kFastMax / kFastThreads;  // records per thread
 
-__device__ __forceinline__ uint32_t block_max_scan_excl(uint32_t v, uint32_t *wtot) {
-  // exclusive max-scan of v over the workgroup (0 identity)
-  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  uint32_t incl = v;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
-    if (lane >= o) incl = incl > y ? incl : y;
-  }
-  if (lane == kWave - 1) wtot[w] = incl;
-  __syncthreads();
-  uint32_t pre = 0;
-  for (int j = 0; j < w; j++) pre = pre > wtot[j] ? pre : wtot[j];
-  uint32_t excl = (uint32_t)__shfl_up((int)incl, 1);
-  if (lane == 0) excl = 0;
-  return pre > excl ? pre : excl;
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+// Inclusive max-scan inside each 16-lane row: four DPP row_shr steps (lanes
+// shifted in from outside the row read 0, the identity).
+__device__ __forceinline__ uint32_t row_max_scan(uint32_t v) {
+  v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));
+  v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));
+  v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));
+  v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));
+  return v;
+}
+
+// Maximum of v over the wave (wave-uniform): the DPP butterfly of
+// wave_min_u32 with max.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
+  v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
+  v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));
+  v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));
+  return umax(umax((uint32_t)__builtin_amdgcn_readlane((int)v, 0),
+                   (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+              umax((uint32_t)__builtin_amdgcn_readlane((int)v, 32),
+                   (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
 }
 
 // Hand key over to the JIT tier (thread 0 only); tell the host there is work.
@@ -672,21 +684,23 @@ __device__ __forceinline__ void fast_tier_handoff(int64_t key, int64_t n, int32_
   if (at == 0) __hip_atomic_store(h_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-constexpr int kPer = kFastMax / kFastThreads;  // records per thread
-
-// 12.4 KB of LDS per workgroup, so 8 workgroups (32 waves) fit on a CU: the
-// residency, i.e. the bytes in flight per CU, is what bounds this kernel.
+// 14.4 KB of LDS per workgroup (7 workgroups per CU at 72 VGPRs).
 // Index k of A/B is mutation position k (version V0+k+1):
 //   A[k] = max(call(m_k), calls of reads of version V0+k) + 1     (= L_k + 1)
 //   B[k] = min(ret(m_k),  rets of reads of version V0+k+1)        (= U_k)
-// Both are single LDS atomics per record; value claims and CAS expectations
-// are checked in a second pass against Val once every mutation is placed.
+// Both are single LDS atomics per record.  Val/Own are plain stores: the
+// value and the key-relative record index of the mutation placed at k; a
+// second pass checks value claims and CAS expectations against Val, and a
+// mutation that finds another record's index in Own[k] shares its version
+// with it (two stores raced, one lost).  Per-wave summaries (counts, flags,
+// verdicts) go to per-wave slots, so there are no same-address atomics and
+// no slots to clear.
 struct FastLds {
-  uint32_t A[kFastMax + 1], B[kFastMax];
+  uint32_t A[kFastMax + 4], B[kFastMax];  // 16-byte aligned rows (timing check)
   int Val[kFastMax];
-  uint32_t held[kFastMax / 32];  // positions taken (duplicate versions)
-  uint32_t wtot[kFastThreads / kWave];
-  int inel, bad, maxpos, nmut, maxread;
+  uint16_t Own[kFastMax];
+  uint32_t wsum[kFastWaves];  // per wave: mutations placed | inel << 16 | bad << 17
+  uint32_t wbad[kFastWaves];  // per wave: 1 if a CAS/read/timing condition failed
 };
 
 // One thread's records of one key, as loaded (decoded only once they land).
@@ -719,14 +733,61 @@ __device__ __forceinline__ void fast_issue(const lc_op *__restrict__ kops, int n
   }
 }
 
+// Timing condition max(A[0..k]) - 1 < B[k] for every position k < M (A holds
+// L + 1).  Thread t owns positions 4t..4t+3 (16-byte LDS reads).  The max
+// over earlier positions is: a DPP row scan, the row totals (v_readlane), and
+// for waves w > 0 the max of A over the earlier waves' positions, which the
+// wave reads itself (3 x 16 B per lane at most) instead of waiting at a
+// barrier for the other waves' totals.  Returns true if a position fails.
+__device__ __forceinline__ bool timing_fails(const FastLds &s, int M, int tid) {
+  const int lane = tid & (kWave - 1), w = tid / kWave, row = lane >> 4;
+  const int k0 = 4 * tid;
+  uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(kNever, kNever, kNever, kNever);
+  if (k0 < M) {
+    a = reinterpret_cast<const uint4 *>(s.A)[tid];
+    b = reinterpret_cast<const uint4 *>(s.B)[tid];
+  }
+  // positions >= M do not exist: neutral values
+  if (k0 + 1 >= M) a.y = 0, b.y = kNever;
+  if (k0 + 2 >= M) a.z = 0, b.z = kNever;
+  if (k0 + 3 >= M) a.w = 0, b.w = kNever;
+  // max of A over the positions of earlier waves (4 * kWave per wave)
+  uint32_t ew = 0;
+#pragma unroll
+  for (int j = 0; j < kFastWaves - 1; j++) {
+    const int kj = 4 * (j * kWave + lane);
+    if (j < w && kj < M) {
+      uint4 e = reinterpret_cast<const uint4 *>(s.A)[j * kWave + lane];
+      if (kj + 1 >= M) e.y = 0;
+      if (kj + 2 >= M) e.z = 0;
+      if (kj + 3 >= M) e.w = 0;
+      ew = umax(ew, umax(umax(e.x, e.y), umax(e.z, e.w)));
+    }
+  }
+  const uint32_t pre = w ? wave_max_u32(ew) : 0u;
+  const uint32_t p1 = umax(a.x, a.y), p2 = umax(p1, a.z), p3 = umax(p2, a.w);
+  const uint32_t rs = row_max_scan(p3);
+  uint32_t ex = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rs, 0x111, 0xF, 0xF, false);
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rs, 15);
+  const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)rs, 31);
+  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)rs, 47);
+  const uint32_t r01 = umax(r0, r1);
+  ex = umax(umax(ex, pre), row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r01 : umax(r01, r2));
+  // need max call < U, i.e. prefix max of A (= call + 1) <= B
+  return ((int)(umax(ex, a.x) > b.x) | (int)(umax(ex, p1) > b.y) |
+          (int)(umax(ex, p2) > b.z) | (int)(umax(ex, p3) > b.w)) != 0;
+}
+
 // Decide one key (records in b when 0 < n64 <= kFastMax) or hand it over.
+// Three barriers: after the LDS init, after pass 1, before thread 0 reads
+// the per-wave verdicts.
 __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *__restrict__ kops,
                                          const FastRecs &b, const KParams &p, FastLds &s,
                                          lc_key_result *__restrict__ out,
                                          int32_t *__restrict__ jit_keys,
                                          KStatus *__restrict__ status,
                                          int32_t *__restrict__ h_handoff) {
-  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   if (n64 <= 0 || n64 > kFastMax) {
     if (tid == 0) {
       if (n64 == 0)
@@ -737,22 +798,29 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     return;
   }
   const int n = (int)n64;
-  for (int k = tid; k <= n; k += kFastThreads) {
-    s.A[k] = 0;  // 0 = nothing constrains t_k from below
-    if (k < n) s.B[k] = kNever;
+#if LC_FAST_DEV == 2  // dev timing only: loads, no decision
+  {
+    int64_t x = 0;
+#pragma unroll
+    for (int u = 0; u < kPer; u++)
+      x ^= b.w[u].a.x ^ b.w[u].a.y ^ b.w[u].b.x ^ b.w[u].b.y ^ b.w[u].c.x ^ b.w[u].c.y ^ b.pc[u];
+    if (x == 0x123456789) out[key].configs_explored = x;
+    if (tid == 0) out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
+    return;
   }
-  for (int k = tid; k < (n + 31) / 32; k += kFastThreads) s.held[k] = 0;
-  if (tid == 0) {
-    s.inel = 0;
-    s.bad = 0;
-    s.maxpos = -1;
-    s.nmut = 0;
-    s.maxread = -1;
+#endif
+  // thread t clears positions 4t..4t+3 of A and B (one 16-byte store each);
+  // A[kFastMax] (reads of the version after the last possible mutation) by
+  // thread 0
+  if (4 * tid <= n) {
+    reinterpret_cast<uint4 *>(s.A)[tid] = make_uint4(0, 0, 0, 0);  // nothing constrains t_k from below
+    reinterpret_cast<uint4 *>(s.B)[tid] = make_uint4(kNever, kNever, kNever, kNever);
   }
+  if (tid == 0) s.A[kFastMax] = 0;
   __syncthreads();
   const int64_t base_idx = kops[0].call;
   const int V0 = p.init_ver;
-  int inel = 0, bad = 0, maxread = -1;
+  int inel = 0, bad = 0, nmut = 0;
   // pass 1: place mutations, fold read intervals into A / B
 #pragma unroll
   for (int u = 0; u < kPer; u++) {
@@ -761,87 +829,86 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     // the scalar-loaded one
     int64_t prev = __shfl_up(b.w[u].c.x, 1);
     if (lane == 0) prev = b.pc[u];
-    if (r >= n) continue;
-    const Rec d = decode(b.w[u], base_idx);
-    if (d.bad || d.f > LC_F_CAS || (r > 0 && prev >= b.w[u].c.x)) {
-      inel = 1;  // the JIT tier reports malformed / unknown :f
-      continue;
-    }
-    if (d.f == LC_F_READ) {
-      if (d.ret == kNever || (d.ver == -1 && d.val == -1)) continue;  // never constrains
-      if (d.ver == -1) {
-        inel = 1;  // read [nil x]: its version is free
-        continue;
-      }
-      const int k = d.ver - V0;
-      if (k < 0 || k > n) {
-        bad = 1;
-        continue;
-      }
-      maxread = max(maxread, k);
-      atomicMax(&s.A[k], d.call + 1);
-      if (k > 0) atomicMin(&s.B[k - 1], d.ret);
-    } else {
-      if (d.ret == kNever || d.ver == -1) {
+    bool placed = false;
+    if (r < n) {
+      const Rec d = decode(b.w[u], base_idx);
+      if (d.bad || d.f > LC_F_CAS || (r > 0 && prev >= b.w[u].c.x)) {
+        inel = 1;  // the JIT tier reports malformed / unknown :f
+      } else if (d.f == LC_F_READ) {
+        if (d.ret != kNever && !(d.ver == -1 && d.val == -1)) {  // else never constrains
+          if (d.ver == -1) {
+            inel = 1;  // read [nil x]: its version is free
+          } else {
+            const int k = d.ver - V0;
+            if (k < 0 || k > n) {
+              bad = 1;
+            } else {
+              atomicMax(&s.A[k], d.call + 1);
+              if (k > 0) atomicMin(&s.B[k - 1], d.ret);
+            }
+          }
+        }
+      } else if (d.ret == kNever || d.ver == -1) {
         inel = 1;  // crashed, or no version: order not pinned
-        continue;
+      } else {
+        const int pos = d.ver - V0 - 1;
+        if (pos < 0 || pos >= n) {
+          bad = 1;
+        } else {
+          atomicMax(&s.A[pos], d.call + 1);
+          atomicMin(&s.B[pos], d.ret);
+          s.Val[pos] = d.val;
+          s.Own[pos] = (uint16_t)r;
+          placed = true;
+        }
       }
-      const int pos = d.ver - V0 - 1;
-      if (pos < 0 || pos >= n) {
-        bad = 1;
-        continue;
-      }
-      if (atomicOr(&s.held[pos >> 5], 1u << (pos & 31)) & (1u << (pos & 31))) {
-        bad = 1;  // two mutations claim one version
-        continue;
-      }
-      atomicMax(&s.A[pos], d.call + 1);
-      atomicMin(&s.B[pos], d.ret);
-      s.Val[pos] = d.val;
-      atomicMax(&s.maxpos, pos);
-      atomicAdd(&s.nmut, 1);
     }
+    nmut += __popcll(__ballot(placed));
   }
-  if (inel) atomicOr(&s.inel, 1);
-  if (bad) atomicOr(&s.bad, 1);
-  if (maxread >= 0) atomicMax(&s.maxread, maxread);
+  // (ballots outside the lane-0 branch: they must see every lane)
+  const uint32_t wsum = (uint32_t)nmut | (__ballot(inel) ? 1u << 16 : 0u) |
+                        (__ballot(bad) ? 1u << 17 : 0u);
+  if (lane == 0) s.wsum[w] = wsum;
   __syncthreads();
-  const int M = s.maxpos + 1;
-  // positions 0..M-1 each held once (no duplicates, so nmut == M means no
-  // gap), and no read beyond the last version
-  bool decided = !s.inel && !s.bad && s.nmut == M && s.maxread <= M;
-  if (decided) {
-    // pass 2: CAS expectations and read claims against the placed values
-#pragma unroll
-    for (int u = 0; u < kPer; u++) {
-      const int r = tid + u * kFastThreads;
-      if (r >= n) continue;
-      const int f = (int)b.w[u].a.x, val = (int)b.w[u].a.y, exp = (int)b.w[u].b.x;
-      const int ver = (int)b.w[u].b.y;
-      if (f == LC_F_CAS) {
-        const int pos = ver - V0 - 1;
-        if (exp != (pos == 0 ? p.init_val : s.Val[pos - 1])) bad = 1;
-      } else if (f == LC_F_READ && ver != -1 && val != -1 && b.w[u].c.y != kInf) {
-        const int k = ver - V0;
-        if (val != (k == 0 ? p.init_val : s.Val[k - 1])) bad = 1;
-      }
-    }
-    // timing: prefix max of L below U
-    const int per = (M + kFastThreads - 1) / kFastThreads;
-    const int k0 = tid * per, k1 = min(k0 + per, M);
-    uint32_t loc = 0;
-    for (int k = k0; k < k1; k++) loc = max(loc, s.A[k]);
-    uint32_t pm = block_max_scan_excl(loc, s.wtot);
-    for (int k = k0; k < k1; k++) {
-      pm = max(pm, s.A[k]);
-      if (pm - 1 >= s.B[k]) bad = 1;  // need max call < U (A holds call + 1)
-    }
-    if (bad) atomicOr(&s.bad, 1);
-    __syncthreads();
-    decided = !s.bad;
+  const uint4 ws = *reinterpret_cast<const uint4 *>(s.wsum);
+  const uint32_t wor = ws.x | ws.y | ws.z | ws.w;
+  // M = mutations placed; M distinct positions all below M <=> positions
+  // 0..M-1 each held once (pass 2 checks both)
+  const int M = (int)((ws.x & 0xFFFF) + (ws.y & 0xFFFF) + (ws.z & 0xFFFF) + (ws.w & 0xFFFF));
+  if (wor >> 16) {  // ineligible or a version out of range: hand over
+    if (tid == 0) fast_tier_handoff(key, n64, jit_keys, status, h_handoff);
+    return;
   }
+  // pass 2: positions, duplicates, CAS expectations and read claims against
+  // the placed values
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int r = tid + u * kFastThreads;
+    if (r >= n) continue;
+    const int f = (int)b.w[u].a.x, val = (int)b.w[u].a.y, exp = (int)b.w[u].b.x;
+    const int ver = (int)b.w[u].b.y;
+    if (f != LC_F_READ) {
+      const int pos = ver - V0 - 1;
+      if (pos >= M || s.Own[pos] != r) {
+        bad = 1;  // a gap below the last version, or a version held twice
+      } else if (f == LC_F_CAS && exp != (pos == 0 ? p.init_val : s.Val[pos - 1])) {
+        bad = 1;
+      }
+    } else if (ver != -1 && b.w[u].c.y != kInf) {
+      const int k = ver - V0;
+      if (k > M)
+        bad = 1;  // a version no mutation wrote
+      else if (val != -1 && val != (k == 0 ? p.init_val : s.Val[k - 1]))
+        bad = 1;
+    }
+  }
+  if (timing_fails(s, M, tid)) bad = 1;
+  const uint32_t wbad = __ballot(bad) ? 1u : 0u;
+  if (lane == 0) s.wbad[w] = wbad;
+  __syncthreads();
   if (tid == 0) {
-    if (decided)
+    const uint4 wb = *reinterpret_cast<const uint4 *>(s.wbad);
+    if (!(wb.x | wb.y | wb.z | wb.w))
       out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
     else
       fast_tier_handoff(key, n64, jit_keys, status, h_handoff);

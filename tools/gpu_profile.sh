@@ -9,19 +9,19 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 TAG=${1:-r01}
 STEPS=${STEPS:-20}
-mkdir -p $O
+mkdir -p $O $O/prof_$TAG
 cd $R
 timeout -k 10 400 python3 bench.py --steps $STEPS --warmup 3 > $O/bench_$TAG.json 2> $O/bench_$TAG.err
 echo "bench done"; cat $O/bench_$TAG.json
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG/kt -o kt --output-format csv -- \
-  python3 $R/bench.py --steps $STEPS --warmup 3 --no-cpu-baseline > $O/prof_$TAG/kt.log 2>&1
+  python3 $R/bench.py --steps $STEPS --warmup 3 --bare > $O/prof_$TAG/kt.log 2>&1
 echo "kernel trace done"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/prof_$TAG/fetch -o fetch --output-format csv -- \
-  python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_$TAG/fetch.log 2>&1
+  python3 $R/bench.py --steps 5 --warmup 1 --bare > $O/prof_$TAG/fetch.log 2>&1
 echo "fetch done"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/prof_$TAG/write -o write --output-format csv -- \
-  python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_$TAG/write.log 2>&1
+  python3 $R/bench.py --steps 5 --warmup 1 --bare > $O/prof_$TAG/write.log 2>&1
 echo "write done"
 find $O/prof_$TAG -name '*.csv' | head -50
