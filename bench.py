@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--ops-per-key", type=int, default=1000)
     ap.add_argument("--concurrency", type=int, default=20)
     ap.add_argument("--p-info", type=float, default=0.0)
-    ap.add_argument("--cpu-sample-keys", type=int, default=5000)
+    ap.add_argument("--cpu-sample-keys", type=int, default=10000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bare", action="store_true",
@@ -88,10 +88,13 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ctx = abi.Context(device_mask=1 << local)
 
+    opts = abi.default_opts()
+    st_buf = abi.LcStats()
+    p_ops, p_off, p_out, p_st = d_ops.data_ptr(), d_off.data_ptr(), d_out.data_ptr(), stream.cuda_stream
+
     def step():
-        ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), args.keys,
-                         d_out.data_ptr(), stream=stream.cuda_stream)
-        return ctx.stats()
+        ctx.check_device(p_ops, p_off, args.keys, p_out, stream=p_st, opts=opts)
+        return ctx.stats_raw(st_buf)
 
     for _ in range(args.warmup):
         step()
@@ -102,12 +105,12 @@ def main():
     kms, hms, fms, jms, gms, njit = [], [], [], [], [], []
     for _ in range(args.steps):
         s = step()
-        kms.append(s["kernel_ms"])
-        hms.append(s["hbm_kernel_ms"])
-        fms.append(s["fast_kernel_ms"])
-        jms.append(s["jit_kernel_ms"])
-        gms.append(s["gap_kernel_ms"])
-        njit.append(s["n_jit_keys"])
+        kms.append(s.kernel_ms)
+        hms.append(s.hbm_kernel_ms)
+        fms.append(s.fast_kernel_ms)
+        jms.append(s.jit_kernel_ms)
+        gms.append(s.gap_kernel_ms)
+        njit.append(s.n_jit_keys)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -180,6 +183,8 @@ def main():
     }
     if rank == 0 and not args.bare:
         line["hot_key"] = hot_key(ctx, abi)
+        line["search_leg"] = search_leg(ctx, abi, d_ops, d_off, d_out, args, stream, n_ops)
+        line["mixed_leg"] = mixed_leg(ctx, abi, dev, stream)
 
     if rank == 0 and world == 1 and not (args.no_cpu_baseline or args.bare):
         line["cpu_baseline"] = cpu_baseline(args, ops, key_off, res)
@@ -206,6 +211,65 @@ def hot_key(ctx, abi):
             "verdict": int(r["verdict"][0]), "crashed_ops": int((ops[:, 5] == abi.LC_INF).sum()),
             "matchings": int(r["configs_explored"][0]), "gaps": int(r["max_frontier"][0]),
             "gap_kernel_ms": float(np.median(gap[1:])), "call_ms": float(np.median(times[1:]))}
+
+
+def search_leg(ctx, abi, d_ops, d_off, d_out, args, stream, n_ops):
+    """The same resident C2 batch with the version-order and gap tiers off
+    (LC_FLAG_NO_FAST_PATH): every key goes through the JIT frontier search
+    (lds_tier_kernel).  Not part of `value`; shows the search kernel's rate."""
+    import torch
+    opts = abi.default_opts(flags=abi.LC_FLAG_NO_FAST_PATH)
+    ms, wall = [], []
+    for i in range(4):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), args.keys, d_out.data_ptr(),
+                         stream=stream.cuda_stream, opts=opts)
+        wall.append(time.perf_counter() - t0)
+        ms.append(ctx.stats()["jit_kernel_ms"])
+    res = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
+    k = float(np.median(ms[1:]))
+    return {"workload": "C2 batch, JIT search for every key (LC_FLAG_NO_FAST_PATH)",
+            "kernel": "lds_tier_kernel", "kernel_ms": k,
+            "ops_per_s": n_ops / (float(np.median(wall[1:]))),
+            "kernel_ops_per_s": n_ops / (k * 1e-3),
+            "valid": int((res["verdict"] == 1).sum()),
+            "max_frontier": int(res["max_frontier"].max())}
+
+
+def mixed_leg(ctx, abi, dev, stream):
+    """BASELINE configs[4] (C5): 1,000 keys x 200 ops, concurrency 10, 10 %
+    of keys with an injected stale read or lost CAS.  Invalid keys pass from
+    the version-order tier to the gap tier, which names the counterexample.
+    Device-resident; verdicts and fail ops checked against the oracle's JIT
+    restatement (not part of `value`)."""
+    import torch
+    import oracle
+    ops, off, labels, _ = abi.synth(1000, 200, concurrency=10, p_anomaly=0.1,
+                                    seed=0x5EED0005)
+    d_ops = torch.from_numpy(ops).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_out = torch.zeros(1000 * abi.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    opts = abi.default_opts()
+    wall, st = [], []
+    for i in range(6):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), 1000, d_out.data_ptr(),
+                         stream=stream.cuda_stream, opts=opts)
+        wall.append((time.perf_counter() - t0) * 1e3)
+        st.append(ctx.stats())
+    res = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
+    _, ref = oracle.check(ops, off, algo=oracle.JIT, n_threads=16)
+    mism = int(((res["verdict"] != ref["verdict"]) | (res["fail_op"] != ref["fail_op"])).sum())
+    med = lambda f: float(np.median([x[f] for x in st[1:]]))
+    return {"workload": "C5: 1000 keys x 200 ops, concurrency 10, 10 % injected anomalies",
+            "call_ms": float(np.median(wall[1:])), "fast_kernel_ms": med("fast_kernel_ms"),
+            "gap_kernel_ms": med("gap_kernel_ms"), "jit_kernel_ms": med("jit_kernel_ms"),
+            "invalid": int((res["verdict"] == 0).sum()),
+            "unknown": int((res["verdict"] == -1).sum()),
+            "ops_per_s": int(off[-1]) / (float(np.median(wall[1:])) * 1e-3),
+            "verdict_or_fail_op_mismatches_vs_oracle": mism}
 
 
 def reduce_run(elapsed, n_ops, res, world, dev):

@@ -164,9 +164,14 @@ class Context:
         return lib().lc_last_error(self._h).decode()
 
     def stats(self):
-        s = LcStats()
-        lib().lc_last_stats(self._h, ctypes.byref(s))
+        s = self.stats_raw()
         return {f: getattr(s, f) for f, _ in LcStats._fields_}
+
+    def stats_raw(self, into=None):
+        """lc_last_stats into an LcStats struct (reused when given)."""
+        s = into if into is not None else LcStats()
+        lib().lc_last_stats(self._h, ctypes.byref(s))
+        return s
 
     def check(self, ops, key_off, opts=None, raise_on_error=True):
         """Host-buffer check. Returns (rc, results structured array)."""

@@ -10,7 +10,7 @@ out=../../../tools/variants/$name
 mkdir -p $out/obj
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c check_kernel.hip -o $out/obj/k.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c gap_tier.hip -o $out/obj/g.o
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -x hip --offload-arch=gfx950 -c lincheck.cpp -o $out/obj/h.o
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC "$@" -x hip --offload-arch=gfx950 -c lincheck.cpp -o $out/obj/h.o
 g++ -O3 -std=c++17 -fPIC -c synth.cpp -o $out/obj/s.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/liblincheck.so $out/obj/*.o -lpthread
 rm -rf $out/obj
