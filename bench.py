@@ -102,7 +102,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kms, hms, fms, jms, gms, njit = [], [], [], [], [], []
+    kms, hms, fms, jms, gms, njit, cms = [], [], [], [], [], [], []
     for _ in range(args.steps):
         s = step()
         kms.append(s.kernel_ms)
@@ -111,6 +111,7 @@ def main():
         jms.append(s.jit_kernel_ms)
         gms.append(s.gap_kernel_ms)
         njit.append(s.n_jit_keys)
+        cms.append(s.total_ms)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -175,7 +176,8 @@ def main():
             "algorithmic_bytes": "48 B/op record read + 40 B/key result (DESIGN.md §6)",
         },
         "tiers": {"fast_kernel_ms": fast_ms, "gap_kernel_ms": gap_ms, "jit_kernel_ms": jit_ms,
-                  "jit_keys": float(np.mean(njit)), "all_kernels_ms": kernel_ms},
+                  "jit_keys": float(np.mean(njit)), "all_kernels_ms": kernel_ms,
+                  "c_call_ms": float(np.mean(cms))},
         "verdicts": {"valid": n_valid, "invalid": n_invalid, "unknown": n_unknown},
         "hbm_tier_ms": float(np.mean(hms)),
         "cpu_baseline": None,
