@@ -18,13 +18,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(abi.LIB_PATH)
     names = []
-    for h in ("lincheck.h", "lincheck_synth.h"):
+    for h in ("lincheck.h", "lincheck_synth.h", "lincheck_edn.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         names += re.findall(r"^\s*(?:const\s+)?\w+\s+\**(lc_\w+)\s*\(", src, re.M)
     assert set(names) == {
         "lc_open", "lc_check", "lc_check_device", "lc_last_stats", "lc_last_error",
         "lc_close", "lc_default_opts", "lc_plan_partition", "lc_abi_version",
-        "lc_synth_register", "lc_synth_key"}
+        "lc_synth_register", "lc_synth_key", "lc_edn_parse", "lc_edn_n_keys", "lc_edn_n_ops",
+        "lc_edn_n_events", "lc_edn_ops", "lc_edn_key_off", "lc_edn_key", "lc_edn_op_text",
+        "lc_edn_value", "lc_edn_free"}
     for n in names:
         assert hasattr(lib, n), n
     assert abi.lib().lc_abi_version() == 1

@@ -12,5 +12,6 @@ mkdir -p $out/obj
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c gap_tier.hip -o $out/obj/g.o
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC "$@" -x hip --offload-arch=gfx950 -c lincheck.cpp -o $out/obj/h.o
 g++ -O3 -std=c++17 -fPIC -c synth.cpp -o $out/obj/s.o
+g++ -O3 -std=c++17 -fPIC -c edn.cpp -o $out/obj/e.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/liblincheck.so $out/obj/*.o -lpthread
 rm -rf $out/obj
