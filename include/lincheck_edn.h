@@ -28,7 +28,8 @@
  *   - :f :read/:write/:cas with a value [version x] (version nil or an
  *     integer; x = [old new] for :cas) packs to (f, value, expected,
  *     version); anything else packs as f = 3 (the device reports :unknown,
- *     as the model's condp would throw);
+ *     as the model's condp would throw).  Other models: LC_EDN_*_REGISTER,
+ *     LC_EDN_MUTEX below;
  *   - values are interned per key by EDN equality (nil -> LC_NIL; integers
  *     and big integers by value, floats apart from integers, vectors equal
  *     to lists, maps and sets order-free), in the order history.py interns
@@ -57,6 +58,16 @@ extern "C" {
 #endif
 
 #define LC_EDN_INDEPENDENT 1 /* values are [k v] tuples: split per key */
+
+/* Model (flags bits 8..11), as in jepsen/etcd_amd/history.py: how an op's
+ * value becomes (value, expected, version).  The initial state is the
+ * model's nil / free state (lc_opts.init_value = LC_NIL, or 0 for MUTEX). */
+#define LC_EDN_VERSIONED_REGISTER (0 << 8) /* register.clj:55-96: [version x] */
+#define LC_EDN_CAS_REGISTER       (1 << 8) /* knossos cas-register: x, cas [old new] */
+#define LC_EDN_REGISTER           (2 << 8) /* knossos register: no :cas step */
+#define LC_EDN_MUTEX              (3 << 8) /* knossos mutex (lock.clj:244): :acquire/:release
+                                              as CAS free(0)->held(1) / held->free */
+#define LC_EDN_MODEL_MASK         (15 << 8)
 
 typedef struct lc_edn_history lc_edn_history;
 

@@ -35,8 +35,32 @@ class VersionedRegister:
         self.version = version
         self.value = value
 
+    name = "versioned-register"
+
     def __repr__(self):  # register.clj:57
         return "v%s: %s" % (self.version, self.value)
+
+
+class CASRegister:
+    """knossos.model/cas-register: a value, read/write/cas, no versions."""
+    name = "cas-register"
+    version = 0
+
+    def __init__(self, value=None):
+        self.value = value
+
+
+class Register(CASRegister):
+    """knossos.model/register: read/write only (a :cas is :unknown)."""
+    name = "register"
+
+
+class Mutex:
+    """knossos.model/mutex, the lock workload's model (lock.clj:244):
+    :acquire / :release of one lock, initially free."""
+    name = "mutex"
+    version = 0
+    value = None
 
 
 def _merge_valid(vs):
@@ -49,12 +73,17 @@ def _merge_valid(vs):
 
 
 class RegisterChecker:
-    """Drop-in for independent/checker + checker/linearizable(VersionedRegister)."""
+    """Drop-in for independent/checker + checker/linearizable(VersionedRegister)
+    (register.clj:108-112).  With independent=False it is a plain
+    checker/linearizable over the whole history, e.g. the lock workload's
+    (checker/linearizable {:model (model/mutex)}) at lock.clj:243-244; the
+    result is then one key's map (no :results)."""
 
-    def __init__(self, model=None, device_mask=0, max_configs_per_key=0):
+    def __init__(self, model=None, device_mask=0, max_configs_per_key=0, independent=True):
         self.model = model or VersionedRegister(0, None)
         self.device_mask = device_mask
         self.max_configs_per_key = max_configs_per_key
+        self.independent = independent
         self._ctx = None
 
     def _context(self):
@@ -63,15 +92,15 @@ class RegisterChecker:
         return self._ctx
 
     def check(self, test, history, opts=None):
-        keys, ops, key_off, done = H.pack(history)
+        m = self.model
+        keys, ops, key_off, done = H.pack(history, model=m.name, independent=self.independent,
+                                          init_value=m.value)
         if not keys:
             return {"valid?": True, "results": {}, "failures": []}
-        interned_init = H.LC_NIL
-        if self.model.value is not None:
-            # the initial value must share the per-key id space; only nil
-            # (the reference's model, register.clj:111) is supported here.
-            raise ValueError("only (->VersionedRegister v nil) initial states are supported")
-        o = abi.default_opts(self.max_configs_per_key, self.model.version, interned_init)
+        # the initial value is interned first in every key (id 0); the mutex
+        # starts free (id MUTEX_FREE)
+        init = H.MUTEX_FREE if m.name == "mutex" else (0 if m.value is not None else H.LC_NIL)
+        o = abi.default_opts(self.max_configs_per_key, m.version, init)
         _, res = self._context().check(ops, key_off, o)
         results = {}
         for i, k in enumerate(keys):
@@ -87,6 +116,8 @@ class RegisterChecker:
             elif v == UNKNOWN:
                 out["cause"] = abi.REASONS.get(int(r["reason"]), "?")
             results[k] = out
+        if not self.independent:
+            return results[None]
         return {"valid?": _merge_valid(r["valid?"] for r in results.values()),
                 "results": results,
                 "failures": [k for k, r in results.items() if r["valid?"] is False]}
@@ -99,6 +130,12 @@ class RegisterChecker:
 
 def register_checker(**kw):
     return RegisterChecker(**kw)
+
+
+def linearizable(model, **kw):
+    """checker/linearizable {:model model} over the whole history (no
+    independent split)."""
+    return RegisterChecker(model=model, independent=False, **kw)
 
 
 def check_safe(checker, test, history, opts=None):

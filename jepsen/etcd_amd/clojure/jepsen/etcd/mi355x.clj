@@ -101,23 +101,43 @@
             (let [i (count @ids)] (vswap! ids assoc v i) i))))))
 
 (defn- record
-  "[f value expected version call ret] for one completed op
-  (register.clj:22-44, 98-100); f 3 (unknown) if the shape does not match,
-  which the GPU reports as :unknown like the model's throwing step (:63)."
-  [intern {:keys [op call ret]}]
-  (let [[version v] (:value op)
-        f (case (:f op) :read 0 :write 1 :cas 2 3)]
-    (if (or (= f 3) (and (some? version) (not (integer? version)))
-            (and (= f 2) (not (sequential? v))))
-      [3 LC_NIL LC_NIL LC_NIL call ret]
-      (let [ver (if (nil? version) LC_NIL (long version))]
-        (if (= f 2)
-          [2 (intern (second v)) (intern (first v)) ver call ret]
-          [f (intern v) LC_NIL ver call ret])))))
+  "[f value expected version call ret] for one completed op under model
+  (register.clj:22-44, 98-100 for :versioned-register); f 3 (unknown) if the
+  shape does not match, which the GPU reports as :unknown like the model's
+  throwing step (:63).  Other knossos models are packings of the same
+  records (jepsen/etcd_amd/history.py, \"Models\"): :cas-register and
+  :register values carry no version; :mutex (lock.clj:244) packs :acquire
+  as a CAS free(0) -> held(1) and :release as the reverse."
+  [model intern {:keys [op call ret]}]
+  (case model
+    :mutex
+    (case (:f op)
+      :acquire [2 1 0 LC_NIL call ret]
+      :release [2 0 1 LC_NIL call ret]
+      [3 LC_NIL LC_NIL LC_NIL call ret])
+
+    (:cas-register :register)
+    (let [v (:value op)
+          f (case (:f op) :read 0 :write 1 :cas (if (= model :register) 3 2) 3)]
+      (cond (= f 3)                                 [3 LC_NIL LC_NIL LC_NIL call ret]
+            (and (= f 2) (not (and (sequential? v) (= 2 (count v)))))
+                                                    [3 LC_NIL LC_NIL LC_NIL call ret]
+            (= f 2) [2 (intern (second v)) (intern (first v)) LC_NIL call ret]
+            :else   [f (intern v) LC_NIL LC_NIL call ret]))
+
+    (let [[version v] (:value op)
+          f (case (:f op) :read 0 :write 1 :cas 2 3)]
+      (if (or (= f 3) (and (some? version) (not (integer? version)))
+              (and (= f 2) (not (sequential? v))))
+        [3 LC_NIL LC_NIL LC_NIL call ret]
+        (let [ver (if (nil? version) LC_NIL (long version))]
+          (if (= f 2)
+            [2 (intern (second v)) (intern (first v)) ver call ret]
+            [f (intern v) LC_NIL ver call ret]))))))
 
 (defn- pack
   "Packs all keys: returns [keys completed-per-key ^Memory ops ^Memory key-off]."
-  [subs]
+  [model subs]
   (let [keys  (vec (keys subs))
         done  (mapv (fn [k] (complete (get subs k))) keys)
         n     (reduce + (map count done))
@@ -127,7 +147,7 @@
       (.setLong off (* 8 ki) i)
       (when (< ki (count keys))
         (let [intern (interner)
-              recs   (map (partial record intern) (nth done ki))
+              recs   (map (partial record model intern) (nth done ki))
               i'     (reduce (fn [i r]
                                (dotimes [j 6]
                                  (.setLong ops (+ (* i op-bytes) (* 8 j)) (long (nth r j))))
@@ -141,44 +161,62 @@
         (some #{:unknown} vs)     :unknown
         :else                     true))
 
+(defn- check-keys
+  "One lc_check over subs {k [op ...]}: {k result-map}."
+  [model max-configs-per-key subs]
+  (let [[keys done ops off] (pack model subs)
+        nk   (count keys)
+        out  (Memory. (* result-bytes nk))
+        o    (doto (Memory. 40)
+               (.setLong 0 0) (.setLong 8 (if (= model :mutex) 0 LC_NIL))
+               (.setLong 16 max-configs-per-key)
+               (.setLong 24 0) (.setLong 32 0))
+        rc   (locking ctx
+               (.invokeInt (fun "lc_check")
+                           (object-array [@ctx ops off (long nk) o out])))]
+    (when-not (zero? rc)
+      (throw (ex-info "lc_check failed"
+                      {:rc rc :error (.invoke (fun "lc_last_error")
+                                              String (object-array [@ctx]))})))
+    (into (array-map)
+          (for [ki (range nk)]
+            (let [b       (* ki result-bytes)
+                  verdict (.getInt out b)
+                  reason  (.getInt out (+ b 4))
+                  fail-op (.getLong out (+ b 8))
+                  v       (case verdict 1 true 0 false :unknown)]
+              [(nth keys ki)
+               (cond-> {:valid?   v
+                        :analyzer :mi355x
+                        :configs  (.getLong out (+ b 24))}
+                 (false? v)   (assoc :op (let [r (nth (nth done ki) fail-op)]
+                                           (or (:completion r) (:op r))))
+                 (= v :unknown) (assoc :error [:lincheck-reason reason]))])))))
+
+(defn linearizable
+  "(checker/linearizable {:model m}) over the whole history, for the knossos
+  models this library packs: opts :model one of :versioned-register,
+  :cas-register, :register, :mutex.  The lock workload's checker
+  (lock.clj:243-244) becomes (linearizable {:model :mutex})."
+  [{:keys [model max-configs-per-key] :or {model :versioned-register max-configs-per-key 0}}]
+  (reify checker/Checker
+    (check [_ test history _opts]
+      (let [ops (filterv client-op? history)]
+        (if (empty? ops)
+          {:valid? true :analyzer :mi355x}
+          (get (check-keys model max-configs-per-key {nil ops}) nil))))))
+
 (defn checker
-  "The drop-in (see ns doc).  opts: :max-configs-per-key (0 = default)."
+  "The drop-in (see ns doc).  opts: :max-configs-per-key (0 = default),
+  :model (default :versioned-register, register.clj:111)."
   ([] (checker {}))
-  ([{:keys [max-configs-per-key] :or {max-configs-per-key 0}}]
+  ([{:keys [max-configs-per-key model] :or {max-configs-per-key 0 model :versioned-register}}]
    (reify checker/Checker
      (check [_ test history _opts]
        (let [subs (subhistories history)]
          (if (empty? subs)
            {:valid? true :results {} :failures []}
-           (let [[keys done ops off] (pack subs)
-                 nk   (count keys)
-                 out  (Memory. (* result-bytes nk))
-                 o    (doto (Memory. 40)
-                        (.setLong 0 0) (.setLong 8 LC_NIL)
-                        (.setLong 16 max-configs-per-key)
-                        (.setLong 24 0) (.setLong 32 0))
-                 rc   (locking ctx
-                        (.invokeInt (fun "lc_check")
-                                    (object-array [@ctx ops off (long nk) o out])))]
-             (when-not (zero? rc)
-               (throw (ex-info "lc_check failed"
-                               {:rc rc :error (.invoke (fun "lc_last_error")
-                                                       String (object-array [@ctx]))})))
-             (let [results
-                   (into (array-map)
-                         (for [ki (range nk)]
-                           (let [b       (* ki result-bytes)
-                                 verdict (.getInt out b)
-                                 reason  (.getInt out (+ b 4))
-                                 fail-op (.getLong out (+ b 8))
-                                 v       (case verdict 1 true 0 false :unknown)]
-                             [(nth keys ki)
-                              (cond-> {:valid?   v
-                                       :analyzer :mi355x
-                                       :configs  (.getLong out (+ b 24))}
-                                (false? v)   (assoc :op (let [r (nth (nth done ki) fail-op)]
-                                                          (or (:completion r) (:op r))))
-                                (= v :unknown) (assoc :error [:lincheck-reason reason]))])))]
-               {:valid?   (merge-valid (map :valid? (vals results)))
-                :results  results
-                :failures (vec (for [[k r] results :when (false? (:valid? r))] k))}))))))))
+           (let [results (check-keys model max-configs-per-key subs)]
+             {:valid?   (merge-valid (map :valid? (vals results)))
+              :results  results
+              :failures (vec (for [[k r] results :when (false? (:valid? r))] k))})))))))

@@ -443,7 +443,7 @@ void put_val(const Parser &ps, uint32_t id, std::string &pool, Val &v) {
 }
 
 void parse_chunk(const char *text, const std::vector<std::pair<size_t, size_t>> &forms, size_t f0,
-                 size_t f1, bool independent, uint32_t tid, Chunk &out) {
+                 size_t f1, bool independent, bool versioned, uint32_t tid, Chunk &out) {
   Parser ps;
   ps.s = text;
   out.ops.reserve(f1 - f0);
@@ -476,7 +476,8 @@ void parse_chunk(const char *text, const std::vector<std::pair<size_t, size_t>> 
         o.type = ps.kw_is(v, ":invoke") ? 0 : ps.kw_is(v, ":ok") ? 1 : ps.kw_is(v, ":fail") ? 2
                  : ps.kw_is(v, ":info") ? 3 : -1;
       } else if (ps.kw_is(key, ":f")) {
-        o.f = ps.kw_is(v, ":read") ? 0 : ps.kw_is(v, ":write") ? 1 : ps.kw_is(v, ":cas") ? 2 : 3;
+        o.f = ps.kw_is(v, ":read") ? 0 : ps.kw_is(v, ":write") ? 1 : ps.kw_is(v, ":cas") ? 2
+              : ps.kw_is(v, ":acquire") ? 4 : ps.kw_is(v, ":release") ? 5 : 3;
       } else if (ps.kw_is(key, ":process")) {
         o.client = vn.t == N_INT;
         o.process = vn.i;
@@ -493,7 +494,16 @@ void parse_chunk(const char *text, const std::vector<std::pair<size_t, size_t>> 
         put_val(ps, ps.kid(v, 0), out.pool, o.key);
         v = ps.kid(v, 1);
       }
-      if (ps.is_pair(v)) {
+      if (!versioned) {  // knossos (cas-)register: the value is x itself
+        o.v_pair = 1;
+        o.ver_kind = 0;
+        put_val(ps, v, out.pool, o.x);
+        if (ps.is_pair(v)) {
+          o.x_pair = 1;
+          put_val(ps, ps.kid(v, 0), out.pool, o.x0);
+          put_val(ps, ps.kid(v, 1), out.pool, o.x1);
+        }
+      } else if (ps.is_pair(v)) {
         o.v_pair = 1;
         const Node &ver = ps.nodes[ps.kid(v, 0)];
         o.ver_kind = ver.t == N_NIL ? 0 : ver.t == N_INT ? 1 : 2;
@@ -555,6 +565,8 @@ int lc_edn_parse(const char *text, size_t len, int64_t flags, int n_threads,
   if (!out || (!text && len)) return fail("null argument", 0);
   *out = nullptr;
   const bool independent = flags & LC_EDN_INDEPENDENT;
+  const int64_t model = flags & LC_EDN_MODEL_MASK;
+  if (model > LC_EDN_MUTEX) return fail("unknown model in flags", 0);
   const bool timing = getenv("LC_EDN_TIMING") != nullptr;
   auto t_last = std::chrono::steady_clock::now();
   auto lap = [&](const char *what) {
@@ -598,7 +610,8 @@ int lc_edn_parse(const char *text, size_t len, int64_t flags, int n_threads,
       const size_t f0 = forms.size() * t / T, f1 = forms.size() * (t + 1) / T;
       th.emplace_back([&, f0, f1, t] {
         const auto a = std::chrono::steady_clock::now();
-        parse_chunk(text, forms, f0, f1, independent, (uint32_t)t, ch[t]);
+        parse_chunk(text, forms, f0, f1, independent, model == LC_EDN_VERSIONED_REGISTER,
+                    (uint32_t)t, ch[t]);
         if (timing)
           fprintf(stderr, "  thread %d: %zu forms %.1f ms\n", t, f1 - f0,
                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count());
@@ -706,6 +719,7 @@ int lc_edn_parse(const char *text, size_t len, int64_t flags, int n_threads,
         }
       }
       KeyOut &out = ko[k];
+      if (model == LC_EDN_MUTEX) out.values = {"free", "held"};
       Interner in;
       in.shown = &out.values;
       in.text = text;
@@ -715,7 +729,10 @@ int lc_edn_parse(const char *text, size_t len, int64_t flags, int n_threads,
         const POp &vo = r.type == 1 ? ch[r.cc].ops[r.ci] : inv;  // :ok copies its value in
         lc_op rec{inv.f, LC_NIL, LC_NIL, LC_NIL, r.call, r.ret};
         const bool shape = vo.v_pair && vo.ver_kind != 2 && (inv.f != LC_F_CAS || vo.x_pair);
-        if (inv.f > LC_F_CAS || !shape) {
+        if (model == LC_EDN_MUTEX) {  // acquire: CAS free(0) -> held(1); release: the reverse
+          rec.f = inv.f == 4 || inv.f == 5 ? LC_F_CAS : 3;
+          if (rec.f == LC_F_CAS) rec.value = inv.f == 4 ? 1 : 0, rec.expected = inv.f == 4 ? 0 : 1;
+        } else if (inv.f > LC_F_CAS || !shape || (model == LC_EDN_REGISTER && inv.f == LC_F_CAS)) {
           rec.f = 3;
         } else {
           rec.version = vo.ver_kind == 0 ? LC_NIL : vo.ver;

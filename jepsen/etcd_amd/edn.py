@@ -27,6 +27,8 @@ from . import abi
 from .history import Tuple
 
 LC_EDN_INDEPENDENT = 1
+MODEL_FLAGS = {"versioned-register": 0 << 8, "cas-register": 1 << 8, "register": 2 << 8,
+               "mutex": 3 << 8}
 _bound = False
 
 
@@ -61,7 +63,7 @@ class EdnHistory:
     """A parsed history.  `ops` (n, 6) int64 and `key_off` are copies; the
     source text is kept alive for op_text()."""
 
-    def __init__(self, text, independent=True, n_threads=0):
+    def __init__(self, text, independent=True, n_threads=0, model="versioned-register"):
         L = _lib()
         self._text = text  # bytes / mmap: the C side keeps pointers into it
         if isinstance(text, bytes):
@@ -72,7 +74,8 @@ class EdnHistory:
         h = ctypes.c_void_p()
         err = ctypes.create_string_buffer(256)
         rc = L.lc_edn_parse(ptr, len(text),
-                            LC_EDN_INDEPENDENT if independent else 0, n_threads,
+                            (LC_EDN_INDEPENDENT if independent else 0) | MODEL_FLAGS[model],
+                            n_threads,
                             ctypes.byref(h), err, 256)
         if rc != 0:
             raise abi.LcError(rc, err.value.decode())
@@ -105,25 +108,27 @@ class EdnHistory:
     __del__ = close
 
 
-def read(src, independent=True, n_threads=0):
+def read(src, independent=True, n_threads=0, model="versioned-register"):
     """Parse a history.edn given as a path, bytes or str."""
     if isinstance(src, str) and os.path.exists(src):
         with open(src, "rb") as fh:
             size = os.fstat(fh.fileno()).st_size
             if size == 0:
-                return EdnHistory(b"", independent, n_threads)
+                return EdnHistory(b"", independent, n_threads, model)
             mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_COPY)
-        return EdnHistory(mm, independent, n_threads)
+        return EdnHistory(mm, independent, n_threads, model)
     if isinstance(src, str):
         src = src.encode()
-    return EdnHistory(bytes(src), independent, n_threads)
+    return EdnHistory(bytes(src), independent, n_threads, model)
 
 
-def check(src, device_mask=0, independent=True, ctx=None, opts=None):
+def check(src, device_mask=0, independent=True, ctx=None, opts=None, model="versioned-register"):
     """Decide every key of a history.edn on the GPU.  Returns
     (result map, EdnHistory); the map has independent/checker's shape with
     EDN key texts as keys."""
-    h = src if isinstance(src, EdnHistory) else read(src, independent)
+    h = src if isinstance(src, EdnHistory) else read(src, independent, model=model)
+    if opts is None and model == "mutex":
+        opts = abi.default_opts(init_value=0)  # the lock starts free
     own = ctx is None
     ctx = ctx or abi.Context(device_mask)
     try:
@@ -224,10 +229,12 @@ def main(argv=None):
     ap.add_argument("history")
     ap.add_argument("--single-key", action="store_true",
                     help="values are not independent tuples: one key")
+    ap.add_argument("--model", default="versioned-register", choices=sorted(MODEL_FLAGS),
+                    help="knossos model (lock workload: mutex with --single-key)")
     ap.add_argument("--gpus", type=lambda s: int(s, 0), default=0,
                     help="device mask (0 = all GPUs)")
     a = ap.parse_args(argv)
-    result, h = check(a.history, device_mask=a.gpus, independent=not a.single_key)
+    result, h = check(a.history, device_mask=a.gpus, independent=not a.single_key, model=a.model)
     print(render(result))
     return 0 if result["valid?"] is True else 1
 

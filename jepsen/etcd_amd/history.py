@@ -18,6 +18,22 @@ model's step function for the register workload:
 
 Histories are sequences of dicts {"type", "f", "process", "value"[, "index"]}
 with string keywords ("invoke", "ok", "fail", "info"; "read", "write", "cas").
+
+Models: the record format is the device's model.
+A register op's precondition is a (version, value) match and its effect a
+version bump plus a new value, so knossos's other register-like models are
+packings, not new kernels:
+
+* "versioned-register" — register.clj:55-96: values [version x];
+* "cas-register" — knossos.model/cas-register: values are x itself, no
+  versions (a nil version is never checked, register.clj:64-92); read nil
+  matches any state;
+* "register" — knossos.model/register: as cas-register, and a :cas has no
+  step (knossos's condp throws), so it packs as an unknown f;
+* "mutex" — knossos.model/mutex, the lock workload's model (lock.clj:244):
+  the state is held / free; :acquire is a CAS free -> held, :release a CAS
+  held -> free, with the fixed value ids FREE = 0 and HELD = 1 and the
+  initial state free.
 """
 from collections import namedtuple
 
@@ -150,28 +166,72 @@ def complete(subhistory):
     return [r for r in ops if r["type"] != "fail"]
 
 
-def pack_key(subhistory, intern=None):
+def _fields_plain(f, value, intern):
+    """knossos cas-register: read/write x, cas [old new]; no versions."""
+    if f == LC_F_CAS:
+        if not isinstance(value, (list, tuple)) or len(value) != 2:
+            return None
+        return intern(value[1]), intern(value[0]), LC_NIL
+    return intern(value), LC_NIL, LC_NIL
+
+
+MUTEX_FREE, MUTEX_HELD = 0, 1
+
+
+def _record(model, fk, value, intern):
+    """(f, value, expected, version) of one completed op under `model`."""
+    if model == "mutex":
+        if fk == "acquire":
+            return LC_F_CAS, MUTEX_HELD, MUTEX_FREE, LC_NIL
+        if fk == "release":
+            return LC_F_CAS, MUTEX_FREE, MUTEX_HELD, LC_NIL
+        return F_UNKNOWN, LC_NIL, LC_NIL, LC_NIL
+    f = F_CODES.get(fk, F_UNKNOWN)
+    if model == "register" and f == LC_F_CAS:
+        f = F_UNKNOWN
+    flds = None
+    if f != F_UNKNOWN:
+        flds = (_fields if model == "versioned-register" else _fields_plain)(f, value, intern)
+    if flds is None:
+        return F_UNKNOWN, LC_NIL, LC_NIL, LC_NIL
+    return (f,) + tuple(flds)
+
+
+MODELS = ("versioned-register", "cas-register", "register", "mutex")
+
+
+def pack_key(subhistory, intern=None, model="versioned-register"):
     """One key's subhistory -> (records (n,6) int64, completed ops list)."""
+    if model not in MODELS:
+        raise ValueError("unknown model %r (one of %s)" % (model, ", ".join(MODELS)))
     intern = intern or Interner()
     done = complete(subhistory)
     recs = np.zeros((len(done), 6), dtype=np.int64)
     for i, r in enumerate(done):
-        f = F_CODES.get(r["f"], F_UNKNOWN)
-        flds = _fields(f, r["value"], intern) if f != F_UNKNOWN else None
-        if flds is None:
-            f, flds = F_UNKNOWN, (LC_NIL, LC_NIL, LC_NIL)
-        recs[i] = (f, flds[0], flds[1], flds[2], r["call"], r["ret"])
+        f, v, e, ver = _record(model, r["f"], r["value"], intern)
+        recs[i] = (f, v, e, ver, r["call"], r["ret"])
     return recs, done
 
 
-def pack(history):
-    """Whole history -> (keys, ops (n,6), key_off, per-key completed ops)."""
+def pack(history, model="versioned-register", independent=True, init_value=None):
+    """Whole history -> (keys, ops (n,6), key_off, per-key completed ops).
+
+    independent=False checks the history as one key (checker/linearizable
+    without jepsen.independent, as lock.clj:243-244 does); its key is None.
+    A non-nil init_value is interned first in every key, so it is id 0 there
+    (pass 0 as lc_opts.init_value)."""
     hist = index_history(history)
-    subs = split_by_key(hist)
+    if independent:
+        subs = split_by_key(hist)
+    else:
+        subs = {None: [op for op in hist if is_client(op)]}
     keys = list(subs.keys())
     parts, done = [], []
     for k in keys:
-        recs, d = pack_key(subs[k])
+        it = Interner()
+        if init_value is not None and model != "mutex":
+            it(init_value)
+        recs, d = pack_key(subs[k], it, model)
         parts.append(recs)
         done.append(d)
     key_off = np.zeros(len(keys) + 1, dtype=np.int64)

@@ -105,3 +105,61 @@ def random_tiny(rng, n_ops, p_info=0.2, p_perturb=0.35, n_values=3):
 def tiny_batch(seed, n_keys, max_ops=6):
     rng = random.Random(seed)
     return [random_tiny(rng, rng.randrange(0, max_ops + 1)) for _ in range(n_keys)]
+
+
+# ---- other knossos models (history.py "Models"): record-level generators
+FREE, HELD = 0, 1
+
+
+def _intervals(rng, n, infos, spread=25):
+    """Distinct call/ret indices around linearization points 10i+5."""
+    times = []
+    for i in range(n):
+        lin = 10 * i + 5
+        call = lin - rng.randrange(1, spread)
+        ret = INF if infos[i] else lin + rng.randrange(1, spread)
+        times.append((call, ret))
+    ev = []
+    for i, (c, r) in enumerate(times):
+        ev.append((c, 0, i))
+        if r != INF:
+            ev.append((r, 1, i))
+    ev.sort()
+    cidx, ridx = {}, {}
+    for k, (_, kind, i) in enumerate(ev):
+        (ridx if kind else cidx)[i] = k
+    return [(cidx[i], ridx.get(i, INF)) for i in range(n)]
+
+
+def random_mutex(rng, n_ops, p_info=0.15, p_perturb=0.35):
+    """A knossos mutex history as records (acquire = CAS FREE->HELD, release
+    = CAS HELD->FREE, no versions, initial state FREE): a random sequential
+    run of the lock (an acquire of a held lock or a release of a free one is
+    :fail and dropped), crashed ops that take effect with p = 0.5, intervals
+    around the linearization points, then (with p_perturb) one op flipped."""
+    held = False
+    recs, infos = [], []
+    for _ in range(n_ops):
+        acq = rng.random() < 0.5
+        info = rng.random() < p_info
+        legal = (not held) if acq else held
+        if not legal and not info:
+            continue  # :fail, dropped by completion
+        if legal and (not info or rng.random() < 0.5):
+            held = acq
+        recs.append([C, HELD, FREE, N] if acq else [C, FREE, HELD, N])
+        infos.append(info)
+    out = [r + list(t) for r, t in zip(recs, _intervals(rng, len(recs), infos))]
+    out.sort(key=lambda r: r[4])
+    if out and rng.random() < p_perturb:
+        j = rng.randrange(len(out))
+        out[j][1], out[j][2] = out[j][2], out[j][1]  # acquire <-> release
+    return out
+
+
+def random_casreg(rng, n_ops, p_info=0.2, p_perturb=0.35, n_values=3):
+    """knossos cas-register records: random_tiny with every version nil."""
+    out = random_tiny(rng, n_ops, p_info, p_perturb, n_values)
+    for r in out:
+        r[3] = N
+    return out
