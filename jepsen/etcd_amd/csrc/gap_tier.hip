@@ -35,13 +35,21 @@
 // bisection over r, each probe one decision on the prefix (ops called after
 // r dropped, ops returning after r pending = optional).
 //
-// One 256-thread workgroup decides one key: the record scan, the suffix-min
-// scan, gap/optional-op compaction and every matching pass (greedy, then a
-// level-synchronous BFS per augmenting path over all (frontier gap, op)
-// pairs) are spread over the workgroup; the workspace (O(n) int32 arrays) is
-// per workgroup in HBM/L2.  Keys it cannot decide (an :ok mutation without a
-// version, a read [nil x], malformed records, the branch budget) go on to the
-// JIT tier.
+// One 256-thread workgroup makes one decision (a key's whole history, or one
+// prefix of it): the record scan, the suffix-min scan and the gap/optional-op
+// compaction are spread over the workgroup, with O(n) int32 arrays per
+// workgroup in HBM/L2.  The matching itself is serial in the gaps, so wave 0
+// runs it alone, barrier-free, over compact per-gap / per-op arrays staged in
+// LDS (HBM fallback when they do not fit): first-fit over the free ops
+// (ballot over 64 ops at a time, ops sorted by call so the deadline cuts the
+// scan), then a depth-first augmenting path per gap first-fit cannot fill
+// (Kuhn's algorithm; visit stamps instead of clears).  Branch nodes are warm
+// started: fixing a free gap's value only unmatches the pairs it makes
+// ineligible.  The counterexample search is a multisection: P workgroups
+// probe P prefixes of each open interval per round (GapJob, kernels.h), so a
+// single hot key (BASELINE configs[3]) spreads over the whole GPU.  Keys it
+// cannot decide (an :ok mutation without a version, a read [nil x], malformed
+// records, the branch budget) go on to the JIT tier.
 #include <algorithm>
 #include <climits>
 
@@ -52,57 +60,63 @@ namespace lcdev {
 namespace {
 
 constexpr int kGapThreads = 256;
-constexpr int kAny = INT_MIN;  // no value required / not a CAS
+constexpr int kGapWaves = kGapThreads / kWave;
+constexpr int kAny = INT_MIN;      // no value required / not a CAS
 constexpr int kNodeBudget = 4096;  // matching passes per decision
-constexpr int kGapArrays = 21;     // 32-bit arrays in GapWs
+constexpr int kGapArrays = 24;     // 32-bit arrays of `cap` entries per workgroup
 
-enum { GD_VALID = 1, GD_INVALID = 0, GD_NA = -1, GD_BUDGET = -2 };
+enum { GD_VALID = 1, GD_INVALID = 0, GD_NA = -1, GD_BUDGET = -2, GD_SKIP = -3 };
 enum { F_NA = 1, F_INVALID = 2 };
 
-// Per-workgroup workspace: kGapArrays arrays of `cap` 32-bit entries.
+// Matching footprint of one decision in LDS: per gap a 16-byte record and 4
+// ints, per op a 16-byte record and 2 ints.
+__host__ __device__ constexpr int match_lds_bytes(int G, int n_opt) {
+  return 32 * G + 24 * n_opt;
+}
+
+extern __shared__ int4 lds_dyn[];
+
+// Per-workgroup workspace: kGapArrays arrays of `cap` 32-bit entries (cap a
+// multiple of 4, so the 16-byte record regions stay aligned).
+//   0 A  1 B  2 Uh  3 Pin  4 Val  5 PinExp  6 Claim  7 Req  8 (spare)  9 Gap
+//   10..13 Opt: the optional ops as 16-byte records (call, value, exp, pos)
+//   14..17 gap records, 18..23 the matching's scalar arrays — the HBM homes
+//   of the matching when it does not fit in LDS; during gap_setup 18..23
+//   also hold the ballot masks and prefix counts of the compactions.
 struct GapWs {
-  uint32_t *A, *B, *Uh, *OptCall;
-  int *Pin, *Val, *PinExp, *Claim, *Req, *GI, *Gap, *OptVal, *OptExp, *OptPos;
-  int *MatchOp, *MatchGap, *Par, *Fr0, *Fr1, *StPos, *StVal;
+  int32_t *base;
+  int64_t cap;
+  uint32_t *A, *B, *Uh;
+  int *Pin, *Val, *PinExp, *Claim, *Req, *Gap;
+  int4 *Opt;
+  uint64_t *Mask;  // compaction ballots (array 18..)
+  int *Pre;        // compaction prefix counts (array 20..)
 };
 
 struct GapSh {
-  int flag, maxpos, maxread, n_opt, n_gap, total;
-  int found, n_next, viol, cand;
+  int flag, maxpos, maxread, n_opt, n_gap;
+  int res;
   uint32_t maxret;
-  int wtot[kGapThreads / kWave];
-  uint32_t wtotu[kGapThreads / kWave];
+  int wtot[kGapWaves];
+  uint32_t wtotu[kGapWaves];
 };
 
 __device__ __forceinline__ GapWs gap_ws(int32_t *base, int64_t cap) {
   GapWs w;
-  int32_t *p = base;
-  auto nxt = [&]() {
-    int32_t *q = p;
-    p += cap;
-    return q;
-  };
-  w.A = (uint32_t *)nxt();
-  w.B = (uint32_t *)nxt();
-  w.Uh = (uint32_t *)nxt();
-  w.OptCall = (uint32_t *)nxt();
-  w.Pin = nxt();
-  w.Val = nxt();
-  w.PinExp = nxt();
-  w.Claim = nxt();
-  w.Req = nxt();
-  w.GI = nxt();
-  w.Gap = nxt();
-  w.OptVal = nxt();
-  w.OptExp = nxt();
-  w.OptPos = nxt();
-  w.MatchOp = nxt();
-  w.MatchGap = nxt();
-  w.Par = nxt();
-  w.Fr0 = nxt();
-  w.Fr1 = nxt();
-  w.StPos = nxt();
-  w.StVal = nxt();
+  w.base = base;
+  w.cap = cap;
+  w.A = (uint32_t *)(base + 0 * cap);
+  w.B = (uint32_t *)(base + 1 * cap);
+  w.Uh = (uint32_t *)(base + 2 * cap);
+  w.Pin = base + 3 * cap;
+  w.Val = base + 4 * cap;
+  w.PinExp = base + 5 * cap;
+  w.Claim = base + 6 * cap;
+  w.Req = base + 7 * cap;
+  w.Gap = base + 9 * cap;
+  w.Opt = reinterpret_cast<int4 *>(base + 10 * cap);
+  w.Mask = reinterpret_cast<uint64_t *>(base + 18 * cap);
+  w.Pre = base + 20 * cap;
   return w;
 }
 
@@ -119,7 +133,7 @@ __device__ __forceinline__ int block_excl_sum(int v, GapSh &sh, int *total) {
   __syncthreads();
   int pre = 0, tot = 0;
 #pragma unroll
-  for (int j = 0; j < kGapThreads / kWave; j++) {
+  for (int j = 0; j < kGapWaves; j++) {
     if (j < w) pre += sh.wtot[j];
     tot += sh.wtot[j];
   }
@@ -141,12 +155,53 @@ __device__ __forceinline__ uint32_t block_suffix_min_excl(uint32_t v, GapSh &sh)
   __syncthreads();
   uint32_t post = kNever;
 #pragma unroll
-  for (int j = 0; j < kGapThreads / kWave; j++)
+  for (int j = 0; j < kGapWaves; j++)
     if (j > w) post = post < sh.wtotu[j] ? post : sh.wtotu[j];
   uint32_t excl = (uint32_t)__shfl_down((int)incl, 1);
   if (lane == kWave - 1) excl = kNever;
   __syncthreads();
   return post < excl ? post : excl;
+}
+
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+
+__device__ __forceinline__ int first_lane(uint64_t b) { return (int)__builtin_ctzll(b); }
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ int4 uni4(int4 v) {
+  return make_int4(uni(v.x), uni(v.y), uni(v.z), uni(v.w));
+}
+
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+  const int lane = threadIdx.x & (kWave - 1);
+  return __popcll(m & ((1ull << lane) - 1));
+}
+
+// Makes this wave's earlier stores to the matching arrays visible to all of
+// its lanes (LDS: lgkmcnt; HBM fallback: vmcnt, same CU so L1-coherent).
+__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+// Stable compaction, phase 2: word-level exclusive prefix of the ballot
+// masks Mask[0..nw) into Pre[0..nw); returns the total.  Two barriers.
+__device__ int mask_prefix(const GapWs &w, int nw, GapSh &sh) {
+  const int tid = threadIdx.x;
+  const int per = (nw + kGapThreads - 1) / kGapThreads;
+  const int k0 = min(tid * per, nw), k1 = min(k0 + per, nw);
+  int loc = 0;
+  for (int k = k0; k < k1; k++) loc += __popcll(w.Mask[k]);
+  int tot;
+  int run = block_excl_sum(loc, sh, &tot);
+  for (int k = k0; k < k1; k++) {
+    w.Pre[k] = run;
+    run += __popcll(w.Mask[k]);
+  }
+  __syncthreads();
+  return tot;
 }
 
 struct GapKey {
@@ -158,31 +213,84 @@ struct GapKey {
   GapSh *sh;
 };
 
-__device__ __forceinline__ int value_before(const GapKey &g, int pos) {
-  if (pos == 0) return g.init;
-  return g.ws.Pin[pos - 1] != -1 ? g.ws.Val[pos - 1] : g.ws.Req[pos - 1];
+// One record of the prefix at `cut`, classified.
+enum { K_NONE, K_READ, K_PIN, K_OPT };
+struct Cls {
+  int kind;   // K_*
+  int k;      // K_READ: version index; K_PIN: position
+  int val;    // K_READ: claimed value (-1 none); K_PIN: value written
+  int exp;    // K_PIN: CAS expectation (kAny for a write)
+  uint32_t call, ret;
+  int4 op;    // K_OPT: the optional op's record (call, value, exp, pos)
+};
+
+__device__ __forceinline__ Cls classify(const GapKey &g, const Raw &raw, int64_t prev_call,
+                                        int r, uint32_t cut, int *flag, uint32_t *maxret) {
+  Cls c;
+  c.kind = K_NONE;
+  const int n = g.n;
+  const Rec d = decode(raw, g.base);
+  if (d.bad || d.f > LC_F_CAS || (r > 0 && prev_call >= raw.c.x) || raw.c.x < 0) {
+    *flag |= F_NA;  // the JIT tier reports malformed / unknown :f
+    return c;
+  }
+  if (d.call > cut) return c;
+  const uint32_t ret = d.ret > cut ? kNever : d.ret;  // pending at the cut
+  if (ret != kNever) *maxret = max(*maxret, ret);
+  c.call = d.call;
+  c.ret = ret;
+  if (d.f == LC_F_READ) {
+    if (ret == kNever || (d.ver == -1 && d.val == -1)) return c;  // never constrains
+    if (d.ver == -1) {
+      *flag |= F_NA;  // read [nil x]: its version is free
+      return c;
+    }
+    const int k = d.ver - g.V0;
+    if (k < 0 || k > n) {
+      *flag |= F_INVALID;
+      return c;
+    }
+    c.kind = K_READ;
+    c.k = k;
+    c.val = d.val;
+    return c;
+  }
+  if (ret == kNever) {
+    const int pos = d.ver == -1 ? -1 : d.ver - g.V0 - 1;
+    if (d.ver != -1 && (pos < 0 || pos >= n)) return c;  // never placeable
+    c.kind = K_OPT;
+    c.op = make_int4((int)d.call, d.val, d.f == LC_F_CAS ? d.exp : kAny, pos);
+    return c;
+  }
+  if (d.ver == -1) {
+    *flag |= F_NA;  // :ok mutation without a version: order not pinned
+    return c;
+  }
+  const int pos = d.ver - g.V0 - 1;
+  if (pos < 0 || pos >= n) {
+    *flag |= F_INVALID;  // impossible version
+    return c;
+  }
+  c.kind = K_PIN;
+  c.k = pos;
+  c.val = d.val;
+  c.exp = d.f == LC_F_CAS ? d.exp : kAny;
+  return c;
 }
 
-// May optional op o fill gap gi under the current value requirements?
-__device__ __forceinline__ bool eligible(const GapKey &g, int gi, int o) {
-  const int pos = g.ws.Gap[gi];
-  if (g.ws.OptCall[o] >= g.ws.Uh[pos]) return false;  // deadline
-  const int opos = g.ws.OptPos[o];
-  if (opos != -1 && opos != pos) return false;  // pending :ok op: its own version only
-  const int rq = g.ws.Req[pos];
-  if (rq != kAny && g.ws.OptVal[o] != rq) return false;
-  const int e = g.ws.OptExp[o];
-  if (e == kAny) return true;  // a write
-  const int b = value_before(g, pos);
-  return b == kAny || e == b;  // kAny: the gap before is free (checked later)
-}
+constexpr int kSetupBatch = 2;  // record chunks whose loads are in flight together
 
 // Build the skeleton of the key's prefix at `cut` (key-relative event index;
 // kNever = the whole history).  Returns GD_VALID when the skeleton is
 // consistent (then sh.n_gap / sh.n_opt / sh.maxret are set), else
-// GD_INVALID / GD_NA.
+// GD_INVALID / GD_NA.  Two passes over the records, each issuing the loads
+// of kSetupBatch chunks at once: pass 1 folds bounds with fire-and-forget
+// atomics and claims positions / read values with plain owner stores; pass 2
+// checks the owners (two mutations on one version, two values claimed for
+// one version) and appends the optional ops.  Optional ops and gaps are
+// compacted stably through per-wave ballot words: no barrier per chunk.
 __device__ int gap_setup(const GapKey &g, uint32_t cut) {
-  const int tid = threadIdx.x, n = g.n;
+  const int tid = threadIdx.x, n = g.n, wv = tid / kWave, lane = tid & (kWave - 1);
   GapSh &sh = *g.sh;
   const GapWs &w = g.ws;
   for (int k = tid; k <= n; k += kGapThreads) {
@@ -195,90 +303,75 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
     sh.flag = 0;
     sh.maxpos = -1;
     sh.maxread = -1;
-    sh.n_opt = 0;
     sh.maxret = 0;
+    sh.n_opt = 0;
+    sh.n_gap = 0;
   }
   __syncthreads();
   int flag = 0, maxpos = -1, maxread = -1;
   uint32_t maxret = 0;
-  for (int r0 = 0; r0 < n; r0 += kGapThreads) {
-    const int r = r0 + tid;
-    bool opt = false;
-    uint32_t ocall = 0;
-    int oval = 0, oexp = 0, opos = 0;
-    if (r < n) {
-      const Raw raw = load_raw(g.kops, r, n);
-      const Rec d = decode(raw, g.base);
-      const bool unsorted = r > 0 && g.kops[r - 1].call >= raw.c.x;
-      if (d.bad || d.f > LC_F_CAS || unsorted || raw.c.x < 0) {
-        flag |= F_NA;  // the JIT tier reports malformed / unknown :f
-      } else if (d.call <= cut) {
-        const uint32_t ret = d.ret > cut ? kNever : d.ret;  // pending at the cut
-        if (ret != kNever) maxret = max(maxret, ret);
-        if (d.f == LC_F_READ) {
-          if (ret == kNever || (d.ver == -1 && d.val == -1)) {
-            // an optional or [nil nil] read never constrains
-          } else if (d.ver == -1) {
-            flag |= F_NA;  // read [nil x]: its version is free
-          } else {
-            const int k = d.ver - g.V0;
-            if (k < 0 || k > n) {
-              flag |= F_INVALID;
-            } else {
-              maxread = max(maxread, k);
-              atomicMax(&w.A[k], d.call + 1);
-              if (k > 0) atomicMin(&w.B[k - 1], ret);
-              if (d.val != -1) {
-                const int prev = atomicCAS(&w.Claim[k], kAny, d.val);
-                if (prev != kAny && prev != d.val) flag |= F_INVALID;
-              }
-            }
+  const int nch = (n + kGapThreads - 1) / kGapThreads;
+  for (int pass = 1; pass <= 2; pass++) {
+    for (int c0 = 0; c0 < nch; c0 += kSetupBatch) {
+      Raw raw[kSetupBatch];
+      int64_t pc[kSetupBatch];
+#pragma unroll
+      for (int b = 0; b < kSetupBatch; b++) {
+        const int r = (c0 + b) * kGapThreads + tid;
+        raw[b] = load_raw(g.kops, r, n);
+        pc[b] = (r > 0 && r < n) ? g.kops[r - 1].call : -1;
+      }
+#pragma unroll
+      for (int b = 0; b < kSetupBatch; b++) {
+        const int ch = c0 + b, r = ch * kGapThreads + tid;
+        if (ch >= nch) break;
+        Cls c;
+        c.kind = K_NONE;
+        if (r < n) c = classify(g, raw[b], pc[b], r, cut, &flag, &maxret);
+        if (pass == 1) {
+          if (c.kind == K_READ) {
+            maxread = max(maxread, c.k);
+            atomicMax(&w.A[c.k], c.call + 1);
+            if (c.k > 0) atomicMin(&w.B[c.k - 1], c.ret);
+            if (c.val != -1) w.Claim[c.k] = c.val;
+          } else if (c.kind == K_PIN) {
+            atomicMax(&w.A[c.k], c.call + 1);
+            atomicMin(&w.B[c.k], c.ret);
+            w.Pin[c.k] = r;
+            w.Val[c.k] = c.val;
+            w.PinExp[c.k] = c.exp;
+            maxpos = max(maxpos, c.k);
           }
-        } else if (ret == kNever) {
-          const int pos = d.ver == -1 ? -1 : d.ver - g.V0 - 1;
-          if (d.ver == -1 || (pos >= 0 && pos < n)) {  // else never placeable
-            opt = true;
-            ocall = d.call;
-            oval = d.val;
-            oexp = d.f == LC_F_CAS ? d.exp : kAny;
-            opos = pos;
-          }
-        } else if (d.ver == -1) {
-          flag |= F_NA;  // :ok mutation without a version: order not pinned
+          const uint64_t m = __ballot(c.kind == K_OPT);
+          if (lane == 0) w.Mask[ch * kGapWaves + wv] = m;
         } else {
-          const int pos = d.ver - g.V0 - 1;
-          if (pos < 0 || pos >= n || atomicCAS(&w.Pin[pos], -1, r) != -1) {
-            flag |= F_INVALID;  // impossible version, or two mutations claim one
-          } else {
-            atomicMax(&w.A[pos], d.call + 1);
-            atomicMin(&w.B[pos], ret);
-            w.Val[pos] = d.val;
-            w.PinExp[pos] = d.f == LC_F_CAS ? d.exp : kAny;
-            maxpos = max(maxpos, pos);
+          if (c.kind == K_READ && c.val != -1 && w.Claim[c.k] != c.val)
+            flag |= F_INVALID;  // two values claimed for one version
+          else if (c.kind == K_PIN && w.Pin[c.k] != r)
+            flag |= F_INVALID;  // two mutations claim one version
+          const int wi = ch * kGapWaves + wv;
+          if (c.kind == K_OPT) {
+            const uint64_t m = w.Mask[wi];
+            w.Opt[w.Pre[wi] + lanes_below(m)] = c.op;
           }
         }
       }
     }
-    // stable append of the optional ops (record order)
-    int tot;
-    const int at = block_excl_sum(opt ? 1 : 0, sh, &tot);
-    if (opt) {
-      const int i = sh.n_opt + at;
-      w.OptCall[i] = ocall;
-      w.OptVal[i] = oval;
-      w.OptExp[i] = oexp;
-      w.OptPos[i] = opos;
+    if (pass == 1) {
+      if (flag) atomicOr(&sh.flag, flag);
+      if (maxpos >= 0) atomicMax(&sh.maxpos, maxpos);
+      if (maxread >= 0) atomicMax(&sh.maxread, maxread);
+      if (maxret) atomicMax(&sh.maxret, maxret);
+      __syncthreads();
+      if (sh.flag & (F_NA | F_INVALID)) return (sh.flag & F_NA) ? GD_NA : GD_INVALID;
+      sh.n_opt = mask_prefix(w, nch * kGapWaves, sh);  // same value in every thread
+      flag = 0;
     }
-    __syncthreads();
-    if (tid == 0) sh.n_opt += tot;
   }
   if (flag) atomicOr(&sh.flag, flag);
-  if (maxpos >= 0) atomicMax(&sh.maxpos, maxpos);
-  if (maxread >= 0) atomicMax(&sh.maxread, maxread);
-  if (maxret) atomicMax(&sh.maxret, maxret);
   __syncthreads();
-  if (sh.flag & F_NA) return GD_NA;
   if (sh.flag & F_INVALID) return GD_INVALID;
+  const int n_opt = sh.n_opt;
   const int M = max(sh.maxpos + 1, sh.maxread);
   // Uh[k] = min(B[k..M-1]): chunked suffix-min scan
   const int per = (M + kGapThreads - 1) / kGapThreads;
@@ -292,193 +385,317 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
   }
   __syncthreads();
   // fixed checks: pinned / read-only lower bounds below the deadline, and
-  // the value chain around pinned positions; the requirement on each gap
+  // the value chain around pinned positions; the requirement on each gap;
+  // one ballot word of gap positions per wave chunk
   flag = 0;
   if (tid == 0) {
     if (w.Claim[0] != kAny && w.Claim[0] != g.init) flag |= F_INVALID;
     if (M > 0 && w.Pin[0] != -1 && w.PinExp[0] != kAny && w.PinExp[0] != g.init)
       flag |= F_INVALID;
   }
-  for (int k = tid; k < M; k += kGapThreads) {
-    const uint32_t lo = w.A[k];
-    if (lo != 0 && lo - 1 >= w.Uh[k]) flag |= F_INVALID;
-    int rq = w.Claim[k + 1];
-    if (k + 1 < M && w.Pin[k + 1] != -1 && w.PinExp[k + 1] != kAny) {
-      if (rq != kAny && rq != w.PinExp[k + 1]) flag |= F_INVALID;
-      rq = w.PinExp[k + 1];
+  const int mch = (M + kGapThreads - 1) / kGapThreads;
+  for (int ch = 0; ch < mch; ch++) {
+    const int k = ch * kGapThreads + tid;
+    bool gap = false;
+    if (k < M) {
+      const uint32_t lo = w.A[k];
+      if (lo != 0 && lo - 1 >= w.Uh[k]) flag |= F_INVALID;
+      int rq = w.Claim[k + 1];
+      if (k + 1 < M && w.Pin[k + 1] != -1 && w.PinExp[k + 1] != kAny) {
+        if (rq != kAny && rq != w.PinExp[k + 1]) flag |= F_INVALID;
+        rq = w.PinExp[k + 1];
+      }
+      if (w.Pin[k] != -1) {
+        if (rq != kAny && rq != w.Val[k]) flag |= F_INVALID;
+      } else {
+        w.Req[k] = rq;
+        gap = true;
+      }
     }
-    if (w.Pin[k] != -1) {
-      if (rq != kAny && rq != w.Val[k]) flag |= F_INVALID;
-    } else {
-      w.Req[k] = rq;
-    }
-  }
-  // stable compaction of the gap positions
-  if (tid == 0) sh.n_gap = 0;
-  __syncthreads();
-  for (int c0 = 0; c0 < M; c0 += kGapThreads) {
-    const int k = c0 + tid;
-    const bool gap = k < M && w.Pin[k] == -1;
-    int tot;
-    const int at = block_excl_sum(gap ? 1 : 0, sh, &tot);
-    if (gap) {
-      w.Gap[sh.n_gap + at] = k;
-      w.GI[k] = sh.n_gap + at;
-    }
-    __syncthreads();
-    if (tid == 0) sh.n_gap += tot;
+    const uint64_t m = __ballot(gap);
+    if (lane == 0) w.Mask[ch * kGapWaves + wv] = m;
   }
   if (flag) atomicOr(&sh.flag, flag);
   __syncthreads();
-  return (sh.flag & F_INVALID) ? GD_INVALID : GD_VALID;
+  if (sh.flag & F_INVALID) return GD_INVALID;
+  const int G = mask_prefix(w, mch * kGapWaves, sh);
+  for (int ch = 0; ch < mch; ch++) {
+    const int wi = ch * kGapWaves + wv;
+    const uint64_t m = w.Mask[wi];
+    if ((m >> lane) & 1) w.Gap[w.Pre[wi] + lanes_below(m)] = ch * kGapThreads + tid;
+  }
+  if (tid == 0) {
+    sh.n_opt = n_opt;
+    sh.n_gap = G;
+  }
+  __syncthreads();
+  return GD_VALID;
 }
 
-// Maximum matching of the gaps; true iff every gap is filled.
-__device__ bool gap_match(const GapKey &g, int G, int n_opt) {
-  const int tid = threadIdx.x;
-  GapSh &sh = *g.sh;
-  const GapWs &w = g.ws;
-  for (int o = tid; o < n_opt; o += kGapThreads) w.MatchOp[o] = -1;
-  for (int i = tid; i < G; i += kGapThreads) w.MatchGap[i] = -1;
-  __syncthreads();
-  for (int gi = 0; gi < G; gi++) {
-    // greedy: the first free eligible op
-    if (tid == 0) sh.cand = INT_MAX;
-    __syncthreads();
-    for (int o = tid; o < n_opt; o += kGapThreads)
-      if (w.MatchOp[o] == -1 && eligible(g, gi, o)) atomicMin(&sh.cand, o);
-    __syncthreads();
-    const int c = sh.cand;
-    __syncthreads();
-    if (c != INT_MAX) {
-      if (tid == 0) {
-        w.MatchOp[c] = gi;
-        w.MatchGap[gi] = c;
+// ---------------------------------------------------------------------------
+// The matching, over compact arrays.  Per gap gi a 16-byte record (deadline
+// D: ops called at or after it cannot fill the gap; value requirement R;
+// value before the gap B, kAny when the position before is a free gap;
+// position P), the matched op and the DFS stack (gap, resume op, chosen op).
+// Per optional op o a 16-byte record (call C, value V, expectation E = kAny
+// for a write, pinned position OP = -1 for a crashed op), the matched gap
+// and a visit stamp.  In LDS when L (tight, sized by G and n_opt), else in
+// the workspace.
+enum { aMG, aSG, aSR, aSO, aMO, aVis };
+
+template <bool L>
+struct Cmp {
+  int32_t *ws;   // workspace base (HBM fallback)
+  int G, n_opt;
+  int cap;
+  // LDS: gap records [0, 16G), op records [16G, 16(G+n_opt)), then the
+  // int arrays MG SG SR SO (G each), MO Vis (n_opt each).
+  // HBM: Opt at array 10, gap records at 14, int arrays at 18..23.
+  __device__ __forceinline__ int4 *gaps() const {
+    if constexpr (L)
+      return lds_dyn;
+    else
+      return reinterpret_cast<int4 *>(ws + 14 * cap);
+  }
+  __device__ __forceinline__ int4 *ops() const {
+    if constexpr (L)
+      return lds_dyn + G;
+    else
+      return reinterpret_cast<int4 *>(ws + 10 * cap);
+  }
+  __device__ __forceinline__ int &at(int a, int i) const {
+    if constexpr (L) {
+      int *b = reinterpret_cast<int *>(lds_dyn + G + n_opt);
+      return b[a < aMO ? a * G + i : 4 * G + (a - aMO) * n_opt + i];
+    } else {
+      return ws[(18 + a) * cap + i];
+    }
+  }
+};
+
+// gap record: x = D, y = R, z = B, w = P;  op record: x = C, y = V, z = E, w = OP
+__device__ __forceinline__ bool elig(const int4 gp, const int4 op) {
+  return (uint32_t)op.x < (uint32_t)gp.x && (op.w == -1 || op.w == gp.w) &&
+         (gp.y == kAny || op.y == gp.y) && (op.z == kAny || gp.z == kAny || op.z == gp.z);
+}
+
+#ifdef GAP_PROFILE
+__shared__ unsigned long long prof_ctr[8];
+#define PROF(i, v) do { if ((threadIdx.x & 63) == 0) prof_ctr[i] += (v); } while (0)
+#else
+#define PROF(i, v) do {} while (0)
+#endif
+
+// First free op eligible for gap gi (or -1); *ff = first possibly-free op.
+template <bool L>
+__device__ int first_fit(const Cmp<L> &c, int gi, int n_opt, int *ff) {
+  const int lane = threadIdx.x & (kWave - 1);
+  int base = *ff;
+  for (;;) {  // skip the matched prefix
+    if (base >= n_opt) {
+      *ff = base;
+      return -1;
+    }
+    const int o = base + lane;
+    const uint64_t b = __ballot(o < n_opt && c.at(aMO, o) == -1);
+    if (b) {
+      base += first_lane(b);
+      break;
+    }
+    base += kWave;
+  }
+  *ff = base;
+  const int4 gp = uni4(c.gaps()[gi]);
+  const int4 *ops = c.ops();
+  PROF(0, 1);
+  for (; base < n_opt; base += kWave) {
+    PROF(1, 1);
+    if ((uint32_t)uni(ops[base].x) >= (uint32_t)gp.x) break;  // sorted by call
+    const int o = base + lane;
+    const bool e = o < n_opt && c.at(aMO, o) == -1 && elig(gp, ops[o]);
+    const uint64_t b = __ballot(e);
+    if (b) return base + first_lane(b);
+  }
+  return -1;
+}
+
+// Depth-first augmenting path from the unmatched gap g0 (Kuhn).  Ops
+// visited in this search carry `stamp`.  True iff g0 was matched.
+template <bool L>
+__device__ bool augment(const Cmp<L> &c, int g0, int n_opt, int stamp) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int4 *ops = c.ops();
+  int depth = 0, g = g0, base = 0;
+  PROF(2, 1);
+  for (;;) {
+    const int4 gp = uni4(c.gaps()[g]);
+    int found = -1;
+    PROF(3, 1);
+    for (; base < n_opt; base += kWave) {
+      PROF(4, 1);
+      if ((uint32_t)uni(ops[base].x) >= (uint32_t)gp.x) break;
+      const int o = base + lane;
+      const bool e = o < n_opt && c.at(aVis, o) != stamp && elig(gp, ops[o]);
+      const uint64_t b = __ballot(e);
+      if (b) {
+        found = base + first_lane(b);
+        break;
       }
-      __syncthreads();
+    }
+    if (found < 0) {  // dead end: back to the previous gap
+      if (depth == 0) return false;
+      depth--;
+      g = uni(c.at(aSG, depth));
+      base = uni(c.at(aSR, depth));
       continue;
     }
-    // augmenting path: level-synchronous BFS over (frontier gap, op) pairs
-    for (int o = tid; o < n_opt; o += kGapThreads) w.Par[o] = -1;
-    if (tid == 0) {
-      w.Fr0[0] = gi;
-      sh.found = INT_MAX;
-    }
-    int nf = 1;
-    int *fr = w.Fr0, *fn = w.Fr1;
-    __syncthreads();
-    for (;;) {
-      if (tid == 0) sh.n_next = 0;
-      __syncthreads();
-      const int64_t total = (int64_t)nf * n_opt;
-      for (int64_t idx = tid; idx < total; idx += kGapThreads) {
-        const int f = fr[idx / n_opt], o = (int)(idx % n_opt);
-        if (eligible(g, f, o) && atomicCAS(&w.Par[o], -1, f) == -1) {
-          const int m = w.MatchOp[o];
-          if (m == -1)
-            atomicMin(&sh.found, o);
-          else
-            fn[atomicAdd(&sh.n_next, 1)] = m;
+    c.at(aSG, depth) = g;
+    c.at(aSR, depth) = found + 1;
+    c.at(aSO, depth) = found;
+    c.at(aVis, found) = stamp;
+    const int m = uni(c.at(aMO, found));
+    if (m == -1) {  // flip the path
+      wave_fence();
+      for (int d0 = 0; d0 <= depth; d0 += kWave) {
+        const int d = d0 + lane;
+        if (d <= depth) {
+          const int gg = c.at(aSG, d), oo = c.at(aSO, d);
+          c.at(aMG, gg) = oo;
+          c.at(aMO, oo) = gg;
         }
       }
-      __syncthreads();
-      nf = sh.n_next;
-      const int found = sh.found;
-      __syncthreads();
-      if (found != INT_MAX || nf == 0) break;
-      int *t = fr;
-      fr = fn;
-      fn = t;
+      wave_fence();
+      return true;
     }
-    const int found = sh.found;
-    if (found == INT_MAX) return false;  // Hall's condition fails at gi
-    if (tid == 0) {
-      int o = found;
-      for (;;) {
-        const int gg = w.Par[o];
-        const int prev = w.MatchGap[gg];
-        w.MatchGap[gg] = o;
-        w.MatchOp[o] = gg;
-        if (gg == gi) break;
-        o = prev;
+    depth++;
+    g = m;
+    base = 0;
+  }
+}
+
+// Fill every unmatched gap (first-fit, else an augmenting path).  False as
+// soon as one cannot be filled: no matching covers all gaps (once no path
+// leaves a gap, none ever will in Kuhn's algorithm).
+template <bool L>
+__device__ bool fill(const Cmp<L> &c, int G, int n_opt, int *ff, int *stamp) {
+  const int lane = threadIdx.x & (kWave - 1);
+  for (int g0 = 0; g0 < G; g0 += kWave) {
+    uint64_t todo = __ballot(g0 + lane < G && c.at(aMG, g0 + lane) == -1);
+    while (todo) {
+      const int gi = g0 + first_lane(todo);
+      todo &= todo - 1;
+      const int o = first_fit(c, gi, n_opt, ff);
+      if (o >= 0) {
+        c.at(aMG, gi) = o;
+        c.at(aMO, o) = gi;
+        wave_fence();
+        continue;
       }
+      if (!augment(c, gi, n_opt, ++*stamp)) return false;
     }
-    __syncthreads();
   }
   return true;
 }
 
-// Smallest value > last among the ops eligible for the gap at position pos
-// (INT_MAX if none).
-__device__ int next_value(const GapKey &g, int pos, int last, int n_opt) {
-  GapSh &sh = *g.sh;
-  if (threadIdx.x == 0) sh.cand = INT_MAX;
-  __syncthreads();
-  const int gi = g.ws.GI[pos];
-  for (int o = threadIdx.x; o < n_opt; o += kGapThreads) {
-    const int v = g.ws.OptVal[o];
-    if (v > last && eligible(g, gi, o)) atomicMin(&sh.cand, v);
+// Smallest value > last among the ops eligible for gap gi (INT_MAX if none).
+template <bool L>
+__device__ int next_value(const Cmp<L> &c, int gi, int last, int n_opt) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int4 gp = uni4(c.gaps()[gi]);
+  const int4 *ops = c.ops();
+  int best = INT_MAX;
+  for (int base = 0; base < n_opt; base += kWave) {
+    if ((uint32_t)uni(ops[base].x) >= (uint32_t)gp.x) break;
+    const int o = base + lane;
+    if (o < n_opt) {
+      const int4 op = ops[o];
+      if (elig(gp, op) && op.y > last) best = min(best, op.y);
+    }
   }
-  __syncthreads();
-  const int c = sh.cand;
-  __syncthreads();
-  return c;
+  return wave_min_i32(best);
 }
 
-// Decide the prefix at `cut`.  *nodes accumulates matching passes.
-__device__ int gap_decide(const GapKey &g, uint32_t cut, int64_t *nodes, int *n_gaps) {
-  const int tid = threadIdx.x;
-  GapSh &sh = *g.sh;
-  const GapWs &w = g.ws;
-  const int st = gap_setup(g, cut);
-  if (st != GD_VALID) return st;
-  const int G = sh.n_gap, n_opt = sh.n_opt;
-  *n_gaps = G;
-  if (G == 0) return GD_VALID;
-  if (G > n_opt) return GD_INVALID;
-  int depth = 0;
+// Set gap gi's value requirement to v (kAny = free), with the value-before
+// of the gap after it, and unmatch the pairs this makes ineligible.  *ff is
+// lowered to any op freed.
+template <bool L>
+__device__ void set_req(const Cmp<L> &c, int gi, int v, int G, int *ff) {
+  int4 *gaps = c.gaps();
+  reinterpret_cast<int *>(&gaps[gi])[1] = v;
+  const bool next = gi + 1 < G && uni(gaps[gi + 1].w) == uni(gaps[gi].w) + 1;
+  if (next) reinterpret_cast<int *>(&gaps[gi + 1])[2] = v;
+  wave_fence();
+  for (int k = 0; k < (next ? 2 : 1); k++) {
+    const int g = gi + k;
+    const int o = uni(c.at(aMG, g));
+    if (o < 0) continue;
+    if (!elig(uni4(gaps[g]), uni4(c.ops()[o]))) {
+      c.at(aMG, g) = -1;
+      c.at(aMO, o) = -1;
+      *ff = min(*ff, o);
+      wave_fence();
+    }
+  }
+}
+
+// Decide the gap filling by matching plus depth-first branching on the
+// values of free gaps that a matched CAS depends on.  Wave 0 only.  The
+// branch stack (gap, value) lives in the skeleton's Claim / Req arrays,
+// free once the compact arrays are built.
+template <bool L>
+__device__ int match_branch(const Cmp<L> &c, int G, int n_opt, int *brPos, int *brVal,
+                            int64_t *nodes) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int4 *gaps = c.gaps(), *ops = c.ops();
+  int ff = 0, stamp = 0, depth = 0;
   for (int node = 0;; node++) {
     if (node >= kNodeBudget) return GD_BUDGET;
     (*nodes)++;
-    if (gap_match(g, G, n_opt)) {
+#ifdef GAP_PROFILE
+    const uint64_t tn = wall_clock64();
+#endif
+    const bool filled = fill(c, G, n_opt, &ff, &stamp);
+    PROF(5, wall_clock64() - tn);
+    if (filled) {
       // the matching ignored CAS expectations after free gaps: check them
-      if (tid == 0) sh.viol = INT_MAX;
-      __syncthreads();
-      for (int gi = tid; gi < G; gi += kGapThreads) {
-        const int pos = w.Gap[gi];
-        if (pos == 0 || w.Pin[pos - 1] != -1 || w.Req[pos - 1] != kAny) continue;
-        const int e = w.OptExp[w.MatchGap[gi]];
-        if (e != kAny && w.OptVal[w.MatchGap[w.GI[pos - 1]]] != e) atomicMin(&sh.viol, pos - 1);
+      int viol = INT_MAX;
+      for (int g0 = 1; g0 < G && viol == INT_MAX; g0 += kWave) {
+        const int gi = g0 + lane;
+        bool bad = false;
+        if (gi < G && gaps[gi].z == kAny) {  // gap gi-1 sits just before, free
+          const int e = ops[c.at(aMG, gi)].z;
+          bad = e != kAny && ops[c.at(aMG, gi - 1)].y != e;
+        }
+        const uint64_t b = __ballot(bad);
+        if (b) viol = g0 + first_lane(b) - 1;
       }
-      __syncthreads();
-      const int viol = sh.viol;
-      __syncthreads();
+#ifdef GAP_PROFILE
+      const uint64_t tv = wall_clock64();
+      PROF(6, tv - tn);
+#endif
       if (viol == INT_MAX) return GD_VALID;
-      // branch on the value of the free gap at position viol
-      const int v = next_value(g, viol, INT_MIN, n_opt);
-      if (tid == 0) {
-        w.StPos[depth] = viol;
-        w.StVal[depth] = v;
-        w.Req[viol] = v;
+      // branch on the value of free gap `viol`
+      const int v = next_value(c, viol, INT_MIN, n_opt);
+#ifdef GAP_PROFILE
+      PROF(7, wall_clock64() - tv);
+#endif
+      if (lane == 0) {
+        brPos[depth] = viol;
+        brVal[depth] = v;
       }
       depth++;
-      __syncthreads();
+      set_req(c, viol, v, G, &ff);
       continue;
     }
     // no filling: next value of the deepest branch, else backtrack
     for (;;) {
       if (depth == 0) return GD_INVALID;
-      const int pos = w.StPos[depth - 1], last = w.StVal[depth - 1];
-      __syncthreads();
-      if (tid == 0) w.Req[pos] = kAny;
-      __syncthreads();
-      const int v = next_value(g, pos, last, n_opt);
+      const int gi = uni(brPos[depth - 1]), last = uni(brVal[depth - 1]);
+      set_req(c, gi, kAny, G, &ff);
+      const int v = next_value(c, gi, last, n_opt);
       if (v != INT_MAX) {
-        if (tid == 0) {
-          w.StVal[depth - 1] = v;
-          w.Req[pos] = v;
-        }
-        __syncthreads();
+        if (lane == 0) brVal[depth - 1] = v;
+        set_req(c, gi, v, G, &ff);
         break;
       }
       depth--;
@@ -486,11 +703,99 @@ __device__ int gap_decide(const GapKey &g, uint32_t cut, int64_t *nodes, int *n_
   }
 }
 
+// Decide the prefix at `cut`.  *nodes accumulates matching passes.
+__device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t *nodes,
+                          int *n_gaps) {
+  const int tid = threadIdx.x;
+  GapSh &sh = *g.sh;
+  const GapWs &w = g.ws;
+#ifdef GAP_PROFILE
+  const uint64_t t0 = wall_clock64();
+  if (tid < 8) prof_ctr[tid] = 0;
+#endif
+  const int st = gap_setup(g, cut);
+  if (st != GD_VALID) return st;
+#ifdef GAP_PROFILE
+  const uint64_t t1 = wall_clock64();
+#endif
+  const int G = sh.n_gap, n_opt = sh.n_opt;
+  *n_gaps = G;
+  if (G == 0) return GD_VALID;
+  if (G > n_opt) return GD_INVALID;
+  const bool in_lds = match_lds_bytes(G, n_opt) <= lds_bytes;
+  Cmp<true> cl;
+  Cmp<false> cg;
+  cl.ws = cg.ws = w.base;
+  cl.G = cg.G = G;
+  cl.n_opt = cg.n_opt = n_opt;
+  cl.cap = cg.cap = (int)w.cap;
+  int4 *gaps = in_lds ? cl.gaps() : cg.gaps();
+  int *mg = in_lds ? &cl.at(aMG, 0) : &cg.at(aMG, 0);
+  int *mo = in_lds ? &cl.at(aMO, 0) : &cg.at(aMO, 0);
+  int *vis = in_lds ? &cl.at(aVis, 0) : &cg.at(aVis, 0);
+  for (int gi = tid; gi < G; gi += kGapThreads) {
+    const int pos = w.Gap[gi];
+    const int before =
+        pos == 0 ? g.init : (w.Pin[pos - 1] != -1 ? w.Val[pos - 1] : w.Req[pos - 1]);
+    gaps[gi] = make_int4((int)w.Uh[pos], w.Req[pos], before, pos);
+    mg[gi] = -1;
+  }
+  for (int o = tid; o < n_opt; o += kGapThreads) {
+    if (in_lds) cl.ops()[o] = w.Opt[o];
+    mo[o] = -1;
+    vis[o] = 0;
+  }
+  __syncthreads();
+#ifdef GAP_PROFILE
+  const uint64_t t2 = wall_clock64();
+#endif
+  if (tid < kWave) {
+    const int r = in_lds ? match_branch(cl, G, n_opt, w.Claim, w.Req, nodes)
+                         : match_branch(cg, G, n_opt, w.Claim, w.Req, nodes);
+    if (tid == 0) sh.res = r;
+  }
+  __syncthreads();
+  const int r = sh.res;
+  __syncthreads();
+#ifdef GAP_PROFILE
+  if (tid == 0 && blockIdx.x == 0) {
+    printf("  ff calls %llu chunks %llu | aug calls %llu steps %llu chunks %llu | fill ticks %llu +viol %llu nextval %llu\n",
+           prof_ctr[0], prof_ctr[1], prof_ctr[2], prof_ctr[3], prof_ctr[4], prof_ctr[5], prof_ctr[6], prof_ctr[7]);
+  }
+  if (tid == 0 && blockIdx.x < 2)
+    printf("gap_decide wg %d cut %u n %d G %d n_opt %d lds %d nodes %ld: setup %lu compact %lu match %lu (x10ns)\n",
+           (int)blockIdx.x, cut, g.n, G, n_opt, (int)in_lds, (long)*nodes, (unsigned long)(t1 - t0),
+           (unsigned long)(t2 - t1), (unsigned long)(wall_clock64() - t2));
+#endif
+  return r;
+}
+
+__device__ __forceinline__ int64_t key_fail_op(const GapKey &g, uint32_t at, GapSh &sh) {
+  // the record whose return is event `at` (key-relative)
+  if (threadIdx.x == 0) sh.res = INT_MAX;
+  __syncthreads();
+  for (int r = threadIdx.x; r < g.n; r += kGapThreads)
+    if (g.kops[r].ret == g.base + (int64_t)at) atomicMin(&sh.res, r);
+  __syncthreads();
+  const int r = sh.res;
+  __syncthreads();
+  return r == INT_MAX ? -1 : r;
+}
+
+// Probe j of P on the interval [lo, hi]: the candidates are lo..hi-1 (hi is
+// known to fail).  Returns kNever when probe j has nothing to test.
+__host__ __device__ __forceinline__ uint32_t probe_cut(uint32_t lo, uint32_t hi, int j, int P) {
+  if (lo >= hi) return kNever;
+  const uint64_t len = (uint64_t)(hi - lo);
+  if (len <= (uint64_t)P) return (uint64_t)j < len ? lo + (uint32_t)j : kNever;
+  return lo + (uint32_t)((uint64_t)(j + 1) * len / (uint64_t)(P + 1));
+}
+
 __global__ __launch_bounds__(kGapThreads) void gap_tier_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
-    const int32_t *__restrict__ keys, const int32_t n_list, const KParams p,
-    lc_key_result *__restrict__ out, int32_t *__restrict__ ws, const int64_t cap,
-    int32_t *__restrict__ pass_keys, KStatus *__restrict__ status) {
+    const int32_t *__restrict__ keys, const KParams p, lc_key_result *__restrict__ out,
+    int32_t *__restrict__ ws, const int64_t cap, int32_t *__restrict__ pass_keys,
+    KStatus *__restrict__ status, const GapJob job) {
   __shared__ GapSh sh;
   const int64_t key_base = key_off[0];
   GapKey g;
@@ -498,55 +803,159 @@ __global__ __launch_bounds__(kGapThreads) void gap_tier_kernel(
   g.sh = &sh;
   g.V0 = p.init_ver;
   g.init = p.init_val;
-  for (int li = blockIdx.x; li < n_list; li += gridDim.x) {
-    const int64_t key = keys[li];
+  for (int t = blockIdx.x; t < job.n_tasks; t += gridDim.x) {
+    int ci = -1;  // counterexample index (probe / bisect)
+    int64_t key;
+    if (job.mode == kGapFull) {
+      key = keys[t];
+    } else {
+      ci = t / job.P;
+      key = job.cex_key[ci];
+    }
     const int64_t beg = key_off[key], end = key_off[key + 1];
-    int res = GD_NA;
-    int64_t nodes = 0, fail_op = -1, fail_end = -1;
-    int G = 0;
-    if (end - beg > 0 && end - beg + 2 <= cap) {
-      g.kops = ops + (beg - key_base);
-      g.n = (int)(end - beg);
-      g.base = g.kops[0].call;
-      res = gap_decide(g, kNever, &nodes, &G);
-      if (res == GD_INVALID) {
-        // bisection for the first return whose prefix is not linearizable
-        uint32_t lo = 0, hi = sh.maxret;
-        __syncthreads();
-        int g2 = 0;
-        while (lo < hi && res == GD_INVALID) {
-          const uint32_t mid = lo + (hi - lo) / 2;
-          const int r = gap_decide(g, mid, &nodes, &g2);
-          if (r == GD_INVALID)
-            hi = mid;
-          else if (r == GD_VALID)
-            lo = mid + 1;
-          else
-            res = r;  // not decidable on a prefix: leave it to the JIT tier
+    if (end - beg <= 0 || end - beg + 2 > cap) {  // cannot happen past kGapFull
+      if (threadIdx.x == 0 && job.mode == kGapFull)
+        pass_keys[atomicAdd(&status->n_jit2, 1)] = (int32_t)key;
+      continue;
+    }
+    g.kops = ops + (beg - key_base);
+    g.n = (int)(end - beg);
+    g.base = g.kops[0].call;
+    int64_t nodes = 0;
+    int G = 0, G_full = 0;
+    // One decision (full / probe), or a bisection of decisions.  A single
+    // call site of gap_decide keeps the kernel's register budget in check.
+    uint32_t lo = 0, hi = 0, cut = kNever;
+    bool bis = false;  // bisecting a counterexample in this workgroup
+    if (job.mode == kGapProbe)
+      cut = job.cex_state[ci] ? kNever
+                              : probe_cut(job.cex_lo[ci], job.cex_hi[ci], t - ci * job.P, job.P);
+    int res = GD_SKIP;
+    if (job.mode == kGapFull || cut != kNever) {
+      for (;;) {
+        res = gap_decide(g, cut, job.lds_bytes, &nodes, &G);
+        if (!bis) {
+          if (job.mode != kGapFull || !job.bisect || res != GD_INVALID) break;
+          bis = true;  // counterexample: the first return whose prefix fails
+          G_full = G;
+          lo = 0;
+          hi = sh.maxret;
+        } else if (res == GD_INVALID) {
+          hi = cut;
+        } else if (res == GD_VALID) {
+          lo = cut + 1;
+        } else {
+          break;  // not decidable on a prefix: leave it to the JIT tier
         }
-        if (res == GD_INVALID) {
-          if (threadIdx.x == 0) sh.cand = INT_MAX;
-          __syncthreads();
-          for (int r = threadIdx.x; r < g.n; r += kGapThreads)
-            if (g.kops[r].ret == g.base + (int64_t)lo) atomicMin(&sh.cand, r);
-          __syncthreads();
-          if (sh.cand == INT_MAX) res = GD_NA;  // not a return: cannot happen
-          fail_op = sh.cand;
-          fail_end = g.base + (int64_t)lo;
-          __syncthreads();
+        if (lo >= hi) {
+          res = GD_INVALID;
+          break;
         }
+        cut = lo + (hi - lo) / 2;
       }
     }
-    if (threadIdx.x == 0) {
-      if (res == GD_VALID)
-        out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, nodes, G};
-      else if (res == GD_INVALID)
-        out[key] = lc_key_result{LC_INVALID, LC_REASON_NONLINEARIZABLE, fail_op, fail_end,
-                                 nodes, G};
-      else
-        pass_keys[atomicAdd(&status->n_jit2, 1)] = (int32_t)key;
+    if (bis) {
+      int64_t fail_op = -1;
+      if (res == GD_INVALID) {
+        fail_op = key_fail_op(g, lo, sh);
+        if (fail_op < 0) res = GD_NA;  // not a return: cannot happen
+      }
+      if (threadIdx.x == 0) {
+        if (res == GD_INVALID)
+          out[key] = lc_key_result{LC_INVALID, LC_REASON_NONLINEARIZABLE, fail_op,
+                                   g.base + (int64_t)lo, nodes, G_full};
+        else
+          pass_keys[atomicAdd(&status->n_jit2, 1)] = (int32_t)key;
+      }
+    } else if (job.mode == kGapFull) {
+      if (threadIdx.x == 0) {
+        if (res == GD_VALID) {
+          out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, nodes, G};
+        } else if (res == GD_INVALID) {
+          const int i = atomicAdd(&status->n_cex, 1);
+          job.cex_key[i] = (int32_t)key;
+          job.cex_lo[i] = 0;
+          job.cex_hi[i] = sh.maxret;
+          job.cex_gaps[i] = G;
+          job.cex_state[i] = 0;
+          job.cex_nodes[i] = nodes;
+          atomicMax(&status->max_lds, match_lds_bytes(G, sh.n_opt));
+        } else {
+          pass_keys[atomicAdd(&status->n_jit2, 1)] = (int32_t)key;
+        }
+      }
+    } else {  // kGapProbe
+      if (threadIdx.x == 0) {
+        job.probe[t] = res;
+        if (nodes) atomicAdd((unsigned long long *)&job.cex_nodes[ci], (unsigned long long)nodes);
+      }
     }
     __syncthreads();
+  }
+}
+
+// One wave per counterexample interval: shrink [lo, hi] by the probes'
+// verdicts; close it (result written) when lo == hi.
+__global__ __launch_bounds__(kWave) void gap_narrow_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off, const int32_t n_cex,
+    lc_key_result *__restrict__ out, int32_t *__restrict__ pass_keys,
+    KStatus *__restrict__ status, const GapJob job) {
+  const int ci = blockIdx.x, lane = threadIdx.x;
+  if (ci >= n_cex || job.cex_state[ci]) return;
+  const uint32_t lo = job.cex_lo[ci], hi = job.cex_hi[ci];
+  uint32_t min_bad = hi;  // smallest failing cut
+  uint32_t good_hi = lo;  // largest linearizable cut + 1
+  bool na = false;
+  for (int j = lane; j < job.P; j += kWave) {
+    const uint32_t cut = probe_cut(lo, hi, j, job.P);
+    if (cut == kNever) continue;
+    const int r = job.probe[(int64_t)ci * job.P + j];
+    if (r == GD_INVALID)
+      min_bad = min(min_bad, cut);
+    else if (r == GD_VALID)
+      good_hi = max(good_hi, cut + 1);
+    else
+      na = true;
+  }
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    min_bad = min(min_bad, (uint32_t)__shfl_xor((int)min_bad, o));
+    good_hi = max(good_hi, (uint32_t)__shfl_xor((int)good_hi, o));
+    na = na | (bool)__shfl_xor((int)na, o);
+  }
+  const int64_t key = job.cex_key[ci];
+  const int64_t beg = key_off[key], end = key_off[key + 1];
+  const lc_op *kops = ops + (beg - key_off[0]);
+  // prefix-closed: every linearizable cut lies below every failing one
+  if (na || good_hi > min_bad) {
+    if (lane == 0) {
+      job.cex_state[ci] = 1;
+      pass_keys[atomicAdd(&status->n_jit2, 1)] = (int32_t)key;
+    }
+    return;
+  }
+  if (good_hi < min_bad) {
+    if (lane == 0) {
+      job.cex_lo[ci] = good_hi;
+      job.cex_hi[ci] = min_bad;
+      atomicAdd(&status->n_open, 1);
+    }
+    return;
+  }
+  // closed: the first failing return is event `min_bad`
+  const int64_t base = kops[0].call, at = base + (int64_t)min_bad;
+  int fo = INT_MAX;
+  for (int r = lane; r < (int)(end - beg); r += kWave)
+    if (kops[r].ret == at) fo = min(fo, r);
+  fo = wave_min_i32(fo);
+  if (lane == 0) {
+    job.cex_state[ci] = 1;
+    job.cex_lo[ci] = job.cex_hi[ci] = min_bad;
+    if (fo == INT_MAX)
+      pass_keys[atomicAdd(&status->n_jit2, 1)] = (int32_t)key;
+    else
+      out[key] = lc_key_result{LC_INVALID, LC_REASON_NONLINEARIZABLE, fo, at, job.cex_nodes[ci],
+                               job.cex_gaps[ci]};
   }
 }
 
@@ -557,13 +966,22 @@ size_t gap_tier_ws_bytes(int n_wg, int64_t cap) {
 }
 
 hipError_t launch_gap_tier(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
-                           int32_t n_list, const KParams &p, lc_key_result *d_out,
-                           int32_t *d_ws, int n_wg, int64_t cap, int32_t *d_pass_keys,
-                           KStatus *d_status, hipStream_t stream) {
-  if (n_list <= 0) return hipSuccess;
-  hipLaunchKernelGGL(gap_tier_kernel, dim3((unsigned)n_wg), dim3(kGapThreads), 0, stream,
-                     d_ops, d_key_off, d_keys, n_list, p, d_out, d_ws, cap, d_pass_keys,
-                     d_status);
+                           const KParams &p, lc_key_result *d_out, int32_t *d_ws, int n_wg,
+                           int64_t cap, int32_t *d_pass_keys, KStatus *d_status,
+                           const GapJob &job, hipStream_t stream) {
+  if (job.n_tasks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gap_tier_kernel, dim3((unsigned)n_wg), dim3(kGapThreads),
+                     (unsigned)job.lds_bytes, stream, d_ops, d_key_off, d_keys, p, d_out, d_ws,
+                     cap, d_pass_keys, d_status, job);
+  return hipGetLastError();
+}
+
+hipError_t launch_gap_narrow(const lc_op *d_ops, const int64_t *d_key_off, int32_t n_cex,
+                             lc_key_result *d_out, int32_t *d_pass_keys, KStatus *d_status,
+                             const GapJob &job, hipStream_t stream) {
+  if (n_cex <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gap_narrow_kernel, dim3((unsigned)n_cex), dim3(kWave), 0, stream, d_ops,
+                     d_key_off, n_cex, d_out, d_pass_keys, d_status, job);
   return hipGetLastError();
 }
 

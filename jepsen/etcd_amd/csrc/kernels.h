@@ -24,6 +24,9 @@ struct KStatus {
   int32_t n_jit;        // keys handed over by the fast tier
   int32_t max_len;      // longest key among them (records)
   int32_t n_jit2;       // keys the gap tier passes on to the JIT search
+  int32_t n_cex;        // gap tier: invalid keys awaiting their counterexample
+  int32_t n_open;       // gap tier: counterexample intervals still open after a round
+  int32_t max_lds;      // gap tier: largest matching footprint (bytes) of a full decision
 };
 
 constexpr int kWave = 64;
@@ -70,14 +73,44 @@ hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
                            int32_t *d_ovf_out, int32_t *d_n_ovf_out, int last_tier,
                            hipStream_t stream);
 
-// Gap tier (gap_tier.hip): one 256-thread workgroup per key of d_keys decides
-// version-pinned keys with crashed writes/CAS by matching gaps to optional
-// ops; keys it cannot decide are appended to d_pass_keys (status->n_jit2).
+// Gap tier (gap_tier.hip): version-pinned keys with crashed writes/CAS are
+// decided by matching gaps to optional ops; keys it cannot decide are
+// appended to d_pass_keys (status->n_jit2).  A call runs two kinds of launch
+// (GapJob::mode):
+//   kGapFull   one 256-thread workgroup per listed key decides the whole
+//              history.  With `bisect` the same workgroup then bisects an
+//              invalid key's prefixes for its counterexample (many or short
+//              keys); without, invalid keys go to the counterexample list
+//              (cex_*, status->n_cex) with the interval [0, last return].
+//   kGapProbe  P workgroups per open counterexample interval each decide one
+//              history prefix (a multisection of the interval), then
+//              launch_gap_narrow shrinks the intervals by the probes' verdicts
+//              (status->n_open = intervals still open) and writes the results
+//              of closed ones.  Rounds repeat until none is open: a single
+//              hot key (BASELINE configs[3]) spreads over the whole GPU.
 // Workspace: gap_tier_ws_bytes(n_wg, cap) with cap >= longest key + 2.
+enum { kGapFull = 0, kGapProbe = 1 };
+struct GapJob {
+  int32_t mode;        // kGapFull / kGapProbe
+  int32_t bisect;      // kGapFull: bisect invalid keys in place
+  int32_t P;           // probes per interval (kGapProbe)
+  int32_t lds_bytes;   // dynamic LDS per workgroup for the matching arrays
+  int32_t n_tasks;     // keys (full), intervals x P (probe)
+  int32_t *cex_key;    // per counterexample: the key
+  uint32_t *cex_lo;    // key-relative event interval [lo, hi] holding the
+  uint32_t *cex_hi;    //   first return whose prefix is not linearizable
+  int32_t *cex_gaps;   // gaps of the full history (reported as max_frontier)
+  int32_t *cex_state;  // 0 open, 1 closed
+  int64_t *cex_nodes;  // matching passes spent on the key
+  int32_t *probe;      // [n_cex * P] probe verdicts
+};
 size_t gap_tier_ws_bytes(int n_wg, int64_t cap);
 hipError_t launch_gap_tier(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
-                           int32_t n_list, const KParams &p, lc_key_result *d_out,
-                           int32_t *d_ws, int n_wg, int64_t cap, int32_t *d_pass_keys,
-                           KStatus *d_status, hipStream_t stream);
+                           const KParams &p, lc_key_result *d_out, int32_t *d_ws, int n_wg,
+                           int64_t cap, int32_t *d_pass_keys, KStatus *d_status,
+                           const GapJob &job, hipStream_t stream);
+hipError_t launch_gap_narrow(const lc_op *d_ops, const int64_t *d_key_off, int32_t n_cex,
+                             lc_key_result *d_out, int32_t *d_pass_keys, KStatus *d_status,
+                             const GapJob &job, hipStream_t stream);
 
 }  // namespace lcdev

@@ -36,9 +36,15 @@ constexpr int64_t kDefaultBudget = 1 << 24;   // configurations per key
 constexpr int64_t kHbmCap[2] = {1 << 16, 1 << 21};
 constexpr int kHbmWaves[2] = {512, 16};
 // Gap tier: at most this many workgroups, and this much workspace (each
-// workgroup needs 84 B per record of the longest key handed over).
+// workgroup needs 92 B per record of the longest key handed over).  Dynamic
+// LDS for the matching arrays: up to kGapLdsFull per workgroup for whole-key
+// decisions (occupancy), up to kGapLdsProbe for counterexample probes.
 constexpr int kGapMaxWG = 1024;
 constexpr size_t kGapWsBytes = size_t(1) << 30;
+constexpr int kGapLdsFull = 48 << 10;
+constexpr int kGapLdsProbe = 48 << 10;
+constexpr int kGapMaxRounds = 64;
+constexpr int kGapProbeMinLen = 1024;
 
 struct Dev {
   int id = -1;
@@ -60,6 +66,8 @@ struct Dev {
   size_t jit2_cap = 0;
   int32_t *d_gws = nullptr;            // gap-tier workspace
   size_t gws_cap = 0;
+  char *d_cex = nullptr;               // gap-tier counterexample intervals + probes
+  size_t cex_cap = 0;
   hipEvent_t eg = nullptr;
   double gap_ms = 0;
   int64_t n_gap = 0;
@@ -186,19 +194,73 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     return 0;
   }
   hipEvent_t before_jit = d.ef;
-  const int64_t gap_cap = (int64_t)d.h_status->max_len + 2;
+  const int64_t gap_cap = ((int64_t)d.h_status->max_len + 2 + 3) & ~int64_t(3);  // 16-B records
   const size_t gap_per_wg = lcdev::gap_tier_ws_bytes(1, gap_cap);
   if (!(flags & (LC_FLAG_NO_FAST_PATH | LC_FLAG_NO_GAP_TIER)) && gap_per_wg <= kGapWsBytes) {
     // tier 1: gap matching for version-pinned keys (crashed writes/CAS, long
     // keys, invalid keys); what it cannot decide goes on to the JIT search
-    const int n_wg = (int)std::min<int64_t>(
-        {n_jit, (int64_t)kGapMaxWG, std::max<int64_t>(1, (int64_t)(kGapWsBytes / gap_per_wg))});
+    const int wg_cap = (int)std::min<int64_t>(
+        (int64_t)kGapMaxWG, std::max<int64_t>(1, (int64_t)(kGapWsBytes / gap_per_wg)));
     rc = ensure(c, reinterpret_cast<char **>(&d.d_gws), &d.gws_cap,
-                lcdev::gap_tier_ws_bytes(n_wg, gap_cap));
+                lcdev::gap_tier_ws_bytes((int)std::min<int64_t>(n_jit, wg_cap), gap_cap));
     if (!rc) rc = ensure(c, &d.d_jit2, &d.jit2_cap, sizeof(int32_t) * (size_t)n_keys);
+    // counterexample intervals: key, lo, hi, gaps, state (int32), nodes
+    // (int64) per invalid key, and one int32 per probe workgroup
+    const size_t nk = (size_t)n_jit;
+    if (!rc) rc = ensure(c, &d.d_cex, &d.cex_cap, nk * (5 * 4 + 8) + 4 * (size_t)wg_cap + 64);
     if (rc) return rc;
-    HIP_TRY(c, lcdev::launch_gap_tier(d_ops, d_off, jit_list, (int32_t)n_jit, p, d_out,
-                                      d.d_gws, n_wg, gap_cap, d.d_jit2, d.d_status, st));
+    lcdev::GapJob job{};
+    job.cex_nodes = reinterpret_cast<int64_t *>(d.d_cex);
+    job.cex_key = reinterpret_cast<int32_t *>(d.d_cex + 8 * nk);
+    job.cex_lo = reinterpret_cast<uint32_t *>(job.cex_key + nk);
+    job.cex_hi = job.cex_lo + nk;
+    job.cex_gaps = reinterpret_cast<int32_t *>(job.cex_hi + nk);
+    job.cex_state = job.cex_gaps + nk;
+    job.probe = job.cex_state + nk;
+    job.mode = lcdev::kGapFull;
+    job.n_tasks = (int32_t)n_jit;
+    // Bisect counterexamples in place unless the keys are long and few
+    // enough for multisection rounds to pay (each round costs two launches
+    // and a sync; a probe of a short key costs less than that).
+    job.bisect = d.h_status->max_len < kGapProbeMinLen || 2 * n_jit > wg_cap;
+    job.lds_bytes = (int)std::min<int64_t>(kGapLdsFull, 56 * (gap_cap + 2));
+    // LC_GAP_LDS=0 (tests): keep every matching in the HBM workspace
+    const char *lds_env = getenv("LC_GAP_LDS");
+    const bool no_lds = lds_env && lds_env[0] == '0';
+    if (no_lds) job.lds_bytes = 0;
+    HIP_TRY(c, lcdev::launch_gap_tier(d_ops, d_off, jit_list, p, d_out, d.d_gws,
+                                      (int)std::min<int64_t>(n_jit, wg_cap), gap_cap, d.d_jit2,
+                                      d.d_status, job, st));
+    HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
+                              hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    const int32_t n_cex = d.h_status->n_cex;
+    if (n_cex > 0) {
+      // counterexamples of long keys: P probes per interval per round, over
+      // the whole GPU
+      job.mode = lcdev::kGapProbe;
+      job.P = wg_cap / n_cex;
+      job.n_tasks = n_cex * job.P;
+      job.lds_bytes = no_lds ? 0 : kGapLdsProbe;
+      rc = ensure(c, reinterpret_cast<char **>(&d.d_gws), &d.gws_cap,
+                  lcdev::gap_tier_ws_bytes(job.n_tasks, gap_cap));
+      if (rc) return rc;
+      for (int round = 0;; round++) {
+        if (round == kGapMaxRounds) {
+          set_err(c, "gap tier: counterexample search did not converge");
+          return -EIO;
+        }
+        HIP_TRY(c, hipMemsetAsync(&d.d_status->n_open, 0, sizeof(int32_t), st));
+        HIP_TRY(c, lcdev::launch_gap_tier(d_ops, d_off, nullptr, p, d_out, d.d_gws, job.n_tasks,
+                                          gap_cap, d.d_jit2, d.d_status, job, st));
+        HIP_TRY(c, lcdev::launch_gap_narrow(d_ops, d_off, n_cex, d_out, d.d_jit2, d.d_status,
+                                            job, st));
+        HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
+                                  hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipStreamSynchronize(st));
+        if (d.h_status->n_open == 0) break;
+      }
+    }
     HIP_TRY(c, hipEventRecord(d.eg, st));
     HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                               hipMemcpyDeviceToHost, st));
@@ -330,6 +392,7 @@ void lc_close(lc_ctx *c) {
     if (d.d_jit) (void)hipFree(d.d_jit);
     if (d.d_jit2) (void)hipFree(d.d_jit2);
     if (d.d_gws) (void)hipFree(d.d_gws);
+    if (d.d_cex) (void)hipFree(d.d_cex);
     if (d.eg) (void)hipEventDestroy(d.eg);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }

@@ -227,6 +227,37 @@ def test_c4_hot_key(ctx, seed, anom):
         assert want == 0  # an injected stale read is always visible
 
 
+def test_gap_tier_many_invalid_keys_bisect(ctx):
+    """More invalid crash-heavy keys than half the gap tier's workgroups: the
+    counterexamples are found by one bisecting workgroup per key instead of
+    the multisection rounds; both agree with the oracle."""
+    ops, off, lab, _ = abi.synth(1500, 50, concurrency=8, p_info=0.2,
+                                 p_anomaly=0.9, seed=41)
+    _, g = ctx.check(ops, off)
+    assert (g["verdict"] == 0).sum() > 600  # > kGapMaxWG / 2: bisect mode
+    _, j = oracle.check(ops, off, algo=oracle.JITC, n_threads=8, max_configs=1 << 20)
+    known = j["verdict"] != -1
+    assert known.sum() > 1000
+    for f in ("verdict", "fail_op", "fail_prefix_end"):
+        assert (g[f][known] == j[f][known]).all(), f
+
+
+@pytest.mark.parametrize("seed,anom", [(0x5EED0004, 0.0), (1006, 1.0)])
+def test_gap_tier_hbm_fallback_agrees(ctx, seed, anom, monkeypatch):
+    """The matching arrays normally live in LDS; LC_GAP_LDS=0 keeps them in
+    the HBM workspace.  Both placements give the same results (C4 hot key,
+    valid and invalid, and a batch of small crash-heavy keys)."""
+    cases = [abi.synth(1, 5000, concurrency=50, p_info=0.2, p_anomaly=anom, seed=seed),
+             abi.synth(300, 80, concurrency=12, p_info=0.2, p_anomaly=0.4, seed=seed + 1)]
+    for ops, off, _, _ in cases:
+        _, a = ctx.check(ops, off)
+        monkeypatch.setenv("LC_GAP_LDS", "0")
+        _, b = ctx.check(ops, off)
+        monkeypatch.delenv("LC_GAP_LDS")
+        for f in ("verdict", "reason", "fail_op", "fail_prefix_end", "max_frontier"):
+            assert (a[f] == b[f]).all(), f
+
+
 def test_gap_tier_and_search_agree(ctx):
     """Where the JIT search decides crash-heavy keys, the gap tier agrees."""
     z = np.load(os.path.join(GOLDEN, "info.npz"))
