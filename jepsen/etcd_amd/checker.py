@@ -17,12 +17,17 @@ jepsen.independent/checker's shape:
 
 with merged = false > "unknown" > true, and "failures" the keys whose
 :valid? is false (jepsen.independent keeps :unknown keys out of :failures,
-since :unknown is truthy in Clojure).  The timeline renderer is out of scope.
+since :unknown is truthy in Clojure).  Each key's map has checker/compose's
+shape, {"valid?", "linear": <the GPU verdict>, "timeline": ...}; with
+timeline_dir set, the timeline half renders <dir>/independent/<k>/
+timeline.html on the host (timeline.py), as jepsen's timeline/html would.
 Errors: a malformed history raises LcError (-EINVAL); jepsen's check-safe
 would turn an exception into {:valid? :unknown :error ...}, which
 `check_safe` reproduces.
 """
-from . import abi, history as H
+import os
+
+from . import abi, history as H, timeline as TL
 
 UNKNOWN = "unknown"
 
@@ -79,11 +84,13 @@ class RegisterChecker:
     (checker/linearizable {:model (model/mutex)}) at lock.clj:243-244; the
     result is then one key's map (no :results)."""
 
-    def __init__(self, model=None, device_mask=0, max_configs_per_key=0, independent=True):
+    def __init__(self, model=None, device_mask=0, max_configs_per_key=0, independent=True,
+                 timeline_dir=None):
         self.model = model or VersionedRegister(0, None)
         self.device_mask = device_mask
         self.max_configs_per_key = max_configs_per_key
         self.independent = independent
+        self.timeline_dir = timeline_dir
         self._ctx = None
 
     def _context(self):
@@ -118,9 +125,22 @@ class RegisterChecker:
             results[k] = out
         if not self.independent:
             return results[None]
+        subs = H.split_by_key(H.index_history(history)) if self.timeline_dir else None
+        for k, lin in results.items():
+            results[k] = self._composed(k, lin, subs)
         return {"valid?": _merge_valid(r["valid?"] for r in results.values()),
                 "results": results,
                 "failures": [k for k, r in results.items() if r["valid?"] is False]}
+
+    def _composed(self, k, linear, subs):
+        """checker/compose's per-key map (register.clj:109-112)."""
+        if subs is None:
+            return {"valid?": linear["valid?"], "linear": linear}
+        path = os.path.join(self.timeline_dir, "independent", str(k), "timeline.html")
+        tl = TL.write(path, subs[k], title="key %s" % (k,),
+                      cex_index=linear.get("fail-prefix-end"))
+        return {"valid?": _merge_valid([linear["valid?"], tl["valid?"]]),
+                "linear": linear, "timeline": tl}
 
     def close(self):
         if self._ctx is not None:

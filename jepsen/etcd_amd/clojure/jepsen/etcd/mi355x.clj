@@ -15,8 +15,12 @@
   =) and packs one 48-byte lc_op record per operation into off-heap memory.
   One lc_check call (JNA, liblincheck.so; C ABI in include/lincheck.h) then
   decides every key on the MI355X GPUs of the control node.  The result has
-  jepsen.independent/checker's shape.  The timeline renderer is not
-  reproduced (out of scope); compose it separately if wanted.
+  jepsen.independent/checker's shape, and each key's entry has
+  checker/compose's shape: {:valid? merged, :linear <the GPU verdict>,
+  :timeline <jepsen's own timeline/html over that key's subhistory, written
+  under the key's independent/ subdirectory>}.  Only :linear moves to the
+  GPU; the timeline stays jepsen's renderer (pass :timeline? false to skip
+  it, e.g. for benchmarks).
 
   Usage, in register.clj's workload:
 
@@ -25,6 +29,7 @@
   Untested in the build container (no JVM there); the same contract is
   exercised from Python by tests/test_gpu.py::test_register_checker_end_to_end."
   (:require [jepsen.checker :as checker]
+            [jepsen.checker.timeline :as timeline]
             [jepsen.independent :as independent])
   (:import (com.sun.jna Function Memory NativeLibrary Pointer)
            (com.sun.jna.ptr PointerByReference)))
@@ -206,17 +211,36 @@
           {:valid? true :analyzer :mi355x}
           (get (check-keys model max-configs-per-key {nil ops}) nil))))))
 
+(defn- composed
+  "checker/compose's per-key map (register.clj:109-112): the GPU's :linear
+  result beside jepsen's own timeline/html, which renders into the key's
+  independent/ subdirectory as jepsen.independent/checker would direct it."
+  [test opts k sub linear timeline?]
+  (if-not timeline?
+    {:valid? (:valid? linear) :linear linear}
+    (let [subdir (concat (:subdirectory opts) ["independent" k])
+          tl     (checker/check-safe (timeline/html) test sub
+                                     {:subdirectory subdir :history-key k})]
+      {:valid?   (merge-valid [(:valid? linear) (:valid? tl)])
+       :linear   linear
+       :timeline tl})))
+
 (defn checker
   "The drop-in (see ns doc).  opts: :max-configs-per-key (0 = default),
-  :model (default :versioned-register, register.clj:111)."
+  :model (default :versioned-register, register.clj:111), :timeline?
+  (default true: keep register.clj:112's timeline/html per key)."
   ([] (checker {}))
-  ([{:keys [max-configs-per-key model] :or {max-configs-per-key 0 model :versioned-register}}]
+  ([{:keys [max-configs-per-key model timeline?]
+     :or {max-configs-per-key 0 model :versioned-register timeline? true}}]
    (reify checker/Checker
-     (check [_ test history _opts]
+     (check [_ test history opts]
        (let [subs (subhistories history)]
          (if (empty? subs)
            {:valid? true :results {} :failures []}
-           (let [results (check-keys model max-configs-per-key subs)]
+           (let [linear  (check-keys model max-configs-per-key subs)
+                 results (into (array-map)
+                               (for [[k r] linear]
+                                 [k (composed test opts k (get subs k) r timeline?)]))]
              {:valid?   (merge-valid (map :valid? (vals results)))
               :results  results
               :failures (vec (for [[k r] results :when (false? (:valid? r))] k))})))))))

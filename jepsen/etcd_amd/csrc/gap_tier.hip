@@ -293,6 +293,10 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
   const int tid = threadIdx.x, n = g.n, wv = tid / kWave, lane = tid & (kWave - 1);
   GapSh &sh = *g.sh;
   const GapWs &w = g.ws;
+  // Every wave must be done reading the previous decision's shared words
+  // (sh.flag on its early-return paths, sh.maxret) before thread 0 resets
+  // them: decisions follow each other without a barrier in the bisection.
+  __syncthreads();
   for (int k = tid; k <= n; k += kGapThreads) {
     w.A[k] = 0;  // max call + 1 of what must precede t_k; 0 = nothing
     w.B[k] = kNever;

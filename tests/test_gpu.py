@@ -258,6 +258,24 @@ def test_gap_tier_hbm_fallback_agrees(ctx, seed, anom, monkeypatch):
             assert (a[f] == b[f]).all(), f
 
 
+def test_gap_tier_repeatable(ctx):
+    """Same batch, same answers, call after call: the gap tier's decisions
+    within one workgroup follow each other without extra barriers, so a
+    shared-word race would show as run-to-run differences here (C5 fixture:
+    short invalid keys, bisected in place; a crash-heavy batch)."""
+    z = np.load(os.path.join(GOLDEN, "c5.npz"))
+    cases = [(z["ops"], z["key_off"]),
+             abi.synth(400, 120, concurrency=12, p_info=0.2, p_anomaly=0.5, seed=77)[:2]]
+    for ops, off in cases:
+        _, first = ctx.check(ops, off)
+        for _ in range(4):
+            _, again = ctx.check(ops, off)
+            for f in ("verdict", "fail_op", "fail_prefix_end", "max_frontier"):
+                assert (again[f] == first[f]).all(), f
+    _, r = ctx.check(z["ops"], z["key_off"])
+    assert (r["verdict"] == z["verdict"]).all() and (r["fail_op"] == z["fail_op"]).all()
+
+
 def test_gap_tier_and_search_agree(ctx):
     """Where the JIT search decides crash-heavy keys, the gap tier agrees."""
     z = np.load(os.path.join(GOLDEN, "info.npz"))
@@ -306,16 +324,17 @@ def test_check_device_path_with_torch(ctx):
     ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), b - a, d_out.data_ptr(),
                      stream=s.cuda_stream)
     r = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
-    assert (r["verdict"] == z["verdict"][a:b]).all()
-    assert (r["fail_op"] == z["fail_op"][a:b]).all()
+    bad = np.nonzero((r["verdict"] != z["verdict"][a:b]) | (r["fail_op"] != z["fail_op"][a:b]))[0]
+    assert len(bad) == 0, [(a + int(k), r[k].tolist(), int(z["verdict"][a + k]),
+                            int(z["fail_op"][a + k])) for k in bad[:5]] + [ctx.stats()]
     assert ctx.stats()["kernel_ms"] > 0
 
 
-def test_register_checker_end_to_end():
+def test_register_checker_end_to_end(tmp_path):
     from jepsen.etcd_amd import checker as C, synth
     hist, labels = synth.jepsen_history(60, 120, concurrency=10, p_info=0.03,
                                         p_anomaly=0.3, seed=5)
-    chk = C.register_checker(device_mask=1)
+    chk = C.register_checker(device_mask=1, timeline_dir=str(tmp_path))
     res = chk.check({"name": "etcd register"}, hist, {})
     chk.close()
     from jepsen.etcd_amd import history as H
@@ -327,6 +346,9 @@ def test_register_checker_end_to_end():
     assert sorted(res["failures"]) == bad
     for k in bad:
         r = res["results"][k]
-        assert r["valid?"] is False and r["op"]["type"] == "ok"
+        assert r["valid?"] is False and r["linear"]["op"]["type"] == "ok"
+        page = open(r["timeline"]["file"]).read()  # independent/<k>/timeline.html
+        assert 'cex"' in page and os.path.dirname(r["timeline"]["file"]).endswith("/%d" % k)
+    assert res["results"][0]["timeline"]["valid?"] is True
     assert C.check_safe(chk, {}, [{"type": "invoke", "process": 0, "value": None}]) == \
         {"valid?": True, "results": {}, "failures": []}

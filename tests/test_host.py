@@ -154,3 +154,31 @@ def test_plan_partition_balanced_and_contiguous():
 def test_kat_file_consistent():
     for k in load_kats():
         assert k["fail_prefix_end"] == (k["ops"][k["fail_op"]][5] if k["fail_op"] >= 0 else -1)
+
+
+def test_timeline_render():
+    """The :timeline half of register.clj:112 (host-side renderer): one box
+    per client op, spanning invoke..completion, classed by completion type;
+    the counterexample op outlined, later ops dimmed; text escaped."""
+    from jepsen.etcd_amd import timeline as TL
+    T = H.tuple_
+    hist = [
+        {"type": "invoke", "process": 0, "f": "write", "value": T(1, [None, 1])},
+        {"type": "ok", "process": 0, "f": "write", "value": T(1, [1, 1])},
+        {"type": "invoke", "process": 1, "f": "read", "value": T(1, [None, None])},
+        {"type": "invoke", "process": "nemesis", "f": "kill", "value": None},
+        {"type": "ok", "process": 1, "f": "read", "value": T(1, [1, "<b>"])},
+        {"type": "invoke", "process": 2, "f": "cas", "value": T(1, [None, [1, 2]])},
+        {"type": "info", "process": 2, "f": "cas", "value": T(1, [None, [1, 2]])},
+        {"type": "invoke", "process": 0, "f": "read", "value": T(1, [None, None])},
+    ]
+    sub = H.split_by_key(H.index_history(hist))[1]
+    ps = TL.pairs(sub)
+    assert [(i["index"], c["index"] if c else None) for i, c in ps] == \
+        [(0, 1), (2, 4), (5, 6), (7, None)]
+    page = TL.render(sub, title="key 1", cex_index=4)
+    assert page.count('class="op ') == 4
+    assert 'class="op ok cex"' in page and 'class="op info after"' in page
+    assert 'class="op invoke after"' in page
+    assert "&lt;b&gt;" in page and "<b>" not in page.split("<body>")[1]
+    assert ">0<" in page and ">2<" in page and "nemesis" not in page
