@@ -201,18 +201,29 @@ def main():
 def hot_key(ctx, abi):
     """BASELINE configs[3]: one key, 5k ops, concurrency 50, 20 % :info,
     decided by the gap tier (every frontier search, knossos's included, runs
-    out of budget on it).  Not part of `value`; median of 5 calls."""
-    ops, off, _, n_inv = abi.synth(1, 5000, concurrency=50, p_info=0.2, seed=0x5EED0004)
-    times, gap = [], []
-    for _ in range(6):
-        t0 = time.perf_counter()
-        _, r = ctx.check(ops, off)
-        times.append((time.perf_counter() - t0) * 1e3)
-        gap.append(ctx.stats()["gap_kernel_ms"])
-    return {"workload": "C4: 1 key x 5000 ops, concurrency 50, p_info 0.2 (host buffers)",
-            "verdict": int(r["verdict"][0]), "crashed_ops": int((ops[:, 5] == abi.LC_INF).sum()),
-            "matchings": int(r["configs_explored"][0]), "gaps": int(r["max_frontier"][0]),
-            "gap_kernel_ms": float(np.median(gap[1:])), "call_ms": float(np.median(times[1:]))}
+    out of budget on it); also the same shape with injected anomalies, whose
+    counterexample search (multisection rounds over the whole GPU) is timed
+    too.  Not part of `value`; median of 5 calls after one warm-up."""
+    out = {}
+    for tag, anom, seed in (("valid", 0.0, 0x5EED0004), ("invalid", 1.0, 1006)):
+        ops, off, _, n_inv = abi.synth(1, 5000, concurrency=50, p_info=0.2,
+                                       p_anomaly=anom, seed=seed)
+        times, gap = [], []
+        for _ in range(6):
+            t0 = time.perf_counter()
+            _, r = ctx.check(ops, off)
+            times.append((time.perf_counter() - t0) * 1e3)
+            gap.append(ctx.stats()["gap_kernel_ms"])
+        out[tag] = {"verdict": int(r["verdict"][0]),
+                    "crashed_ops": int((ops[:, 5] == abi.LC_INF).sum()),
+                    "matchings": int(r["configs_explored"][0]), "gaps": int(r["max_frontier"][0]),
+                    "gap_kernel_ms": float(np.median(gap[1:])),
+                    "call_ms": float(np.median(times[1:]))}
+        if tag == "invalid":
+            out[tag]["fail_op"] = int(r["fail_op"][0])
+    v = out["valid"]
+    return dict(v, workload="C4: 1 key x 5000 ops, concurrency 50, p_info 0.2 (host buffers)",
+                invalid=out["invalid"])
 
 
 def search_leg(ctx, abi, d_ops, d_off, d_out, args, stream, n_ops):
