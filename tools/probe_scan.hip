@@ -123,6 +123,41 @@ __global__ __launch_bounds__(kT) void persist(const longlong2 *__restrict__ p, c
   }
 }
 
+// LDS-DMA: the key's 48 KB straight into LDS (global_load_lds_dwordx4, 1 KB
+// per wave-instruction), then folded from LDS.  AUX 0 = default policy, 2 = nt.
+template <int AUX>
+__global__ __launch_bounds__(kT) void glds(const longlong2 *__restrict__ p, const int64_t *__restrict__ off,
+                                           int64_t *__restrict__ out) {
+  __shared__ longlong2 L[3 * 1024];
+  const int64_t beg = off[blockIdx.x], n = off[blockIdx.x + 1] - beg;
+  const longlong2 *q = p + beg * 3;
+  const int nch = (int)n * 3;
+  const int w = threadIdx.x / 64;
+#pragma unroll
+  for (int u = 0; u < 12; u++) {
+    const int ch = threadIdx.x + u * kT;
+    if (u * kT + w * 64 < nch)  // wave-uniform: the whole 1 KB row is in range (n = 1000)
+      __builtin_amdgcn_global_load_lds((const void *)(q + ch), (__attribute__((address_space(3))) void *)(L + u * kT + w * 64), 16, 0, AUX);
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0) expcnt(0)
+  __syncthreads();
+  int64_t acc = 0;
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int r = threadIdx.x + u * kT;
+    if (r < n) {
+      const longlong2 x = L[3 * r], y = L[3 * r + 1], z = L[3 * r + 2];
+      acc += x.x ^ y.y ^ z.x ^ z.y;
+    }
+  }
+  __shared__ int64_t s;
+  if (threadIdx.x == 0) s = 0;
+  __syncthreads();
+  atomicXor((unsigned long long *)&s, (unsigned long long)acc);
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
 int main() {
   const size_t nrec = (size_t)kRec * kKeys;
   std::vector<int64_t> h(nrec * 6), ho(kKeys + 1);
@@ -155,6 +190,9 @@ int main() {
   run("strided", [&] { strided<<<kKeys, kT>>>(d, doff, dout); });
   run("coal", [&] { coal<<<kKeys, kT>>>(d, doff, dout); });
   run("coal_lds", [&] { coal_lds<<<kKeys, kT>>>(d, doff, dout); });
+  run("glds", [&] { glds<0><<<kKeys, kT>>>(d, doff, dout); });
+  run("glds_nt", [&] { glds<2><<<kKeys, kT>>>(d, doff, dout); });
+  run("strided", [&] { strided<<<kKeys, kT>>>(d, doff, dout); });
   for (int g : {256, 512, 1024, 2048})
   {
     char nm[32];
