@@ -198,6 +198,32 @@ class Context:
         return rc
 
 
+    def bind_check_device(self, d_ops, d_key_off, n_keys, d_out, stream=None, opts=None,
+                          stats=None):
+        """check_device with its arguments converted once: returns a
+        zero-argument callable that runs the check (and fills `stats`, an
+        LcStats, when given) and raises LcError on failure.  For loops that
+        time the same call over and over (bench.py)."""
+        L = lib()
+        o = opts if opts is not None else default_opts()
+        args = (self._h, ctypes.c_void_p(d_ops), ctypes.c_void_p(d_key_off),
+                ctypes.c_int64(n_keys), ctypes.byref(o), ctypes.c_void_p(d_out),
+                ctypes.c_void_p(stream) if stream else None)
+        fn, st_fn = L.lc_check_device, L.lc_last_stats
+        st_args = (self._h, ctypes.byref(stats)) if stats is not None else None
+
+        def call():
+            rc = fn(*args)
+            if rc != 0:
+                raise LcError(rc, self.last_error())
+            if st_args is not None:
+                st_fn(*st_args)
+            return stats
+
+        call._keep = (o, stats)  # the byref targets must outlive the closure
+        return call
+
+
 def plan_partition(key_off, n_parts):
     key_off = np.ascontiguousarray(key_off, dtype=np.int64)
     bounds = np.zeros(n_parts + 1, dtype=np.int64)

@@ -328,6 +328,14 @@ def test_check_device_path_with_torch(ctx):
     assert len(bad) == 0, [(a + int(k), r[k].tolist(), int(z["verdict"][a + k]),
                             int(z["fail_op"][a + k])) for k in bad[:5]] + [ctx.stats()]
     assert ctx.stats()["kernel_ms"] > 0
+    # the pre-bound form bench.py times gives the same results and stats
+    d_out.zero_()
+    st = abi.LcStats()
+    call = ctx.bind_check_device(d_ops.data_ptr(), d_off.data_ptr(), b - a, d_out.data_ptr(),
+                                 stream=s.cuda_stream, stats=st)
+    assert call() is st and st.n_keys == b - a and st.kernel_ms > 0
+    r2 = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
+    assert (r2 == r).all()
 
 
 def test_register_checker_end_to_end(tmp_path):

@@ -123,6 +123,30 @@ __global__ __launch_bounds__(kT) void persist(const longlong2 *__restrict__ p, c
   }
 }
 
+// strided with non-temporal register loads (global_load_dwordx4 ... nt)
+typedef long long v2ll __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(kT) void strided_nt(const longlong2 *__restrict__ p, const int64_t *__restrict__ off,
+                                                  int64_t *__restrict__ out) {
+  const int64_t beg = off[blockIdx.x], n = off[blockIdx.x + 1] - beg;
+  const v2ll *q = reinterpret_cast<const v2ll *>(p + beg * 3);
+  int64_t acc = 0;
+  v2ll a[4], b[4], c[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int r = threadIdx.x + u * kT;
+    if (r < n) { a[u] = __builtin_nontemporal_load(q + 3 * r); b[u] = __builtin_nontemporal_load(q + 3 * r + 1); c[u] = __builtin_nontemporal_load(q + 3 * r + 2); }
+    else { a[u] = b[u] = c[u] = (v2ll){0, 0}; }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; u++) acc += a[u].x ^ a[u].y ^ b[u].x ^ b[u].y ^ c[u].x ^ c[u].y;
+  __shared__ int64_t s;
+  if (threadIdx.x == 0) s = 0;
+  __syncthreads();
+  atomicXor((unsigned long long *)&s, (unsigned long long)acc);
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
 // LDS-DMA: the key's 48 KB straight into LDS (global_load_lds_dwordx4, 1 KB
 // per wave-instruction), then folded from LDS.  AUX 0 = default policy, 2 = nt.
 template <int AUX>
@@ -190,9 +214,11 @@ int main() {
   run("strided", [&] { strided<<<kKeys, kT>>>(d, doff, dout); });
   run("coal", [&] { coal<<<kKeys, kT>>>(d, doff, dout); });
   run("coal_lds", [&] { coal_lds<<<kKeys, kT>>>(d, doff, dout); });
+  run("strided_nt", [&] { strided_nt<<<kKeys, kT>>>(d, doff, dout); });
   run("glds", [&] { glds<0><<<kKeys, kT>>>(d, doff, dout); });
   run("glds_nt", [&] { glds<2><<<kKeys, kT>>>(d, doff, dout); });
   run("strided", [&] { strided<<<kKeys, kT>>>(d, doff, dout); });
+  run("strided_nt", [&] { strided_nt<<<kKeys, kT>>>(d, doff, dout); });
   for (int g : {256, 512, 1024, 2048})
   {
     char nm[32];
