@@ -83,14 +83,23 @@ extern __shared__ int4 lds_dyn[];
 //   14..17 gap records, 18..23 the matching's scalar arrays — the HBM homes
 //   of the matching when it does not fit in LDS; during gap_setup 18..23
 //   also hold the ballot masks and prefix counts of the compactions.
+// A key short enough (kSkelLdsBytes per record with its matching) keeps the
+// whole skeleton in LDS instead: arrays 0..13, the masks at 14..15 and the
+// prefix counts at 16, followed by the matching's LDS region.  Then the
+// setup's barriers wait for LDS stores only, not for HBM write acks.
+constexpr int kSkelArrays = 17;
+constexpr int kSkelLdsBytes = 4 * kSkelArrays + 56;  // + the matching's worst case (G = n_opt = cap)
+
 struct GapWs {
   int32_t *base;
   int64_t cap;
+  bool lds;        // skeleton in LDS (base points into lds_dyn)
+  int moff;        // int4 offset of the matching's LDS region in lds_dyn
   uint32_t *A, *B, *Uh;
   int *Pin, *Val, *PinExp, *Claim, *Req, *Gap;
   int4 *Opt;
-  uint64_t *Mask;  // compaction ballots (array 18..)
-  int *Pre;        // compaction prefix counts (array 20..)
+  uint64_t *Mask;  // compaction ballots
+  int *Pre;        // compaction prefix counts
 };
 
 struct GapSh {
@@ -101,10 +110,12 @@ struct GapSh {
   uint32_t wtotu[kGapWaves];
 };
 
-__device__ __forceinline__ GapWs gap_ws(int32_t *base, int64_t cap) {
+__device__ __forceinline__ GapWs gap_ws(int32_t *base, int64_t cap, bool lds) {
   GapWs w;
   w.base = base;
   w.cap = cap;
+  w.lds = lds;
+  w.moff = lds ? (int)(kSkelArrays * cap / 4) : 0;
   w.A = (uint32_t *)(base + 0 * cap);
   w.B = (uint32_t *)(base + 1 * cap);
   w.Uh = (uint32_t *)(base + 2 * cap);
@@ -115,8 +126,8 @@ __device__ __forceinline__ GapWs gap_ws(int32_t *base, int64_t cap) {
   w.Req = base + 7 * cap;
   w.Gap = base + 9 * cap;
   w.Opt = reinterpret_cast<int4 *>(base + 10 * cap);
-  w.Mask = reinterpret_cast<uint64_t *>(base + 18 * cap);
-  w.Pre = base + 20 * cap;
+  w.Mask = reinterpret_cast<uint64_t *>(base + (lds ? 14 : 18) * cap);
+  w.Pre = base + (lds ? 16 : 20) * cap;
   return w;
 }
 
@@ -452,24 +463,25 @@ struct Cmp {
   int32_t *ws;   // workspace base (HBM fallback)
   int G, n_opt;
   int cap;
+  int moff;      // LDS: int4 offset of the region in lds_dyn
   // LDS: gap records [0, 16G), op records [16G, 16(G+n_opt)), then the
   // int arrays MG SG SR SO (G each), MO Vis (n_opt each).
   // HBM: Opt at array 10, gap records at 14, int arrays at 18..23.
   __device__ __forceinline__ int4 *gaps() const {
     if constexpr (L)
-      return lds_dyn;
+      return lds_dyn + moff;
     else
       return reinterpret_cast<int4 *>(ws + 14 * cap);
   }
   __device__ __forceinline__ int4 *ops() const {
     if constexpr (L)
-      return lds_dyn + G;
+      return lds_dyn + moff + G;
     else
       return reinterpret_cast<int4 *>(ws + 10 * cap);
   }
   __device__ __forceinline__ int &at(int a, int i) const {
     if constexpr (L) {
-      int *b = reinterpret_cast<int *>(lds_dyn + G + n_opt);
+      int *b = reinterpret_cast<int *>(lds_dyn + moff + G + n_opt);
       return b[a < aMO ? a * G + i : 4 * G + (a - aMO) * n_opt + i];
     } else {
       return ws[(18 + a) * cap + i];
@@ -726,13 +738,15 @@ __device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t 
   *n_gaps = G;
   if (G == 0) return GD_VALID;
   if (G > n_opt) return GD_INVALID;
-  const bool in_lds = match_lds_bytes(G, n_opt) <= lds_bytes;
+  const bool in_lds = 16 * w.moff + match_lds_bytes(G, n_opt) <= lds_bytes;
+  if (w.lds && !in_lds) return GD_NA;  // cannot happen: sized for G = n_opt = cap
   Cmp<true> cl;
   Cmp<false> cg;
   cl.ws = cg.ws = w.base;
   cl.G = cg.G = G;
   cl.n_opt = cg.n_opt = n_opt;
   cl.cap = cg.cap = (int)w.cap;
+  cl.moff = cg.moff = w.moff;
   int4 *gaps = in_lds ? cl.gaps() : cg.gaps();
   int *mg = in_lds ? &cl.at(aMG, 0) : &cg.at(aMG, 0);
   int *mo = in_lds ? &cl.at(aMO, 0) : &cg.at(aMO, 0);
@@ -803,7 +817,7 @@ __global__ __launch_bounds__(kGapThreads) void gap_tier_kernel(
   __shared__ GapSh sh;
   const int64_t key_base = key_off[0];
   GapKey g;
-  g.ws = gap_ws(ws + (size_t)blockIdx.x * kGapArrays * cap, cap);
+  int32_t *const ws_hbm = ws + (size_t)blockIdx.x * kGapArrays * cap;
   g.sh = &sh;
   g.V0 = p.init_ver;
   g.init = p.init_val;
@@ -825,6 +839,10 @@ __global__ __launch_bounds__(kGapThreads) void gap_tier_kernel(
     g.kops = ops + (beg - key_base);
     g.n = (int)(end - beg);
     g.base = g.kops[0].call;
+    const int64_t capk = (end - beg + 2 + 3) & ~int64_t(3);
+    g.ws = kSkelLdsBytes * capk <= job.lds_bytes
+               ? gap_ws(reinterpret_cast<int32_t *>(lds_dyn), capk, true)
+               : gap_ws(ws_hbm, cap, false);
     int64_t nodes = 0;
     int G = 0, G_full = 0;
     // One decision (full / probe), or a bisection of decisions.  A single

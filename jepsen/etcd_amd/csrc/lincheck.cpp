@@ -223,7 +223,9 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     // enough for multisection rounds to pay (each round costs two launches
     // and a sync; a probe of a short key costs less than that).
     job.bisect = d.h_status->max_len < kGapProbeMinLen || 2 * n_jit > wg_cap;
-    job.lds_bytes = (int)std::min<int64_t>(kGapLdsFull, 56 * (gap_cap + 2));
+    // room for the longest key's whole skeleton + matching in LDS (68 B per
+    // record for the skeleton, 56 B for the matching) up to kGapLdsFull
+    job.lds_bytes = (int)std::min<int64_t>(kGapLdsFull, 124 * gap_cap);
     // LC_GAP_LDS=0 (tests): keep every matching in the HBM workspace
     const char *lds_env = getenv("LC_GAP_LDS");
     const bool no_lds = lds_env && lds_env[0] == '0';
