@@ -140,12 +140,13 @@ def main():
                        ("lds_tier_kernel", jit_ms)), key=lambda t: t[1])
     algo_bytes = ALGO_BYTES_PER_OP * n_ops + ALGO_BYTES_PER_KEY * args.keys
     achieved = algo_bytes / (dom_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = l2_hit = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             if tj.get("n_ops") == n_ops and tj.get("kernel") == dom:
                 traffic = tj.get("hbm_bytes_per_launch")
+                l2_hit = tj.get("l2_hit_rate")
         except (ValueError, OSError):
             traffic = None
 
@@ -184,6 +185,9 @@ def main():
             "kernel_ms": dom_ms,
             "algorithmic_bytes_per_launch": algo_bytes,
             "algorithmic_bytes": "48 B/op record read + 40 B/key result (DESIGN.md §6)",
+            "traffic_source": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch, profiles/"
+                              + os.path.basename(args.traffic_json),
+            "l2_hit_rate": l2_hit,
         },
         "tiers": {"fast_kernel_ms": fast_ms, "gap_kernel_ms": gap_ms, "jit_kernel_ms": jit_ms,
                   "jit_keys": float(np.mean(njit)), "all_kernels_ms": kernel_ms,

@@ -24,4 +24,7 @@ echo "fetch done"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/prof_$TAG/write -o write --output-format csv -- \
   python3 $R/bench.py --steps 5 --warmup 1 --bare > $O/prof_$TAG/write.log 2>&1
 echo "write done"
+timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d $O/prof_$TAG/l2 -o l2 --output-format csv -- \
+  python3 $R/bench.py --steps 5 --warmup 1 --bare > $O/prof_$TAG/l2.log 2>&1
+echo "l2 done"
 find $O/prof_$TAG -name '*.csv' | head -50

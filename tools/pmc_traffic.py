@@ -31,6 +31,11 @@ def main():
     write_kib, nw = counter(os.path.join(src, "write", "write_counter_collection.csv"), "WRITE_SIZE")
     read_b = fetch_kib * 1024 * 2      # gfx950 correction for 16-B/lane reads
     write_b = write_kib * 1024
+    l2 = os.path.join(src, "l2", "l2_counter_collection.csv")
+    hit = miss = None
+    if os.path.exists(l2):
+        hit, _ = counter(l2, "TCC_HIT_sum")
+        miss, _ = counter(l2, "TCC_MISS_sum")
     stats = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))))
     k = [r for r in stats if KERNEL in r["Name"]][0]
     out = {
@@ -42,12 +47,15 @@ def main():
         "hbm_bytes_per_launch": read_b + write_b,
         "hbm_bytes_per_op": (read_b + write_b) / n_ops,
         "rocprof_avg_ns": float(k["AverageNs"]), "rocprof_calls": int(k["Calls"]),
+        "l2_hits": hit, "l2_misses": miss,
+        "l2_hit_rate": (hit / (hit + miss)) if hit is not None and hit + miss > 0 else None,
         "note": "FETCH_SIZE doubled (gfx950 wide-read undercount); WRITE_SIZE as reported",
     }
     json.dump(out, open(os.path.join(dst, "traffic_%s.json" % tag), "w"), indent=1)
     for sub, f in (("kt", "kt_kernel_stats.csv"), ("kt", "kt_domain_stats.csv"),
                    ("fetch", "fetch_counter_collection.csv"),
-                   ("write", "write_counter_collection.csv")):
+                   ("write", "write_counter_collection.csv"),
+                   ("l2", "l2_counter_collection.csv")):
         p = os.path.join(src, sub, f)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, tag, f))
