@@ -72,7 +72,8 @@ typedef struct lc_opts {
   int64_t init_version;        /* 0 */
   int64_t init_value;          /* LC_NIL */
   int64_t max_configs_per_key; /* <=0: library default; exceeding -> :unknown */
-  int64_t time_budget_ms;      /* <=0: none (reserved; budget is by configs) */
+  int64_t time_budget_ms;      /* <=0: none; else a key whose frontier search runs longer
+                                  than this is :unknown (LC_REASON_TIME_BUDGET) */
   int64_t flags;               /* LC_FLAG_* */
 } lc_opts;
 
@@ -94,6 +95,7 @@ typedef struct lc_opts {
 #define LC_REASON_MALFORMED       4 /* record out of range / unsorted -> :unknown, call returns -EINVAL */
 #define LC_REASON_UNKNOWN_F       5 /* f not in {read,write,cas}: model throws (register.clj:63) -> :unknown */
 #define LC_REASON_FRONTIER_LDS    6 /* internal: LDS tier overflowed (never returned when HBM retry runs) */
+#define LC_REASON_TIME_BUDGET     7 /* lc_opts.time_budget_ms exceeded by the frontier search -> :unknown */
 
 /* Largest number of simultaneously open (called, not yet returned, or
  * crashed-but-unlinearized) operations one key may have. */

@@ -25,6 +25,7 @@ REASONS = {
     3: "window-overflow",
     4: "malformed",
     5: "unknown-f",
+    7: "time-budget",
     6: "frontier-lds",
 }
 LC_REASON_NONLINEARIZABLE = 1
@@ -114,10 +115,12 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
 
-def default_opts(max_configs_per_key=0, init_version=0, init_value=LC_NIL, flags=0):
+def default_opts(max_configs_per_key=0, init_version=0, init_value=LC_NIL, flags=0,
+                 time_budget_ms=0):
     o = LcOpts()
     lib().lc_default_opts(ctypes.byref(o))
     o.max_configs_per_key = max_configs_per_key
+    o.time_budget_ms = time_budget_ms
     o.init_version = init_version
     o.init_value = init_value
     o.flags = flags

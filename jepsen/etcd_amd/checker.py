@@ -85,12 +85,13 @@ class RegisterChecker:
     result is then one key's map (no :results)."""
 
     def __init__(self, model=None, device_mask=0, max_configs_per_key=0, independent=True,
-                 timeline_dir=None):
+                 timeline_dir=None, time_budget_ms=0):
         self.model = model or VersionedRegister(0, None)
         self.device_mask = device_mask
         self.max_configs_per_key = max_configs_per_key
         self.independent = independent
         self.timeline_dir = timeline_dir
+        self.time_budget_ms = time_budget_ms
         self._ctx = None
 
     def _context(self):
@@ -107,7 +108,8 @@ class RegisterChecker:
         # the initial value is interned first in every key (id 0); the mutex
         # starts free (id MUTEX_FREE)
         init = H.MUTEX_FREE if m.name == "mutex" else (0 if m.value is not None else H.LC_NIL)
-        o = abi.default_opts(self.max_configs_per_key, m.version, init)
+        o = abi.default_opts(self.max_configs_per_key, m.version, init,
+                             time_budget_ms=self.time_budget_ms)
         _, res = self._context().check(ops, key_off, o)
         results = {}
         for i, k in enumerate(keys):

@@ -168,14 +168,14 @@
 
 (defn- check-keys
   "One lc_check over subs {k [op ...]}: {k result-map}."
-  [model max-configs-per-key subs]
+  [model max-configs-per-key time-budget-ms subs]
   (let [[keys done ops off] (pack model subs)
         nk   (count keys)
         out  (Memory. (* result-bytes nk))
         o    (doto (Memory. 40)
                (.setLong 0 0) (.setLong 8 (if (= model :mutex) 0 LC_NIL))
                (.setLong 16 max-configs-per-key)
-               (.setLong 24 0) (.setLong 32 0))
+               (.setLong 24 time-budget-ms) (.setLong 32 0))
         rc   (locking ctx
                (.invokeInt (fun "lc_check")
                            (object-array [@ctx ops off (long nk) o out])))]
@@ -203,13 +203,14 @@
   models this library packs: opts :model one of :versioned-register,
   :cas-register, :register, :mutex.  The lock workload's checker
   (lock.clj:243-244) becomes (linearizable {:model :mutex})."
-  [{:keys [model max-configs-per-key] :or {model :versioned-register max-configs-per-key 0}}]
+  [{:keys [model max-configs-per-key time-budget-ms]
+    :or {model :versioned-register max-configs-per-key 0 time-budget-ms 0}}]
   (reify checker/Checker
     (check [_ test history _opts]
       (let [ops (filterv client-op? history)]
         (if (empty? ops)
           {:valid? true :analyzer :mi355x}
-          (get (check-keys model max-configs-per-key {nil ops}) nil))))))
+          (get (check-keys model max-configs-per-key time-budget-ms {nil ops}) nil))))))
 
 (defn- composed
   "checker/compose's per-key map (register.clj:109-112): the GPU's :linear
@@ -228,16 +229,18 @@
 (defn checker
   "The drop-in (see ns doc).  opts: :max-configs-per-key (0 = default),
   :model (default :versioned-register, register.clj:111), :timeline?
-  (default true: keep register.clj:112's timeline/html per key)."
+  (default true: keep register.clj:112's timeline/html per key),
+  :time-budget-ms (0 = none: a key whose frontier search runs longer is
+  :unknown, as knossos's aborts are)."
   ([] (checker {}))
-  ([{:keys [max-configs-per-key model timeline?]
-     :or {max-configs-per-key 0 model :versioned-register timeline? true}}]
+  ([{:keys [max-configs-per-key model timeline? time-budget-ms]
+     :or {max-configs-per-key 0 model :versioned-register timeline? true time-budget-ms 0}}]
    (reify checker/Checker
      (check [_ test history opts]
        (let [subs (subhistories history)]
          (if (empty? subs)
            {:valid? true :results {} :failures []}
-           (let [linear  (check-keys model max-configs-per-key subs)
+           (let [linear  (check-keys model max-configs-per-key time-budget-ms subs)
                  results (into (array-map)
                                (for [[k r] linear]
                                  [k (composed test opts k (get subs k) r timeline?)]))]

@@ -390,6 +390,7 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
   Masks mk{0, 0, 0, 0};
 
   const int64_t base_idx = kops[0].call;  // scalar load (key is wave-uniform)
+  const uint64_t t0 = p.time_ticks ? wall_clock64() : 0;
   uint32_t last_call = kNever;
   Rec cur = decode(load_raw(kops, lane, n), base_idx);
   check_order(cur, last_call, lane);
@@ -538,6 +539,13 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
       }
     }
     if (!single) {
+      // the time budget is checked where time goes: returns on the general
+      // (multi-configuration) path
+      if (p.time_ticks && wall_clock64() - t0 > p.time_ticks) {
+        o.verdict = LC_UNKNOWN;
+        o.reason = LC_REASON_TIME_BUDGET;
+        return;
+      }
       const int r = general_return(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
       if (r < 0) {
         o.verdict = LC_UNKNOWN;

@@ -13,7 +13,8 @@ namespace lcdev {
 struct KParams {
   int32_t init_ver;
   int32_t init_val;
-  int64_t budget;  // max configurations generated per key
+  int64_t budget;      // max configurations generated per key
+  uint64_t time_ticks; // max device wall-clock ticks per key in the search tiers (0: none)
 };
 
 // Device-side status words, zeroed before every call.

@@ -139,6 +139,15 @@ int opts_to_params(lc_ctx *c, const lc_opts *o, lcdev::KParams *p) {
   p->init_ver = (int32_t)o->init_version;
   p->init_val = (int32_t)o->init_value;
   p->budget = o->max_configs_per_key > 0 ? o->max_configs_per_key : kDefaultBudget;
+  p->time_ticks = 0;
+  if (o->time_budget_ms > 0) {
+    // device wall clock (s_memrealtime) rate, kHz = ticks per ms
+    int dev = 0, khz = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+      khz = 100000;
+    p->time_ticks = (uint64_t)o->time_budget_ms * (uint64_t)khz;
+  }
   return 0;
 }
 

@@ -288,6 +288,25 @@ def test_gap_tier_and_search_agree(ctx):
     assert ((a["verdict"] != -1) | (b["verdict"] == -1)).all()
 
 
+def test_time_budget_is_unknown(ctx):
+    """lc_opts.time_budget_ms bounds the frontier search per key: the C4 hot
+    key with the gap tier off blows up every search (11.8 s to the
+    configuration budget); with a 30 ms time budget it is :unknown
+    (LC_REASON_TIME_BUDGET) in well under a second, while the clean keys of
+    the same call are still decided."""
+    import time
+    hot, hoff, _, _ = abi.synth(1, 5000, concurrency=50, p_info=0.2, seed=0x5EED0004)
+    ops, off, _, _ = abi.synth(20, 100, concurrency=5, seed=3)
+    allops = np.concatenate([hot, ops])
+    alloff = np.concatenate([hoff, off[1:] + hoff[-1]])
+    t = time.perf_counter()
+    _, r = ctx.check(allops, alloff, abi.default_opts(flags=abi.LC_FLAG_NO_GAP_TIER,
+                                                      time_budget_ms=30))
+    assert time.perf_counter() - t < 2.0
+    assert r["verdict"][0] == -1 and r["reason"][0] == 7
+    assert (r["verdict"][1:] == 1).all()
+
+
 def test_malformed_and_unknown_f(ctx):
     bad_order = [[1, 1, -1, 1, 5, 6], [1, 2, -1, 2, 3, 4]]
     bad_ret = [[1, 1, -1, 1, 5, 5]]
