@@ -490,47 +490,65 @@ struct Cmp {
 };
 
 // gap record: x = D, y = R, z = B, w = P;  op record: x = C, y = V, z = E, w = OP
+// (bitwise, no short-circuit: the wave's loops stay uniform, see below)
 __device__ __forceinline__ bool elig(const int4 gp, const int4 op) {
-  return (uint32_t)op.x < (uint32_t)gp.x && (op.w == -1 || op.w == gp.w) &&
-         (gp.y == kAny || op.y == gp.y) && (op.z == kAny || gp.z == kAny || op.z == gp.z);
+  return ((uint32_t)op.x < (uint32_t)gp.x) & ((op.w == -1) | (op.w == gp.w)) &
+         ((gp.y == kAny) | (op.y == gp.y)) & ((op.z == kAny) | (gp.z == kAny) | (op.z == gp.z));
 }
 
-#ifdef GAP_PROFILE
-__shared__ unsigned long long prof_ctr[8];
-#define PROF(i, v) do { if ((threadIdx.x & 63) == 0) prof_ctr[i] += (v); } while (0)
-#else
-#define PROF(i, v) do {} while (0)
-#endif
+// The matching runs on one wave.  Its loops are written so the compiler
+// keeps them uniform (SGPR counters, scalar branches): loop variables pass
+// through readfirstlane (uni), and lane predicates are branch-free over
+// clamped indices — a short-circuit `o < n && a[o] ...` makes the loop a
+// divergent exec-mask loop and costs several times the instructions.
+
+// Stores of the matching arrays must be visible to the wave's later loads
+// from other lanes.  In LDS a wave's DS instructions execute in order, so a
+// compiler barrier is enough; in the HBM fallback wait for the stores
+// (same CU, so L1-coherent).
+template <bool L>
+__device__ __forceinline__ void match_fence() {
+  if constexpr (L)
+    __asm__ volatile("" ::: "memory");
+  else
+    wave_fence();
+}
+
+// One chunk of 64 ops from `base` against gap record gp: bit l of *hit = op
+// base+l is eligible (and free / unvisited per `pred`); returns false when
+// the chunk reaches the gap's deadline (ops are sorted by call: none later
+// can be eligible).
+template <bool L, class Pred>
+__device__ __forceinline__ bool scan_chunk(const Cmp<L> &c, const int4 gp, int base, int n_opt,
+                                           Pred pred, uint64_t *hit) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int o = base + lane, oc = min(o, n_opt - 1);
+  const int4 op = c.ops()[oc];
+  const bool in = o < n_opt;
+  const bool before = in & ((uint32_t)op.x < (uint32_t)gp.x);
+  const bool e = elig(gp, op);
+  const bool ok = pred(oc);
+  *hit = __ballot(before & e & ok);
+  return __ballot(before) == ~0ull;  // every op of the chunk is before the deadline
+}
 
 // First free op eligible for gap gi (or -1); *ff = first possibly-free op.
 template <bool L>
 __device__ int first_fit(const Cmp<L> &c, int gi, int n_opt, int *ff) {
   const int lane = threadIdx.x & (kWave - 1);
-  int base = *ff;
-  for (;;) {  // skip the matched prefix
-    if (base >= n_opt) {
-      *ff = base;
-      return -1;
-    }
-    const int o = base + lane;
-    const uint64_t b = __ballot(o < n_opt && c.at(aMO, o) == -1);
-    if (b) {
-      base += first_lane(b);
-      break;
-    }
-    base += kWave;
-  }
-  *ff = base;
   const int4 gp = uni4(c.gaps()[gi]);
-  const int4 *ops = c.ops();
-  PROF(0, 1);
-  for (; base < n_opt; base += kWave) {
-    PROF(1, 1);
-    if ((uint32_t)uni(ops[base].x) >= (uint32_t)gp.x) break;  // sorted by call
-    const int o = base + lane;
-    const bool e = o < n_opt && c.at(aMO, o) == -1 && elig(gp, ops[o]);
-    const uint64_t b = __ballot(e);
-    if (b) return base + first_lane(b);
+  int base = uni(*ff);
+  auto free_op = [&](int oc) { return c.at(aMO, oc) == -1; };
+  for (bool first = true; base < n_opt; base = uni(base + kWave), first = false) {
+    if (first) {  // advance *ff past the matched prefix with the same chunk
+      const int o = base + lane;
+      const uint64_t fb = __ballot((o < n_opt) & free_op(min(o, n_opt - 1)));
+      *ff = fb ? uni(base + first_lane(fb)) : uni(base + kWave);
+    }
+    uint64_t hit;
+    const bool more = scan_chunk(c, gp, base, n_opt, free_op, &hit);
+    if (hit) return uni(base + first_lane(hit));
+    if (!more) break;
   }
   return -1;
 }
@@ -540,23 +558,19 @@ __device__ int first_fit(const Cmp<L> &c, int gi, int n_opt, int *ff) {
 template <bool L>
 __device__ bool augment(const Cmp<L> &c, int g0, int n_opt, int stamp) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int4 *ops = c.ops();
-  int depth = 0, g = g0, base = 0;
-  PROF(2, 1);
+  int depth = 0, g = uni(g0), base = 0;
+  auto unvisited = [&](int oc) { return c.at(aVis, oc) != stamp; };
   for (;;) {
     const int4 gp = uni4(c.gaps()[g]);
     int found = -1;
-    PROF(3, 1);
-    for (; base < n_opt; base += kWave) {
-      PROF(4, 1);
-      if ((uint32_t)uni(ops[base].x) >= (uint32_t)gp.x) break;
-      const int o = base + lane;
-      const bool e = o < n_opt && c.at(aVis, o) != stamp && elig(gp, ops[o]);
-      const uint64_t b = __ballot(e);
-      if (b) {
-        found = base + first_lane(b);
+    for (; base < n_opt; base = uni(base + kWave)) {
+      uint64_t hit;
+      const bool more = scan_chunk(c, gp, base, n_opt, unvisited, &hit);
+      if (hit) {
+        found = uni(base + first_lane(hit));
         break;
       }
+      if (!more) break;
     }
     if (found < 0) {  // dead end: back to the previous gap
       if (depth == 0) return false;
@@ -571,7 +585,7 @@ __device__ bool augment(const Cmp<L> &c, int g0, int n_opt, int stamp) {
     c.at(aVis, found) = stamp;
     const int m = uni(c.at(aMO, found));
     if (m == -1) {  // flip the path
-      wave_fence();
+      match_fence<L>();
       for (int d0 = 0; d0 <= depth; d0 += kWave) {
         const int d = d0 + lane;
         if (d <= depth) {
@@ -580,7 +594,7 @@ __device__ bool augment(const Cmp<L> &c, int g0, int n_opt, int stamp) {
           c.at(aMO, oo) = gg;
         }
       }
-      wave_fence();
+      match_fence<L>();
       return true;
     }
     depth++;
@@ -595,19 +609,21 @@ __device__ bool augment(const Cmp<L> &c, int g0, int n_opt, int stamp) {
 template <bool L>
 __device__ bool fill(const Cmp<L> &c, int G, int n_opt, int *ff, int *stamp) {
   const int lane = threadIdx.x & (kWave - 1);
-  for (int g0 = 0; g0 < G; g0 += kWave) {
-    uint64_t todo = __ballot(g0 + lane < G && c.at(aMG, g0 + lane) == -1);
+  for (int g0 = 0; g0 < G; g0 = uni(g0 + kWave)) {
+    const int gl = g0 + lane;
+    uint64_t todo = __ballot((gl < G) & (c.at(aMG, min(gl, G - 1)) == -1));
     while (todo) {
-      const int gi = g0 + first_lane(todo);
+      const int gi = uni(g0 + first_lane(todo));
       todo &= todo - 1;
       const int o = first_fit(c, gi, n_opt, ff);
       if (o >= 0) {
         c.at(aMG, gi) = o;
         c.at(aMO, o) = gi;
-        wave_fence();
+        match_fence<L>();
         continue;
       }
-      if (!augment(c, gi, n_opt, ++*stamp)) return false;
+      *stamp = uni(*stamp + 1);
+      if (!augment(c, gi, n_opt, *stamp)) return false;
     }
   }
   return true;
@@ -620,15 +636,15 @@ __device__ int next_value(const Cmp<L> &c, int gi, int last, int n_opt) {
   const int4 gp = uni4(c.gaps()[gi]);
   const int4 *ops = c.ops();
   int best = INT_MAX;
-  for (int base = 0; base < n_opt; base += kWave) {
-    if ((uint32_t)uni(ops[base].x) >= (uint32_t)gp.x) break;
+  for (int base = 0; base < n_opt; base = uni(base + kWave)) {
     const int o = base + lane;
-    if (o < n_opt) {
-      const int4 op = ops[o];
-      if (elig(gp, op) && op.y > last) best = min(best, op.y);
-    }
+    const int4 op = ops[min(o, n_opt - 1)];
+    const bool before = (o < n_opt) & ((uint32_t)op.x < (uint32_t)gp.x);
+    const bool e = elig(gp, op);
+    best = (before & e & (op.y > last)) ? min(best, op.y) : best;
+    if (__ballot(before) != ~0ull) break;  // the deadline falls in this chunk
   }
-  return wave_min_i32(best);
+  return uni(wave_min_i32(best));
 }
 
 // Set gap gi's value requirement to v (kAny = free), with the value-before
@@ -640,7 +656,7 @@ __device__ void set_req(const Cmp<L> &c, int gi, int v, int G, int *ff) {
   reinterpret_cast<int *>(&gaps[gi])[1] = v;
   const bool next = gi + 1 < G && uni(gaps[gi + 1].w) == uni(gaps[gi].w) + 1;
   if (next) reinterpret_cast<int *>(&gaps[gi + 1])[2] = v;
-  wave_fence();
+  match_fence<L>();
   for (int k = 0; k < (next ? 2 : 1); k++) {
     const int g = gi + k;
     const int o = uni(c.at(aMG, g));
@@ -648,8 +664,8 @@ __device__ void set_req(const Cmp<L> &c, int gi, int v, int G, int *ff) {
     if (!elig(uni4(gaps[g]), uni4(c.ops()[o]))) {
       c.at(aMG, g) = -1;
       c.at(aMO, o) = -1;
-      *ff = min(*ff, o);
-      wave_fence();
+      *ff = uni(min(*ff, o));
+      match_fence<L>();
     }
   }
 }
@@ -667,34 +683,22 @@ __device__ int match_branch(const Cmp<L> &c, int G, int n_opt, int *brPos, int *
   for (int node = 0;; node++) {
     if (node >= kNodeBudget) return GD_BUDGET;
     (*nodes)++;
-#ifdef GAP_PROFILE
-    const uint64_t tn = wall_clock64();
-#endif
-    const bool filled = fill(c, G, n_opt, &ff, &stamp);
-    PROF(5, wall_clock64() - tn);
-    if (filled) {
+    if (fill(c, G, n_opt, &ff, &stamp)) {
       // the matching ignored CAS expectations after free gaps: check them
       int viol = INT_MAX;
-      for (int g0 = 1; g0 < G && viol == INT_MAX; g0 += kWave) {
-        const int gi = g0 + lane;
-        bool bad = false;
-        if (gi < G && gaps[gi].z == kAny) {  // gap gi-1 sits just before, free
-          const int e = ops[c.at(aMG, gi)].z;
-          bad = e != kAny && ops[c.at(aMG, gi - 1)].y != e;
+      for (int g0 = 1; g0 < G; g0 = uni(g0 + kWave)) {
+        const int gi = min(g0 + lane, G - 1);  // gaps gi-1, gi; gi-1 free if B = kAny
+        const int e = ops[c.at(aMG, gi)].z, pv = ops[c.at(aMG, gi - 1)].y;
+        const uint64_t b =
+            __ballot((g0 + lane < G) & (gaps[gi].z == kAny) & (e != kAny) & (pv != e));
+        if (b) {
+          viol = uni(g0 + first_lane(b) - 1);
+          break;
         }
-        const uint64_t b = __ballot(bad);
-        if (b) viol = g0 + first_lane(b) - 1;
       }
-#ifdef GAP_PROFILE
-      const uint64_t tv = wall_clock64();
-      PROF(6, tv - tn);
-#endif
       if (viol == INT_MAX) return GD_VALID;
       // branch on the value of free gap `viol`
       const int v = next_value(c, viol, INT_MIN, n_opt);
-#ifdef GAP_PROFILE
-      PROF(7, wall_clock64() - tv);
-#endif
       if (lane == 0) {
         brPos[depth] = viol;
         brVal[depth] = v;
@@ -727,7 +731,6 @@ __device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t 
   const GapWs &w = g.ws;
 #ifdef GAP_PROFILE
   const uint64_t t0 = wall_clock64();
-  if (tid < 8) prof_ctr[tid] = 0;
 #endif
   const int st = gap_setup(g, cut);
   if (st != GD_VALID) return st;
@@ -776,10 +779,6 @@ __device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t 
   const int r = sh.res;
   __syncthreads();
 #ifdef GAP_PROFILE
-  if (tid == 0 && blockIdx.x == 0) {
-    printf("  ff calls %llu chunks %llu | aug calls %llu steps %llu chunks %llu | fill ticks %llu +viol %llu nextval %llu\n",
-           prof_ctr[0], prof_ctr[1], prof_ctr[2], prof_ctr[3], prof_ctr[4], prof_ctr[5], prof_ctr[6], prof_ctr[7]);
-  }
   if (tid == 0 && blockIdx.x < 2)
     printf("gap_decide wg %d cut %u n %d G %d n_opt %d lds %d nodes %ld: setup %lu compact %lu match %lu (x10ns)\n",
            (int)blockIdx.x, cut, g.n, G, n_opt, (int)in_lds, (long)*nodes, (unsigned long)(t1 - t0),
