@@ -198,6 +198,7 @@ def main():
         "hot_key": None,
     }
     if rank == 0 and not args.bare:
+        line["host_leg"] = host_leg(ctx, abi, ops, key_off, n_inv)
         line["hot_key"] = hot_key(ctx, abi)
         line["search_leg"] = search_leg(ctx, abi, d_ops, d_off, d_out, args, stream, n_ops)
         line["mixed_leg"] = mixed_leg(ctx, abi, dev, stream)
@@ -210,6 +211,21 @@ def main():
     ctx.close()
     if distributed:
         dist.destroy_process_group()
+
+
+def host_leg(ctx, abi, ops, key_off, n_inv):
+    """The same C2 batch handed over as host buffers (lc_check: H2D copy of
+    the 480 MB of records, the kernels, D2H of the results), as a JVM caller
+    would: the PCIe-inclusive rate.  Never `value`; median of 3 calls."""
+    times = []
+    for _ in range(4):
+        t0 = time.perf_counter()
+        _, r = ctx.check(ops, key_off)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times[1:]))
+    return {"workload": "C2 batch from host memory (lc_check)", "call_ms": t * 1e3,
+            "ops_per_s": int(key_off[-1]) / t, "h2d_gb_per_s": ops.nbytes / t / 1e9,
+            "valid": int((r["verdict"] == 1).sum())}
 
 
 def hot_key(ctx, abi):

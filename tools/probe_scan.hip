@@ -182,6 +182,45 @@ __global__ __launch_bounds__(kT) void glds(const longlong2 *__restrict__ p, cons
   if (threadIdx.x == 0) out[blockIdx.x] = s;
 }
 
+// Hybrid: per record, chunks a and b by register loads, chunk c (call, ret)
+// by LDS-DMA nt into a 16 KB per-workgroup LDS array (per-lane source
+// addresses, contiguous LDS destination).
+__global__ __launch_bounds__(kT) void hybrid(const longlong2 *__restrict__ p, const int64_t *__restrict__ off,
+                                             int64_t *__restrict__ out) {
+  __shared__ longlong2 C[1024];
+  const int64_t beg = off[blockIdx.x], n = off[blockIdx.x + 1] - beg;
+  const longlong2 *q = p + beg * 3;
+  const int w = threadIdx.x / 64;
+  longlong2 a[4], b[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int r = threadIdx.x + u * kT;
+    if (r < n) {
+      __builtin_amdgcn_global_load_lds((const void *)(q + 3 * r + 2),
+                                       (__attribute__((address_space(3))) void *)(C + u * kT + w * 64), 16, 0, 2);
+      a[u] = q[3 * r];
+      b[u] = q[3 * r + 1];
+    } else {
+      a[u] = b[u] = make_longlong2(0, 0);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  int64_t acc = 0;
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int r = threadIdx.x + u * kT;
+    const longlong2 c = r < n ? C[r] : make_longlong2(0, 0);
+    acc += a[u].x ^ a[u].y ^ b[u].x ^ b[u].y ^ c.x ^ c.y;
+  }
+  __shared__ int64_t s;
+  if (threadIdx.x == 0) s = 0;
+  __syncthreads();
+  atomicXor((unsigned long long *)&s, (unsigned long long)acc);
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
 int main() {
   const size_t nrec = (size_t)kRec * kKeys;
   std::vector<int64_t> h(nrec * 6), ho(kKeys + 1);
@@ -215,10 +254,12 @@ int main() {
   run("coal", [&] { coal<<<kKeys, kT>>>(d, doff, dout); });
   run("coal_lds", [&] { coal_lds<<<kKeys, kT>>>(d, doff, dout); });
   run("strided_nt", [&] { strided_nt<<<kKeys, kT>>>(d, doff, dout); });
+  run("hybrid", [&] { hybrid<<<kKeys, kT>>>(d, doff, dout); });
   run("glds", [&] { glds<0><<<kKeys, kT>>>(d, doff, dout); });
   run("glds_nt", [&] { glds<2><<<kKeys, kT>>>(d, doff, dout); });
   run("strided", [&] { strided<<<kKeys, kT>>>(d, doff, dout); });
   run("strided_nt", [&] { strided_nt<<<kKeys, kT>>>(d, doff, dout); });
+  run("hybrid", [&] { hybrid<<<kKeys, kT>>>(d, doff, dout); });
   for (int g : {256, 512, 1024, 2048})
   {
     char nm[32];
