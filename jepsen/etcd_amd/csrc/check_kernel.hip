@@ -682,8 +682,20 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 }
 
 // Hand key over to the JIT tier (thread 0 only); tell the host there is work.
+// With direct_keys set, a key the gap tier could only pass on (jit_only: an
+// :ok mutation without a version, a read [nil x], malformed records) goes
+// straight to the JIT search's list (count status->n_jit2, which the gap
+// tier appends to as well).
 __device__ __forceinline__ void fast_tier_handoff(int64_t key, int64_t n, int32_t *jit_keys,
-                                                  KStatus *status, int32_t *h_handoff) {
+                                                  KStatus *status, int32_t *h_handoff,
+                                                  int32_t *direct_keys = nullptr,
+                                                  bool jit_only = false) {
+  if (jit_only && direct_keys) {
+    const int at = atomicAdd(&status->n_jit2, 1);
+    direct_keys[at] = (int32_t)key;
+    if (at == 0) __hip_atomic_store(h_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   const int at = atomicAdd(&status->n_jit, 1);
   jit_keys[at] = (int32_t)key;
   atomicMax(&status->max_len, (int32_t)(n < 0 ? 0 : n > INT_MAX ? INT_MAX : n));
@@ -794,7 +806,8 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
                                          lc_key_result *__restrict__ out,
                                          int32_t *__restrict__ jit_keys,
                                          KStatus *__restrict__ status,
-                                         int32_t *__restrict__ h_handoff) {
+                                         int32_t *__restrict__ h_handoff,
+                                         int32_t *__restrict__ direct_keys) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   if (n64 <= 0 || n64 > kFastMax) {
     if (tid == 0) {
@@ -828,7 +841,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
   __syncthreads();
   const int64_t base_idx = kops[0].call;
   const int V0 = p.init_ver;
-  int inel = 0, bad = 0, nmut = 0;
+  int inel = 0, bad = 0, nmut = 0, jit_only = 0;
   // pass 1: place mutations, fold read intervals into A / B
 #pragma unroll
   for (int u = 0; u < kPer; u++) {
@@ -841,11 +854,11 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     if (r < n) {
       const Rec d = decode(b.w[u], base_idx);
       if (d.bad || d.f > LC_F_CAS || (r > 0 && prev >= b.w[u].c.x)) {
-        inel = 1;  // the JIT tier reports malformed / unknown :f
+        inel = jit_only = 1;  // the JIT tier reports malformed / unknown :f
       } else if (d.f == LC_F_READ) {
         if (d.ret != kNever && !(d.ver == -1 && d.val == -1)) {  // else never constrains
           if (d.ver == -1) {
-            inel = 1;  // read [nil x]: its version is free
+            inel = jit_only = 1;  // read [nil x]: its version is free
           } else {
             const int k = d.ver - V0;
             if (k < 0 || k > n) {
@@ -857,7 +870,8 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
           }
         }
       } else if (d.ret == kNever || d.ver == -1) {
-        inel = 1;  // crashed, or no version: order not pinned
+        inel = 1;  // crashed (the gap tier's case), or no version: order not pinned
+        if (d.ret != kNever) jit_only = 1;
       } else {
         const int pos = d.ver - V0 - 1;
         if (pos < 0 || pos >= n) {
@@ -875,7 +889,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
   }
   // (ballots outside the lane-0 branch: they must see every lane)
   const uint32_t wsum = (uint32_t)nmut | (__ballot(inel) ? 1u << 16 : 0u) |
-                        (__ballot(bad) ? 1u << 17 : 0u);
+                        (__ballot(bad) ? 1u << 17 : 0u) | (__ballot(jit_only) ? 1u << 18 : 0u);
   if (lane == 0) s.wsum[w] = wsum;
   __syncthreads();
   const uint4 ws = *reinterpret_cast<const uint4 *>(s.wsum);
@@ -884,7 +898,8 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
   // 0..M-1 each held once (pass 2 checks both)
   const int M = (int)((ws.x & 0xFFFF) + (ws.y & 0xFFFF) + (ws.z & 0xFFFF) + (ws.w & 0xFFFF));
   if (wor >> 16) {  // ineligible or a version out of range: hand over
-    if (tid == 0) fast_tier_handoff(key, n64, jit_keys, status, h_handoff);
+    if (tid == 0)
+      fast_tier_handoff(key, n64, jit_keys, status, h_handoff, direct_keys, (wor >> 18) & 1);
     return;
   }
   // pass 2: positions, duplicates, CAS expectations and read claims against
@@ -931,14 +946,14 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
     const KParams p, lc_key_result *__restrict__ out,
     int32_t *__restrict__ jit_keys, KStatus *__restrict__ status,
-    int32_t *__restrict__ h_handoff) {
+    int32_t *__restrict__ h_handoff, int32_t *__restrict__ direct_keys) {
   __shared__ FastLds s;
   const int64_t key = blockIdx.x;
   const int64_t beg = key_off[key], end = key_off[key + 1];
   const lc_op *kops = ops + (beg - key_off[0]);
   FastRecs r;
   if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
-  fast_key(key, end - beg, kops, r, p, s, out, jit_keys, status, h_handoff);
+  fast_key(key, end - beg, kops, r, p, s, out, jit_keys, status, h_handoff, direct_keys);
 }
 
 // Workspace layout per wave: 3 regions of cap Cfg, 2 tables of 2*cap Cfg,
@@ -985,10 +1000,12 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_jit_keys,
-                            KStatus *d_status, int32_t *h_handoff, hipStream_t stream) {
+                            KStatus *d_status, int32_t *h_handoff, int32_t *d_direct_keys,
+                            hipStream_t stream) {
   if (n_keys <= 0) return hipSuccess;
   hipLaunchKernelGGL(fast_tier_kernel, dim3((unsigned)n_keys), dim3(kFastThreads), 0,
-                     stream, d_ops, d_key_off, p, d_out, d_jit_keys, d_status, h_handoff);
+                     stream, d_ops, d_key_off, p, d_out, d_jit_keys, d_status, h_handoff,
+                     d_direct_keys);
   return hipGetLastError();
 }
 

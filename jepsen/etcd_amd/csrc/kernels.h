@@ -41,12 +41,16 @@ constexpr int kLdsCap = 128;     // configurations per LDS region (3 regions/wav
 // zeroes *h_handoff (host-coherent memory) before it.  A workgroup that hands
 // its key over also stores 1 to *h_handoff, so when every key is decided the
 // host needs no memset or copy around this kernel: one launch plus one sync.
+// With d_direct_keys non-null, keys the gap tier could only pass on (an :ok
+// mutation without a version, a read [nil x], malformed records) are appended
+// there instead (count status->n_jit2), for the JIT search directly.
 // (A grid-wide "last workgroup" counter instead costs 10k same-address
 // atomics per launch: measured 0.115 -> 0.345 ms.)
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_jit_keys,
-                            KStatus *d_status, int32_t *h_handoff, hipStream_t stream);
+                            KStatus *d_status, int32_t *h_handoff, int32_t *d_direct_keys,
+                            hipStream_t stream);
 
 // LDS tier (JIT search): one wavefront per key, for the keys in d_keys
 // (n_keys of them), or for keys 0..n_keys-1 when d_keys is null.  In every

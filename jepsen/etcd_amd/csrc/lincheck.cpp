@@ -166,7 +166,13 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   int rc = ensure(c, &d.d_ovf, &d.ovf_cap, sizeof(int32_t) * (size_t)n_keys);
   if (!rc) rc = ensure(c, &d.d_ovf2, &d.ovf2_cap, sizeof(int32_t) * (size_t)n_keys);
   if (!rc) rc = ensure(c, &d.d_jit, &d.jit_cap, sizeof(int32_t) * (size_t)n_keys);
+  if (!rc) rc = ensure(c, &d.d_jit2, &d.jit2_cap, sizeof(int32_t) * (size_t)n_keys);
   if (rc) return rc;
+  // With the gap tier on, the fast tier sends keys it can only pass on (no
+  // version on an :ok mutation, a read [nil x], malformed) straight to the
+  // JIT list d_jit2, which the gap tier then appends to.
+  const bool gap_on = !(flags & (LC_FLAG_NO_FAST_PATH | LC_FLAG_NO_GAP_TIER));
+  int64_t n_direct = 0;
   // d_status is zero on entry (the fast tier re-zeroes it; later tiers are
   // followed by a memset).  Until this call ends cleanly, assume it is not.
   if (d.status_dirty)
@@ -181,7 +187,8 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     // Only when some workgroup raised h_handoff is the count copied back.
     __atomic_store_n(d.h_handoff, 0, __ATOMIC_RELEASE);
     HIP_TRY(c, lcdev::launch_fast_tier(d_ops, d_off, n_keys, p, d_out, d.d_jit,
-                                       d.d_status, d.h_handoff_dev, st));
+                                       d.d_status, d.h_handoff_dev,
+                                       gap_on ? d.d_jit2 : nullptr, st));
     HIP_TRY(c, hipEventRecord(d.ef, st));
     HIP_TRY(c, hipEventSynchronize(d.ef));
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.ef));
@@ -192,12 +199,13 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                                 hipMemcpyDeviceToHost, st));
       HIP_TRY(c, hipStreamSynchronize(st));
       n_jit = d.h_status->n_jit;
+      n_direct = d.h_status->n_jit2;
     }
     jit_list = d.d_jit;
   } else {
     HIP_TRY(c, hipEventRecord(d.ef, st));
   }
-  if (n_jit == 0) {
+  if (n_jit == 0 && n_direct == 0) {
     d.kernel_ms = d.fast_ms;
     d.status_dirty = false;
     return 0;
@@ -205,14 +213,20 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   hipEvent_t before_jit = d.ef;
   const int64_t gap_cap = ((int64_t)d.h_status->max_len + 2 + 3) & ~int64_t(3);  // 16-B records
   const size_t gap_per_wg = lcdev::gap_tier_ws_bytes(1, gap_cap);
-  if (!(flags & (LC_FLAG_NO_FAST_PATH | LC_FLAG_NO_GAP_TIER)) && gap_per_wg <= kGapWsBytes) {
+  if (gap_on && (n_jit == 0 || gap_per_wg > kGapWsBytes)) {
+    // no gap-tier pass: its queue (if any) joins the direct keys for the JIT
+    if (n_jit > 0)
+      HIP_TRY(c, hipMemcpyAsync(d.d_jit2 + n_direct, d.d_jit, sizeof(int32_t) * (size_t)n_jit,
+                                hipMemcpyDeviceToDevice, st));
+    n_jit += n_direct;
+    jit_list = d.d_jit2;
+  } else if (gap_on) {
     // tier 1: gap matching for version-pinned keys (crashed writes/CAS, long
     // keys, invalid keys); what it cannot decide goes on to the JIT search
     const int wg_cap = (int)std::min<int64_t>(
         (int64_t)kGapMaxWG, std::max<int64_t>(1, (int64_t)(kGapWsBytes / gap_per_wg)));
     rc = ensure(c, reinterpret_cast<char **>(&d.d_gws), &d.gws_cap,
                 lcdev::gap_tier_ws_bytes((int)std::min<int64_t>(n_jit, wg_cap), gap_cap));
-    if (!rc) rc = ensure(c, &d.d_jit2, &d.jit2_cap, sizeof(int32_t) * (size_t)n_keys);
     // counterexample intervals: key, lo, hi, gaps, state (int32), nodes
     // (int64) per invalid key, and one int32 per probe workgroup
     const size_t nk = (size_t)n_jit;
