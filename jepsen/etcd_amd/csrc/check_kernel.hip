@@ -34,6 +34,7 @@
 // unchanged, and the 2^k subsets of concurrent reads never materialise.
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 
 #include "kernels.h"
 #include "records.h"
@@ -152,7 +153,16 @@ struct LdsStore {
 // valid when their epoch tag equals the current return's epoch, so a table is
 // "cleared" by bumping the epoch.  One wave owns one workspace.  Probing is
 // linear from the start of the hashed bucket, whole buckets at a time.
+// Per-return copy of the window's slots in LDS, so each lane can test any
+// slot against its own configuration (HBM tier's lane-parallel expansion).
+struct SlotLds {
+  int4 pre[kWave];      // (nv, nvm, nl, nlm)
+  int val[kWave];
+  uint64_t pbit[kWave];
+};
+
 struct HbmStore {
+  SlotLds *sl;    // slot staging (LDS)
   Cfg *base;      // 3 regions of cap configurations, contiguous
   Cfg *tabs;      // 2 tables (roles R, W) of 2*cap entries
   uint32_t *tags; // 2 tag arrays of 2*cap
@@ -193,6 +203,39 @@ struct HbmStore {
       }
       h = (h + 1) & tmask;
     }
+  }
+  // Lane-parallel dedup insert: every lane with `want` inserts its own c
+  // into table `role`, probing linearly from its bucket start (as
+  // add_unique_lane and insert do).  In lock-step rounds: read the entry's
+  // tag; a stale tag is claimed with atomicCAS (one lane of a racing set
+  // wins and writes the configuration), a live one is compared.  A lane
+  // that lost a race re-reads the same entry next round, after the winner's
+  // store has been fenced, so equal configurations inserted together are
+  // kept once.  Returns 1 (inserted), 0 (already there), per lane.
+  __device__ __forceinline__ int insert_lanes(int role, const Cfg &c, bool want) {
+    uint32_t h = (hash(c.mask, c.sv) & tmask) & ~7u;
+    int res = 0;
+    bool pend = want;
+    while (__ballot(pend)) {
+      if (pend) {
+        const uint32_t old = tag(role)[h];
+        if (old != epoch) {
+          if (atomicCAS(&tag(role)[h], old, epoch) == old) {
+            tab(role)[h] = c;
+            res = 1;
+            pend = false;
+          }
+        } else {
+          const Cfg e = tab(role)[h];
+          if (e.mask == c.mask && e.sv == c.sv)
+            pend = false;  // already there
+          else
+            h = (h + 1) & tmask;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
+    return res;
   }
   // Wave-uniform dedup insert: probe one 128-byte bucket (8 lanes x 16 B)
   // per step.
@@ -335,6 +378,98 @@ __device__ __forceinline__ int general_return(Store &st, const Slot &sl, const M
       if (r < 0) return -1;
       if (o.explored > p.budget) return -2;
     }
+  }
+  return nR;
+}
+
+// HBM tier: the same expansion as general_return, lane-parallel.  The
+// worklist W is taken 64 configurations at a time, one per lane; each lane
+// tests every pending mutation against its own configuration (slots staged
+// in LDS), emits one successor per round with its eager read closure, and
+// the round's successors are deduplicated into the R / W tables together
+// (insert_lanes) and appended to the regions by ballot prefix.  Every W
+// configuration is still expanded exactly once, so R, the explored count and
+// the verdicts equal the serial expansion's; only the order differs.
+__device__ __forceinline__ int general_return_par(HbmStore &st, const Slot &sl, const Masks &mk,
+                                                  int s, int rF, int rR, int rW, int nF,
+                                                  const KParams &p, KeyOut &o, int lane) {
+  const uint64_t bs = 1ull << s;
+  st.begin_return();
+  SlotLds &L = *st.sl;
+  L.pre[lane] = make_int4(sl.nv, sl.nvm, sl.nl, sl.nlm);
+  L.val[lane] = sl.val;
+  L.pbit[lane] = sl.pbit;
+  int nR = 0, nW = 0;
+  for (int j0 = 0; j0 < nF; j0 += kWave) {  // split F into R and W, as serially
+    const int j = j0 + lane;
+    const bool v = j < nF;
+    Cfg c{0, 0};
+    if (v) c = st.get(rF, j);
+    const bool has = v && (c.mask & bs);
+    const bool lacks = v && !(c.mask & bs);
+    const uint64_t mh = __ballot(has), ml = __ballot(lacks);
+    if (has) st.add_unique_lane(ROLE_R, rR, nR + lanes_below(mh), Cfg{c.mask & ~bs, c.sv});
+    if (lacks) st.add_unique_lane(ROLE_W, rW, nW + lanes_below(ml), c);
+    nR += __popcll(mh);
+    nW += __popcll(ml);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  const uint64_t muts = mk.occ & ~mk.rdm, reads = mk.occ & mk.rdm;
+  for (int head = 0; head < nW;) {
+    const int j = head + lane;
+    const bool act = j < nW;  // this batch: W[head, min(head + 64, nW)) as of now
+    const int taken = min(kWave, nW - head);
+    const Cfg c = st.get(rW, act ? j : head);
+    const int cver = sv_ver(c.sv), cval = sv_val(c.sv);
+    // candidates: legal pending mutations; a crashed one only if it is the
+    // earliest unlinearized member of its class
+    uint64_t cand = 0;
+    if (act) {
+      uint64_t m = muts & ~c.mask;
+      while (m) {
+        const int t = __builtin_ctzll(m);
+        m &= m - 1;
+        const int4 pr = L.pre[t];
+        if (pre_ok(pr.x, pr.y, pr.z, pr.w, cver, cval) &&
+            (!((mk.crashed >> t) & 1) || (L.pbit[t] & ~c.mask) == 0))
+          cand |= 1ull << t;
+      }
+    }
+    for (;;) {
+      const bool has = cand != 0;
+      const uint64_t hb = __ballot(has);
+      if (!hb) break;
+      Cfg nc{0, 0};
+      bool toR = false;
+      if (has) {
+        const int t = __builtin_ctzll(cand);
+        cand &= cand - 1;
+        const int nver = cver + 1, nval = L.val[t];
+        uint64_t nm = c.mask | (1ull << t);
+        uint64_t r = reads & ~nm;  // eager read closure at the successor
+        while (r) {
+          const int u = __builtin_ctzll(r);
+          r &= r - 1;
+          const int4 pr = L.pre[u];
+          if (pre_ok(pr.x, pr.y, pr.z, pr.w, nver, nval)) nm |= 1ull << u;
+        }
+        toR = (nm & bs) != 0;
+        nc = Cfg{toR ? nm & ~bs : nm, pack_sv(nver, nval)};
+      }
+      o.explored += __popcll(hb);
+      // dedup into R and W (two rounds of inserts, one per role)
+      const int insR = st.insert_lanes(ROLE_R, nc, has && toR);
+      const int insW = st.insert_lanes(ROLE_W, nc, has && !toR);
+      const uint64_t bR = __ballot(insR), bW = __ballot(insW);
+      if (nR + __popcll(bR) > st.cap || nW + __popcll(bW) > st.cap) return -1;
+      if (insR) st.reg(rR)[nR + lanes_below(bR)] = nc;
+      if (insW) st.reg(rW)[nW + lanes_below(bW)] = nc;
+      nR += __popcll(bR);
+      nW += __popcll(bW);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      if (o.explored > p.budget) return -2;
+    }
+    head += taken;  // entries appended meanwhile are taken by a later batch
   }
   return nR;
 }
@@ -546,7 +681,11 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
         o.reason = LC_REASON_TIME_BUDGET;
         return;
       }
-      const int r = general_return(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
+      int r;
+      if constexpr (std::is_same<Store, HbmStore>::value)
+        r = general_return_par(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
+      else
+        r = general_return(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
       if (r < 0) {
         o.verdict = LC_UNKNOWN;
         o.reason = r == -1 ? LC_REASON_FRONTIER_LDS : LC_REASON_CONFIG_BUDGET;
@@ -970,7 +1109,9 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
     const int last_tier) {
   const int lane = threadIdx.x;
   char *w = ws + (size_t)blockIdx.x * hbm_wave_bytes(cap);
+  __shared__ SlotLds slots;
   HbmStore st;
+  st.sl = &slots;
   st.base = reinterpret_cast<Cfg *>(w);
   st.tabs = st.base + 3 * cap;
   st.tags = reinterpret_cast<uint32_t *>(st.tabs + 4 * cap);

@@ -33,8 +33,11 @@ namespace {
 constexpr int64_t kDefaultBudget = 1 << 24;   // configurations per key
 // HBM tiers: (configurations per set, concurrent keys).  Workspace per key
 // is ~128 B per configuration of capacity (3 regions + 2 hash tables).
-constexpr int64_t kHbmCap[2] = {1 << 16, 1 << 21};
-constexpr int kHbmWaves[2] = {512, 16};
+// Each tier's workspace is <= 4 GiB; the first has the most waves (the
+// lane-parallel expansion is latency-bound per wave).
+constexpr int kHbmTiers = 3;
+constexpr int64_t kHbmCap[kHbmTiers] = {1 << 14, 1 << 18, 1 << 21};
+constexpr int kHbmWaves[kHbmTiers] = {2048, 128, 16};
 // Gap tier: at most this many workgroups, and this much workspace (each
 // workgroup needs 92 B per record of the longest key handed over).  Dynamic
 // LDS for the matching arrays: up to kGapLdsFull per workgroup for whole-key
@@ -321,7 +324,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     int32_t n_list = n_ovf;
     int32_t *list = d.d_ovf, *next = d.d_ovf2;
     HIP_TRY(c, hipEventRecord(d.e1, st));
-    for (int tier = 0; tier < 2 && n_list > 0; tier++) {
+    for (int tier = 0; tier < kHbmTiers && n_list > 0; tier++) {
       const int waves = std::min<int>(kHbmWaves[tier], n_list);
       const size_t ws = lcdev::hbm_tier_ws_bytes(waves, kHbmCap[tier]);
       rc = ensure(c, reinterpret_cast<char **>(&d.d_ws), &d.ws_cap, ws);
@@ -330,11 +333,11 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       HIP_TRY(c, hipMemsetAsync(&d.d_status->n_overflow2, 0, sizeof(int32_t), st));
       HIP_TRY(c, lcdev::launch_hbm_tier(d_ops, d_off, list, n_list, p,
                                         d_out, d.d_ws, waves, kHbmCap[tier], next,
-                                        &d.d_status->n_overflow2, tier == 1, st));
+                                        &d.d_status->n_overflow2, tier == kHbmTiers - 1, st));
       HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                                 hipMemcpyDeviceToHost, st));
       HIP_TRY(c, hipStreamSynchronize(st));
-      n_list = tier == 0 ? d.h_status->n_overflow2 : 0;
+      n_list = tier < kHbmTiers - 1 ? d.h_status->n_overflow2 : 0;
       std::swap(list, next);
     }
     HIP_TRY(c, hipEventRecord(d.e2, st));
