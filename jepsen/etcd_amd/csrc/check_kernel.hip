@@ -1027,8 +1027,10 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     nmut += __popcll(__ballot(placed));
   }
   // (ballots outside the lane-0 branch: they must see every lane)
-  const uint32_t wsum = (uint32_t)nmut | (__ballot(inel) ? 1u << 16 : 0u) |
-                        (__ballot(bad) ? 1u << 17 : 0u) | (__ballot(jit_only) ? 1u << 18 : 0u);
+  // (the jit-only ballot only when something is ineligible: a uniform branch
+  // that a clean key never takes)
+  const uint32_t winel = __ballot(inel) ? (1u << 16) | (__ballot(jit_only) ? 1u << 18 : 0u) : 0u;
+  const uint32_t wsum = (uint32_t)nmut | winel | (__ballot(bad) ? 1u << 17 : 0u);
   if (lane == 0) s.wsum[w] = wsum;
   __syncthreads();
   const uint4 ws = *reinterpret_cast<const uint4 *>(s.wsum);
