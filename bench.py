@@ -202,6 +202,7 @@ def main():
         line["hot_key"] = hot_key(ctx, abi)
         line["search_leg"] = search_leg(ctx, abi, d_ops, d_off, d_out, args, stream, n_ops)
         line["mixed_leg"] = mixed_leg(ctx, abi, dev, stream)
+        line["model_leg"] = model_leg(ctx, abi)
 
     if rank == 0 and world == 1 and not (args.no_cpu_baseline or args.bare):
         line["cpu_baseline"] = cpu_baseline(args, ops, key_off, res)
@@ -313,6 +314,31 @@ def mixed_leg(ctx, abi, dev, stream):
             "unknown": int((res["verdict"] == -1).sum()),
             "ops_per_s": int(off[-1]) / (float(np.median(wall[1:])) * 1e-3),
             "verdict_or_fail_op_mismatches_vs_oracle": mism}
+
+
+def model_leg(ctx, abi):
+    """knossos's cas-register model (no versions) on C2-shaped histories,
+    1,000 keys x 1,000 ops, concurrency 20: without version pinning every key
+    needs the frontier search and its HBM tier (§9 of DESIGN.md).  Not part
+    of `value`; median of 3 calls after one warm-up."""
+    ops, off, _, _ = abi.synth(1000, 1000, concurrency=20, seed=7)
+    ops = ops.copy()
+    ops[:, 3] = abi.LC_NIL  # cas-register: the same histories without versions
+    times, st = [], []
+    for _ in range(4):
+        t0 = time.perf_counter()
+        _, r = ctx.check(ops, off)
+        times.append((time.perf_counter() - t0) * 1e3)
+        st.append(ctx.stats())
+    t = float(np.median(times[1:]))
+    return {"workload": "cas-register model: 1000 keys x 1000 ops, concurrency 20 (host buffers)",
+            "call_ms": t, "ops_per_s": int(off[-1]) / (t * 1e-3),
+            "jit_kernel_ms": float(np.median([x["jit_kernel_ms"] for x in st[1:]])),
+            "hbm_kernel_ms": float(np.median([x["hbm_kernel_ms"] for x in st[1:]])),
+            "hbm_keys": int(st[-1]["n_hbm_keys"]),
+            "configs_explored": int(r["configs_explored"].sum()),
+            "max_frontier": int(r["max_frontier"].max()),
+            "valid": int((r["verdict"] == 1).sum()), "unknown": int((r["verdict"] == -1).sum())}
 
 
 def reduce_run(elapsed, n_ops, res, distributed, dev):

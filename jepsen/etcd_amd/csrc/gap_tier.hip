@@ -65,7 +65,7 @@ constexpr int kAny = INT_MIN;      // no value required / not a CAS
 constexpr int kNodeBudget = 4096;  // matching passes per decision
 constexpr int kGapArrays = 24;     // 32-bit arrays of `cap` entries per workgroup
 
-enum { GD_VALID = 1, GD_INVALID = 0, GD_NA = -1, GD_BUDGET = -2, GD_SKIP = -3 };
+enum { GD_VALID = 1, GD_INVALID = 0, GD_NA = -1, GD_BUDGET = -2, GD_SKIP = -3, GD_RETRY = -4 };
 enum { F_NA = 1, F_INVALID = 2 };
 
 // Matching footprint of one decision in LDS: per gap a 16-byte record and 4
@@ -88,7 +88,8 @@ extern __shared__ int4 lds_dyn[];
 // prefix counts at 16, followed by the matching's LDS region.  Then the
 // setup's barriers wait for LDS stores only, not for HBM write acks.
 constexpr int kSkelArrays = 17;
-constexpr int kSkelLdsBytes = 4 * kSkelArrays + 56;  // + the matching's worst case (G = n_opt = cap)
+constexpr int kSkelLdsBytes = 4 * kSkelArrays;  // per record; the matching follows it
+constexpr int kMatchReserve = 8 << 10;           // LDS kept for the matching after a skeleton
 
 struct GapWs {
   int32_t *base;
@@ -742,7 +743,9 @@ __device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t 
   if (G == 0) return GD_VALID;
   if (G > n_opt) return GD_INVALID;
   const bool in_lds = 16 * w.moff + match_lds_bytes(G, n_opt) <= lds_bytes;
-  if (w.lds && !in_lds) return GD_NA;  // cannot happen: sized for G = n_opt = cap
+  // skeleton in LDS but no room left for this matching: the caller redoes the
+  // decision with the skeleton in HBM (the whole LDS then holds the matching)
+  if (w.lds && !in_lds) return GD_RETRY;
   Cmp<true> cl;
   Cmp<false> cg;
   cl.ws = cg.ws = w.base;
@@ -838,10 +841,11 @@ __global__ __launch_bounds__(kGapThreads) void gap_tier_kernel(
     g.kops = ops + (beg - key_base);
     g.n = (int)(end - beg);
     g.base = g.kops[0].call;
+    // the skeleton goes to LDS when it fits with room for a small matching
     const int64_t capk = (end - beg + 2 + 3) & ~int64_t(3);
-    g.ws = kSkelLdsBytes * capk <= job.lds_bytes
-               ? gap_ws(reinterpret_cast<int32_t *>(lds_dyn), capk, true)
-               : gap_ws(ws_hbm, cap, false);
+    const bool skel_lds = kSkelLdsBytes * capk + kMatchReserve <= job.lds_bytes;
+    g.ws = skel_lds ? gap_ws(reinterpret_cast<int32_t *>(lds_dyn), capk, true)
+                    : gap_ws(ws_hbm, cap, false);
     int64_t nodes = 0;
     int G = 0, G_full = 0;
     // One decision (full / probe), or a bisection of decisions.  A single
@@ -855,6 +859,11 @@ __global__ __launch_bounds__(kGapThreads) void gap_tier_kernel(
     if (job.mode == kGapFull || cut != kNever) {
       for (;;) {
         res = gap_decide(g, cut, job.lds_bytes, &nodes, &G);
+        if (res == GD_RETRY) {  // rare: a matching larger than the LDS left
+          g.ws = gap_ws(ws_hbm, cap, false);
+          res = gap_decide(g, cut, job.lds_bytes, &nodes, &G);
+          g.ws = gap_ws(reinterpret_cast<int32_t *>(lds_dyn), capk, true);
+        }
         if (!bis) {
           if (job.mode != kGapFull || !job.bisect || res != GD_INVALID) break;
           bis = true;  // counterexample: the first return whose prefix fails
@@ -991,6 +1000,12 @@ hipError_t launch_gap_tier(const lc_op *d_ops, const int64_t *d_key_off, const i
                            int64_t cap, int32_t *d_pass_keys, KStatus *d_status,
                            const GapJob &job, hipStream_t stream) {
   if (job.n_tasks <= 0) return hipSuccess;
+  if (job.lds_bytes > (64 << 10)) {  // beyond the default dynamic-LDS limit (gfx950: 160 KB per CU)
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(gap_tier_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             job.lds_bytes);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(gap_tier_kernel, dim3((unsigned)n_wg), dim3(kGapThreads),
                      (unsigned)job.lds_bytes, stream, d_ops, d_key_off, d_keys, p, d_out, d_ws,
                      cap, d_pass_keys, d_status, job);

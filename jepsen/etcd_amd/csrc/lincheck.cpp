@@ -45,6 +45,7 @@ constexpr int kHbmWaves[kHbmTiers] = {2048, 128, 16};
 constexpr int kGapMaxWG = 1024;
 constexpr size_t kGapWsBytes = size_t(1) << 30;
 constexpr int kGapLdsFull = 48 << 10;
+constexpr int64_t kGapSkelLdsMax = 78 << 10;  // two such workgroups per CU (160 KB)
 constexpr int kGapLdsProbe = 48 << 10;
 constexpr int kGapMaxRounds = 64;
 constexpr int kGapProbeMinLen = 1024;
@@ -249,9 +250,13 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     // enough for multisection rounds to pay (each round costs two launches
     // and a sync; a probe of a short key costs less than that).
     job.bisect = d.h_status->max_len < kGapProbeMinLen || 2 * n_jit > wg_cap;
-    // room for the longest key's whole skeleton + matching in LDS (68 B per
-    // record for the skeleton, 56 B for the matching) up to kGapLdsFull
-    job.lds_bytes = (int)std::min<int64_t>(kGapLdsFull, 124 * gap_cap);
+    // LDS per workgroup: the longest key's skeleton (68 B per record) plus
+    // 8 KB for its matching when that stays within kGapSkelLdsMax (two
+    // workgroups per CU); else room for the matching alone (56 B per record
+    // at worst), up to kGapLdsFull
+    const int64_t skel = 68 * gap_cap + (8 << 10);
+    job.lds_bytes = (int)(skel <= kGapSkelLdsMax ? skel
+                                                 : std::min<int64_t>(kGapLdsFull, 56 * gap_cap));
     // LC_GAP_LDS=0 (tests): keep every matching in the HBM workspace
     const char *lds_env = getenv("LC_GAP_LDS");
     const bool no_lds = lds_env && lds_env[0] == '0';
