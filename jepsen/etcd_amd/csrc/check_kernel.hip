@@ -821,26 +821,19 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 }
 
 // Hand key over to the JIT tier (thread 0 only); tell the host there is work.
-// With direct_keys set, a key the gap tier could only pass on (jit_only: an
-// :ok mutation without a version, a read [nil x], malformed records) goes
-// straight to the JIT search's list (count status->n_jit2, which the gap
-// tier appends to as well).
-__device__ __forceinline__ void fast_tier_handoff(int64_t key, int64_t n, int32_t *jit_keys,
-                                                  KStatus *status, int32_t *h_handoff,
-                                                  int32_t *direct_keys = nullptr,
-                                                  bool jit_only = false) {
-  if (jit_only && direct_keys) {
-    const int at = atomicAdd(&status->n_jit2, 1);
-    direct_keys[at] = (int32_t)key;
-    if (at == 0) __hip_atomic_store(h_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return;
+// Hand key over (thread 0 only): a plain store of its flag (1: gap tier;
+// 2: jit-only — an :ok mutation without a version, a read [nil x],
+// malformed records).  The host is told there is work by one store to host
+// memory: a store over PCIe per handoff costs ~50 ns each (10k handed-over
+// keys: 0.11 -> 0.67 ms), so a workgroup stores only if the device-side
+// any_handoff word still reads 0 (a few racing stores at most).
+__device__ __forceinline__ void fast_tier_handoff(int64_t key, int32_t *flags, KStatus *status,
+                                                  int32_t *h_handoff, bool jit_only = false) {
+  flags[key] = jit_only ? 2 : 1;
+  if (__hip_atomic_load(&status->any_handoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+    __hip_atomic_store(&status->any_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(h_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  const int at = atomicAdd(&status->n_jit, 1);
-  jit_keys[at] = (int32_t)key;
-  atomicMax(&status->max_len, (int32_t)(n < 0 ? 0 : n > INT_MAX ? INT_MAX : n));
-  // one host store per launch: a store over PCIe per handoff costs ~50 ns
-  // each (10k handed-over keys: 0.11 -> 0.67 ms)
-  if (at == 0) __hip_atomic_store(h_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // 14.4 KB of LDS per workgroup (7 workgroups per CU at 72 VGPRs).
@@ -943,17 +936,16 @@ __device__ __forceinline__ bool timing_fails(const FastLds &s, int M, int tid) {
 __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *__restrict__ kops,
                                          const FastRecs &b, const KParams &p, FastLds &s,
                                          lc_key_result *__restrict__ out,
-                                         int32_t *__restrict__ jit_keys,
+                                         int32_t *__restrict__ flags,
                                          KStatus *__restrict__ status,
-                                         int32_t *__restrict__ h_handoff,
-                                         int32_t *__restrict__ direct_keys) {
+                                         int32_t *__restrict__ h_handoff) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   if (n64 <= 0 || n64 > kFastMax) {
     if (tid == 0) {
       if (n64 == 0)
         out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 0};
       else
-        fast_tier_handoff(key, n64, jit_keys, status, h_handoff);
+        fast_tier_handoff(key, flags, status, h_handoff);
     }
     return;
   }
@@ -1040,7 +1032,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
   const int M = (int)((ws.x & 0xFFFF) + (ws.y & 0xFFFF) + (ws.z & 0xFFFF) + (ws.w & 0xFFFF));
   if (wor >> 16) {  // ineligible or a version out of range: hand over
     if (tid == 0)
-      fast_tier_handoff(key, n64, jit_keys, status, h_handoff, direct_keys, (wor >> 18) & 1);
+      fast_tier_handoff(key, flags, status, h_handoff, (wor >> 18) & 1);
     return;
   }
   // pass 2: positions, duplicates, CAS expectations and read claims against
@@ -1075,7 +1067,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     if (!(wb.x | wb.y | wb.z | wb.w))
       out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
     else
-      fast_tier_handoff(key, n64, jit_keys, status, h_handoff);
+      fast_tier_handoff(key, flags, status, h_handoff);
   }
 }
 
@@ -1086,15 +1078,15 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
 __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
     const KParams p, lc_key_result *__restrict__ out,
-    int32_t *__restrict__ jit_keys, KStatus *__restrict__ status,
-    int32_t *__restrict__ h_handoff, int32_t *__restrict__ direct_keys) {
+    int32_t *__restrict__ flags, KStatus *__restrict__ status,
+    int32_t *__restrict__ h_handoff) {
   __shared__ FastLds s;
   const int64_t key = blockIdx.x;
   const int64_t beg = key_off[key], end = key_off[key + 1];
   const lc_op *kops = ops + (beg - key_off[0]);
   FastRecs r;
   if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
-  fast_key(key, end - beg, kops, r, p, s, out, jit_keys, status, h_handoff, direct_keys);
+  fast_key(key, end - beg, kops, r, p, s, out, flags, status, h_handoff);
 }
 
 // Workspace layout per wave: 3 regions of cap Cfg, 2 tables of 2*cap Cfg,
@@ -1138,17 +1130,88 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
   }
 }
 
+// Build the handoff lists from the fast tier's per-key flags (and clear
+// them): one list reservation (atomicAdd) and one max per workgroup chunk.
+constexpr int kCompactThreads = 256;
+__global__ __launch_bounds__(kCompactThreads) void handoff_compact_kernel(
+    int32_t *__restrict__ flags, const int64_t *__restrict__ key_off, const int64_t n_keys,
+    const int route_direct, int32_t *__restrict__ jit_keys, int32_t *__restrict__ direct_keys,
+    KStatus *__restrict__ status) {
+  __shared__ int wg[kCompactThreads / kWave], wd[kCompactThreads / kWave];
+  __shared__ int base_g, base_d;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  int32_t maxlen = 0;
+  for (int64_t k0 = (int64_t)blockIdx.x * kCompactThreads; k0 < n_keys;
+       k0 += (int64_t)gridDim.x * kCompactThreads) {
+    const int64_t k = k0 + tid;
+    int f = 0;
+    if (k < n_keys) {
+      f = flags[k];
+      if (f) flags[k] = 0;
+    }
+    const bool dir = f == 2 && route_direct;
+    const bool gap = f != 0 && !dir;
+    if (gap) {
+      const int64_t n = key_off[k + 1] - key_off[k];
+      maxlen = max(maxlen, (int32_t)(n > INT_MAX ? INT_MAX : n));
+    }
+    const uint64_t bg = __ballot(gap), bd = __ballot(dir);
+    if (lane == 0) {
+      wg[w] = __popcll(bg);
+      wd[w] = __popcll(bd);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int tg = 0, td = 0;
+      for (int j = 0; j < kCompactThreads / kWave; j++) {
+        tg += wg[j];
+        td += wd[j];
+      }
+      base_g = tg ? atomicAdd(&status->n_jit, tg) : 0;
+      base_d = td ? atomicAdd(&status->n_jit2, td) : 0;
+    }
+    __syncthreads();
+    int pg = base_g, pd = base_d;
+    for (int j = 0; j < w; j++) {
+      pg += wg[j];
+      pd += wd[j];
+    }
+    const uint64_t below = (1ull << lane) - 1;
+    if (gap) jit_keys[pg + __popcll(bg & below)] = (int32_t)k;
+    if (dir) direct_keys[pd + __popcll(bd & below)] = (int32_t)k;
+    __syncthreads();
+  }
+  // max over the workgroup, one atomic
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) maxlen = max(maxlen, __shfl_xor(maxlen, o));
+  if (lane == 0) wg[w] = maxlen;
+  __syncthreads();
+  if (tid == 0) {
+    int m = 0;
+    for (int j = 0; j < kCompactThreads / kWave; j++) m = max(m, wg[j]);
+    if (m) atomicMax(&status->max_len, m);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_handoff_compact(int32_t *d_flags, const int64_t *d_key_off, int64_t n_keys,
+                                  int route_direct, int32_t *d_jit_keys, int32_t *d_direct_keys,
+                                  KStatus *d_status, hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  const int64_t wgs = std::min<int64_t>((n_keys + kCompactThreads - 1) / kCompactThreads, 1024);
+  hipLaunchKernelGGL(handoff_compact_kernel, dim3((unsigned)wgs), dim3(kCompactThreads), 0, stream,
+                     d_flags, d_key_off, n_keys, route_direct, d_jit_keys, d_direct_keys, d_status);
+  return hipGetLastError();
+}
 
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
-                            lc_key_result *d_out, int32_t *d_jit_keys,
-                            KStatus *d_status, int32_t *h_handoff, int32_t *d_direct_keys,
-                            hipStream_t stream) {
+                            lc_key_result *d_out, int32_t *d_flags,
+                            KStatus *d_status, int32_t *h_handoff, hipStream_t stream) {
   if (n_keys <= 0) return hipSuccess;
   hipLaunchKernelGGL(fast_tier_kernel, dim3((unsigned)n_keys), dim3(kFastThreads), 0,
-                     stream, d_ops, d_key_off, p, d_out, d_jit_keys, d_status, h_handoff,
-                     d_direct_keys);
+                     stream, d_ops, d_key_off, p, d_out, d_flags, d_status, h_handoff);
   return hipGetLastError();
 }
 

@@ -28,6 +28,7 @@ struct KStatus {
   int32_t n_cex;        // gap tier: invalid keys awaiting their counterexample
   int32_t n_open;       // gap tier: counterexample intervals still open after a round
   int32_t max_lds;      // gap tier: largest matching footprint (bytes) of a full decision
+  int32_t any_handoff;  // fast tier: some key was handed over (read before the host store)
 };
 
 constexpr int kWave = 64;
@@ -35,22 +36,29 @@ constexpr int kWavesPerWG = 4;   // independent keys per 256-thread workgroup
 constexpr int kLdsCap = 128;     // configurations per LDS region (3 regions/wave)
 
 // Fast tier: one 256-thread workgroup per key decides version-pinned keys
-// (check_kernel.hip, "Version-order fast tier"); the others are appended to
-// d_jit_keys (count in status->n_jit) for the JIT search.
+// (check_kernel.hip, "Version-order fast tier"); the others are handed over
+// to the gap tier or the JIT search (below).
 // Status protocol: *d_status is all-zero when the launch starts, and the host
 // zeroes *h_handoff (host-coherent memory) before it.  A workgroup that hands
 // its key over also stores 1 to *h_handoff, so when every key is decided the
 // host needs no memset or copy around this kernel: one launch plus one sync.
-// With d_direct_keys non-null, keys the gap tier could only pass on (an :ok
-// mutation without a version, a read [nil x], malformed records) are appended
-// there instead (count status->n_jit2), for the JIT search directly.
+// A workgroup hands its key over by a plain store of d_flags[key] (1: for
+// the gap tier, 2: jit-only — an :ok mutation without a version, a read
+// [nil x], malformed records); launch_handoff_compact then builds the lists
+// (d_jit_keys / status->n_jit for the gap tier, status->max_len; with
+// route_direct the jit-only keys go to d_direct_keys / status->n_jit2 for the
+// JIT search, else to d_jit_keys too) and clears the flags.  (One returning
+// same-address atomicAdd per handed-over key serialised: 10k handoffs cost
+// the launch 0.16 ms.)
 // (A grid-wide "last workgroup" counter instead costs 10k same-address
 // atomics per launch: measured 0.115 -> 0.345 ms.)
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
-                            lc_key_result *d_out, int32_t *d_jit_keys,
-                            KStatus *d_status, int32_t *h_handoff, int32_t *d_direct_keys,
-                            hipStream_t stream);
+                            lc_key_result *d_out, int32_t *d_flags,
+                            KStatus *d_status, int32_t *h_handoff, hipStream_t stream);
+hipError_t launch_handoff_compact(int32_t *d_flags, const int64_t *d_key_off, int64_t n_keys,
+                                  int route_direct, int32_t *d_jit_keys, int32_t *d_direct_keys,
+                                  KStatus *d_status, hipStream_t stream);
 
 // LDS tier (JIT search): one wavefront per key, for the keys in d_keys
 // (n_keys of them), or for keys 0..n_keys-1 when d_keys is null.  In every

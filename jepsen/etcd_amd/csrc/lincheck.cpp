@@ -66,6 +66,8 @@ struct Dev {
   size_t ovf2_cap = 0;
   int32_t *d_jit = nullptr;
   size_t jit_cap = 0;
+  int32_t *d_flags = nullptr;          // per key: handed over by the fast tier (zero between calls)
+  size_t flags_cap = 0;
   int32_t *d_jit2 = nullptr;           // keys the gap tier passes on
   size_t jit2_cap = 0;
   int32_t *d_gws = nullptr;            // gap-tier workspace
@@ -171,7 +173,11 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   if (!rc) rc = ensure(c, &d.d_ovf2, &d.ovf2_cap, sizeof(int32_t) * (size_t)n_keys);
   if (!rc) rc = ensure(c, &d.d_jit, &d.jit_cap, sizeof(int32_t) * (size_t)n_keys);
   if (!rc) rc = ensure(c, &d.d_jit2, &d.jit2_cap, sizeof(int32_t) * (size_t)n_keys);
+  const bool flags_new = d.flags_cap < sizeof(int32_t) * (size_t)n_keys || !d.d_flags;
+  if (!rc) rc = ensure(c, &d.d_flags, &d.flags_cap, sizeof(int32_t) * (size_t)n_keys);
   if (rc) return rc;
+  if (flags_new || d.status_dirty)  // the flags are all-zero between clean calls
+    HIP_TRY(c, hipMemsetAsync(d.d_flags, 0, d.flags_cap, st));
   // With the gap tier on, the fast tier sends keys it can only pass on (no
   // version on an :ok mutation, a read [nil x], malformed) straight to the
   // JIT list d_jit2, which the gap tier then appends to.
@@ -190,15 +196,16 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     // tier 0: version-order decision for every key; the rest go to the JIT.
     // Only when some workgroup raised h_handoff is the count copied back.
     __atomic_store_n(d.h_handoff, 0, __ATOMIC_RELEASE);
-    HIP_TRY(c, lcdev::launch_fast_tier(d_ops, d_off, n_keys, p, d_out, d.d_jit,
-                                       d.d_status, d.h_handoff_dev,
-                                       gap_on ? d.d_jit2 : nullptr, st));
+    HIP_TRY(c, lcdev::launch_fast_tier(d_ops, d_off, n_keys, p, d_out, d.d_flags,
+                                       d.d_status, d.h_handoff_dev, st));
     HIP_TRY(c, hipEventRecord(d.ef, st));
     HIP_TRY(c, hipEventSynchronize(d.ef));
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.ef));
     d.fast_ms = ms;
     n_jit = 0;
     if (__atomic_load_n(d.h_handoff, __ATOMIC_ACQUIRE)) {
+      HIP_TRY(c, lcdev::launch_handoff_compact(d.d_flags, d_off, n_keys, gap_on ? 1 : 0, d.d_jit,
+                                               d.d_jit2, d.d_status, st));
       HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                                 hipMemcpyDeviceToHost, st));
       HIP_TRY(c, hipStreamSynchronize(st));
@@ -424,6 +431,7 @@ void lc_close(lc_ctx *c) {
     if (d.ef) (void)hipEventDestroy(d.ef);
     if (d.d_jit) (void)hipFree(d.d_jit);
     if (d.d_jit2) (void)hipFree(d.d_jit2);
+    if (d.d_flags) (void)hipFree(d.d_flags);
     if (d.d_gws) (void)hipFree(d.d_gws);
     if (d.d_cex) (void)hipFree(d.d_cex);
     if (d.eg) (void)hipEventDestroy(d.eg);
