@@ -290,7 +290,7 @@ __device__ __forceinline__ Cls classify(const GapKey &g, const Raw &raw, int64_t
   return c;
 }
 
-constexpr int kSetupBatch = 2;  // record chunks whose loads are in flight together
+constexpr int kSetupBatch = 4;  // record chunks whose loads are in flight together
 
 // Build the skeleton of the key's prefix at `cut` (key-relative event index;
 // kNever = the whole history).  Returns GD_VALID when the skeleton is
@@ -327,15 +327,20 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
   int flag = 0, maxpos = -1, maxread = -1;
   uint32_t maxret = 0;
   const int nch = (n + kGapThreads - 1) / kGapThreads;
+  // A key of at most kSetupBatch chunks is loaded once: pass 2 reuses the
+  // registers (one load round trip per decision instead of two).
+  const bool resident = nch <= kSetupBatch;
+  Raw raw[kSetupBatch];
+  int64_t pc[kSetupBatch];
   for (int pass = 1; pass <= 2; pass++) {
     for (int c0 = 0; c0 < nch; c0 += kSetupBatch) {
-      Raw raw[kSetupBatch];
-      int64_t pc[kSetupBatch];
+      if (pass == 1 || !resident) {
 #pragma unroll
-      for (int b = 0; b < kSetupBatch; b++) {
-        const int r = (c0 + b) * kGapThreads + tid;
-        raw[b] = load_raw(g.kops, r, n);
-        pc[b] = (r > 0 && r < n) ? g.kops[r - 1].call : -1;
+        for (int b = 0; b < kSetupBatch; b++) {
+          const int r = (c0 + b) * kGapThreads + tid;
+          raw[b] = load_raw(g.kops, r, n);
+          pc[b] = (r > 0 && r < n) ? g.kops[r - 1].call : -1;
+        }
       }
 #pragma unroll
       for (int b = 0; b < kSetupBatch; b++) {
