@@ -203,6 +203,7 @@ def main():
         line["search_leg"] = search_leg(ctx, abi, d_ops, d_off, d_out, args, stream, n_ops)
         line["mixed_leg"] = mixed_leg(ctx, abi, dev, stream)
         line["model_leg"] = model_leg(ctx, abi)
+        line["crash_leg"] = crash_leg(ctx, abi, dev, stream)
 
     if rank == 0 and world == 1 and not (args.no_cpu_baseline or args.bare):
         line["cpu_baseline"] = cpu_baseline(args, ops, key_off, res)
@@ -314,6 +315,37 @@ def mixed_leg(ctx, abi, dev, stream):
             "unknown": int((res["verdict"] == -1).sum()),
             "ops_per_s": int(off[-1]) / (float(np.median(wall[1:])) * 1e-3),
             "verdict_or_fail_op_mismatches_vs_oracle": mism}
+
+
+def crash_leg(ctx, abi, dev, stream):
+    """C2 with crashes: 10,000 keys x 1,000 ops, concurrency 20, 5 % of the
+    writes/CAS crashed (:info), as a run under a partition nemesis leaves
+    them.  Every key has crashed ops, so the version-order tier hands each
+    over (flag + compaction) and the gap tier decides it.  Device-resident,
+    median of 5 calls after one warm-up; not part of `value`."""
+    import torch
+    ops, off, _, _ = abi.synth(10000, 1000, concurrency=20, p_info=0.05, seed=0x5EED0012)
+    d_ops = torch.from_numpy(ops).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_out = torch.zeros(10000 * abi.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    st = abi.LcStats()
+    call = ctx.bind_check_device(d_ops.data_ptr(), d_off.data_ptr(), 10000, d_out.data_ptr(),
+                                 stream=stream.cuda_stream, stats=st)
+    wall, fast, gap = [], [], []
+    for _ in range(6):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        call()
+        wall.append((time.perf_counter() - t0) * 1e3)
+        fast.append(st.fast_kernel_ms)
+        gap.append(st.gap_kernel_ms)
+    res = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
+    t = float(np.median(wall[1:]))
+    return {"workload": "C2 with 5 % crashed writes/CAS: 10000 keys x 1000 ops, concurrency 20",
+            "call_ms": t, "ops_per_s": int(off[-1]) / (t * 1e-3),
+            "fast_kernel_ms": float(np.median(fast[1:])), "gap_kernel_ms": float(np.median(gap[1:])),
+            "crashed_ops": int((ops[:, 5] == abi.LC_INF).sum()),
+            "valid": int((res["verdict"] == 1).sum()), "unknown": int((res["verdict"] == -1).sum())}
 
 
 def model_leg(ctx, abi):
