@@ -133,6 +133,7 @@ __device__ __forceinline__ GapWs gap_ws(int32_t *base, int64_t cap, bool lds) {
 }
 
 // Exclusive prefix sum over the workgroup; *total = the sum of all v.
+template <int T>
 __device__ __forceinline__ int block_excl_sum(int v, GapSh &sh, int *total) {
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   int incl = v;
@@ -145,7 +146,7 @@ __device__ __forceinline__ int block_excl_sum(int v, GapSh &sh, int *total) {
   __syncthreads();
   int pre = 0, tot = 0;
 #pragma unroll
-  for (int j = 0; j < kGapWaves; j++) {
+  for (int j = 0; j < (T / kWave); j++) {
     if (j < w) pre += sh.wtot[j];
     tot += sh.wtot[j];
   }
@@ -155,6 +156,7 @@ __device__ __forceinline__ int block_excl_sum(int v, GapSh &sh, int *total) {
 }
 
 // Exclusive suffix minimum over the workgroup (threads above this one).
+template <int T>
 __device__ __forceinline__ uint32_t block_suffix_min_excl(uint32_t v, GapSh &sh) {
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   uint32_t incl = v;
@@ -167,7 +169,7 @@ __device__ __forceinline__ uint32_t block_suffix_min_excl(uint32_t v, GapSh &sh)
   __syncthreads();
   uint32_t post = kNever;
 #pragma unroll
-  for (int j = 0; j < kGapWaves; j++)
+  for (int j = 0; j < (T / kWave); j++)
     if (j > w) post = post < sh.wtotu[j] ? post : sh.wtotu[j];
   uint32_t excl = (uint32_t)__shfl_down((int)incl, 1);
   if (lane == kWave - 1) excl = kNever;
@@ -200,14 +202,15 @@ __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_S
 
 // Stable compaction, phase 2: word-level exclusive prefix of the ballot
 // masks Mask[0..nw) into Pre[0..nw); returns the total.  Two barriers.
+template <int T>
 __device__ int mask_prefix(const GapWs &w, int nw, GapSh &sh) {
   const int tid = threadIdx.x;
-  const int per = (nw + kGapThreads - 1) / kGapThreads;
+  const int per = (nw + T - 1) / T;
   const int k0 = min(tid * per, nw), k1 = min(k0 + per, nw);
   int loc = 0;
   for (int k = k0; k < k1; k++) loc += __popcll(w.Mask[k]);
   int tot;
-  int run = block_excl_sum(loc, sh, &tot);
+  int run = block_excl_sum<T>(loc, sh, &tot);
   for (int k = k0; k < k1; k++) {
     w.Pre[k] = run;
     run += __popcll(w.Mask[k]);
@@ -301,6 +304,7 @@ constexpr int kSetupBatch = 4;  // record chunks whose loads are in flight toget
 // checks the owners (two mutations on one version, two values claimed for
 // one version) and appends the optional ops.  Optional ops and gaps are
 // compacted stably through per-wave ballot words: no barrier per chunk.
+template <int T>
 __device__ int gap_setup(const GapKey &g, uint32_t cut) {
   const int tid = threadIdx.x, n = g.n, wv = tid / kWave, lane = tid & (kWave - 1);
   GapSh &sh = *g.sh;
@@ -309,7 +313,7 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
   // (sh.flag on its early-return paths, sh.maxret) before thread 0 resets
   // them: decisions follow each other without a barrier in the bisection.
   __syncthreads();
-  for (int k = tid; k <= n; k += kGapThreads) {
+  for (int k = tid; k <= n; k += T) {
     w.A[k] = 0;  // max call + 1 of what must precede t_k; 0 = nothing
     w.B[k] = kNever;
     w.Pin[k] = -1;
@@ -326,7 +330,7 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
   __syncthreads();
   int flag = 0, maxpos = -1, maxread = -1;
   uint32_t maxret = 0;
-  const int nch = (n + kGapThreads - 1) / kGapThreads;
+  const int nch = (n + T - 1) / T;
   // A key of at most kSetupBatch chunks is loaded once: pass 2 reuses the
   // registers (one load round trip per decision instead of two).
   const bool resident = nch <= kSetupBatch;
@@ -337,14 +341,14 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
       if (pass == 1 || !resident) {
 #pragma unroll
         for (int b = 0; b < kSetupBatch; b++) {
-          const int r = (c0 + b) * kGapThreads + tid;
+          const int r = (c0 + b) * T + tid;
           raw[b] = load_raw(g.kops, r, n);
           pc[b] = (r > 0 && r < n) ? g.kops[r - 1].call : -1;
         }
       }
 #pragma unroll
       for (int b = 0; b < kSetupBatch; b++) {
-        const int ch = c0 + b, r = ch * kGapThreads + tid;
+        const int ch = c0 + b, r = ch * T + tid;
         if (ch >= nch) break;
         Cls c;
         c.kind = K_NONE;
@@ -364,13 +368,13 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
             maxpos = max(maxpos, c.k);
           }
           const uint64_t m = __ballot(c.kind == K_OPT);
-          if (lane == 0) w.Mask[ch * kGapWaves + wv] = m;
+          if (lane == 0) w.Mask[ch * (T / kWave) + wv] = m;
         } else {
           if (c.kind == K_READ && c.val != -1 && w.Claim[c.k] != c.val)
             flag |= F_INVALID;  // two values claimed for one version
           else if (c.kind == K_PIN && w.Pin[c.k] != r)
             flag |= F_INVALID;  // two mutations claim one version
-          const int wi = ch * kGapWaves + wv;
+          const int wi = ch * (T / kWave) + wv;
           if (c.kind == K_OPT) {
             const uint64_t m = w.Mask[wi];
             w.Opt[w.Pre[wi] + lanes_below(m)] = c.op;
@@ -385,7 +389,7 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
       if (maxret) atomicMax(&sh.maxret, maxret);
       __syncthreads();
       if (sh.flag & (F_NA | F_INVALID)) return (sh.flag & F_NA) ? GD_NA : GD_INVALID;
-      sh.n_opt = mask_prefix(w, nch * kGapWaves, sh);  // same value in every thread
+      sh.n_opt = mask_prefix<T>(w, nch * (T / kWave), sh);  // same value in every thread
       flag = 0;
     }
   }
@@ -395,11 +399,11 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
   const int n_opt = sh.n_opt;
   const int M = max(sh.maxpos + 1, sh.maxread);
   // Uh[k] = min(B[k..M-1]): chunked suffix-min scan
-  const int per = (M + kGapThreads - 1) / kGapThreads;
+  const int per = (M + T - 1) / T;
   const int k0 = min(tid * per, M), k1 = min(k0 + per, M);
   uint32_t loc = kNever;
   for (int k = k0; k < k1; k++) loc = min(loc, w.B[k]);
-  uint32_t run = block_suffix_min_excl(loc, sh);
+  uint32_t run = block_suffix_min_excl<T>(loc, sh);
   for (int k = k1 - 1; k >= k0; k--) {
     run = min(run, w.B[k]);
     w.Uh[k] = run;
@@ -414,9 +418,9 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
     if (M > 0 && w.Pin[0] != -1 && w.PinExp[0] != kAny && w.PinExp[0] != g.init)
       flag |= F_INVALID;
   }
-  const int mch = (M + kGapThreads - 1) / kGapThreads;
+  const int mch = (M + T - 1) / T;
   for (int ch = 0; ch < mch; ch++) {
-    const int k = ch * kGapThreads + tid;
+    const int k = ch * T + tid;
     bool gap = false;
     if (k < M) {
       const uint32_t lo = w.A[k];
@@ -434,16 +438,16 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
       }
     }
     const uint64_t m = __ballot(gap);
-    if (lane == 0) w.Mask[ch * kGapWaves + wv] = m;
+    if (lane == 0) w.Mask[ch * (T / kWave) + wv] = m;
   }
   if (flag) atomicOr(&sh.flag, flag);
   __syncthreads();
   if (sh.flag & F_INVALID) return GD_INVALID;
-  const int G = mask_prefix(w, mch * kGapWaves, sh);
+  const int G = mask_prefix<T>(w, mch * (T / kWave), sh);
   for (int ch = 0; ch < mch; ch++) {
-    const int wi = ch * kGapWaves + wv;
+    const int wi = ch * (T / kWave) + wv;
     const uint64_t m = w.Mask[wi];
-    if ((m >> lane) & 1) w.Gap[w.Pre[wi] + lanes_below(m)] = ch * kGapThreads + tid;
+    if ((m >> lane) & 1) w.Gap[w.Pre[wi] + lanes_below(m)] = ch * T + tid;
   }
   if (tid == 0) {
     sh.n_opt = n_opt;
@@ -730,6 +734,7 @@ __device__ int match_branch(const Cmp<L> &c, int G, int n_opt, int *brPos, int *
 }
 
 // Decide the prefix at `cut`.  *nodes accumulates matching passes.
+template <int T>
 __device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t *nodes,
                           int *n_gaps) {
   const int tid = threadIdx.x;
@@ -738,7 +743,7 @@ __device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t 
 #ifdef GAP_PROFILE
   const uint64_t t0 = wall_clock64();
 #endif
-  const int st = gap_setup(g, cut);
+  const int st = gap_setup<T>(g, cut);
   if (st != GD_VALID) return st;
 #ifdef GAP_PROFILE
   const uint64_t t1 = wall_clock64();
@@ -762,14 +767,14 @@ __device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t 
   int *mg = in_lds ? &cl.at(aMG, 0) : &cg.at(aMG, 0);
   int *mo = in_lds ? &cl.at(aMO, 0) : &cg.at(aMO, 0);
   int *vis = in_lds ? &cl.at(aVis, 0) : &cg.at(aVis, 0);
-  for (int gi = tid; gi < G; gi += kGapThreads) {
+  for (int gi = tid; gi < G; gi += T) {
     const int pos = w.Gap[gi];
     const int before =
         pos == 0 ? g.init : (w.Pin[pos - 1] != -1 ? w.Val[pos - 1] : w.Req[pos - 1]);
     gaps[gi] = make_int4((int)w.Uh[pos], w.Req[pos], before, pos);
     mg[gi] = -1;
   }
-  for (int o = tid; o < n_opt; o += kGapThreads) {
+  for (int o = tid; o < n_opt; o += T) {
     if (in_lds) cl.ops()[o] = w.Opt[o];
     mo[o] = -1;
     vis[o] = 0;
@@ -795,11 +800,12 @@ __device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t 
   return r;
 }
 
+template <int T>
 __device__ __forceinline__ int64_t key_fail_op(const GapKey &g, uint32_t at, GapSh &sh) {
   // the record whose return is event `at` (key-relative)
   if (threadIdx.x == 0) sh.res = INT_MAX;
   __syncthreads();
-  for (int r = threadIdx.x; r < g.n; r += kGapThreads)
+  for (int r = threadIdx.x; r < g.n; r += T)
     if (g.kops[r].ret == g.base + (int64_t)at) atomicMin(&sh.res, r);
   __syncthreads();
   const int r = sh.res;
@@ -816,7 +822,8 @@ __host__ __device__ __forceinline__ uint32_t probe_cut(uint32_t lo, uint32_t hi,
   return lo + (uint32_t)((uint64_t)(j + 1) * len / (uint64_t)(P + 1));
 }
 
-__global__ __launch_bounds__(kGapThreads) void gap_tier_kernel(
+template <int T>
+__global__ __launch_bounds__(T) void gap_tier_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
     const int32_t *__restrict__ keys, const KParams p, lc_key_result *__restrict__ out,
     int32_t *__restrict__ ws, const int64_t cap, int32_t *__restrict__ pass_keys,
@@ -863,10 +870,10 @@ __global__ __launch_bounds__(kGapThreads) void gap_tier_kernel(
     int res = GD_SKIP;
     if (job.mode == kGapFull || cut != kNever) {
       for (;;) {
-        res = gap_decide(g, cut, job.lds_bytes, &nodes, &G);
+        res = gap_decide<T>(g, cut, job.lds_bytes, &nodes, &G);
         if (res == GD_RETRY) {  // rare: a matching larger than the LDS left
           g.ws = gap_ws(ws_hbm, cap, false);
-          res = gap_decide(g, cut, job.lds_bytes, &nodes, &G);
+          res = gap_decide<T>(g, cut, job.lds_bytes, &nodes, &G);
           g.ws = gap_ws(reinterpret_cast<int32_t *>(lds_dyn), capk, true);
         }
         if (!bis) {
@@ -892,7 +899,7 @@ __global__ __launch_bounds__(kGapThreads) void gap_tier_kernel(
     if (bis) {
       int64_t fail_op = -1;
       if (res == GD_INVALID) {
-        fail_op = key_fail_op(g, lo, sh);
+        fail_op = key_fail_op<T>(g, lo, sh);
         if (fail_op < 0) res = GD_NA;  // not a return: cannot happen
       }
       if (threadIdx.x == 0) {
@@ -1000,21 +1007,33 @@ size_t gap_tier_ws_bytes(int n_wg, int64_t cap) {
   return (size_t)n_wg * kGapArrays * (size_t)cap * sizeof(int32_t);
 }
 
+template <int T>
+hipError_t launch_gap_tier_t(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
+                             const KParams &p, lc_key_result *d_out, int32_t *d_ws, int n_wg,
+                             int64_t cap, int32_t *d_pass_keys, KStatus *d_status,
+                             const GapJob &job, hipStream_t stream) {
+  if (job.lds_bytes > (64 << 10)) {  // beyond the default dynamic-LDS limit (gfx950: 160 KB per CU)
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(gap_tier_kernel<T>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             job.lds_bytes);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(gap_tier_kernel<T>, dim3((unsigned)n_wg), dim3(T), (unsigned)job.lds_bytes,
+                     stream, d_ops, d_key_off, d_keys, p, d_out, d_ws, cap, d_pass_keys, d_status,
+                     job);
+  return hipGetLastError();
+}
+
 hipError_t launch_gap_tier(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
                            const KParams &p, lc_key_result *d_out, int32_t *d_ws, int n_wg,
                            int64_t cap, int32_t *d_pass_keys, KStatus *d_status,
                            const GapJob &job, hipStream_t stream) {
   if (job.n_tasks <= 0) return hipSuccess;
-  if (job.lds_bytes > (64 << 10)) {  // beyond the default dynamic-LDS limit (gfx950: 160 KB per CU)
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(gap_tier_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             job.lds_bytes);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(gap_tier_kernel, dim3((unsigned)n_wg), dim3(kGapThreads),
-                     (unsigned)job.lds_bytes, stream, d_ops, d_key_off, d_keys, p, d_out, d_ws,
-                     cap, d_pass_keys, d_status, job);
-  return hipGetLastError();
+  return job.threads == kWave
+             ? launch_gap_tier_t<kWave>(d_ops, d_key_off, d_keys, p, d_out, d_ws, n_wg, cap,
+                                        d_pass_keys, d_status, job, stream)
+             : launch_gap_tier_t<kGapThreads>(d_ops, d_key_off, d_keys, p, d_out, d_ws, n_wg, cap,
+                                              d_pass_keys, d_status, job, stream);
 }
 
 hipError_t launch_gap_narrow(const lc_op *d_ops, const int64_t *d_key_off, int32_t n_cex,

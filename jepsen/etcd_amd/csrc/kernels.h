@@ -108,6 +108,7 @@ struct GapJob {
   int32_t bisect;      // kGapFull: bisect invalid keys in place
   int32_t P;           // probes per interval (kGapProbe)
   int32_t lds_bytes;   // dynamic LDS per workgroup for the matching arrays
+  int32_t threads;     // workgroup size: 256, or 64 for short keys (one wave per decision)
   int32_t n_tasks;     // keys (full), intervals x P (probe)
   int32_t *cex_key;    // per counterexample: the key
   uint32_t *cex_lo;    // key-relative event interval [lo, hi] holding the

@@ -49,6 +49,11 @@ constexpr int64_t kGapSkelLdsMax = 78 << 10;  // two such workgroups per CU (160
 constexpr int kGapLdsProbe = 48 << 10;
 constexpr int kGapMaxRounds = 64;
 constexpr int kGapProbeMinLen = 1024;
+#ifndef LC_GAP_WAVE_MAX_LEN
+#define LC_GAP_WAVE_MAX_LEN 256
+#endif
+constexpr int kGapWaveMaxLen = LC_GAP_WAVE_MAX_LEN;  // keys up to this long: one-wave gap-tier workgroups
+constexpr int64_t kGapWaveMinKeys = 1024;             // ... when there are more of them than this
 
 struct Dev {
   int id = -1;
@@ -236,8 +241,13 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     // keys, invalid keys); what it cannot decide goes on to the JIT search
     const int wg_cap = (int)std::min<int64_t>(
         (int64_t)kGapMaxWG, std::max<int64_t>(1, (int64_t)(kGapWsBytes / gap_per_wg)));
+    // many short keys: one-wave workgroups, four times as many decisions in
+    // flight (10k 200-op keys: 0.78 -> 0.45 ms); few keys are latency-bound
+    // and decide faster with 256 threads each (94 keys: 0.19 vs 0.145 ms)
+    const bool wave_wg = d.h_status->max_len <= kGapWaveMaxLen && n_jit > kGapWaveMinKeys;
+    const int full_wg = (int)std::min<int64_t>(n_jit, wave_wg ? 4 * (int64_t)wg_cap : wg_cap);
     rc = ensure(c, reinterpret_cast<char **>(&d.d_gws), &d.gws_cap,
-                lcdev::gap_tier_ws_bytes((int)std::min<int64_t>(n_jit, wg_cap), gap_cap));
+                lcdev::gap_tier_ws_bytes(full_wg, gap_cap));
     // counterexample intervals: key, lo, hi, gaps, state (int32), nodes
     // (int64) per invalid key, and one int32 per probe workgroup
     const size_t nk = (size_t)n_jit;
@@ -253,6 +263,9 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     job.probe = job.cex_state + nk;
     job.mode = lcdev::kGapFull;
     job.n_tasks = (int32_t)n_jit;
+    // short keys: one-wave workgroups (barriers nearly free, 4x the decisions
+    // in flight); longer keys: 256 threads share each decision's setup
+    job.threads = wave_wg ? 64 : 256;
     // Bisect counterexamples in place unless the keys are long and few
     // enough for multisection rounds to pay (each round costs two launches
     // and a sync; a probe of a short key costs less than that).
@@ -269,7 +282,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     const bool no_lds = lds_env && lds_env[0] == '0';
     if (no_lds) job.lds_bytes = 0;
     HIP_TRY(c, lcdev::launch_gap_tier(d_ops, d_off, jit_list, p, d_out, d.d_gws,
-                                      (int)std::min<int64_t>(n_jit, wg_cap), gap_cap, d.d_jit2,
+                                      full_wg, gap_cap, d.d_jit2,
                                       d.d_status, job, st));
     HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                               hipMemcpyDeviceToHost, st));
@@ -279,6 +292,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       // counterexamples of long keys: P probes per interval per round, over
       // the whole GPU
       job.mode = lcdev::kGapProbe;
+      job.threads = 256;
       job.P = wg_cap / n_cex;
       job.n_tasks = n_cex * job.P;
       job.lds_bytes = no_lds ? 0 : kGapLdsProbe;

@@ -227,6 +227,30 @@ def test_c4_hot_key(ctx, seed, anom):
         assert want == 0  # an injected stale read is always visible
 
 
+def test_gap_tier_c2_with_crashes(ctx):
+    """C2-shaped keys (1,000 ops, concurrency 20) with 5 % crashed
+    writes/CAS and injected anomalies: the shape of bench.py's crash_leg, with
+    the skeleton in LDS.  Beyond the oracle's searches at this size (most keys
+    exceed 4M configurations), so verdicts and counterexamples are checked
+    against the restated procedure (tests/gapmatch_ref.py, itself checked
+    against the oracle on smaller keys) and against the oracle's WGL wherever
+    it decides."""
+    import gapmatch_ref as gm
+    ops, off, lab, _ = abi.synth(24, 1000, concurrency=20, p_info=0.05, p_anomaly=0.4,
+                                 seed=0x5EED0013)
+    _, g = ctx.check(ops, off)
+    assert ctx.stats()["n_gap_keys"] == 24 and (g["verdict"] != -1).all()
+    for k in range(24):
+        recs = _gm_recs(ops, off, k)
+        assert g["verdict"][k] == gm.decide(recs)
+        if g["verdict"][k] == 0:
+            assert (g["fail_op"][k], g["fail_prefix_end"][k]) == gm.first_failure(recs)
+    assert (g["verdict"] == 0).sum() >= 3 and (g["verdict"] == 1).sum() >= 3
+    _, w = oracle.check(ops, off, algo=oracle.WGL, n_threads=8, max_configs=1 << 18)
+    known = w["verdict"] != -1
+    assert (g["verdict"][known] == w["verdict"][known]).all()
+
+
 def test_gap_tier_many_invalid_keys_bisect(ctx):
     """More invalid crash-heavy keys than half the gap tier's workgroups: the
     counterexamples are found by one bisecting workgroup per key instead of
