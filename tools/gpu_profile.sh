@@ -27,4 +27,8 @@ echo "write done"
 timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d $O/prof_$TAG/l2 -o l2 --output-format csv -- \
   python3 $R/bench.py --steps 5 --warmup 1 --bare > $O/prof_$TAG/l2.log 2>&1
 echo "l2 done"
+# every leg of the bench line (gap, JIT, HBM tiers, compaction, narrowing)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG/kt_all -o kt_all --output-format csv -- \
+  python3 $R/bench.py --steps $STEPS --warmup 3 --no-cpu-baseline > $O/prof_$TAG/kt_all.log 2>&1
+echo "all-legs kernel trace done"
 find $O/prof_$TAG -name '*.csv' | head -50

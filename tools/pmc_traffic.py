@@ -55,7 +55,8 @@ def main():
     for sub, f in (("kt", "kt_kernel_stats.csv"), ("kt", "kt_domain_stats.csv"),
                    ("fetch", "fetch_counter_collection.csv"),
                    ("write", "write_counter_collection.csv"),
-                   ("l2", "l2_counter_collection.csv")):
+                   ("l2", "l2_counter_collection.csv"),
+                   ("kt_all", "kt_all_kernel_stats.csv")):
         p = os.path.join(src, sub, f)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, tag, f))
