@@ -1,0 +1,85 @@
+"""Dev: broad differential fuzz, GPU vs the oracle, over random histories:
+tiny random keys (brute-force sized), synthetic register keys across crash and
+anomaly rates and concurrencies, version-stripped keys (cas-register), mutex
+and cas-register record generators.  Prints mismatches; exits 1 on any.
+    python tools/fuzz_gpu.py [rounds]"""
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import numpy as np  # noqa: E402
+
+import oracle  # noqa: E402
+from helpers import pack_keys, random_casreg, random_mutex, tiny_batch  # noqa: E402
+from jepsen.etcd_amd import abi  # noqa: E402
+
+rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+bad_total = 0
+t_start = time.time()
+
+
+def compare(tag, ops, off, opts=None, algo=oracle.JITC, budget=1 << 18):
+    global bad_total
+    with abi.Context(device_mask=1) as ctx:
+        _, g = ctx.check(ops, off, opts)
+    _, o = oracle.check(ops, off, algo=algo, n_threads=16, max_configs=budget,
+                        init_version=opts.init_version if opts is not None else 0,
+                        init_value=opts.init_value if opts is not None else -1)
+    known = (o["verdict"] != -1) & (g["verdict"] != -1)
+    diff = g["verdict"] != o["verdict"]
+    if algo != oracle.WGL:  # WGL gives verdicts only
+        diff |= g["fail_op"] != o["fail_op"]
+    bad = np.nonzero(known & diff)[0]
+    gpu_unknown = int(((g["verdict"] == -1) & (o["verdict"] != -1)).sum())
+    print("%-34s keys %5d decided %5d gpu-only-unknown %3d mismatches %d (%.0fs)"
+          % (tag, len(off) - 1, int(known.sum()), gpu_unknown, len(bad), time.time() - t_start),
+          flush=True)
+    for k in bad[:5]:
+        print("   key", int(k), "gpu", g[k].tolist(), "oracle", int(o["verdict"][k]), int(o["fail_op"][k]))
+    bad_total += len(bad)
+
+
+for rd in range(rounds):
+    base = 1000 * rd + 17
+    ops, off = pack_keys(tiny_batch(base, 4000, max_ops=7))
+    compare("tiny r%d" % rd, ops, off)
+    for conc, pinf, pan, opk in ((4, 0.3, 0.5, 40), (8, 0.2, 0.4, 80), (12, 0.1, 0.3, 150),
+                                 (20, 0.05, 0.3, 300), (6, 0.0, 0.5, 500)):
+        ops, off, _, _ = abi.synth(300, opk, concurrency=conc, p_info=pinf, p_anomaly=pan,
+                                   seed=base + conc)
+        compare("synth c%d i%.2f a%.1f n%d r%d" % (conc, pinf, pan, opk, rd), ops, off)
+        ops2 = ops.copy()
+        ops2[:, 3] = -1
+        if pinf <= 0.1 and conc <= 8:
+            compare("unversioned c%d n%d r%d" % (conc, opk, rd), ops2, off, algo=oracle.WGL)
+            compare("unversioned-jit c%d n%d r%d" % (conc, opk, rd), ops2, off)
+    # few long crash-heavy keys: full-history decision + multisection probes
+    # (beyond the oracle: checked against the restated procedure)
+    import gapmatch_ref as gm
+    ops, off, _, _ = abi.synth(6, 1500, concurrency=24, p_info=0.1, p_anomaly=0.7, seed=base + 99)
+    with abi.Context(device_mask=1) as ctx:
+        _, g = ctx.check(ops, off)
+    nbad = 0
+    for k in range(6):
+        recs = [tuple(r) for r in ops[off[k]:off[k + 1]].tolist()]
+        want = gm.decide(recs)
+        got = (int(g["verdict"][k]), int(g["fail_op"][k]), int(g["fail_prefix_end"][k]))
+        exp = (want,) + (gm.first_failure(recs) if want == 0 else (-1, -1))
+        if want is not None and got != exp:
+            nbad += 1
+            print("   long key", k, "gpu", got, "restated", exp)
+    print("%-34s keys %5d mismatches %d" % ("long crash-heavy r%d" % rd, 6, nbad), flush=True)
+    bad_total += nbad
+    rng = random.Random(base)
+    keys = [random_mutex(rng, rng.randrange(1, 24)) for _ in range(1500)]
+    ops, off = pack_keys(keys)
+    compare("mutex r%d" % rd, ops, off, abi.default_opts(init_value=0))
+    keys = [random_casreg(rng, rng.randrange(1, 24)) for _ in range(1500)]
+    ops, off = pack_keys(keys)
+    compare("casreg r%d" % rd, ops, off)
+print("TOTAL mismatches", bad_total)
+sys.exit(1 if bad_total else 0)
