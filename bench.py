@@ -198,6 +198,7 @@ def main():
         "hot_key": None,
     }
     if rank == 0 and not args.bare:
+        line["c1_leg"] = c1_leg(ctx, abi)
         line["host_leg"] = host_leg(ctx, abi, ops, key_off, n_inv)
         line["hot_key"] = hot_key(ctx, abi)
         line["search_leg"] = search_leg(ctx, abi, d_ops, d_off, d_out, args, stream, n_ops)
@@ -213,6 +214,32 @@ def main():
     ctx.close()
     if distributed:
         dist.destroy_process_group()
+
+
+def c1_leg(ctx, abi):
+    """BASELINE configs[0] (C1): 100 keys x 200 ops, concurrency 10, the
+    configuration the reference's CPU checker is quoted on.  GPU call (host
+    buffers) against the oracle's C restatement of knossos on one host thread,
+    verdicts compared key by key.  Not part of `value`."""
+    import oracle
+    ops, off, _, _ = abi.synth(100, 200, concurrency=10, seed=0x5EED0001)
+    times = []
+    for _ in range(6):
+        t0 = time.perf_counter()
+        _, r = ctx.check(ops, off)
+        times.append((time.perf_counter() - t0) * 1e3)
+    best = None
+    for name, algo in (("jit", oracle.JIT), ("wgl", oracle.WGL)):
+        t0 = time.perf_counter()
+        _, o = oracle.check(ops, off, algo=algo, n_threads=1)
+        dt = (time.perf_counter() - t0) * 1e3
+        if best is None or dt < best[1]:
+            best = (name, dt, o)
+    return {"workload": "C1: 100 keys x 200 ops, concurrency 10 (host buffers)",
+            "gpu_call_ms": float(np.median(times[1:])),
+            "cpu_oracle_ms": best[1], "cpu_oracle": best[0] + ", 1 thread",
+            "valid": int((r["verdict"] == 1).sum()),
+            "verdict_mismatches_vs_oracle": int((r["verdict"] != best[2]["verdict"]).sum())}
 
 
 def host_leg(ctx, abi, ops, key_off, n_inv):
