@@ -35,6 +35,13 @@ constexpr int64_t kDefaultBudget = 1 << 24;   // configurations per key
 // is ~128 B per configuration of capacity (3 regions + 2 hash tables).
 // Each tier's workspace is <= 4 GiB; the first has the most waves (the
 // lane-parallel expansion is latency-bound per wave).
+// Timing events.  LC_EVENT_FLAGS (dev A/B): hipEventDisableSystemFence skips
+// the event's own system-scope fence (cache writeback + invalidate) when it
+// is recorded; kernel completion already releases the kernel's writes.
+#ifndef LC_EVENT_FLAGS
+#define LC_EVENT_FLAGS hipEventDisableSystemFence
+#endif
+constexpr unsigned kEventFlags = LC_EVENT_FLAGS;
 constexpr int kHbmTiers = 3;
 constexpr int64_t kHbmCap[kHbmTiers] = {1 << 14, 1 << 18, 1 << 21};
 constexpr int kHbmWaves[kHbmTiers] = {2048, 128, 16};
@@ -404,9 +411,11 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
     d.id = i;
     if (hipSetDevice(i) != hipSuccess ||
         hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&d.e0) != hipSuccess || hipEventCreate(&d.e1) != hipSuccess ||
-        hipEventCreate(&d.e2) != hipSuccess || hipEventCreate(&d.ef) != hipSuccess ||
-        hipEventCreate(&d.eg) != hipSuccess ||
+        hipEventCreateWithFlags(&d.e0, kEventFlags) != hipSuccess ||
+        hipEventCreateWithFlags(&d.e1, kEventFlags) != hipSuccess ||
+        hipEventCreateWithFlags(&d.e2, kEventFlags) != hipSuccess ||
+        hipEventCreateWithFlags(&d.ef, kEventFlags) != hipSuccess ||
+        hipEventCreateWithFlags(&d.eg, kEventFlags) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&d.d_status), sizeof(lcdev::KStatus)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&d.h_handoff), sizeof(int32_t),
