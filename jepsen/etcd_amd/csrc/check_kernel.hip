@@ -161,8 +161,29 @@ struct SlotLds {
   uint64_t pbit[kWave];
 };
 
+// Cooperative HBM tier: the waves of one workgroup expand one key's
+// frontier together.  Wave 0 runs the event loop (check_key); at a return on
+// the general path it publishes the expansion here and every wave runs
+// coop_expand (level-synchronous BFS: a level's worklist range is fixed,
+// batches of 64 are claimed with an LDS counter, appends are reserved with
+// LDS atomics, barriers between levels).
+enum { kCoopExpand = 0, kCoopExit = 1 };
+constexpr uint32_t kBusy = 0x80000000u;  // table tag: claimed, configuration being written
+struct CoopShared {
+  int cmd;
+  int rF, rR, rW, nF;
+  uint64_t bs, muts, reads, crashed;
+  uint32_t epoch;
+  int nR, nW, head, lo, hi, go, status;
+  unsigned long long explored;
+  long long budget;
+  SlotLds slots;
+};
+
 struct HbmStore {
   SlotLds *sl;    // slot staging (LDS)
+  CoopShared *coop = nullptr;  // set in the cooperative kernel
+  int nwaves = 1;
   Cfg *base;      // 3 regions of cap configurations, contiguous
   Cfg *tabs;      // 2 tables (roles R, W) of 2*cap entries
   uint32_t *tags; // 2 tag arrays of 2*cap
@@ -234,6 +255,53 @@ struct HbmStore {
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
+    return res;
+  }
+  // Cross-wave variants (cooperative tier): a claimed entry is tagged
+  // epoch|kBusy until its configuration is stored, then released as epoch;
+  // a lane that meets a busy entry retries it next round.
+  __device__ __forceinline__ void claim_unique_lane(int role, int r, int j, const Cfg &c) {
+    reg(r)[j] = c;
+    uint32_t h = (hash(c.mask, c.sv) & tmask) & ~7u;
+    for (;;) {
+      const uint32_t old = __hip_atomic_load(&tag(role)[h], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      if ((old & ~kBusy) != epoch) {
+        if (atomicCAS(&tag(role)[h], old, epoch | kBusy) == old) {
+          tab(role)[h] = c;
+          __hip_atomic_store(&tag(role)[h], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          return;
+        }
+        continue;
+      }
+      h = (h + 1) & tmask;
+    }
+  }
+  __device__ __forceinline__ int insert_lanes_coop(int role, const Cfg &c, bool want) {
+    uint32_t h = (hash(c.mask, c.sv) & tmask) & ~7u;
+    int res = 0;
+    bool pend = want;
+    while (__ballot(pend)) {
+      if (pend) {
+        const uint32_t t = __hip_atomic_load(&tag(role)[h], __ATOMIC_ACQUIRE,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (t == epoch) {
+          const Cfg e = tab(role)[h];
+          if (e.mask == c.mask && e.sv == c.sv)
+            pend = false;  // already there
+          else
+            h = (h + 1) & tmask;
+        } else if (t != (epoch | kBusy)) {  // stale: claim it
+          if (atomicCAS(&tag(role)[h], t, epoch | kBusy) == t) {
+            tab(role)[h] = c;
+            __hip_atomic_store(&tag(role)[h], epoch, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+            res = 1;
+            pend = false;
+          }
+        }  // busy: being written by another lane, retry
+      }
     }
     return res;
   }
@@ -382,6 +450,160 @@ __device__ __forceinline__ int general_return(Store &st, const Slot &sl, const M
   return nR;
 }
 
+__device__ __forceinline__ void coop_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// One wave's share of a cooperative expansion (every wave of the workgroup
+// calls it; the parameters are in C).  Barrier count is uniform: one after
+// the split, two per BFS level.
+__device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
+  const int nw = st.nwaves;
+  st.epoch = C.epoch;
+  const uint64_t bs = C.bs, muts = C.muts, reads = C.reads, crashed = C.crashed;
+  const int rF = C.rF, rR = C.rR, rW = C.rW, nF = C.nF;
+  const SlotLds &L = C.slots;
+  // split F into R (x linearized, its bit dropped) and W
+  for (int j0 = wave * kWave; j0 < nF; j0 += nw * kWave) {
+    const int j = j0 + lane;
+    const bool v = j < nF;
+    Cfg c{0, 0};
+    if (v) c = st.get(rF, j);
+    const bool has = v && (c.mask & bs);
+    const bool lacks = v && !(c.mask & bs);
+    const uint64_t mh = __ballot(has), ml = __ballot(lacks);
+    int bR = 0, bW = 0;
+    if (lane == 0) {
+      bR = mh ? atomicAdd(&C.nR, __popcll(mh)) : 0;
+      bW = ml ? atomicAdd(&C.nW, __popcll(ml)) : 0;
+    }
+    bR = __builtin_amdgcn_readfirstlane(bR);
+    bW = __builtin_amdgcn_readfirstlane(bW);
+    if (has) st.claim_unique_lane(ROLE_R, rR, bR + lanes_below(mh), Cfg{c.mask & ~bs, c.sv});
+    if (lacks) st.claim_unique_lane(ROLE_W, rW, bW + lanes_below(ml), c);
+  }
+  // Level bounds and the go flag are written by wave 0 between two barriers,
+  // while no wave appends, so every wave reads the same values.
+  coop_barrier();
+  if (wave == 0 && lane == 0) {
+    C.lo = 0;
+    C.hi = C.nW;
+    C.head = 0;
+    C.go = C.hi > 0 && C.status == 0;
+  }
+  coop_barrier();
+  while (C.go) {
+    const int lo = C.lo, hi = C.hi;
+    // this level: W[lo, hi) in batches of 64 claimed from C.head
+    for (;;) {
+      int b = 0;
+      if (lane == 0) b = atomicAdd(&C.head, kWave);
+      b = __builtin_amdgcn_readfirstlane(b) + lo;
+      if (b >= hi || __hip_atomic_load(&C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+        break;
+      const int j = b + lane;
+      const bool act = j < hi;
+      const Cfg c = st.get(rW, act ? j : b);
+      const int cver = sv_ver(c.sv), cval = sv_val(c.sv);
+      uint64_t cand = 0;
+      if (act) {
+        uint64_t m = muts & ~c.mask;
+        while (m) {
+          const int t = __builtin_ctzll(m);
+          m &= m - 1;
+          const int4 pr = L.pre[t];
+          if (pre_ok(pr.x, pr.y, pr.z, pr.w, cver, cval) &&
+              (!((crashed >> t) & 1) || (L.pbit[t] & ~c.mask) == 0))
+            cand |= 1ull << t;
+        }
+      }
+      for (;;) {
+        const bool has = cand != 0;
+        const uint64_t hb = __ballot(has);
+        if (!hb) break;
+        Cfg nc{0, 0};
+        bool toR = false;
+        if (has) {
+          const int t = __builtin_ctzll(cand);
+          cand &= cand - 1;
+          const int nver = cver + 1, nval = L.val[t];
+          uint64_t nm = c.mask | (1ull << t);
+          uint64_t r = reads & ~nm;
+          while (r) {
+            const int u = __builtin_ctzll(r);
+            r &= r - 1;
+            const int4 pr = L.pre[u];
+            if (pre_ok(pr.x, pr.y, pr.z, pr.w, nver, nval)) nm |= 1ull << u;
+          }
+          toR = (nm & bs) != 0;
+          nc = Cfg{toR ? nm & ~bs : nm, pack_sv(nver, nval)};
+        }
+        const int insR = st.insert_lanes_coop(ROLE_R, nc, has && toR);
+        const int insW = st.insert_lanes_coop(ROLE_W, nc, has && !toR);
+        const uint64_t bR = __ballot(insR), bW = __ballot(insW);
+        int aR = 0, aW = 0;
+        unsigned long long ex = 0;
+        if (lane == 0) {
+          aR = bR ? atomicAdd(&C.nR, __popcll(bR)) : 0;
+          aW = bW ? atomicAdd(&C.nW, __popcll(bW)) : 0;
+          ex = atomicAdd(&C.explored, (unsigned long long)__popcll(hb)) + __popcll(hb);
+        }
+        aR = __builtin_amdgcn_readfirstlane(aR);
+        aW = __builtin_amdgcn_readfirstlane(aW);
+        const bool fullR = aR + __popcll(bR) > st.cap, fullW = aW + __popcll(bW) > st.cap;
+        if (insR && !fullR) st.reg(rR)[aR + lanes_below(bR)] = nc;
+        if (insW && !fullW) st.reg(rW)[aW + lanes_below(bW)] = nc;
+        if (lane == 0) {
+          if (fullR || fullW) atomicMin(&C.status, -1);
+          else if ((long long)ex > C.budget && C.status == 0) atomicMin(&C.status, -2);
+        }
+        if (fullR || fullW) break;
+      }
+    }
+    coop_barrier();  // the level's appends are done
+    if (wave == 0 && lane == 0) {
+      C.lo = hi;
+      C.hi = C.nW;
+      C.head = 0;
+      C.go = C.lo < C.hi && C.status == 0;
+    }
+    coop_barrier();
+  }
+}
+
+// Wave 0's side of a cooperative return: publish, expand with the others.
+__device__ int coop_return(HbmStore &st, const Slot &sl, const Masks &mk, int s, int rF, int rR,
+                           int rW, int nF, const KParams &p, KeyOut &o, int lane) {
+  CoopShared &C = *st.coop;
+  st.begin_return();
+  C.slots.pre[lane] = make_int4(sl.nv, sl.nvm, sl.nl, sl.nlm);
+  C.slots.val[lane] = sl.val;
+  C.slots.pbit[lane] = sl.pbit;
+  if (lane == 0) {
+    C.cmd = kCoopExpand;
+    C.rF = rF;
+    C.rR = rR;
+    C.rW = rW;
+    C.nF = nF;
+    C.bs = 1ull << s;
+    C.muts = mk.occ & ~mk.rdm;
+    C.reads = mk.occ & mk.rdm;
+    C.crashed = mk.crashed;
+    C.epoch = st.epoch;
+    C.nR = 0;
+    C.nW = 0;
+    C.status = 0;
+    C.explored = (unsigned long long)o.explored;
+    C.budget = (long long)p.budget;
+  }
+  coop_barrier();  // the workers' start barrier
+  coop_expand(st, C, lane, 0);
+  o.explored = (int64_t)C.explored;
+  return C.status < 0 ? C.status : C.nR;
+}
+
 // HBM tier: the same expansion as general_return, lane-parallel.  The
 // worklist W is taken 64 configurations at a time, one per lane; each lane
 // tests every pending mutation against its own configuration (slots staged
@@ -393,6 +615,7 @@ __device__ __forceinline__ int general_return(Store &st, const Slot &sl, const M
 __device__ __forceinline__ int general_return_par(HbmStore &st, const Slot &sl, const Masks &mk,
                                                   int s, int rF, int rR, int rW, int nF,
                                                   const KParams &p, KeyOut &o, int lane) {
+  if (st.coop) return coop_return(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
   const uint64_t bs = 1ull << s;
   st.begin_return();
   SlotLds &L = *st.sl;
@@ -1193,6 +1416,55 @@ __global__ __launch_bounds__(kCompactThreads) void handoff_compact_kernel(
   }
 }
 
+// Cooperative HBM tier: one workgroup of NW waves per key (few, large keys:
+// the higher-capacity tiers).  Wave 0 runs the event loop; waves 1..NW-1
+// serve its expansions until told to exit.
+template <int NW>
+__global__ __launch_bounds__(NW * kWave) void hbm_coop_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
+    const int32_t *__restrict__ keys, const int32_t n_list,
+    const KParams p, lc_key_result *__restrict__ out, char *__restrict__ ws,
+    const int64_t cap, int32_t *__restrict__ ovf_out, int32_t *__restrict__ n_ovf_out,
+    const int last_tier) {
+  __shared__ CoopShared C;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  char *w = ws + (size_t)blockIdx.x * hbm_wave_bytes(cap);
+  HbmStore st;
+  st.sl = &C.slots;
+  st.coop = &C;
+  st.nwaves = NW;
+  st.base = reinterpret_cast<Cfg *>(w);
+  st.tabs = st.base + 3 * cap;
+  st.tags = reinterpret_cast<uint32_t *>(st.tabs + 4 * cap);
+  st.cap = (int)cap;
+  st.tmask = (uint32_t)(2 * cap - 1);
+  st.epoch = 0;  // tags zeroed by the host; epochs start at 1
+  if (wave == 0) {
+    const int64_t key_base = key_off[0];
+    for (int li = blockIdx.x; li < n_list; li += gridDim.x) {
+      const int64_t key = keys[li];
+      const int64_t beg = key_off[key], end = key_off[key + 1];
+      KeyOut o;
+      check_key(ops + (beg - key_base), (int)(end - beg), p, st, o, lane);
+      if (o.reason == LC_REASON_FRONTIER_LDS) {
+        if (last_tier)
+          o.reason = LC_REASON_CONFIG_BUDGET;
+        else if (lane == 0)
+          ovf_out[atomicAdd(n_ovf_out, 1)] = (int32_t)key;
+      }
+      if (lane == 0) write_result(&out[key], o);
+    }
+    if (lane == 0) C.cmd = kCoopExit;
+    coop_barrier();
+  } else {
+    for (;;) {
+      coop_barrier();
+      if (C.cmd == kCoopExit) break;
+      coop_expand(st, C, lane, wave);
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_handoff_compact(int32_t *d_flags, const int64_t *d_key_off, int64_t n_keys,
@@ -1229,6 +1501,22 @@ hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
 
 size_t hbm_tier_ws_bytes(int n_waves, int64_t cap) {
   return hbm_wave_bytes(cap) * (size_t)n_waves;
+}
+
+hipError_t launch_hbm_coop(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
+                           int32_t n_list, const KParams &p, lc_key_result *d_out, void *d_ws,
+                           int n_wg, int64_t cap, int32_t *d_ovf_out, int32_t *d_n_ovf_out,
+                           int last_tier, int waves_per_key, hipStream_t stream) {
+  if (n_list <= 0) return hipSuccess;
+  if (waves_per_key >= 16)
+    hipLaunchKernelGGL(hbm_coop_kernel<16>, dim3((unsigned)n_wg), dim3(16 * kWave), 0, stream,
+                       d_ops, d_key_off, d_keys, n_list, p, d_out, static_cast<char *>(d_ws), cap,
+                       d_ovf_out, d_n_ovf_out, last_tier);
+  else
+    hipLaunchKernelGGL(hbm_coop_kernel<4>, dim3((unsigned)n_wg), dim3(4 * kWave), 0, stream,
+                       d_ops, d_key_off, d_keys, n_list, p, d_out, static_cast<char *>(d_ws), cap,
+                       d_ovf_out, d_n_ovf_out, last_tier);
+  return hipGetLastError();
 }
 
 hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,

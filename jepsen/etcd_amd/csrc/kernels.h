@@ -79,6 +79,14 @@ hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
 // d_ovf_out (count *d_n_ovf_out) unless last_tier, where they become
 // LC_REASON_CONFIG_BUDGET (:unknown).
 size_t hbm_tier_ws_bytes(int n_waves, int64_t cap);
+// Cooperative variant: one workgroup of waves_per_key (4 or 16) wavefronts
+// per key, its waves expanding the key's frontier together (for short key
+// lists, where a wavefront per key leaves SIMDs idle).  Workspace:
+// hbm_tier_ws_bytes(n_wg, cap).
+hipError_t launch_hbm_coop(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
+                           int32_t n_list, const KParams &p, lc_key_result *d_out, void *d_ws,
+                           int n_wg, int64_t cap, int32_t *d_ovf_out, int32_t *d_n_ovf_out,
+                           int last_tier, int waves_per_key, hipStream_t stream);
 hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
                            const int32_t *d_keys,
                            int32_t n_list, const KParams &p, lc_key_result *d_out,

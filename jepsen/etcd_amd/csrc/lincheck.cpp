@@ -45,6 +45,13 @@ constexpr unsigned kEventFlags = LC_EVENT_FLAGS;
 constexpr int kHbmTiers = 3;
 constexpr int64_t kHbmCap[kHbmTiers] = {1 << 14, 1 << 18, 1 << 21};
 constexpr int kHbmWaves[kHbmTiers] = {2048, 128, 16};
+// HBM tier lists up to these sizes get a workgroup of 16 (4) wavefronts per
+// key; longer lists a wavefront per key.  Measured (tools/hbm_probe.py,
+// DESIGN.md §4): 16 wins on 512 crash-heavy keys (4.9 s vs 13.1 s with 4,
+// 40 s with 1), 4 on 1000-2000 version-less keys (71 vs 113 vs 119 ms),
+// 1 on 10,000 (331 vs 355 ms with 4).
+constexpr int kHbmCoop16MaxKeys = 512;
+constexpr int kHbmCoop4MaxKeys = 4096;
 // Gap tier: at most this many workgroups, and this much workspace (each
 // workgroup needs 92 B per record of the longest key handed over).  Dynamic
 // LDS for the matching arrays: up to kGapLdsFull per workgroup for whole-key
@@ -357,16 +364,32 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     int32_t n_list = n_ovf;
     int32_t *list = d.d_ovf, *next = d.d_ovf2;
     HIP_TRY(c, hipEventRecord(d.e1, st));
+    // LC_HBM_COOP (test/A-B knob): 0 one wavefront per key throughout,
+    // 4 / 16 a workgroup of that many wavefronts per key throughout; default:
+    // 16 for short lists, 4 for medium ones, 1 once a wavefront per key
+    // already fills the SIMDs.
+    const char *coop_env = getenv("LC_HBM_COOP");
+    const int coop_mode = coop_env ? atoi(coop_env) : 1;
     for (int tier = 0; tier < kHbmTiers && n_list > 0; tier++) {
+      int wpk = coop_mode == 1 ? (n_list <= kHbmCoop16MaxKeys  ? 16
+                                  : n_list <= kHbmCoop4MaxKeys ? 4
+                                                               : 0)
+                               : coop_mode;
+      const bool coop = wpk == 4 || wpk == 16;
       const int waves = std::min<int>(kHbmWaves[tier], n_list);
       const size_t ws = lcdev::hbm_tier_ws_bytes(waves, kHbmCap[tier]);
       rc = ensure(c, reinterpret_cast<char **>(&d.d_ws), &d.ws_cap, ws);
       if (rc) return rc;
       HIP_TRY(c, hipMemsetAsync(d.d_ws, 0, ws, st));
       HIP_TRY(c, hipMemsetAsync(&d.d_status->n_overflow2, 0, sizeof(int32_t), st));
-      HIP_TRY(c, lcdev::launch_hbm_tier(d_ops, d_off, list, n_list, p,
-                                        d_out, d.d_ws, waves, kHbmCap[tier], next,
-                                        &d.d_status->n_overflow2, tier == kHbmTiers - 1, st));
+      const int last = tier == kHbmTiers - 1;
+      if (coop)
+        HIP_TRY(c, lcdev::launch_hbm_coop(d_ops, d_off, list, n_list, p, d_out, d.d_ws, waves,
+                                          kHbmCap[tier], next, &d.d_status->n_overflow2, last, wpk, st));
+      else
+        HIP_TRY(c, lcdev::launch_hbm_tier(d_ops, d_off, list, n_list, p,
+                                          d_out, d.d_ws, waves, kHbmCap[tier], next,
+                                          &d.d_status->n_overflow2, last, st));
       HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                                 hipMemcpyDeviceToHost, st));
       HIP_TRY(c, hipStreamSynchronize(st));

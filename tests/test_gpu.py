@@ -139,6 +139,31 @@ def test_hbm_tier_resolves_lds_overflow(ctx):
     assert (full["fail_op"] == z["fail_op"]).all()
 
 
+@pytest.mark.parametrize("mode", ["0", "4", "16"])
+def test_hbm_tier_cooperative_agrees(ctx, mode, monkeypatch):
+    """The HBM tier with one wavefront per key (LC_HBM_COOP=0) and with a
+    workgroup of 4 or 16 wavefronts per key reaches the same configuration sets: same
+    verdicts, counterexamples and largest frontier as the golden vectors /
+    each other (unversioned crash-heavy keys, gap tier off)."""
+    z = np.load(os.path.join(GOLDEN, "info.npz"))
+    o = abi.default_opts(flags=abi.LC_FLAG_NO_GAP_TIER)
+    monkeypatch.setenv("LC_HBM_COOP", mode)
+    _, r = ctx.check(z["ops"], z["key_off"], o)
+    assert ctx.stats()["n_hbm_keys"] > 0
+    assert (r["verdict"] == z["verdict"]).all()
+    assert (r["fail_op"] == z["fail_op"]).all()
+    ops, off, _, _ = abi.synth(64, 300, concurrency=20, p_info=0.0, seed=99)
+    ops[:, 3] = -1  # version-less: every key through the frontier search
+    o = abi.default_opts(flags=abi.LC_FLAG_NO_GAP_TIER, time_budget_ms=5000)
+    _, a = ctx.check(ops, off, o)
+    monkeypatch.setenv("LC_HBM_COOP", "1")
+    _, b = ctx.check(ops, off, o)
+    done = (a["reason"] == 0) & (b["reason"] == 0)
+    assert done.sum() >= len(done) // 2
+    for f in ("verdict", "fail_op", "max_frontier"):
+        assert (a[f][done] == b[f][done]).all(), f
+
+
 def test_edge_cases(ctx):
     W, R_ = 1, 0
     keys = [
