@@ -52,6 +52,7 @@
 // records, the branch budget) go on to the JIT tier.
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 
 #include "kernels.h"
 #include "records.h"
@@ -91,16 +92,23 @@ constexpr int kSkelArrays = 17;
 constexpr int kSkelLdsBytes = 4 * kSkelArrays;  // per record; the matching follows it
 constexpr int kMatchReserve = 8 << 10;           // LDS kept for the matching after a skeleton
 
+// Skeleton arrays are addressed through pointers typed by placement: LDS
+// (address space 3) when SL, global otherwise, so the setup compiles to ds_*
+// / global_* instructions rather than flat ones (a flat access waits on both
+// the LDS and the vector-memory counters, and flat atomics to LDS are slow).
+template <bool SL, class X>
+using WsP = std::conditional_t<SL, __attribute__((address_space(3))) X *, X *>;
+
+template <bool SL>
 struct GapWs {
-  int32_t *base;
+  int32_t *base;   // HBM workspace base (the matching's HBM homes; unused when SL)
   int64_t cap;
-  bool lds;        // skeleton in LDS (base points into lds_dyn)
-  int moff;        // int4 offset of the matching's LDS region in lds_dyn
-  uint32_t *A, *B, *Uh;
-  int *Pin, *Val, *PinExp, *Claim, *Req, *Gap;
-  int4 *Opt;
-  uint64_t *Mask;  // compaction ballots
-  int *Pre;        // compaction prefix counts
+  int moff;        // int4 offset of the matching's LDS region in lds_dyn (SL)
+  WsP<SL, uint32_t> A, B, Uh;
+  WsP<SL, int> Pin, Val, PinExp, Claim, Req, Gap;
+  WsP<SL, int4> Opt;
+  WsP<SL, uint64_t> Mask;  // compaction ballots
+  WsP<SL, int> Pre;        // compaction prefix counts
 };
 
 struct GapSh {
@@ -109,27 +117,53 @@ struct GapSh {
   uint32_t maxret;
   int wtot[kGapWaves];
   uint32_t wtotu[kGapWaves];
+#ifdef GAP_PROFILE
+  uint64_t prof[12];
+#endif
 };
 
-__device__ __forceinline__ GapWs gap_ws(int32_t *base, int64_t cap, bool lds) {
-  GapWs w;
+// SL: the skeleton at the start of lds_dyn (cap entries per array); else the
+// workgroup's HBM workspace at base.
+template <bool SL>
+__device__ __forceinline__ GapWs<SL> gap_ws(int32_t *base, int64_t cap) {
+  GapWs<SL> w;
+  int32_t *b = SL ? reinterpret_cast<int32_t *>(lds_dyn) : base;
   w.base = base;
   w.cap = cap;
-  w.lds = lds;
-  w.moff = lds ? (int)(kSkelArrays * cap / 4) : 0;
-  w.A = (uint32_t *)(base + 0 * cap);
-  w.B = (uint32_t *)(base + 1 * cap);
-  w.Uh = (uint32_t *)(base + 2 * cap);
-  w.Pin = base + 3 * cap;
-  w.Val = base + 4 * cap;
-  w.PinExp = base + 5 * cap;
-  w.Claim = base + 6 * cap;
-  w.Req = base + 7 * cap;
-  w.Gap = base + 9 * cap;
-  w.Opt = reinterpret_cast<int4 *>(base + 10 * cap);
-  w.Mask = reinterpret_cast<uint64_t *>(base + (lds ? 14 : 18) * cap);
-  w.Pre = base + (lds ? 16 : 20) * cap;
+  w.moff = SL ? (int)(kSkelArrays * cap / 4) : 0;
+  auto P = [&](int a) { return (WsP<SL, int>)(b + a * cap); };
+  w.A = (WsP<SL, uint32_t>)P(0);
+  w.B = (WsP<SL, uint32_t>)P(1);
+  w.Uh = (WsP<SL, uint32_t>)P(2);
+  w.Pin = P(3);
+  w.Val = P(4);
+  w.PinExp = P(5);
+  w.Claim = P(6);
+  w.Req = P(7);
+  w.Gap = P(9);
+  w.Opt = (WsP<SL, int4>)P(10);
+  w.Mask = (WsP<SL, uint64_t>)P(SL ? 14 : 18);
+  w.Pre = P(SL ? 16 : 20);
   return w;
+}
+
+// int4's members take a generic `this`: 16-byte skeleton records go through
+// a cast (folded back to the pointer's address space after inlining)
+template <class P>
+__device__ __forceinline__ int4 ws_ld4(P p) {
+  return *(const int4 *)p;
+}
+template <class P>
+__device__ __forceinline__ void ws_st4(P p, int4 v) {
+  *(int4 *)p = v;
+}
+template <class P>
+__device__ __forceinline__ void ws_max(P p, uint32_t v) {
+  atomicMax((uint32_t *)p, v);
+}
+template <class P>
+__device__ __forceinline__ void ws_min(P p, uint32_t v) {
+  atomicMin((uint32_t *)p, v);
 }
 
 // Exclusive prefix sum over the workgroup; *total = the sum of all v.
@@ -202,8 +236,8 @@ __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_S
 
 // Stable compaction, phase 2: word-level exclusive prefix of the ballot
 // masks Mask[0..nw) into Pre[0..nw); returns the total.  Two barriers.
-template <int T>
-__device__ int mask_prefix(const GapWs &w, int nw, GapSh &sh) {
+template <int T, bool SL>
+__device__ int mask_prefix(const GapWs<SL> &w, int nw, GapSh &sh) {
   const int tid = threadIdx.x;
   const int per = (nw + T - 1) / T;
   const int k0 = min(tid * per, nw), k1 = min(k0 + per, nw);
@@ -224,7 +258,6 @@ struct GapKey {
   int n;
   int64_t base;  // call index of the key's first record
   int V0, init;
-  GapWs ws;
   GapSh *sh;
 };
 
@@ -239,57 +272,47 @@ struct Cls {
   int4 op;    // K_OPT: the optional op's record (call, value, exp, pos)
 };
 
+// Branch-free: every condition is computed and the outcome selected, so a
+// wave runs one straight-line path per record instead of a divergent branch
+// tree (which cost ~2,000 instructions per chunk with exec-mask bookkeeping).
+// Past the end (r >= n) the record is K_NONE.
 __device__ __forceinline__ Cls classify(const GapKey &g, const Raw &raw, int64_t prev_call,
                                         int r, uint32_t cut, int *flag, uint32_t *maxret) {
-  Cls c;
-  c.kind = K_NONE;
   const int n = g.n;
   const Rec d = decode(raw, g.base);
-  if (d.bad || d.f > LC_F_CAS || (r > 0 && prev_call >= raw.c.x) || raw.c.x < 0) {
-    *flag |= F_NA;  // the JIT tier reports malformed / unknown :f
-    return c;
-  }
-  if (d.call > cut) return c;
+  const bool in = r < n;
+  const bool malformed = in & (d.bad | (d.f > LC_F_CAS) | ((r > 0) & (prev_call >= raw.c.x)) |
+                               (raw.c.x < 0));
+  const bool live = in & !malformed & (d.call <= cut);
   const uint32_t ret = d.ret > cut ? kNever : d.ret;  // pending at the cut
-  if (ret != kNever) *maxret = max(*maxret, ret);
-  c.call = d.call;
-  c.ret = ret;
-  if (d.f == LC_F_READ) {
-    if (ret == kNever || (d.ver == -1 && d.val == -1)) return c;  // never constrains
-    if (d.ver == -1) {
-      *flag |= F_NA;  // read [nil x]: its version is free
-      return c;
-    }
-    const int k = d.ver - g.V0;
-    if (k < 0 || k > n) {
-      *flag |= F_INVALID;
-      return c;
-    }
-    c.kind = K_READ;
-    c.k = k;
-    c.val = d.val;
-    return c;
-  }
-  if (ret == kNever) {
-    const int pos = d.ver == -1 ? -1 : d.ver - g.V0 - 1;
-    if (d.ver != -1 && (pos < 0 || pos >= n)) return c;  // never placeable
-    c.kind = K_OPT;
-    c.op = make_int4((int)d.call, d.val, d.f == LC_F_CAS ? d.exp : kAny, pos);
-    return c;
-  }
-  if (d.ver == -1) {
-    *flag |= F_NA;  // :ok mutation without a version: order not pinned
-    return c;
-  }
+  const bool crashed = ret == kNever;
+  const bool isread = d.f == LC_F_READ;
+  // reads: crashed or [nil nil] never constrain; [nil x] is the JIT tier's
+  const bool rd_uncon = crashed | ((d.ver == -1) & (d.val == -1));
+  const bool rd_na = !rd_uncon & (d.ver == -1);
+  const int kr = d.ver - g.V0;
+  const bool rd_bad = !rd_uncon & !rd_na & ((kr < 0) | (kr > n));
+  // mutations: crashed ones are optional (unless never placeable); an :ok
+  // one without a version is the JIT tier's; one past the key is invalid
   const int pos = d.ver - g.V0 - 1;
-  if (pos < 0 || pos >= n) {
-    *flag |= F_INVALID;  // impossible version
-    return c;
-  }
-  c.kind = K_PIN;
-  c.k = pos;
+  const bool pos_out = (pos < 0) | (pos >= n);
+  const bool mu_na = !crashed & (d.ver == -1);
+  const bool mu_bad = !crashed & !mu_na & pos_out;
+  const bool is_read = live & isread & !rd_uncon & !rd_na & !rd_bad;
+  const bool is_pin = live & !isread & !crashed & !mu_na & !mu_bad;
+  const bool is_opt = live & !isread & crashed & ((d.ver == -1) | !pos_out);
+  const bool na = malformed | (live & (isread ? rd_na : mu_na));
+  const bool inv = live & (isread ? rd_bad : mu_bad);
+  *flag |= (na ? F_NA : 0) | (inv ? F_INVALID : 0);
+  *maxret = (live & !crashed) ? max(*maxret, ret) : *maxret;
+  Cls c;
+  c.kind = is_read ? K_READ : is_pin ? K_PIN : is_opt ? K_OPT : K_NONE;
+  c.k = is_read ? kr : pos;
   c.val = d.val;
   c.exp = d.f == LC_F_CAS ? d.exp : kAny;
+  c.call = d.call;
+  c.ret = ret;
+  c.op = make_int4((int)d.call, d.val, c.exp, d.ver == -1 ? -1 : pos);
   return c;
 }
 
@@ -304,11 +327,10 @@ constexpr int kSetupBatch = 4;  // record chunks whose loads are in flight toget
 // checks the owners (two mutations on one version, two values claimed for
 // one version) and appends the optional ops.  Optional ops and gaps are
 // compacted stably through per-wave ballot words: no barrier per chunk.
-template <int T>
-__device__ int gap_setup(const GapKey &g, uint32_t cut) {
+template <int T, bool SL>
+__device__ int gap_setup(const GapKey &g, const GapWs<SL> &w, uint32_t cut) {
   const int tid = threadIdx.x, n = g.n, wv = tid / kWave, lane = tid & (kWave - 1);
   GapSh &sh = *g.sh;
-  const GapWs &w = g.ws;
   // Every wave must be done reading the previous decision's shared words
   // (sh.flag on its early-return paths, sh.maxret) before thread 0 resets
   // them: decisions follow each other without a barrier in the bisection.
@@ -328,6 +350,9 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
     sh.n_gap = 0;
   }
   __syncthreads();
+#ifdef GAP_PROFILE
+  if (tid == 0) sh.prof[0] = wall_clock64();
+#endif
   int flag = 0, maxpos = -1, maxread = -1;
   uint32_t maxret = 0;
   const int nch = (n + T - 1) / T;
@@ -346,40 +371,45 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
           pc[b] = (r > 0 && r < n) ? g.kops[r - 1].call : -1;
         }
       }
+#ifdef GAP_PROFILE
+      if (pass == 1 && c0 == 0) {
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0) sh.prof[7] = wall_clock64();
+      }
+#endif
 #pragma unroll
       for (int b = 0; b < kSetupBatch; b++) {
         const int ch = c0 + b, r = ch * T + tid;
         if (ch >= nch) break;
-        Cls c;
-        c.kind = K_NONE;
-        if (r < n) c = classify(g, raw[b], pc[b], r, cut, &flag, &maxret);
+        const Cls c = classify(g, raw[b], pc[b], r, cut, &flag, &maxret);
+        const bool rd = c.kind == K_READ, pin = c.kind == K_PIN;
+        const bool claim = rd & (c.val != -1);
         if (pass == 1) {
-          if (c.kind == K_READ) {
-            maxread = max(maxread, c.k);
-            atomicMax(&w.A[c.k], c.call + 1);
-            if (c.k > 0) atomicMin(&w.B[c.k - 1], c.ret);
-            if (c.val != -1) w.Claim[c.k] = c.val;
-          } else if (c.kind == K_PIN) {
-            atomicMax(&w.A[c.k], c.call + 1);
-            atomicMin(&w.B[c.k], c.ret);
+          maxread = rd ? max(maxread, c.k) : maxread;
+          maxpos = pin ? max(maxpos, c.k) : maxpos;
+          if (rd | pin) ws_max(&w.A[c.k], c.call + 1);
+          if (pin | (rd & (c.k > 0))) ws_min(&w.B[pin ? c.k : c.k - 1], c.ret);
+          if (claim) w.Claim[c.k] = c.val;
+          if (pin) {
             w.Pin[c.k] = r;
             w.Val[c.k] = c.val;
             w.PinExp[c.k] = c.exp;
-            maxpos = max(maxpos, c.k);
           }
           const uint64_t m = __ballot(c.kind == K_OPT);
           if (lane == 0) w.Mask[ch * (T / kWave) + wv] = m;
         } else {
-          if (c.kind == K_READ && c.val != -1 && w.Claim[c.k] != c.val)
-            flag |= F_INVALID;  // two values claimed for one version
-          else if (c.kind == K_PIN && w.Pin[c.k] != r)
-            flag |= F_INVALID;  // two mutations claim one version
+          // two values claimed for one version / two mutations on one version
+          if (claim) flag |= w.Claim[c.k] != c.val ? F_INVALID : 0;
+          if (pin) flag |= w.Pin[c.k] != r ? F_INVALID : 0;
           const int wi = ch * (T / kWave) + wv;
           if (c.kind == K_OPT) {
             const uint64_t m = w.Mask[wi];
-            w.Opt[w.Pre[wi] + lanes_below(m)] = c.op;
+            ws_st4(&w.Opt[w.Pre[wi] + lanes_below(m)], c.op);
           }
         }
+#ifdef GAP_PROFILE
+        if (pass == 1 && tid == 0) sh.prof[8 + b] = wall_clock64();
+#endif
       }
     }
     if (pass == 1) {
@@ -388,13 +418,22 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
       if (maxread >= 0) atomicMax(&sh.maxread, maxread);
       if (maxret) atomicMax(&sh.maxret, maxret);
       __syncthreads();
+#ifdef GAP_PROFILE
+    if (tid == 0) sh.prof[1] = wall_clock64();
+#endif
       if (sh.flag & (F_NA | F_INVALID)) return (sh.flag & F_NA) ? GD_NA : GD_INVALID;
-      sh.n_opt = mask_prefix<T>(w, nch * (T / kWave), sh);  // same value in every thread
+      sh.n_opt = mask_prefix<T, SL>(w, nch * (T / kWave), sh);  // same value in every thread
+#ifdef GAP_PROFILE
+    if (tid == 0) sh.prof[2] = wall_clock64();
+#endif
       flag = 0;
     }
   }
   if (flag) atomicOr(&sh.flag, flag);
   __syncthreads();
+#ifdef GAP_PROFILE
+    if (tid == 0) sh.prof[3] = wall_clock64();
+#endif
   if (sh.flag & F_INVALID) return GD_INVALID;
   const int n_opt = sh.n_opt;
   const int M = max(sh.maxpos + 1, sh.maxread);
@@ -409,6 +448,9 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
     w.Uh[k] = run;
   }
   __syncthreads();
+#ifdef GAP_PROFILE
+    if (tid == 0) sh.prof[4] = wall_clock64();
+#endif
   // fixed checks: pinned / read-only lower bounds below the deadline, and
   // the value chain around pinned positions; the requirement on each gap;
   // one ballot word of gap positions per wave chunk
@@ -442,8 +484,14 @@ __device__ int gap_setup(const GapKey &g, uint32_t cut) {
   }
   if (flag) atomicOr(&sh.flag, flag);
   __syncthreads();
+#ifdef GAP_PROFILE
+    if (tid == 0) sh.prof[5] = wall_clock64();
+#endif
   if (sh.flag & F_INVALID) return GD_INVALID;
-  const int G = mask_prefix<T>(w, mch * (T / kWave), sh);
+  const int G = mask_prefix<T, SL>(w, mch * (T / kWave), sh);
+#ifdef GAP_PROFILE
+    if (tid == 0) sh.prof[6] = wall_clock64();
+#endif
   for (int ch = 0; ch < mch; ch++) {
     const int wi = ch * (T / kWave) + wv;
     const uint64_t m = w.Mask[wi];
@@ -684,8 +732,8 @@ __device__ void set_req(const Cmp<L> &c, int gi, int v, int G, int *ff) {
 // values of free gaps that a matched CAS depends on.  Wave 0 only.  The
 // branch stack (gap, value) lives in the skeleton's Claim / Req arrays,
 // free once the compact arrays are built.
-template <bool L>
-__device__ int match_branch(const Cmp<L> &c, int G, int n_opt, int *brPos, int *brVal,
+template <bool L, class P>
+__device__ int match_branch(const Cmp<L> &c, int G, int n_opt, P brPos, P brVal,
                             int64_t *nodes) {
   const int lane = threadIdx.x & (kWave - 1);
   const int4 *gaps = c.gaps(), *ops = c.ops();
@@ -734,16 +782,15 @@ __device__ int match_branch(const Cmp<L> &c, int G, int n_opt, int *brPos, int *
 }
 
 // Decide the prefix at `cut`.  *nodes accumulates matching passes.
-template <int T>
-__device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t *nodes,
-                          int *n_gaps) {
+template <int T, bool SL>
+__device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int lds_bytes,
+                          int64_t *nodes, int *n_gaps) {
   const int tid = threadIdx.x;
   GapSh &sh = *g.sh;
-  const GapWs &w = g.ws;
 #ifdef GAP_PROFILE
   const uint64_t t0 = wall_clock64();
 #endif
-  const int st = gap_setup<T>(g, cut);
+  const int st = gap_setup<T, SL>(g, w, cut);
   if (st != GD_VALID) return st;
 #ifdef GAP_PROFILE
   const uint64_t t1 = wall_clock64();
@@ -755,7 +802,7 @@ __device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t 
   const bool in_lds = 16 * w.moff + match_lds_bytes(G, n_opt) <= lds_bytes;
   // skeleton in LDS but no room left for this matching: the caller redoes the
   // decision with the skeleton in HBM (the whole LDS then holds the matching)
-  if (w.lds && !in_lds) return GD_RETRY;
+  if (SL && !in_lds) return GD_RETRY;
   Cmp<true> cl;
   Cmp<false> cg;
   cl.ws = cg.ws = w.base;
@@ -763,29 +810,37 @@ __device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t 
   cl.n_opt = cg.n_opt = n_opt;
   cl.cap = cg.cap = (int)w.cap;
   cl.moff = cg.moff = w.moff;
-  int4 *gaps = in_lds ? cl.gaps() : cg.gaps();
-  int *mg = in_lds ? &cl.at(aMG, 0) : &cg.at(aMG, 0);
-  int *mo = in_lds ? &cl.at(aMO, 0) : &cg.at(aMO, 0);
-  int *vis = in_lds ? &cl.at(aVis, 0) : &cg.at(aVis, 0);
-  for (int gi = tid; gi < G; gi += T) {
-    const int pos = w.Gap[gi];
-    const int before =
-        pos == 0 ? g.init : (w.Pin[pos - 1] != -1 ? w.Val[pos - 1] : w.Req[pos - 1]);
-    gaps[gi] = make_int4((int)w.Uh[pos], w.Req[pos], before, pos);
-    mg[gi] = -1;
-  }
-  for (int o = tid; o < n_opt; o += T) {
-    if (in_lds) cl.ops()[o] = w.Opt[o];
-    mo[o] = -1;
-    vis[o] = 0;
-  }
+  // compact per-gap / per-op arrays, then the matching on wave 0; each
+  // placement instantiated apart so every access keeps its address space
+  auto compact = [&](const auto &c) {
+    int4 *gaps = c.gaps();
+    for (int gi = tid; gi < G; gi += T) {
+      const int pos = w.Gap[gi];
+      const int before =
+          pos == 0 ? g.init : (w.Pin[pos - 1] != -1 ? w.Val[pos - 1] : w.Req[pos - 1]);
+      gaps[gi] = make_int4((int)w.Uh[pos], w.Req[pos], before, pos);
+      c.at(aMG, gi) = -1;
+    }
+    for (int o = tid; o < n_opt; o += T) {
+      if (in_lds) c.ops()[o] = ws_ld4(&w.Opt[o]);
+      c.at(aMO, o) = -1;
+      c.at(aVis, o) = 0;
+    }
+  };
+  if (SL || in_lds)
+    compact(cl);
+  else
+    compact(cg);
   __syncthreads();
 #ifdef GAP_PROFILE
   const uint64_t t2 = wall_clock64();
 #endif
   if (tid < kWave) {
-    const int r = in_lds ? match_branch(cl, G, n_opt, w.Claim, w.Req, nodes)
-                         : match_branch(cg, G, n_opt, w.Claim, w.Req, nodes);
+    int r;
+    if (SL || in_lds)
+      r = match_branch(cl, G, n_opt, w.Claim, w.Req, nodes);
+    else
+      r = match_branch(cg, G, n_opt, w.Claim, w.Req, nodes);
     if (tid == 0) sh.res = r;
   }
   __syncthreads();
@@ -793,8 +848,15 @@ __device__ int gap_decide(const GapKey &g, uint32_t cut, int lds_bytes, int64_t 
   __syncthreads();
 #ifdef GAP_PROFILE
   if (tid == 0 && blockIdx.x < 2)
-    printf("gap_decide wg %d cut %u n %d G %d n_opt %d lds %d nodes %ld: setup %lu compact %lu match %lu (x10ns)\n",
+    printf("gap_decide wg %d cut %u n %d G %d n_opt %d lds %d nodes %ld: setup %lu [clr %lu p1 %lu (ld %lu c %lu %lu %lu %lu) pre %lu p2 %lu smin %lu chk %lu gcmp %lu] compact %lu match %lu (x10ns)\n",
            (int)blockIdx.x, cut, g.n, G, n_opt, (int)in_lds, (long)*nodes, (unsigned long)(t1 - t0),
+           (unsigned long)(sh.prof[0] - t0), (unsigned long)(sh.prof[1] - sh.prof[0]),
+           (unsigned long)(sh.prof[7] - sh.prof[0]), (unsigned long)(sh.prof[8] - sh.prof[7]),
+           (unsigned long)(sh.prof[9] - sh.prof[8]), (unsigned long)(sh.prof[10] - sh.prof[9]),
+           (unsigned long)(sh.prof[11] - sh.prof[10]),
+           (unsigned long)(sh.prof[2] - sh.prof[1]), (unsigned long)(sh.prof[3] - sh.prof[2]),
+           (unsigned long)(sh.prof[4] - sh.prof[3]), (unsigned long)(sh.prof[5] - sh.prof[4]),
+           (unsigned long)(t1 - sh.prof[5]),
            (unsigned long)(t2 - t1), (unsigned long)(wall_clock64() - t2));
 #endif
   return r;
@@ -856,12 +918,13 @@ __global__ __launch_bounds__(T) void gap_tier_kernel(
     // the skeleton goes to LDS when it fits with room for a small matching
     const int64_t capk = (end - beg + 2 + 3) & ~int64_t(3);
     const bool skel_lds = kSkelLdsBytes * capk + kMatchReserve <= job.lds_bytes;
-    g.ws = skel_lds ? gap_ws(reinterpret_cast<int32_t *>(lds_dyn), capk, true)
-                    : gap_ws(ws_hbm, cap, false);
+    const GapWs<true> ws_l = gap_ws<true>(ws_hbm, capk);
+    const GapWs<false> ws_g = gap_ws<false>(ws_hbm, cap);
     int64_t nodes = 0;
     int G = 0, G_full = 0;
-    // One decision (full / probe), or a bisection of decisions.  A single
-    // call site of gap_decide keeps the kernel's register budget in check.
+    // One decision (full / probe), or a bisection of decisions.  One call
+    // site per skeleton placement keeps the kernel's code and register budget
+    // in check.
     uint32_t lo = 0, hi = 0, cut = kNever;
     bool bis = false;  // bisecting a counterexample in this workgroup
     if (job.mode == kGapProbe)
@@ -870,12 +933,10 @@ __global__ __launch_bounds__(T) void gap_tier_kernel(
     int res = GD_SKIP;
     if (job.mode == kGapFull || cut != kNever) {
       for (;;) {
-        res = gap_decide<T>(g, cut, job.lds_bytes, &nodes, &G);
-        if (res == GD_RETRY) {  // rare: a matching larger than the LDS left
-          g.ws = gap_ws(ws_hbm, cap, false);
-          res = gap_decide<T>(g, cut, job.lds_bytes, &nodes, &G);
-          g.ws = gap_ws(reinterpret_cast<int32_t *>(lds_dyn), capk, true);
-        }
+        res = GD_RETRY;
+        if (skel_lds) res = gap_decide<T, true>(g, ws_l, cut, job.lds_bytes, &nodes, &G);
+        // skeleton in HBM; or rare: a matching larger than the LDS left
+        if (res == GD_RETRY) res = gap_decide<T, false>(g, ws_g, cut, job.lds_bytes, &nodes, &G);
         if (!bis) {
           if (job.mode != kGapFull || !job.bisect || res != GD_INVALID) break;
           bis = true;  // counterexample: the first return whose prefix fails
