@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 1
+#define LC_ABI_VERSION 2
 
 /* Op kinds: the three :f values of register.clj:98-100 (r / w / cas). */
 #define LC_F_READ  0
@@ -51,6 +51,9 @@ extern "C" {
  *  expected cas: the old value v; otherwise LC_NIL.
  *  version  the version of the :ok completion (register.clj:27,31,38-39);
  *           LC_NIL for :info ops (whose value stays the invoke's [nil ...]).
+ *           Any int64 is accepted: a version no state of the key can reach
+ *           (below init_version, above init_version + the key's op count,
+ *           beyond int32) makes the op illegal at every step, as in knossos.
  *  call     history index of the invocation.
  *  ret      history index of the completion, or LC_INF for :info/unterminated.
  *
@@ -92,7 +95,8 @@ typedef struct lc_opts {
 #define LC_REASON_NONLINEARIZABLE 1 /* frontier emptied at fail_op's return */
 #define LC_REASON_CONFIG_BUDGET   2 /* max_configs_per_key exceeded  -> :unknown */
 #define LC_REASON_WINDOW_OVERFLOW 3 /* > LC_MAX_WINDOW ops open at once -> :unknown */
-#define LC_REASON_MALFORMED       4 /* record out of range / unsorted -> :unknown, call returns -EINVAL */
+#define LC_REASON_MALFORMED       4 /* record out of range / unsorted -> this key :unknown (the call
+                                       still returns 0, as jepsen.independent loses only that key) */
 #define LC_REASON_UNKNOWN_F       5 /* f not in {read,write,cas}: model throws (register.clj:63) -> :unknown */
 #define LC_REASON_FRONTIER_LDS    6 /* internal: LDS tier overflowed (never returned when HBM retry runs) */
 #define LC_REASON_TIME_BUDGET     7 /* lc_opts.time_budget_ms exceeded by the frontier search -> :unknown */
@@ -137,22 +141,62 @@ typedef struct lc_stats {
   int64_t n_jit_keys;      /* keys decided by the JIT search */
   double  gap_kernel_ms;   /* gap-matching tier (keys the version-order tier handed over) */
   int64_t n_gap_keys;      /* keys the gap tier examined */
+  int64_t n_malformed;     /* keys left :unknown with LC_REASON_MALFORMED */
 } lc_stats;
+
+/*
+ * Optional outputs of lc_check_ex / lc_check_device_ex (NULL members are not
+ * written; memory of the same kind as ops: host for lc_check_ex, device for
+ * lc_check_device_ex).
+ *
+ *  witness       one int32 per record, indexed like ops.  For a key with
+ *                witness_kind FULL: a linearization of the whole history —
+ *                witness[r] = p >= 0 when record r is the p-th mutation
+ *                (write / successful CAS, 0-based) of the linearization, -1
+ *                when r is not linearized as a mutation (reads, which sit
+ *                between the mutations their version names, and crashed ops
+ *                left out).  For witness_kind PREFIX (invalid keys) the same
+ *                for the history prefix at event fail_prefix_end - 1: ops
+ *                called after it dropped, ops returning after it pending.
+ *                Together with the verdict this certifies a decision: the
+ *                order is checkable in O(n) by stepping the model
+ *                (register.clj:60-96) and testing real-time order
+ *                (tests/test_witness.py does exactly that, independently).
+ *  witness_kind  one int32 per key, LC_WITNESS_*.
+ */
+typedef struct lc_aux {
+  int32_t *witness;
+  int32_t *witness_kind;
+} lc_aux;
+
+#define LC_WITNESS_NONE   0  /* no witness: decided by a search tier, or :unknown */
+#define LC_WITNESS_FULL   1  /* valid key: a linearization of the whole history */
+#define LC_WITNESS_PREFIX 2  /* invalid key: a linearization of the prefix just before the failing return */
 
 typedef struct lc_ctx lc_ctx;
 
 /* Open a context on the GPUs in device_mask (bit i = HIP device i).
  * device_mask == 0 selects every visible device.  Returns 0, or -ENODEV when
- * no requested GPU is usable (there is no CPU fallback). */
+ * no requested GPU is usable (there is no CPU fallback).
+ * The environment variable LC_VIRTUAL_DEVICES=k (k >= 2) opens k independent
+ * device contexts (own stream and buffers) on the first selected GPU, so the
+ * multi-device fan-out of lc_check can be exercised on a one-GPU machine. */
 int lc_open(uint32_t device_mask, lc_ctx **out);
 
 /* Check n_keys keys.  ops/key_off/out are host memory owned by the caller;
  * key k's records are ops[key_off[k] .. key_off[k+1]).  Synchronous.
  * Keys are partitioned over the context's GPUs in contiguous cost-balanced
- * ranges.  Returns 0, -EINVAL (malformed input; per-key reasons are still
- * written), -ENOMEM, or -EIO (HIP failure); text in lc_last_error(). */
+ * ranges (lc_plan_partition).  Returns 0 (keys with malformed records are
+ * :unknown with LC_REASON_MALFORMED; the others are decided), -EINVAL
+ * (unusable arguments: null buffers, key_off not monotone, bad opts),
+ * -ENOMEM, or -EIO (HIP failure); text in lc_last_error(). */
 int lc_check(lc_ctx *ctx, const lc_op *ops, const int64_t *key_off,
              int64_t n_keys, const lc_opts *opts, lc_key_result *out);
+
+/* lc_check plus the optional outputs of `aux` (may be NULL). */
+int lc_check_ex(lc_ctx *ctx, const lc_op *ops, const int64_t *key_off,
+                int64_t n_keys, const lc_opts *opts, lc_key_result *out,
+                const lc_aux *aux);
 
 /* Same, with ops / key_off / out already resident in device memory of the
  * context's first GPU; `stream` is a hipStream_t (NULL: the context's own).
@@ -160,6 +204,12 @@ int lc_check(lc_ctx *ctx, const lc_op *ops, const int64_t *key_off,
 int lc_check_device(lc_ctx *ctx, const lc_op *d_ops, const int64_t *d_key_off,
                     int64_t n_keys, const lc_opts *opts,
                     lc_key_result *d_out, void *stream);
+
+/* lc_check_device plus the optional outputs of `aux` (device pointers; the
+ * lc_aux struct itself is host memory; may be NULL). */
+int lc_check_device_ex(lc_ctx *ctx, const lc_op *d_ops, const int64_t *d_key_off,
+                       int64_t n_keys, const lc_opts *opts, lc_key_result *d_out,
+                       void *stream, const lc_aux *aux);
 
 int lc_last_stats(lc_ctx *ctx, lc_stats *out);
 const char *lc_last_error(lc_ctx *ctx);
@@ -169,12 +219,26 @@ void lc_close(lc_ctx *ctx);
 void lc_default_opts(lc_opts *out);
 
 /* Contiguous cost-balanced partition of keys over n_parts workers (the
- * static multi-GPU split).  Writes n_parts+1 key boundaries to bounds.
- * Host-only; usable without a GPU. */
+ * static multi-GPU split).  Writes n_parts+1 key boundaries
+ * to bounds.  With ops, each key is priced by the tier that will decide it
+ * (lc_key_cost); with ops == NULL by its record count.  Host-only; usable
+ * without a GPU. */
 int lc_plan_partition(const lc_op *ops, const int64_t *key_off, int64_t n_keys,
                       int32_t n_parts, int64_t *bounds);
 
+/* Estimated device cost of each key, in record-scan units (a record the
+ * version-order tier decides costs 1).  Calibrated from measured tier times
+ * (DESIGN.md §7): a key with crashed writes/CAS goes to the gap tier, one
+ * with version-less :ok mutations to the frontier search, whose cost grows
+ * with the number of concurrently open ops and crashed ops.  costs[n_keys]. */
+int lc_key_cost(const lc_op *ops, const int64_t *key_off, int64_t n_keys, double *costs);
+
 int lc_abi_version(void);
+
+/* Hash of the sources the library was built from (hex string); callers that
+ * build the library from a source tree compare it against the tree's own
+ * hash to refuse a stale binary. */
+const char *lc_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,8 @@
  * Crashed writes/CAS become :info (ret = LC_INF) and take effect with p = 0.5;
  * the crashed process is replaced by a fresh one (Jepsen process semantics).
  *
+ * With info_frac, the crash count is made exact (see lc_synth_params).
+ *
  * Anomalies (p_anomaly per key): a stale read (a read reports the state before
  * a mutation that returned before the read was invoked) or a lost CAS (a CAS
  * reported :ok whose effect never reaches the register).
@@ -35,6 +37,12 @@ typedef struct lc_synth_params {
   double   p_info;       /* P(a write/cas crashes -> :info) */
   double   p_anomaly;    /* P(a key gets one injected anomaly) */
   uint64_t seed;
+  double   info_frac;    /* > 0: exactly round(info_frac * ops_per_key) of a key's
+                            records are crashed writes/CAS (BASELINE configs[3]:
+                            20 %).  After the p_info crashes, uniformly chosen :ok
+                            writes/CAS are reported :info instead (a client timeout
+                            on an op that took effect; its process is replaced),
+                            which keeps the history linearizable.  0: off. */
 } lc_synth_params;
 
 /* Labels written per key by lc_synth_register. */

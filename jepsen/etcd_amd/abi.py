@@ -2,9 +2,12 @@
 
 This is the build's own library, loaded in-process.  It exposes the GPU
 checker (lc_*) and the seeded synthetic-history generator (lc_synth_*).
-Loading fails loudly when the HIP library is missing: there is no fallback.
+Loading fails loudly when the HIP library is missing, and when it was built
+from other sources than the tree it is loaded from (lc_build_id() against
+csrc/build_id.py): there is no fallback and no stale binary.
 """
 import ctypes
+import importlib.util
 import os
 
 import numpy as np
@@ -36,6 +39,7 @@ LC_REASON_UNKNOWN_F = 5
 LC_FLAG_NO_HBM_RETRY = 1
 LC_FLAG_NO_FAST_PATH = 2
 LC_FLAG_NO_GAP_TIER = 4
+LC_WITNESS_NONE, LC_WITNESS_FULL, LC_WITNESS_PREFIX = 0, 1, 2
 
 # lc_op: 6 x int64 (f, value, expected, version, call, ret); arrays are (n, 6).
 OP_FIELDS = ("f", "value", "expected", "version", "call", "ret")
@@ -59,28 +63,59 @@ class LcStats(ctypes.Structure):
                 ("n_ops", ctypes.c_int64), ("n_hbm_keys", ctypes.c_int64),
                 ("n_devices", ctypes.c_int64), ("fast_kernel_ms", ctypes.c_double),
                 ("jit_kernel_ms", ctypes.c_double), ("n_jit_keys", ctypes.c_int64),
-                ("gap_kernel_ms", ctypes.c_double), ("n_gap_keys", ctypes.c_int64)]
+                ("gap_kernel_ms", ctypes.c_double), ("n_gap_keys", ctypes.c_int64),
+                ("n_malformed", ctypes.c_int64)]
+
+
+class LcAux(ctypes.Structure):
+    _fields_ = [("witness", ctypes.c_void_p), ("witness_kind", ctypes.c_void_p)]
 
 
 class LcSynthParams(ctypes.Structure):
     _fields_ = [("n_keys", ctypes.c_int64), ("ops_per_key", ctypes.c_int64),
                 ("concurrency", ctypes.c_int32), ("n_values", ctypes.c_int32),
                 ("p_info", ctypes.c_double), ("p_anomaly", ctypes.c_double),
-                ("seed", ctypes.c_uint64)]
+                ("seed", ctypes.c_uint64), ("info_frac", ctypes.c_double)]
 
 
 _lib = None
 
 
+def source_build_id():
+    """Hash of the csrc/ + include/ sources in this tree (csrc/build_id.py)."""
+    spec = importlib.util.spec_from_file_location(
+        "lincheck_build_id", os.path.join(_HERE, "csrc", "build_id.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.build_id()
+
+
 def lib():
-    """Load liblincheck.so once; raise if it has not been built."""
+    """Load liblincheck.so once; raise if it has not been built, or was built
+    from sources other than this tree's."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(
                 "liblincheck.so not built (%s); run `python -c 'import "
                 "__graft_entry__ as g; g.build()'` — there is no CPU fallback" % LIB_PATH)
+        # torch ships its own HIP runtime (torch/lib/libamdhip64.so) next to
+        # the system one this library links; torch only initialises its GPU
+        # if it is loaded first, so load it first whenever it is installed
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
+        L.lc_build_id.argtypes = []
+        L.lc_build_id.restype = ctypes.c_char_p
+        built = L.lc_build_id().decode()
+        if not os.environ.get("LINCHECK_LIB"):  # dev A/B builds are other sources on purpose
+            want = source_build_id()
+            if built != want:
+                raise RuntimeError(
+                    "stale liblincheck.so: built from sources %s, this tree is %s; rebuild "
+                    "(make -C jepsen/etcd_amd/csrc)" % (built, want))
         p, i64, i32, u32, vp = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                 ctypes.c_uint32, ctypes.c_void_p)
         L.lc_open.argtypes = [u32, ctypes.POINTER(vp)]
@@ -89,6 +124,13 @@ def lib():
         L.lc_check.restype = ctypes.c_int
         L.lc_check_device.argtypes = [vp, vp, vp, i64, ctypes.POINTER(LcOpts), vp, vp]
         L.lc_check_device.restype = ctypes.c_int
+        L.lc_check_ex.argtypes = [vp, p, p, i64, ctypes.POINTER(LcOpts), p, ctypes.POINTER(LcAux)]
+        L.lc_check_ex.restype = ctypes.c_int
+        L.lc_check_device_ex.argtypes = [vp, vp, vp, i64, ctypes.POINTER(LcOpts), vp, vp,
+                                         ctypes.POINTER(LcAux)]
+        L.lc_check_device_ex.restype = ctypes.c_int
+        L.lc_key_cost.argtypes = [p, p, i64, p]
+        L.lc_key_cost.restype = ctypes.c_int
         L.lc_last_stats.argtypes = [vp, ctypes.POINTER(LcStats)]
         L.lc_last_stats.restype = ctypes.c_int
         L.lc_last_error.argtypes = [vp]
@@ -176,26 +218,41 @@ class Context:
         lib().lc_last_stats(self._h, ctypes.byref(s))
         return s
 
-    def check(self, ops, key_off, opts=None, raise_on_error=True):
-        """Host-buffer check. Returns (rc, results structured array)."""
+    def check(self, ops, key_off, opts=None, raise_on_error=True, witness=False):
+        """Host-buffer check. Returns (rc, results structured array), or with
+        witness=True (rc, results, witness per record, witness kind per key)
+        from lc_check_ex (include/lincheck.h, lc_aux)."""
         ops = as_ops(ops)
         key_off = np.ascontiguousarray(key_off, dtype=np.int64)
         n_keys = len(key_off) - 1
         out = np.zeros(max(n_keys, 0), dtype=RESULT_DTYPE)
         o = opts if opts is not None else default_opts()
-        rc = lib().lc_check(self._h, _ptr(ops), _ptr(key_off), n_keys,
-                            ctypes.byref(o), _ptr(out))
+        if witness:
+            wit = np.full(len(ops), -3, dtype=np.int32)
+            kind = np.full(max(n_keys, 0), -3, dtype=np.int32)
+            aux = LcAux(wit.ctypes.data, kind.ctypes.data)
+            rc = lib().lc_check_ex(self._h, _ptr(ops), _ptr(key_off), n_keys,
+                                   ctypes.byref(o), _ptr(out), ctypes.byref(aux))
+        else:
+            rc = lib().lc_check(self._h, _ptr(ops), _ptr(key_off), n_keys,
+                                ctypes.byref(o), _ptr(out))
         if rc != 0 and raise_on_error:
             raise LcError(rc, self.last_error())
-        return rc, out
+        return (rc, out, wit, kind) if witness else (rc, out)
 
-    def check_device(self, d_ops, d_key_off, n_keys, d_out, stream=None, opts=None):
-        """Device-pointer check (ints), e.g. from torch tensors' data_ptr()."""
+    def check_device(self, d_ops, d_key_off, n_keys, d_out, stream=None, opts=None,
+                     d_witness=None, d_witness_kind=None):
+        """Device-pointer check (ints), e.g. from torch tensors' data_ptr();
+        with d_witness / d_witness_kind (device pointers) lc_check_device_ex."""
         o = opts if opts is not None else default_opts()
-        rc = lib().lc_check_device(self._h, ctypes.c_void_p(d_ops),
-                                   ctypes.c_void_p(d_key_off), n_keys,
-                                   ctypes.byref(o), ctypes.c_void_p(d_out),
-                                   ctypes.c_void_p(stream) if stream else None)
+        args = (self._h, ctypes.c_void_p(d_ops), ctypes.c_void_p(d_key_off), n_keys,
+                ctypes.byref(o), ctypes.c_void_p(d_out),
+                ctypes.c_void_p(stream) if stream else None)
+        if d_witness is not None:
+            aux = LcAux(d_witness, d_witness_kind)
+            rc = lib().lc_check_device_ex(*args, ctypes.byref(aux))
+        else:
+            rc = lib().lc_check_device(*args)
         if rc != 0:
             raise LcError(rc, self.last_error())
         return rc
@@ -227,27 +284,44 @@ class Context:
         return call
 
 
-def plan_partition(key_off, n_parts):
+def plan_partition(key_off, n_parts, ops=None):
+    """lc_plan_partition: n_parts+1 key bounds at equal estimated cost (by
+    lc_key_cost with ops; by record count without)."""
     key_off = np.ascontiguousarray(key_off, dtype=np.int64)
+    if ops is not None:
+        ops = as_ops(ops)
     bounds = np.zeros(n_parts + 1, dtype=np.int64)
-    rc = lib().lc_plan_partition(None, _ptr(key_off), len(key_off) - 1, n_parts,
+    rc = lib().lc_plan_partition(_ptr(ops), _ptr(key_off), len(key_off) - 1, n_parts,
                                  _ptr(bounds))
     if rc != 0:
         raise LcError(rc, "lc_plan_partition")
     return bounds
 
 
+def key_cost(ops, key_off):
+    """lc_key_cost: estimated device cost per key (record-scan units)."""
+    ops = as_ops(ops)
+    key_off = np.ascontiguousarray(key_off, dtype=np.int64)
+    out = np.zeros(len(key_off) - 1, dtype=np.float64)
+    rc = lib().lc_key_cost(_ptr(ops), _ptr(key_off), len(out), _ptr(out))
+    if rc != 0:
+        raise LcError(rc, "lc_key_cost")
+    return out
+
+
 def synth_params(n_keys, ops_per_key, concurrency=10, n_values=5, p_info=0.0,
-                 p_anomaly=0.0, seed=0x5EED0000):
+                 p_anomaly=0.0, seed=0x5EED0000, info_frac=0.0):
     return LcSynthParams(n_keys, ops_per_key, concurrency, n_values, p_info,
-                         p_anomaly, seed)
+                         p_anomaly, seed, info_frac)
 
 
 def synth(n_keys, ops_per_key, concurrency=10, n_values=5, p_info=0.0,
-          p_anomaly=0.0, seed=0x5EED0000, n_threads=None):
-    """Packed synthetic histories: (ops (n,6) int64, key_off, labels, n_invocations)."""
+          p_anomaly=0.0, seed=0x5EED0000, n_threads=None, info_frac=0.0):
+    """Packed synthetic histories: (ops (n,6) int64, key_off, labels, n_invocations).
+    info_frac > 0 makes exactly round(info_frac * ops_per_key) records of
+    every key crashed writes/CAS (include/lincheck_synth.h)."""
     prm = synth_params(n_keys, ops_per_key, concurrency, n_values, p_info,
-                       p_anomaly, seed)
+                       p_anomaly, seed, info_frac)
     ops = np.zeros((n_keys * ops_per_key, 6), dtype=np.int64)
     key_off = np.zeros(n_keys + 1, dtype=np.int64)
     labels = np.zeros(n_keys, dtype=np.int32)
@@ -262,9 +336,10 @@ def synth(n_keys, ops_per_key, concurrency=10, n_values=5, p_info=0.0,
 
 
 def synth_key(key, ops_per_key, concurrency=10, n_values=5, p_info=0.0,
-              p_anomaly=0.0, seed=0x5EED0000):
+              p_anomaly=0.0, seed=0x5EED0000, info_frac=0.0):
     """One key's full op stream incl. :fail: (ops, proc, status, label)."""
-    prm = synth_params(1, ops_per_key, concurrency, n_values, p_info, p_anomaly, seed)
+    prm = synth_params(1, ops_per_key, concurrency, n_values, p_info, p_anomaly, seed,
+                       info_frac)
     n = ctypes.c_int64(0)
     lab = ctypes.c_int32(0)
     cap = 4 * ops_per_key + 64

@@ -1056,6 +1056,10 @@ __device__ __forceinline__ void fast_tier_handoff(int64_t key, int32_t *flags, K
   if (__hip_atomic_load(&status->any_handoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
     __hip_atomic_store(&status->any_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(h_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // wait until the host can see it: the host reads the flag after an
+    // event created without a system-scope fence (lincheck.cpp), so the
+    // writer, not the event, makes the store visible before the kernel ends
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
   }
 }
 
@@ -1359,7 +1363,7 @@ constexpr int kCompactThreads = 256;
 __global__ __launch_bounds__(kCompactThreads) void handoff_compact_kernel(
     int32_t *__restrict__ flags, const int64_t *__restrict__ key_off, const int64_t n_keys,
     const int route_direct, int32_t *__restrict__ jit_keys, int32_t *__restrict__ direct_keys,
-    KStatus *__restrict__ status) {
+    KStatus *__restrict__ status, int32_t *__restrict__ witness_kind) {
   __shared__ int wg[kCompactThreads / kWave], wd[kCompactThreads / kWave];
   __shared__ int base_g, base_d;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
@@ -1370,7 +1374,10 @@ __global__ __launch_bounds__(kCompactThreads) void handoff_compact_kernel(
     int f = 0;
     if (k < n_keys) {
       f = flags[k];
-      if (f) flags[k] = 0;
+      if (f) {
+        flags[k] = 0;
+        if (witness_kind) witness_kind[k] = LC_WITNESS_NONE;
+      }
     }
     const bool dir = f == 2 && route_direct;
     const bool gap = f != 0 && !dir;
@@ -1465,15 +1472,44 @@ __global__ __launch_bounds__(NW * kWave) void hbm_coop_kernel(
   }
 }
 
+// Version-order witnesses (lc_aux): a record's pinned mutation position, or
+// -1.  Grid-stride over the records, then over the keys for their kind.
+__global__ __launch_bounds__(256) void witness_init_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off, const int64_t n_keys,
+    const int64_t n_records, const int32_t V0, const int fast_on, int32_t *__restrict__ wit,
+    int32_t *__restrict__ kind) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_records; r += stride) {
+    const lc_op o = ops[r];
+    const bool pinned = (o.f == LC_F_WRITE || o.f == LC_F_CAS) && o.ret != kInf &&
+                        o.version > (int64_t)V0 && o.version - V0 - 1 < (int64_t)INT_MAX;
+    wit[r] = pinned ? (int32_t)(o.version - V0 - 1) : -1;
+  }
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_keys; k += stride)
+    kind[k] = fast_on ? LC_WITNESS_FULL : LC_WITNESS_NONE;
+}
+
 }  // namespace
 
 hipError_t launch_handoff_compact(int32_t *d_flags, const int64_t *d_key_off, int64_t n_keys,
                                   int route_direct, int32_t *d_jit_keys, int32_t *d_direct_keys,
-                                  KStatus *d_status, hipStream_t stream) {
+                                  KStatus *d_status, int32_t *d_witness_kind, hipStream_t stream) {
   if (n_keys <= 0) return hipSuccess;
   const int64_t wgs = std::min<int64_t>((n_keys + kCompactThreads - 1) / kCompactThreads, 1024);
   hipLaunchKernelGGL(handoff_compact_kernel, dim3((unsigned)wgs), dim3(kCompactThreads), 0, stream,
-                     d_flags, d_key_off, n_keys, route_direct, d_jit_keys, d_direct_keys, d_status);
+                     d_flags, d_key_off, n_keys, route_direct, d_jit_keys, d_direct_keys, d_status,
+                     d_witness_kind);
+  return hipGetLastError();
+}
+
+hipError_t launch_witness_init(const lc_op *d_ops, const int64_t *d_key_off, int64_t n_keys,
+                               int64_t n_records, const KParams &p, int fast_on,
+                               int32_t *d_witness, int32_t *d_witness_kind, hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  const int64_t work = std::max(n_records, n_keys);
+  const int64_t wgs = std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 8192));
+  hipLaunchKernelGGL(witness_init_kernel, dim3((unsigned)wgs), dim3(256), 0, stream, d_ops,
+                     d_key_off, n_keys, n_records, p.init_ver, fast_on, d_witness, d_witness_kind);
   return hipGetLastError();
 }
 

@@ -79,7 +79,7 @@ extern __shared__ int4 lds_dyn[];
 
 // Per-workgroup workspace: kGapArrays arrays of `cap` 32-bit entries (cap a
 // multiple of 4, so the 16-byte record regions stay aligned).
-//   0 A  1 B  2 Uh  3 Pin  4 Val  5 PinExp  6 Claim  7 Req  8 (spare)  9 Gap
+//   0 A  1 B  2 Uh  3 Pin  4 Val  5 PinExp  6 Claim  7 Req  8 OptRec  9 Gap
 //   10..13 Opt: the optional ops as 16-byte records (call, value, exp, pos)
 //   14..17 gap records, 18..23 the matching's scalar arrays — the HBM homes
 //   of the matching when it does not fit in LDS; during gap_setup 18..23
@@ -106,6 +106,7 @@ struct GapWs {
   int moff;        // int4 offset of the matching's LDS region in lds_dyn (SL)
   WsP<SL, uint32_t> A, B, Uh;
   WsP<SL, int> Pin, Val, PinExp, Claim, Req, Gap;
+  WsP<SL, int> OptRec;     // record index of each optional op (witnesses)
   WsP<SL, int4> Opt;
   WsP<SL, uint64_t> Mask;  // compaction ballots
   WsP<SL, int> Pre;        // compaction prefix counts
@@ -141,6 +142,7 @@ __device__ __forceinline__ GapWs<SL> gap_ws(int32_t *base, int64_t cap) {
   w.Claim = P(6);
   w.Req = P(7);
   w.Gap = P(9);
+  w.OptRec = P(8);
   w.Opt = (WsP<SL, int4>)P(10);
   w.Mask = (WsP<SL, uint64_t>)P(SL ? 14 : 18);
   w.Pre = P(SL ? 16 : 20);
@@ -404,7 +406,9 @@ __device__ int gap_setup(const GapKey &g, const GapWs<SL> &w, uint32_t cut) {
           const int wi = ch * (T / kWave) + wv;
           if (c.kind == K_OPT) {
             const uint64_t m = w.Mask[wi];
-            ws_st4(&w.Opt[w.Pre[wi] + lanes_below(m)], c.op);
+            const int o = w.Pre[wi] + lanes_below(m);
+            ws_st4(&w.Opt[o], c.op);
+            w.OptRec[o] = r;
           }
         }
 #ifdef GAP_PROFILE
@@ -781,10 +785,31 @@ __device__ int match_branch(const Cmp<L> &c, int G, int n_opt, P brPos, P brVal,
   }
 }
 
-// Decide the prefix at `cut`.  *nodes accumulates matching passes.
+// The linearization a valid decision found (lc_aux witness): every record of
+// the key -1, then each pinned position's record and each gap's matched op
+// their position.  The matched pairs come from the matching's arrays (gap
+// gi -> op aMG[gi] -> record OptRec[op]); with no gaps only the pins.
+template <int T, bool SL, class C>
+__device__ void gap_witness(const GapKey &g, const GapWs<SL> &w, const C *c, int G,
+                            int32_t *__restrict__ wk) {
+  const int tid = threadIdx.x;
+  for (int r = tid; r < g.n; r += T) wk[r] = -1;
+  __syncthreads();  // the -1 stores before the positions (same addresses)
+  for (int k = tid; k <= g.n; k += T) {
+    const int r = w.Pin[k];
+    if (r != -1) wk[r] = k;
+  }
+  if (c)
+    for (int gi = tid; gi < G; gi += T) wk[w.OptRec[c->at(aMG, gi)]] = c->gaps()[gi].w;
+  __syncthreads();
+}
+
+// Decide the prefix at `cut`.  *nodes accumulates matching passes.  With wk
+// (this key's witness records), a valid decision also writes its
+// linearization (gap_witness).
 template <int T, bool SL>
 __device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int lds_bytes,
-                          int64_t *nodes, int *n_gaps) {
+                          int64_t *nodes, int *n_gaps, int32_t *wk) {
   const int tid = threadIdx.x;
   GapSh &sh = *g.sh;
 #ifdef GAP_PROFILE
@@ -797,7 +822,10 @@ __device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int
 #endif
   const int G = sh.n_gap, n_opt = sh.n_opt;
   *n_gaps = G;
-  if (G == 0) return GD_VALID;
+  if (G == 0) {
+    if (wk) gap_witness<T, SL, Cmp<true>>(g, w, nullptr, 0, wk);
+    return GD_VALID;
+  }
   if (G > n_opt) return GD_INVALID;
   const bool in_lds = 16 * w.moff + match_lds_bytes(G, n_opt) <= lds_bytes;
   // skeleton in LDS but no room left for this matching: the caller redoes the
@@ -846,6 +874,12 @@ __device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int
   __syncthreads();
   const int r = sh.res;
   __syncthreads();
+  if (wk && r == GD_VALID) {
+    if (SL || in_lds)
+      gap_witness<T, SL>(g, w, &cl, G, wk);
+    else
+      gap_witness<T, SL>(g, w, &cg, G, wk);
+  }
 #ifdef GAP_PROFILE
   if (tid == 0 && blockIdx.x < 2)
     printf("gap_decide wg %d cut %u n %d G %d n_opt %d lds %d nodes %ld: setup %lu [clr %lu p1 %lu (ld %lu c %lu %lu %lu %lu) pre %lu p2 %lu smin %lu chk %lu gcmp %lu] compact %lu match %lu (x10ns)\n",
@@ -920,26 +954,42 @@ __global__ __launch_bounds__(T) void gap_tier_kernel(
     const bool skel_lds = kSkelLdsBytes * capk + kMatchReserve <= job.lds_bytes;
     const GapWs<true> ws_l = gap_ws<true>(ws_hbm, capk);
     const GapWs<false> ws_g = gap_ws<false>(ws_hbm, cap);
-    int64_t nodes = 0;
+    int64_t nodes = 0, wnodes = 0;
     int G = 0, G_full = 0;
-    // One decision (full / probe), or a bisection of decisions.  One call
-    // site per skeleton placement keeps the kernel's code and register budget
-    // in check.
+    // this key's witness records (lc_aux), when witnesses are wanted
+    int32_t *const kwit = job.wit ? job.wit + (beg - key_base) : nullptr;
+    // One decision (full / probe / witness), or a bisection of decisions,
+    // then with witnesses one more decision on the prefix before the failing
+    // return.  One call site per skeleton placement keeps the kernel's code
+    // and register budget in check.
     uint32_t lo = 0, hi = 0, cut = kNever;
-    bool bis = false;  // bisecting a counterexample in this workgroup
+    bool bis = false;    // bisecting a counterexample in this workgroup
+    bool wpass = false;  // the decision that writes an invalid key's witness
+    int32_t *wk = job.mode == kGapFull ? kwit : nullptr;
     if (job.mode == kGapProbe)
       cut = job.cex_state[ci] ? kNever
                               : probe_cut(job.cex_lo[ci], job.cex_hi[ci], t - ci * job.P, job.P);
-    int res = GD_SKIP;
+    if (job.mode == kGapWitness) {  // a counterexample the multisection closed
+      cut = (job.cex_state[ci] == 1 && job.cex_lo[ci] > 0) ? job.cex_lo[ci] - 1 : kNever;
+      wk = kwit;
+    }
+    int res = GD_SKIP, wres = GD_SKIP;
     if (job.mode == kGapFull || cut != kNever) {
       for (;;) {
+        int64_t *const nd = wpass || job.mode == kGapWitness ? &wnodes : &nodes;
         res = GD_RETRY;
-        if (skel_lds) res = gap_decide<T, true>(g, ws_l, cut, job.lds_bytes, &nodes, &G);
+        if (skel_lds) res = gap_decide<T, true>(g, ws_l, cut, job.lds_bytes, nd, &G, wk);
         // skeleton in HBM; or rare: a matching larger than the LDS left
-        if (res == GD_RETRY) res = gap_decide<T, false>(g, ws_g, cut, job.lds_bytes, &nodes, &G);
+        if (res == GD_RETRY) res = gap_decide<T, false>(g, ws_g, cut, job.lds_bytes, nd, &G, wk);
+        if (wpass) {
+          wres = res;
+          res = GD_INVALID;
+          break;
+        }
         if (!bis) {
           if (job.mode != kGapFull || !job.bisect || res != GD_INVALID) break;
           bis = true;  // counterexample: the first return whose prefix fails
+          wk = nullptr;
           G_full = G;
           lo = 0;
           hi = sh.maxret;
@@ -952,7 +1002,11 @@ __global__ __launch_bounds__(T) void gap_tier_kernel(
         }
         if (lo >= hi) {
           res = GD_INVALID;
-          break;
+          if (!kwit || lo == 0) break;
+          wpass = true;  // the prefix just before the failing return, with its witness
+          wk = kwit;
+          cut = lo - 1;
+          continue;
         }
         cut = lo + (hi - lo) / 2;
       }
@@ -964,16 +1018,19 @@ __global__ __launch_bounds__(T) void gap_tier_kernel(
         if (fail_op < 0) res = GD_NA;  // not a return: cannot happen
       }
       if (threadIdx.x == 0) {
-        if (res == GD_INVALID)
+        if (res == GD_INVALID) {
           out[key] = lc_key_result{LC_INVALID, LC_REASON_NONLINEARIZABLE, fail_op,
                                    g.base + (int64_t)lo, nodes, G_full};
-        else
+          if (kwit) job.wkind[key] = wres == GD_VALID ? LC_WITNESS_PREFIX : LC_WITNESS_NONE;
+        } else {
           pass_keys[atomicAdd(&status->n_jit2, 1)] = (int32_t)key;
+        }
       }
     } else if (job.mode == kGapFull) {
       if (threadIdx.x == 0) {
         if (res == GD_VALID) {
           out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, nodes, G};
+          if (kwit) job.wkind[key] = LC_WITNESS_FULL;
         } else if (res == GD_INVALID) {
           const int i = atomicAdd(&status->n_cex, 1);
           job.cex_key[i] = (int32_t)key;
@@ -987,6 +1044,9 @@ __global__ __launch_bounds__(T) void gap_tier_kernel(
           pass_keys[atomicAdd(&status->n_jit2, 1)] = (int32_t)key;
         }
       }
+    } else if (job.mode == kGapWitness) {
+      if (threadIdx.x == 0 && cut != kNever)
+        job.wkind[key] = res == GD_VALID ? LC_WITNESS_PREFIX : LC_WITNESS_NONE;
     } else {  // kGapProbe
       if (threadIdx.x == 0) {
         job.probe[t] = res;
@@ -1030,9 +1090,11 @@ __global__ __launch_bounds__(kWave) void gap_narrow_kernel(
   const int64_t beg = key_off[key], end = key_off[key + 1];
   const lc_op *kops = ops + (beg - key_off[0]);
   // prefix-closed: every linearizable cut lies below every failing one
-  if (na || good_hi > min_bad) {
+  // (give_up: the rounds did not converge; cannot happen with P >= 2 probes
+  // per interval, but the JIT tier decides the key rather than the call fail)
+  if (na || good_hi > min_bad || (job.give_up && good_hi < min_bad)) {
     if (lane == 0) {
-      job.cex_state[ci] = 1;
+      job.cex_state[ci] = 2;
       pass_keys[atomicAdd(&status->n_jit2, 1)] = (int32_t)key;
     }
     return;
@@ -1052,7 +1114,7 @@ __global__ __launch_bounds__(kWave) void gap_narrow_kernel(
     if (kops[r].ret == at) fo = min(fo, r);
   fo = wave_min_i32(fo);
   if (lane == 0) {
-    job.cex_state[ci] = 1;
+    job.cex_state[ci] = fo == INT_MAX ? 2 : 1;
     job.cex_lo[ci] = job.cex_hi[ci] = min_bad;
     if (fo == INT_MAX)
       pass_keys[atomicAdd(&status->n_jit2, 1)] = (int32_t)key;

@@ -56,9 +56,20 @@ hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_flags,
                             KStatus *d_status, int32_t *h_handoff, hipStream_t stream);
+// With witness_kind, every handed-over key's kind is reset to
+// LC_WITNESS_NONE (a later tier that certifies it sets it again).
 hipError_t launch_handoff_compact(int32_t *d_flags, const int64_t *d_key_off, int64_t n_keys,
                                   int route_direct, int32_t *d_jit_keys, int32_t *d_direct_keys,
-                                  KStatus *d_status, hipStream_t stream);
+                                  KStatus *d_status, int32_t *d_witness_kind, hipStream_t stream);
+
+// Witness (lc_aux) for the keys the version-order tier decides: their
+// linearization is the version order itself, so every record gets its
+// pinned position (an :ok write/CAS with version v: v - V0 - 1; everything
+// else -1) and every key kind LC_WITNESS_FULL (fast_on) or NONE.  Launched
+// before the tiers; later tiers overwrite the keys they take.
+hipError_t launch_witness_init(const lc_op *d_ops, const int64_t *d_key_off, int64_t n_keys,
+                               int64_t n_records, const KParams &p, int fast_on,
+                               int32_t *d_witness, int32_t *d_witness_kind, hipStream_t stream);
 
 // LDS tier (JIT search): one wavefront per key, for the keys in d_keys
 // (n_keys of them), or for keys 0..n_keys-1 when d_keys is null.  In every
@@ -110,21 +121,31 @@ hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
 //              of closed ones.  Rounds repeat until none is open: a single
 //              hot key (BASELINE configs[3]) spreads over the whole GPU.
 // Workspace: gap_tier_ws_bytes(n_wg, cap) with cap >= longest key + 2.
-enum { kGapFull = 0, kGapProbe = 1 };
+//   kGapWitness  (lc_aux witnesses only) one workgroup per counterexample
+//              closed by the multisection re-decides the prefix just before
+//              the failing return and writes its linearization.
+// With `wit`, every valid full decision writes its linearization (the
+// mutation position of each record, lc_aux) and sets wkind[key] =
+// LC_WITNESS_FULL; an invalid key bisected in place gets the witness of
+// the prefix before its failing return (LC_WITNESS_PREFIX).
+enum { kGapFull = 0, kGapProbe = 1, kGapWitness = 2 };
 struct GapJob {
-  int32_t mode;        // kGapFull / kGapProbe
+  int32_t mode;        // kGapFull / kGapProbe / kGapWitness
   int32_t bisect;      // kGapFull: bisect invalid keys in place
-  int32_t P;           // probes per interval (kGapProbe)
+  int32_t P;           // probes per interval (kGapProbe; 1 for kGapWitness)
   int32_t lds_bytes;   // dynamic LDS per workgroup for the matching arrays
   int32_t threads;     // workgroup size: 256, or 64 for short keys (one wave per decision)
-  int32_t n_tasks;     // keys (full), intervals x P (probe)
+  int32_t n_tasks;     // keys (full), intervals x P (probe), intervals (witness)
+  int32_t give_up;     // launch_gap_narrow: pass every open interval on to the JIT tier
   int32_t *cex_key;    // per counterexample: the key
   uint32_t *cex_lo;    // key-relative event interval [lo, hi] holding the
   uint32_t *cex_hi;    //   first return whose prefix is not linearizable
   int32_t *cex_gaps;   // gaps of the full history (reported as max_frontier)
-  int32_t *cex_state;  // 0 open, 1 closed
+  int32_t *cex_state;  // 0 open, 1 closed (decided invalid), 2 passed on to the JIT tier
   int64_t *cex_nodes;  // matching passes spent on the key
   int32_t *probe;      // [n_cex * P] probe verdicts
+  int32_t *wit;        // lc_aux witness (per record, indexed like the ops), or null
+  int32_t *wkind;      // lc_aux witness kind (per key)
 };
 size_t gap_tier_ws_bytes(int n_wg, int64_t cap);
 hipError_t launch_gap_tier(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,

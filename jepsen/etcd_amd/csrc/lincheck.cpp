@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,6 +29,10 @@
 #include "../../../include/lincheck.h"
 #include "kernels.h"
 
+#ifndef LC_BUILD_ID
+#define LC_BUILD_ID "unknown"
+#endif
+
 namespace {
 
 constexpr int64_t kDefaultBudget = 1 << 24;   // configurations per key
@@ -37,7 +42,10 @@ constexpr int64_t kDefaultBudget = 1 << 24;   // configurations per key
 // lane-parallel expansion is latency-bound per wave).
 // Timing events.  LC_EVENT_FLAGS (dev A/B): hipEventDisableSystemFence skips
 // the event's own system-scope fence (cache writeback + invalidate) when it
-// is recorded; kernel completion already releases the kernel's writes.
+// is recorded; kernel completion already releases the kernel's writes to
+// device memory, and the one host-visible word the host reads after such an
+// event (h_handoff) is made visible by its writer with a system-scope fence
+// (fast_tier_handoff, check_kernel.hip).
 #ifndef LC_EVENT_FLAGS
 #define LC_EVENT_FLAGS hipEventDisableSystemFence
 #endif
@@ -106,6 +114,10 @@ struct Dev {
   bool status_dirty = true;             // d_status may be non-zero
   void *d_ws = nullptr;
   size_t ws_cap = 0;
+  int32_t *d_wit = nullptr;            // lc_check_ex: device copies of the lc_aux outputs
+  size_t wit_cap = 0;
+  int32_t *d_kind = nullptr;
+  size_t kind_cap = 0;
   double kernel_ms = 0, hbm_ms = 0;
   int64_t n_hbm = 0;
   int malformed = 0;
@@ -176,10 +188,18 @@ int opts_to_params(lc_ctx *c, const lc_opts *o, lcdev::KParams *p) {
   return 0;
 }
 
-// Run both tiers for n_keys keys whose device arrays are in place.
+// Device-side lc_aux outputs of one run_device call (null: not wanted).
+struct WitOut {
+  int32_t *wit = nullptr;   // per record, indexed like d_ops
+  int32_t *kind = nullptr;  // per key
+  int64_t n_records = 0;
+};
+
+// Run the tiers for n_keys keys whose device arrays are in place.
 int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                int64_t n_keys, const lcdev::KParams &p,
-               lc_key_result *d_out, hipStream_t st, int64_t flags) {
+               lc_key_result *d_out, hipStream_t st, int64_t flags,
+               const WitOut &wo = WitOut()) {
   d.kernel_ms = d.hbm_ms = d.fast_ms = d.jit_ms = d.gap_ms = 0;
   d.n_hbm = d.n_jit = d.n_gap = 0;
   d.malformed = 0;
@@ -210,6 +230,10 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   float ms = 0;
   int64_t n_jit = n_keys;
   const int32_t *jit_list = nullptr;
+  const bool want_wit = wo.wit && wo.kind;
+  if (want_wit)  // the version order is the witness of every key the fast tier decides
+    HIP_TRY(c, lcdev::launch_witness_init(d_ops, d_off, n_keys, wo.n_records, p,
+                                          !(flags & LC_FLAG_NO_FAST_PATH), wo.wit, wo.kind, st));
   HIP_TRY(c, hipEventRecord(d.e0, st));
   if (!(flags & LC_FLAG_NO_FAST_PATH)) {
     // tier 0: version-order decision for every key; the rest go to the JIT.
@@ -224,7 +248,8 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     n_jit = 0;
     if (__atomic_load_n(d.h_handoff, __ATOMIC_ACQUIRE)) {
       HIP_TRY(c, lcdev::launch_handoff_compact(d.d_flags, d_off, n_keys, gap_on ? 1 : 0, d.d_jit,
-                                               d.d_jit2, d.d_status, st));
+                                               d.d_jit2, d.d_status, want_wit ? wo.kind : nullptr,
+                                               st));
       HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                                 hipMemcpyDeviceToHost, st));
       HIP_TRY(c, hipStreamSynchronize(st));
@@ -277,6 +302,8 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     job.probe = job.cex_state + nk;
     job.mode = lcdev::kGapFull;
     job.n_tasks = (int32_t)n_jit;
+    job.wit = want_wit ? wo.wit : nullptr;
+    job.wkind = want_wit ? wo.kind : nullptr;
     // short keys: one-wave workgroups (barriers nearly free, 4x the decisions
     // in flight); longer keys: 256 threads share each decision's setup
     job.threads = wave_wg ? 64 : 256;
@@ -315,8 +342,12 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       if (rc) return rc;
       for (int round = 0;; round++) {
         if (round == kGapMaxRounds) {
-          set_err(c, "gap tier: counterexample search did not converge");
-          return -EIO;
+          // cannot happen (each round cuts an interval by P + 1 >= 3); the
+          // JIT tier decides whatever is still open rather than the call fail
+          job.give_up = 1;
+          HIP_TRY(c, lcdev::launch_gap_narrow(d_ops, d_off, n_cex, d_out, d.d_jit2, d.d_status,
+                                              job, st));
+          break;
         }
         HIP_TRY(c, hipMemsetAsync(&d.d_status->n_open, 0, sizeof(int32_t), st));
         HIP_TRY(c, lcdev::launch_gap_tier(d_ops, d_off, nullptr, p, d_out, d.d_gws, job.n_tasks,
@@ -327,6 +358,15 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                                   hipMemcpyDeviceToHost, st));
         HIP_TRY(c, hipStreamSynchronize(st));
         if (d.h_status->n_open == 0) break;
+      }
+      if (want_wit) {
+        // the witness of each closed counterexample's last linearizable prefix
+        job.mode = lcdev::kGapWitness;
+        job.P = 1;
+        job.n_tasks = n_cex;
+        HIP_TRY(c, lcdev::launch_gap_tier(d_ops, d_off, nullptr, p, d_out, d.d_gws,
+                                          std::min<int>(n_cex, wg_cap), gap_cap, d.d_jit2,
+                                          d.d_status, job, st));
       }
     }
     HIP_TRY(c, hipEventRecord(d.eg, st));
@@ -422,32 +462,45 @@ void lc_default_opts(lc_opts *o) {
   o->flags = 0;
 }
 
+// The id is also findable in the file without loading it ("LC_BUILD_ID:"
+// marker): tests/conftest.py checks it before anything loads a HIP runtime.
+__attribute__((used)) static const char kBuildTag[] = "LC_BUILD_ID:" LC_BUILD_ID;
+const char *lc_build_id(void) { return kBuildTag + 12; }
+
 int lc_open(uint32_t device_mask, lc_ctx **out) {
   if (!out) return -EINVAL;
   *out = nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -ENODEV;
+  // LC_VIRTUAL_DEVICES=k: k device contexts on the first selected GPU (tests
+  // of the multi-device fan-out on a one-GPU box)
+  const char *venv = getenv("LC_VIRTUAL_DEVICES");
+  const int virt = venv ? std::max(0, std::min(32, atoi(venv))) : 0;
   lc_ctx *c = new lc_ctx();
   for (int i = 0; i < n && i < 32; i++) {
     if (device_mask && !(device_mask & (1u << i))) continue;
-    Dev d;
-    d.id = i;
-    if (hipSetDevice(i) != hipSuccess ||
-        hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&d.e0, kEventFlags) != hipSuccess ||
-        hipEventCreateWithFlags(&d.e1, kEventFlags) != hipSuccess ||
-        hipEventCreateWithFlags(&d.e2, kEventFlags) != hipSuccess ||
-        hipEventCreateWithFlags(&d.ef, kEventFlags) != hipSuccess ||
-        hipEventCreateWithFlags(&d.eg, kEventFlags) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&d.d_status), sizeof(lcdev::KStatus)) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void **>(&d.h_handoff), sizeof(int32_t),
-                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void **>(&d.h_handoff_dev), d.h_handoff, 0) != hipSuccess) {
-      lc_close(c);
-      return -ENODEV;
+    for (int v = 0; v < (virt >= 2 ? virt : 1); v++) {
+      Dev d;
+      d.id = i;
+      if (hipSetDevice(i) != hipSuccess ||
+          hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&d.e0, kEventFlags) != hipSuccess ||
+          hipEventCreateWithFlags(&d.e1, kEventFlags) != hipSuccess ||
+          hipEventCreateWithFlags(&d.e2, kEventFlags) != hipSuccess ||
+          hipEventCreateWithFlags(&d.ef, kEventFlags) != hipSuccess ||
+          hipEventCreateWithFlags(&d.eg, kEventFlags) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void **>(&d.d_status), sizeof(lcdev::KStatus)) != hipSuccess ||
+          hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess ||
+          hipHostMalloc(reinterpret_cast<void **>(&d.h_handoff), sizeof(int32_t),
+                        hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+          hipHostGetDevicePointer(reinterpret_cast<void **>(&d.h_handoff_dev), d.h_handoff, 0) != hipSuccess) {
+        c->devs.push_back(d);  // lc_close frees what was created
+        lc_close(c);
+        return -ENODEV;
+      }
+      c->devs.push_back(d);
     }
-    c->devs.push_back(d);
+    if (virt >= 2) break;
   }
   if (c->devs.empty()) {
     delete c;
@@ -480,6 +533,8 @@ void lc_close(lc_ctx *c) {
     if (d.d_flags) (void)hipFree(d.d_flags);
     if (d.d_gws) (void)hipFree(d.d_gws);
     if (d.d_cex) (void)hipFree(d.d_cex);
+    if (d.d_wit) (void)hipFree(d.d_wit);
+    if (d.d_kind) (void)hipFree(d.d_kind);
     if (d.eg) (void)hipEventDestroy(d.eg);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
@@ -494,29 +549,84 @@ int lc_last_stats(lc_ctx *c, lc_stats *out) {
   return 0;
 }
 
-// Contiguous split: key k's cost is its record count plus a fixed per-key
-// overhead (one wave launch + result write); boundaries at equal cost.
+// Per-key device cost in record-scan units.  The tier a key
+// lands in follows from its records alone (check_kernel.hip, fast_key):
+//   * version-order tier (every :ok mutation versioned, nothing crashed):
+//     one pass over the records, cost n;
+//   * gap tier (crashed writes/CAS, versions pinned): two skeleton passes,
+//     the matching and, for an invalid key, the bisection; measured ~6x the
+//     fast tier per record on C2 with 5 % crashed ops (crash_leg), plus the
+//     matching's share, which grows with the crashed ops;
+//   * frontier search (an :ok mutation or a read [nil x] without a version):
+//     the frontier grows with the open window w; measured (model_leg,
+//     tools/frontier_dist.py) ~1,600x the fast tier per record at
+//     concurrency 10 and ~4,700x at 20, i.e. ~12 w^2, and crashed ops
+//     multiply the configurations (capped: the search's budget bounds it).
+// Plus a fixed 64 per key (launch share, result write).
+static double key_cost(const lc_op *o, int64_t n) {
+  int64_t crashed = 0, unpinned = 0;
+  for (int64_t i = 0; i < n; i++) {
+    const bool mut = o[i].f == LC_F_WRITE || o[i].f == LC_F_CAS;
+    if (mut && o[i].ret == LC_INF) crashed++;
+    else if (o[i].ret != LC_INF && o[i].version == LC_NIL &&
+             (mut || (o[i].f == LC_F_READ && o[i].value != LC_NIL)))
+      unpinned++;
+  }
+  const double kOverhead = 64;
+  if (!unpinned && !crashed) return (double)n + kOverhead;
+  if (!unpinned) return (6.0 + 0.01 * (double)crashed) * (double)n + kOverhead;
+  // open window: the most ops called and not yet returned at once
+  std::vector<int64_t> rets;
+  rets.reserve((size_t)n);
+  for (int64_t i = 0; i < n; i++) rets.push_back(o[i].ret);
+  std::sort(rets.begin(), rets.end());
+  int64_t w = 0;
+  size_t j = 0;
+  for (int64_t i = 0; i < n; i++) {  // records are sorted by call
+    while (j < rets.size() && rets[j] < o[i].call) j++;
+    w = std::max<int64_t>(w, i + 1 - (int64_t)j);
+  }
+  const double blow = std::pow(2.0, (double)std::min<int64_t>(crashed, 12));
+  return (double)n * (1.0 + 12.0 * (double)w * (double)w) * blow + kOverhead;
+}
+
+int lc_key_cost(const lc_op *ops, const int64_t *key_off, int64_t n_keys, double *costs) {
+  if (!ops || !key_off || !costs || n_keys < 0) return -EINVAL;
+  for (int64_t k = 0; k < n_keys; k++) {
+    const int64_t n = key_off[k + 1] - key_off[k];
+    if (n < 0) return -EINVAL;
+    costs[k] = key_cost(ops + key_off[k], n);
+  }
+  return 0;
+}
+
+// Contiguous split at equal cost: boundary p is the first key whose cost
+// prefix reaches p/n_parts of the total (keys stay in order, so each device
+// gets one contiguous slice of the caller's arrays).
 int lc_plan_partition(const lc_op *ops, const int64_t *key_off, int64_t n_keys,
                       int32_t n_parts, int64_t *bounds) {
-  (void)ops;
   if (!key_off || !bounds || n_parts < 1 || n_keys < 0) return -EINVAL;
-  const int64_t kOverhead = 64;
-  const int64_t total = (key_off[n_keys] - key_off[0]) + kOverhead * n_keys;
+  std::vector<double> pre((size_t)n_keys + 1, 0.0);
+  for (int64_t k = 0; k < n_keys; k++) {
+    const int64_t n = key_off[k + 1] - key_off[k];
+    if (n < 0) return -EINVAL;
+    pre[(size_t)k + 1] = pre[(size_t)k] +
+                         (ops ? key_cost(ops + key_off[k], n) : (double)n + 64.0);
+  }
+  const double total = pre[(size_t)n_keys];
   bounds[0] = 0;
   int64_t k = 0;
   for (int32_t p = 1; p < n_parts; p++) {
-    const long double goal = (long double)total * p / n_parts;
-    while (k < n_keys &&
-           (long double)((key_off[k] - key_off[0]) + kOverhead * k) < goal)
-      k++;
+    const double goal = total * p / n_parts;
+    while (k < n_keys && pre[(size_t)k] < goal) k++;
     bounds[p] = k;
   }
   bounds[n_parts] = n_keys;
   return 0;
 }
 
-int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
-             int64_t n_keys, const lc_opts *opts, lc_key_result *out) {
+int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
+                int64_t n_keys, const lc_opts *opts, lc_key_result *out, const lc_aux *aux) {
   if (!c) return -EINVAL;
   const auto t0 = std::chrono::steady_clock::now();
   c->stats = lc_stats{};
@@ -538,9 +648,10 @@ int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
   int rc = opts_to_params(c, opts, &p);
   if (rc) return rc;
   const int64_t flags = opts ? opts->flags : 0;
+  const bool want_wit = aux && aux->witness && aux->witness_kind;
   const int nd = (int)c->devs.size();
   std::vector<int64_t> bounds(nd + 1);
-  lc_plan_partition(ops, key_off, n_keys, nd, bounds.data());
+  lc_plan_partition(nd > 1 ? ops : nullptr, key_off, n_keys, nd, bounds.data());
 
   std::vector<int> rcs(nd, 0);
   auto work = [&](int di) {
@@ -553,17 +664,21 @@ int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
       return;
     }
     const int64_t r0 = key_off[a], r1 = key_off[b];
-    const size_t ops_bytes = sizeof(lc_op) * (size_t)(r1 - r0);
+    const int64_t nrec = r1 - r0;
+    const size_t ops_bytes = sizeof(lc_op) * (size_t)nrec;
     int r = ensure(c, reinterpret_cast<char **>(&d.d_ops), &d.ops_cap, ops_bytes);
     if (!r) r = ensure(c, &d.d_off, &d.off_cap, sizeof(int64_t) * (size_t)(nk + 1));
     if (!r) r = ensure(c, &d.d_out, &d.out_cap, sizeof(lc_key_result) * (size_t)nk);
+    if (!r && want_wit) r = ensure(c, &d.d_wit, &d.wit_cap, sizeof(int32_t) * (size_t)nrec);
+    if (!r && want_wit) r = ensure(c, &d.d_kind, &d.kind_cap, sizeof(int32_t) * (size_t)nk);
     if (r) {
       rcs[di] = r;
       return;
     }
     hipError_t e = hipSuccess;
     if (ops_bytes)
-      e = hipMemcpyAsync(d.d_ops, ops + r0, ops_bytes, hipMemcpyHostToDevice, d.stream);
+      e = hipMemcpyAsync(d.d_ops, ops + r0, ops_bytes, hipMemcpyHostToDevice,
+                         d.stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(d.d_off, key_off + a, sizeof(int64_t) * (size_t)(nk + 1),
                          hipMemcpyHostToDevice, d.stream);
@@ -572,14 +687,26 @@ int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
       rcs[di] = -EIO;
       return;
     }
+    WitOut wo;
+    if (want_wit) {
+      wo.wit = d.d_wit;
+      wo.kind = d.d_kind;
+      wo.n_records = nrec;
+    }
     r = run_device(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, nk, p,
-                   d.d_out, d.stream, flags);
+                   d.d_out, d.stream, flags, wo);
     if (r) {
       rcs[di] = r;
       return;
     }
     e = hipMemcpyAsync(out + a, d.d_out, sizeof(lc_key_result) * (size_t)nk,
                        hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess && want_wit && nrec)
+      e = hipMemcpyAsync(aux->witness + r0, d.d_wit, sizeof(int32_t) * (size_t)nrec,
+                         hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess && want_wit)
+      e = hipMemcpyAsync(aux->witness_kind + a, d.d_kind, sizeof(int32_t) * (size_t)nk,
+                         hipMemcpyDeviceToHost, d.stream);
     if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
     if (e != hipSuccess) {
       set_err(c, std::string("hipMemcpyAsync D2H: ") + hipGetErrorString(e));
@@ -593,7 +720,6 @@ int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
     for (int di = 0; di < nd; di++) th.emplace_back(work, di);
     for (auto &t : th) t.join();
   }
-  int malformed = 0;
   for (int di = 0; di < nd; di++) {
     if (rcs[di] && !rc) rc = rcs[di];
     c->stats.kernel_ms += c->devs[di].kernel_ms;
@@ -604,24 +730,24 @@ int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
     c->stats.n_gap_keys += c->devs[di].n_gap;
     c->stats.hbm_kernel_ms += c->devs[di].hbm_ms;
     c->stats.n_hbm_keys += c->devs[di].n_hbm;
-    malformed += c->devs[di].malformed;
+    c->stats.n_malformed += c->devs[di].malformed;
   }
   c->stats.n_keys = n_keys;
   c->stats.n_ops = key_off[n_keys] - key_off[0];
   c->stats.n_devices = nd;
   c->stats.total_ms = std::chrono::duration<double, std::milli>(
                           std::chrono::steady_clock::now() - t0).count();
-  if (rc) return rc;
-  if (malformed) {
-    set_err(c, std::to_string(malformed) + " key(s) hold malformed records");
-    return -EINVAL;
-  }
-  return 0;
+  return rc;
 }
 
-int lc_check_device(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
-                    int64_t n_keys, const lc_opts *opts, lc_key_result *d_out,
-                    void *stream) {
+int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
+             int64_t n_keys, const lc_opts *opts, lc_key_result *out) {
+  return lc_check_ex(c, ops, key_off, n_keys, opts, out, nullptr);
+}
+
+int lc_check_device_ex(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
+                       int64_t n_keys, const lc_opts *opts, lc_key_result *d_out,
+                       void *stream, const lc_aux *aux) {
   if (!c) return -EINVAL;
   const auto t0 = std::chrono::steady_clock::now();
   c->stats = lc_stats{};
@@ -639,10 +765,22 @@ int lc_check_device(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
   Dev &d = c->devs[0];
   HIP_TRY(c, hipSetDevice(d.id));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d.stream;
+  WitOut wo;
+  if (aux && aux->witness && aux->witness_kind && n_keys > 0) {
+    // the record count lives in device memory: key_off[n_keys] - key_off[0]
+    int64_t ends[2] = {0, 0};
+    HIP_TRY(c, hipMemcpyAsync(&ends[0], d_key_off, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipMemcpyAsync(&ends[1], d_key_off + n_keys, sizeof(int64_t), hipMemcpyDeviceToHost,
+                              st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    wo.wit = aux->witness;
+    wo.kind = aux->witness_kind;
+    wo.n_records = ends[1] - ends[0];
+  }
   // d_ops points at the record of index d_key_off[0]; the kernels read that
   // base themselves, so a key_off slice of a larger array may be passed.
   rc = run_device(c, d, d_ops, d_key_off, n_keys, p, d_out, st,
-                  opts ? opts->flags : 0);
+                  opts ? opts->flags : 0, wo);
   c->stats.kernel_ms = d.kernel_ms;
   c->stats.fast_kernel_ms = d.fast_ms;
   c->stats.jit_kernel_ms = d.jit_ms;
@@ -651,17 +789,19 @@ int lc_check_device(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
   c->stats.n_gap_keys = d.n_gap;
   c->stats.hbm_kernel_ms = d.hbm_ms;
   c->stats.n_hbm_keys = d.n_hbm;
+  c->stats.n_malformed = d.malformed;
   c->stats.n_keys = n_keys;
   c->stats.n_ops = -1;  // not read back from device memory
   c->stats.n_devices = 1;
   c->stats.total_ms = std::chrono::duration<double, std::milli>(
                           std::chrono::steady_clock::now() - t0).count();
-  if (rc) return rc;
-  if (d.malformed) {
-    set_err(c, std::to_string(d.malformed) + " key(s) hold malformed records");
-    return -EINVAL;
-  }
-  return 0;
+  return rc;
+}
+
+int lc_check_device(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
+                    int64_t n_keys, const lc_opts *opts, lc_key_result *d_out,
+                    void *stream) {
+  return lc_check_device_ex(c, d_ops, d_key_off, n_keys, opts, d_out, stream, nullptr);
 }
 
 }  // extern "C"

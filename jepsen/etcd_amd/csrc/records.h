@@ -67,13 +67,17 @@ __device__ __forceinline__ Rec decode(const Raw &w, int64_t base_idx) {
   }
   const int64_t rc = call - base_idx, rr = ret - base_idx;
   r.bad = (value < -1) | (value > kFieldMax) | (expected < -1) |
-          (expected > kFieldMax) | (version < -1) | (version > kFieldMax) |
+          (expected > kFieldMax) |
           (call < 0) | (ret <= call) | (rc < 0) | (rc >= (int64_t)kNever) |
           ((ret != kInf) & (rr >= (int64_t)kNever));
   r.f = (f >= 0 && f <= 2) ? (int)f : 3;
   r.val = (int)value;
   r.exp = (int)expected;
-  r.ver = (int)version;
+  // A version outside [-1, kFieldMax] is one no state of the key can hold
+  // (states run from V0 >= 0 up to V0 + n < kFieldMax): knossos rejects the
+  // op at every step, so it is saturated to kFieldMax, which is equally
+  // unreachable, instead of failing the key as malformed.
+  r.ver = (version < -1 || version > kFieldMax) ? (int)kFieldMax : (int)version;
   r.call = (uint32_t)rc;
   r.ret = ret == kInf ? kNever : (uint32_t)rr;
   const int vchk = r.ver != -1 ? -1 : 0;

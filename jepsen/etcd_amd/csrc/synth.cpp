@@ -55,6 +55,8 @@ struct SimOp {
   double call_t, lin_t, ret_t;  // ret_t = inf for crashed
   int status;                   // LC_SYNTH_*
   bool effect;                  // crashed op takes effect
+  bool lost;                    // the injected lost CAS (never made :info)
+  int32_t slot;                 // worker slot (process ids: slot + conc * crashes so far)
   int32_t proc;
   int64_t call_i, ret_i;
 };
@@ -124,6 +126,7 @@ void simulate(const lc_synth_params &p, int64_t key, std::vector<SimOp> &out,
     o.call_t = t;
     o.lin_t = t + rng.uniform() * d;
     o.proc = proc_id[slot];
+    o.slot = slot;
     bool crash = !reader && p.p_info > 0 && rng.uniform() < p.p_info;
     const int64_t idx = (int64_t)out.size();
     if (crash) {
@@ -181,6 +184,7 @@ void simulate(const lc_synth_params &p, int64_t key, std::vector<SimOp> &out,
         if (!lost_done && ok_cas_seen == lost_cas_at) {
           // Lost CAS: reported ok with the next version, effect dropped.
           o.version = ver + 1;
+          o.lost = true;
           lost_done = true;
         } else {
           ver++;
@@ -199,6 +203,30 @@ void simulate(const lc_synth_params &p, int64_t key, std::vector<SimOp> &out,
           start_op(slot, e.t);
         }
       }
+    }
+  }
+
+  // info_frac: top the crashed records up to the exact target by reporting
+  // uniformly chosen :ok writes/CAS as :info (they did take effect, so the
+  // history stays linearizable).  Each such process is replaced: the later
+  // ops of its worker slot move to the next process id.
+  if (p.info_frac > 0) {
+    const int64_t want = std::llround(p.info_frac * (double)target);
+    int64_t have = 0;
+    std::vector<size_t> cand;
+    for (size_t i = 0; i < out.size(); i++) {
+      const SimOp &o = out[i];
+      if (o.status == LC_SYNTH_INFO) have++;
+      else if (o.status == LC_SYNTH_OK && o.f != LC_F_READ && !o.lost) cand.push_back(i);
+    }
+    for (size_t j = 0; have < want && j < cand.size(); j++, have++) {
+      const size_t pick = j + (size_t)rng.below((int)(cand.size() - j));
+      std::swap(cand[j], cand[pick]);
+      SimOp &o = out[cand[j]];
+      o.status = LC_SYNTH_INFO;
+      o.ret_t = inf;
+      for (SimOp &q : out)
+        if (q.slot == o.slot && q.call_t > o.call_t) q.proc += conc;
     }
   }
 

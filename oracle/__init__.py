@@ -51,6 +51,9 @@ def lib():
         L.oracle_check.argtypes = [vp, vp, ctypes.c_int64, ctypes.POINTER(_Opts), vp,
                                    ctypes.c_int, ctypes.c_int]
         L.oracle_check.restype = ctypes.c_int
+        L.oracle_check_witness.argtypes = [vp, vp, ctypes.c_int64, ctypes.POINTER(_Opts), vp, vp,
+                                           vp, vp, vp, ctypes.c_int]
+        L.oracle_check_witness.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -68,3 +71,33 @@ def check(ops, key_off, algo=JIT, n_threads=1, max_configs=0, init_version=0,
                             ctypes.byref(o), out.ctypes.data_as(ctypes.c_void_p),
                             algo, n_threads)
     return rc, out
+
+
+WIT_OK, WIT_NONE = 1, 0
+WIT_CODES = {1: "ok", 0: "none", -1: "bad-position", -2: "not-an-op", -3: "read-unplaceable",
+             -4: "inconsistent", -5: "real-time", -6: "missing-ok-op"}
+
+
+def check_witness(ops, key_off, witness, kind, results=None, init_version=0, init_value=-1,
+                  n_threads=8):
+    """Certify witnesses (lc_aux) independently: per key WIT_OK, WIT_NONE or
+    a negative code (WIT_CODES), plus the length of each rebuilt order.
+    `results` (the GPU's lc_key_result array) gives the cut of PREFIX
+    witnesses: fail_prefix_end - 1."""
+    ops = np.ascontiguousarray(ops, dtype=np.int64).reshape(-1, 6)
+    key_off = np.ascontiguousarray(key_off, dtype=np.int64)
+    witness = np.ascontiguousarray(witness, dtype=np.int32)
+    kind = np.ascontiguousarray(kind, dtype=np.int32)
+    n = len(key_off) - 1
+    cut = np.full(max(n, 0), -1, dtype=np.int64)
+    if results is not None:
+        cut = np.ascontiguousarray(results["fail_prefix_end"] - 1, dtype=np.int64)
+    st = np.zeros(max(n, 0), dtype=np.int32)
+    ln = np.zeros(max(n, 0), dtype=np.int64)
+    o = _Opts(init_version, init_value, 0, 0, 0)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    rc = lib().oracle_check_witness(p(ops), p(key_off), n, ctypes.byref(o), p(witness), p(kind),
+                                    p(cut), p(st), p(ln), n_threads)
+    if rc != 0:
+        raise RuntimeError("oracle_check_witness: %d" % rc)
+    return st, ln

@@ -45,6 +45,26 @@ int oracle_check(const lc_op *ops, const int64_t *key_off, int64_t n_keys,
 int oracle_step(int64_t ver, int64_t val, const lc_op *op,
                 int64_t *nver, int64_t *nval);
 
+/* Witness certification (witness.c): rebuild the total order a witness
+ * (lc_aux, include/lincheck.h) names and check it against the definition —
+ * every :ok op present, model steps legal (oracle_step), real-time order
+ * respected.  Per key status: ORACLE_WIT_OK, ORACLE_WIT_NONE (kind NONE), or
+ * a negative ORACLE_WIT_* code.  cut[k] is the prefix end for kind PREFIX
+ * (fail_prefix_end - 1; may be NULL when no key has that kind).  order_len
+ * (may be NULL) receives the length of each rebuilt order. */
+#define ORACLE_WIT_OK                 1
+#define ORACLE_WIT_NONE               0
+#define ORACLE_WIT_BAD_POSITION     (-1) /* positions not exactly 0..m-1, once each */
+#define ORACLE_WIT_NOT_AN_OP        (-2) /* a position on a read / an op after the cut / unknown f */
+#define ORACLE_WIT_READ_UNPLACEABLE (-3) /* a read's version names no segment of the order */
+#define ORACLE_WIT_INCONSISTENT     (-4) /* the model rejects an op of the order */
+#define ORACLE_WIT_REAL_TIME        (-5) /* an op ordered after one called after it returned */
+#define ORACLE_WIT_MISSING_OK_OP    (-6) /* an :ok write/CAS left out */
+int oracle_check_witness(const lc_op *ops, const int64_t *key_off, int64_t n_keys,
+                         const lc_opts *opts, const int32_t *witness, const int32_t *kind,
+                         const int64_t *cut, int32_t *status, int64_t *order_len,
+                         int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

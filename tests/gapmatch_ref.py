@@ -31,6 +31,10 @@ mutation without a version, a read [nil x], an unknown :f, or the branch
 budget ran out).  first_failure() returns the canonical counterexample
 (index of the :ok op whose return first makes the prefix non-linearizable),
 found by bisection over prefixes (linearizability is prefix-closed).
+decide(..., witness=True) returns (verdict, positions): for a valid key the
+mutation position of every record in the linearization the matching found
+(-1 for records not linearized as mutations) — the lc_aux witness format, so
+oracle.check_witness can certify this restatement's answers too.
 """
 INF = (1 << 63) - 1
 ANY = None  # a gap whose value nothing constrains
@@ -89,7 +93,7 @@ def _setup(recs, v0, init, cutoff):
     b = {}               # position k -> min read ret (reads of version V0+k+1)
     claim = {}           # version index k -> value
     max_read = -1
-    for (f, value, expected, ver, call, ret) in recs:
+    for ri, (f, value, expected, ver, call, ret) in enumerate(recs):
         if f not in (0, 1, 2):
             raise _NA
         if cutoff is not None:
@@ -117,19 +121,26 @@ def _setup(recs, v0, init, cutoff):
             pos = None if ver == -1 else ver - v0 - 1
             if pos is not None and pos < 0:
                 continue  # can never be linearized: leave it out
-            optional.append((f, value, expected if f == 2 else None, call, pos))
+            optional.append((f, value, expected if f == 2 else None, call, pos, ri))
         else:
             if ver == -1:
                 raise _NA
             pos = ver - v0 - 1
             if pos < 0 or pos in pinned:
                 return None
-            pinned[pos] = (f, value, expected if f == 2 else None, call, ret)
+            pinned[pos] = (f, value, expected if f == 2 else None, call, ret, ri)
     m = max(max(pinned) + 1 if pinned else 0, max_read)
     return pinned, optional, a, b, claim, m
 
 
-def decide(recs, v0=0, init=-1, cutoff=None, budget=10000):
+def decide(recs, v0=0, init=-1, cutoff=None, budget=10000, witness=False):
+    if not witness:
+        return _decide(recs, v0, init, cutoff, budget, None)
+    w = [-1] * len(recs)
+    return _decide(recs, v0, init, cutoff, budget, w), w
+
+
+def _decide(recs, v0, init, cutoff, budget, wit):
     try:
         st = _setup(recs, v0, init, cutoff)
     except _NA:
@@ -137,6 +148,9 @@ def decide(recs, v0=0, init=-1, cutoff=None, budget=10000):
     if st is None:
         return 0
     pinned, optional, a, b, claim, m = st
+    if wit is not None:
+        for k, p in pinned.items():
+            wit[p[5]] = k
     # suffix-min deadlines
     u = [min(b.get(k, INF), pinned[k][4] if k in pinned else INF) for k in range(m)]
     uh = [INF] * (m + 1)
@@ -189,7 +203,7 @@ def decide(recs, v0=0, init=-1, cutoff=None, budget=10000):
         for k in gaps:
             before = val_before(k, req)
             lst = []
-            for i, (f, value, exp, call, pos) in enumerate(optional):
+            for i, (f, value, exp, call, pos, _) in enumerate(optional):
                 if call >= uh[k] or (pos is not None and pos != k):
                     continue
                 if req[k] is not ANY and value != req[k]:
@@ -203,7 +217,7 @@ def decide(recs, v0=0, init=-1, cutoff=None, budget=10000):
             return False
         # the relaxation ignored CAS expectations after free gaps: check them
         for gi, k in enumerate(gaps):
-            f, _, exp, _, _ = optional[mg[gi]]
+            f, _, exp, _, _, _ = optional[mg[gi]]
             if f != 2 or val_before(k, req) is not ANY:
                 continue
             # k-1 is a free gap; the op placed there fixes the value
@@ -218,6 +232,9 @@ def decide(recs, v0=0, init=-1, cutoff=None, budget=10000):
                 if solve(r2):
                     return True
             return False
+        if wit is not None:
+            for gi, k in enumerate(gaps):
+                wit[optional[mg[gi]][5]] = k
         return True
 
     try:

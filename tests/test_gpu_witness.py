@@ -1,0 +1,163 @@
+"""GPU decisions certified by their witnesses (lc_aux), checked on the CPU by
+oracle/witness.c — independent of the gap-matching procedure that produced
+them, so this pins the full-size decisions no oracle search finishes:
+BASELINE configs[3] (C4) at its stated 20 % crashed ops, and C2 with crashes.
+Also the multi-device fan-out (LC_VIRTUAL_DEVICES) and per-key error model."""
+import os
+
+import numpy as np
+import pytest
+
+import gapmatch_ref as gm
+import oracle
+from helpers import GOLDEN, INF, pack_keys
+from jepsen.etcd_amd import abi
+
+pytestmark = pytest.mark.gpu
+
+
+def certify(ops, off, r, wit, kind):
+    st, ln = oracle.check_witness(ops, off, wit, kind, results=r, n_threads=16)
+    bad = np.nonzero((kind != abi.LC_WITNESS_NONE) & (st != oracle.WIT_OK))[0]
+    assert len(bad) == 0, [(int(k), int(kind[k]), oracle.WIT_CODES[int(st[k])]) for k in bad[:5]]
+    # kinds match verdicts
+    assert ((kind != abi.LC_WITNESS_FULL) | (r["verdict"] == 1)).all()
+    assert ((kind != abi.LC_WITNESS_PREFIX) | (r["verdict"] == 0)).all()
+    return st, ln
+
+
+@pytest.mark.parametrize("name", ["c1", "c5", "info", "tiny"])
+def test_witnesses_of_golden_fixtures(ctx, name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    _, r, wit, kind = ctx.check(z["ops"], z["key_off"], witness=True)
+    assert (r["verdict"] == z["verdict"]).all() and (r["fail_op"] == z["fail_op"]).all()
+    certify(z["ops"], z["key_off"], r, wit, kind)
+    # the version-order and gap tiers witness every key they decide; only
+    # keys a search tier decides (version-less ops, [nil x] reads) have none
+    n_none = int((kind == abi.LC_WITNESS_NONE).sum())
+    if name in ("c1", "c5"):
+        assert n_none == 0
+    # the witness outputs change nothing else
+    _, r2 = ctx.check(z["ops"], z["key_off"])
+    assert (r2 == r).all()
+
+
+@pytest.mark.parametrize("seed", [0x5EED0004, 1004, 1006])
+@pytest.mark.parametrize("anom", [0.0, 1.0])
+def test_c4_at_20pct_crashed_certified(ctx, seed, anom):
+    """BASELINE configs[3] as stated: one key, 5,000 ops, concurrency 50,
+    1,000 (20 %) crashed writes/CAS.  Valid: the gap tier's linearization of
+    the whole history passes the independent check.  With an injected
+    anomaly: invalid, the counterexample agrees with the restated procedure,
+    and the prefix just before the failing return is certified linearizable
+    by its own witness (so the failing return is the first one that fails,
+    given prefix-closure)."""
+    ops, off, lab, _ = abi.synth(1, 5000, concurrency=50, p_info=0.2, info_frac=0.2,
+                                 p_anomaly=anom, seed=seed)
+    assert int((ops[:, 5] == INF).sum()) == 1000
+    _, r, wit, kind = ctx.check(ops, off, witness=True)
+    recs = [tuple(x) for x in ops.tolist()]
+    want = gm.decide(recs)
+    assert want is not None and r["verdict"][0] == want
+    if want == 0:
+        assert (r["fail_op"][0], r["fail_prefix_end"][0]) == gm.first_failure(recs)
+        assert kind[0] == abi.LC_WITNESS_PREFIX
+    else:
+        assert kind[0] == abi.LC_WITNESS_FULL
+    if lab[0] == 1:
+        assert want == 0
+    st, ln = certify(ops, off, r, wit, kind)
+    assert st[0] == oracle.WIT_OK and ln[0] > 3000
+
+
+def test_crash_leg_every_key_certified(ctx):
+    """bench.py's crash_leg workload at full size: C2 (10,000 keys x 1,000
+    ops, concurrency 20) with 5 % of writes/CAS crashed.  Every key goes to
+    the gap tier; every verdict is valid and every one is certified by its
+    witness on the CPU."""
+    ops, off, _, _ = abi.synth(10000, 1000, concurrency=20, p_info=0.05, seed=0x5EED0012)
+    _, r, wit, kind = ctx.check(ops, off, witness=True)
+    assert ctx.stats()["n_gap_keys"] == 10000
+    assert (r["verdict"] == 1).all() and (kind == abi.LC_WITNESS_FULL).all()
+    st, _ = certify(ops, off, r, wit, kind)
+    assert (st == oracle.WIT_OK).all()
+
+
+def test_mixed_crash_batch_witnesses(ctx):
+    """Many short crash-heavy keys, a third of them invalid: one-wave gap
+    workgroups, in-place bisection, prefix witnesses."""
+    ops, off, _, _ = abi.synth(2000, 120, concurrency=12, p_info=0.2, info_frac=0.15,
+                               p_anomaly=0.35, seed=51)
+    _, r, wit, kind = ctx.check(ops, off, witness=True)
+    st, _ = certify(ops, off, r, wit, kind)
+    assert (kind == abi.LC_WITNESS_PREFIX).sum() > 300
+    assert (kind == abi.LC_WITNESS_FULL).sum() > 1000
+    _, j = oracle.check(ops, off, algo=oracle.JITC, n_threads=16, max_configs=1 << 20)
+    known = j["verdict"] != -1
+    for f in ("verdict", "fail_op", "fail_prefix_end"):
+        assert (r[f][known] == j[f][known]).all(), f
+
+
+def test_witness_device_path_matches_host_path(ctx):
+    import torch
+    ops, off, _, _ = abi.synth(300, 200, concurrency=10, p_info=0.2, p_anomaly=0.3, seed=61)
+    _, r, wit, kind = ctx.check(ops, off, witness=True)
+    dev = torch.device("cuda", 0)
+    d_ops = torch.from_numpy(ops).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_out = torch.zeros(300 * 40, dtype=torch.uint8, device=dev)
+    d_wit = torch.full((len(ops),), -7, dtype=torch.int32, device=dev)
+    d_kind = torch.full((300,), -7, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), 300, d_out.data_ptr(),
+                     stream=s.cuda_stream, d_witness=d_wit.data_ptr(),
+                     d_witness_kind=d_kind.data_ptr())
+    r2 = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
+    assert (r2 == r).all()
+    assert (d_kind.cpu().numpy() == kind).all()
+    w2 = d_wit.cpu().numpy()
+    has = np.repeat(kind != 0, np.diff(off))
+    assert (w2[has] == wit[has]).all()
+
+
+def test_virtual_devices_fan_out_equals_one_device(ctx, monkeypatch):
+    """lc_check's multi-device path (cost partition, one host thread and
+    stream per device, results into one array) run as 3 contexts on one GPU
+    (LC_VIRTUAL_DEVICES): identical results and witnesses to the
+    single-device call, on a batch whose crash-heavy keys are clustered."""
+    heavy, hoff, _, _ = abi.synth(300, 300, concurrency=16, p_info=0.2, p_anomaly=0.3, seed=71)
+    light, loff, _, _ = abi.synth(2700, 300, concurrency=16, p_anomaly=0.05, seed=72)
+    ops = np.concatenate([heavy, light])
+    off = np.concatenate([hoff, loff[1:] + hoff[-1]])
+    _, a, wa, ka = ctx.check(ops, off, witness=True)
+    monkeypatch.setenv("LC_VIRTUAL_DEVICES", "3")
+    with abi.Context(device_mask=1) as c3:
+        _, b, wb, kb = c3.check(ops, off, witness=True)
+        st = c3.stats()
+    assert st["n_devices"] == 3
+    assert (a == b).all() and (ka == kb).all() and (wa == wb).all()
+    bounds = abi.plan_partition(off, 3, ops=ops)
+    assert bounds[1] < 1000  # the clustered heavy keys are spread by cost
+
+
+def test_malformed_key_is_unknown_alone(ctx):
+    """One malformed key no longer fails the call: it is :unknown with reason
+    malformed (jepsen.independent would lose only that key), and the other
+    keys — an invalid one among them — keep their verdicts.  A version no
+    state reaches (beyond int32, or below -1) is not malformed: knossos
+    rejects the op at every step, so the key is invalid."""
+    W, R = 1, 0
+    bad_order = [[W, 1, -1, 1, 5, 6], [W, 2, -1, 2, 3, 4]]
+    stale = [[W, 1, -1, 1, 0, 1], [W, 2, -1, 2, 2, 3], [R, 1, -1, 1, 4, 5]]
+    huge_ver = [[W, 1, -1, 1, 0, 1], [R, 1, -1, 1 << 40, 2, 3]]
+    neg_ver = [[W, 1, -1, -7, 0, 1]]
+    huge_crashed = [[W, 1, -1, 1 << 40, 0, INF], [W, 2, -1, 1, 1, 2]]
+    good = [[W, 1, -1, 1, 0, 1]]
+    keys = [bad_order, stale, huge_ver, neg_ver, huge_crashed, good]
+    ops, off = pack_keys(keys)
+    rc, r = ctx.check(ops, off, raise_on_error=False)
+    assert rc == 0
+    assert list(r["verdict"]) == [-1, 0, 0, 0, 1, 1]
+    assert r["reason"][0] == abi.LC_REASON_MALFORMED and ctx.stats()["n_malformed"] == 1
+    _, o = oracle.check(ops[off[1]:], off[1:] - off[1], algo=oracle.JIT)
+    assert (r["verdict"][1:] == o["verdict"]).all() and (r["fail_op"][1:] == o["fail_op"]).all()

@@ -24,18 +24,29 @@ def test_library_exports_every_declared_symbol():
     assert set(names) == {
         "lc_open", "lc_check", "lc_check_device", "lc_last_stats", "lc_last_error",
         "lc_close", "lc_default_opts", "lc_plan_partition", "lc_abi_version",
+        "lc_check_ex", "lc_check_device_ex", "lc_key_cost", "lc_build_id",
         "lc_synth_register", "lc_synth_key", "lc_edn_parse", "lc_edn_n_keys", "lc_edn_n_ops",
         "lc_edn_n_events", "lc_edn_ops", "lc_edn_key_off", "lc_edn_key", "lc_edn_op_text",
         "lc_edn_value", "lc_edn_free"}
     for n in names:
         assert hasattr(lib, n), n
-    assert abi.lib().lc_abi_version() == 1
+    assert abi.lib().lc_abi_version() == 2
 
 
 def test_struct_sizes():
     assert abi.RESULT_DTYPE.itemsize == 40
     assert ctypes.sizeof(abi.LcOpts) == 40
-    assert ctypes.sizeof(abi.LcSynthParams) == 48
+    assert ctypes.sizeof(abi.LcSynthParams) == 56
+    assert ctypes.sizeof(abi.LcStats) == 104
+    assert ctypes.sizeof(abi.LcAux) == 16
+
+
+def test_library_built_from_this_tree():
+    """lc_build_id() names the sources the loaded library was built from;
+    abi.lib() refuses a library whose id differs from this tree's (tests,
+    smoke() and bench.py can never run a stale binary)."""
+    built = abi.lib().lc_build_id().decode()
+    assert built == abi.source_build_id() and len(built) == 16
 
 
 def test_open_without_gpu_fails_loudly():
@@ -149,6 +160,38 @@ def test_plan_partition_balanced_and_contiguous():
         assert b[0] == 0 and b[-1] == 1000 and (np.diff(b) >= 0).all()
         cost = [(off[b[i + 1]] - off[b[i]]) + 64 * (b[i + 1] - b[i]) for i in range(parts)]
         assert max(cost) - min(cost) <= 2 * (500 + 64)  # one key per boundary
+
+
+def test_key_cost_follows_the_tier():
+    """lc_key_cost prices a key by the tier that will decide it: version-
+    pinned clean keys by their records, crash-heavy keys (gap tier) several
+    times more, version-less keys (frontier search) far more."""
+    clean, off, _, _ = abi.synth(4, 200, concurrency=10, seed=1)
+    crash, _, _, _ = abi.synth(4, 200, concurrency=10, p_info=0.2, seed=1)
+    nover = clean.copy()
+    nover[:, 3] = -1
+    c = [abi.key_cost(x, off) for x in (clean, crash, nover)]
+    assert np.allclose(c[0], 200 + 64)
+    assert (c[1] > 4 * c[0]).all() and (c[2] > 20 * c[1]).all()
+
+
+def test_plan_partition_is_crash_aware():
+    """A batch whose crash-heavy keys are clustered at the front: splitting by
+    records would give the first device all of them; the cost-aware split
+    gives it fewer keys, and every part's cost is within one key of equal."""
+    heavy, hoff, _, _ = abi.synth(250, 400, concurrency=20, p_info=0.2, seed=2)
+    light, loff, _, _ = abi.synth(750, 400, concurrency=20, seed=3)
+    ops = np.concatenate([heavy, light])
+    off = np.concatenate([hoff, loff[1:] + hoff[-1]])
+    cost = abi.key_cost(ops, off)
+    for parts in (2, 4, 8):
+        b = abi.plan_partition(off, parts, ops=ops)
+        assert b[0] == 0 and b[-1] == 1000 and (np.diff(b) >= 0).all()
+        per = [cost[b[i]:b[i + 1]].sum() for i in range(parts)]
+        assert max(per) - min(per) <= 2 * cost.max()
+        naive = abi.plan_partition(off, parts)
+        assert b[1] < naive[1]  # fewer of the clustered heavy keys on device 0
+    assert abi.plan_partition(off, 2, ops=ops)[1] < 250
 
 
 def test_kat_file_consistent():
