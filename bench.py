@@ -4,10 +4,13 @@
 One step = one lc_check_device() call over one batch of resident synthetic
 register histories: by default the C2 workload of BASELINE.json configs[1],
 10k keys x 1k ops (packed records), concurrency 20, valid CAS-register+version
-histories, on one MI355X.  For N GPUs (torchrun, one rank per GPU) every rank
-checks its own 10k-key batch (distinct seeds): per-GPU work is fixed
-("scaling": "weak") and keys are independent, so the data path has no
-collective; the only cross-rank traffic is the timing barrier/max.
+histories, on one MI355X.  For N GPUs (torchrun, one rank per GPU) it is
+BASELINE configs[2] (C3): every rank builds the SAME seeded 10k-key batch,
+lc_plan_partition splits it into N contiguous key ranges of equal estimated
+cost (lc_key_cost), and each rank checks its own range: total work is fixed
+("scaling": "strong").  Keys are independent (register.clj:108), so the
+data path has no collective; the only cross-rank traffic is the timing
+barrier/max and the gather of per-rank ranges and times (RCCL).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with the
 roofline of the dominant kernel (fast_tier_kernel on C2; HIP events on its
@@ -88,21 +91,27 @@ def main():
             os.close(saved)
     dev = torch.device("cuda", local)
 
-    # ---- workload (seeded per rank: configs[1] = C2, seed 0x5EED0002)
-    seed = 0x5EED0002 + 0x1000 * rank
+    # ---- workload: configs[1] = C2, seed 0x5EED0002, the same on every
+    # rank; configs[2] = C3: rank r checks its cost-balanced key range
+    from jepsen.etcd_amd import dist as D
+    seed = 0x5EED0002
     ops, key_off, _, n_inv = abi.synth(args.keys, args.ops_per_key,
                                        concurrency=args.concurrency,
                                        p_info=args.p_info, seed=seed)
-    n_ops = int(key_off[-1])
-    d_ops = torch.from_numpy(ops).to(dev)
-    d_off = torch.from_numpy(key_off).to(dev)
-    d_out = torch.zeros(args.keys * abi.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    bounds = abi.plan_partition(key_off, world, ops=ops)
+    ka, kb = int(bounds[rank]), int(bounds[rank + 1])
+    my_keys = kb - ka
+    n_ops = int(key_off[kb] - key_off[ka])  # this rank's records
+    d_ops = torch.from_numpy(np.ascontiguousarray(ops[key_off[ka]:key_off[kb]])).to(dev)
+    d_off = torch.from_numpy(np.ascontiguousarray(key_off[ka:kb + 1])).to(dev)
+    d_out = torch.zeros(max(my_keys, 1) * abi.RESULT_DTYPE.itemsize, dtype=torch.uint8,
+                        device=dev)
     stream = torch.cuda.current_stream(dev)
     ctx = abi.Context(device_mask=1 << local)
 
     # one step = one lc_check_device call (+ its per-call stats), arguments
     # converted once
-    step = ctx.bind_check_device(d_ops.data_ptr(), d_off.data_ptr(), args.keys,
+    step = ctx.bind_check_device(d_ops.data_ptr(), d_off.data_ptr(), my_keys,
                                  d_out.data_ptr(), stream=stream.cuda_stream,
                                  opts=abi.default_opts(), stats=abi.LcStats())
 
@@ -123,10 +132,15 @@ def main():
         njit.append(s.n_jit_keys)
         cms.append(s.total_ms)
     torch.cuda.synchronize()
+    own = time.perf_counter() - t0  # this rank's own steps, before waiting for the others
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    res = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
+    res = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)[:my_keys]
+    ranks = (D.gather_rows([rank, ka, kb, n_ops, own * 1e3 / args.steps,
+                            float(np.mean(kms))])
+             if distributed else
+             [[0, ka, kb, n_ops, own * 1e3 / args.steps, float(np.mean(kms))]])
     elapsed, (total_ops, n_valid, n_invalid, n_unknown) = reduce_run(
         elapsed, n_ops, res, distributed, dev)
 
@@ -138,7 +152,7 @@ def main():
     # dominates (invalid / crash-heavy workloads)
     dom, dom_ms = max((("fast_tier_kernel", fast_ms), ("gap_tier_kernel", gap_ms),
                        ("lds_tier_kernel", jit_ms)), key=lambda t: t[1])
-    algo_bytes = ALGO_BYTES_PER_OP * n_ops + ALGO_BYTES_PER_KEY * args.keys
+    algo_bytes = ALGO_BYTES_PER_OP * n_ops + ALGO_BYTES_PER_KEY * my_keys
     achieved = algo_bytes / (dom_ms * 1e-3) / 1e9
     traffic = l2_hit = None
     if os.path.exists(args.traffic_json):
@@ -159,21 +173,27 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (seeded register+version histories, lc_synth_register)",
         "config": {
-            "workload": "C2: %d keys x %d ops/key (packed records), concurrency %d, "
-                        "valid CAS-register+version histories, per GPU"
+            "workload": ("C2: %d keys x %d ops/key (packed records), concurrency %d, "
+                         "valid CAS-register+version histories" if world == 1 else
+                         "C3: the C2 batch (%d keys x %d ops/key, concurrency %d) sharded "
+                         "by estimated cost over the GPUs")
                         % (args.keys, args.ops_per_key, args.concurrency),
-            "keys_per_gpu": args.keys,
+            "keys": args.keys,
             "ops_per_key": args.ops_per_key,
-            "invocations_per_gpu_incl_fail": int(n_inv),
+            "invocations_incl_fail": int(n_inv),
             "concurrency": args.concurrency,
             "p_info": args.p_info,
-            "parallelism": "keys sharded, 1 rank per GPU, no data-path collective",
+            "parallelism": "keys sharded by lc_plan_partition, 1 rank per GPU, "
+                           "no data-path collective",
         },
+        "ranks": [{"rank": int(r[0]), "keys": [int(r[1]), int(r[2])], "records": int(r[3]),
+                   "ms_per_step": r[4], "kernel_ms": r[5]} for r in ranks],
+        "rank_ms_per_step_min_max": [min(r[4] for r in ranks), max(r[4] for r in ranks)],
         "roofline": {
             "bound": "hbm",
             "achieved": achieved,
@@ -258,14 +278,15 @@ def host_leg(ctx, abi, ops, key_off, n_inv):
 
 
 def hot_key(ctx, abi):
-    """BASELINE configs[3]: one key, 5k ops, concurrency 50, 20 % :info,
+    """BASELINE configs[3]: one key, 5k ops, concurrency 50, 20 % :info
+    (exactly 1,000 crashed writes/CAS of 5,000 records: info_frac 0.2),
     decided by the gap tier (every frontier search, knossos's included, runs
     out of budget on it); also the same shape with injected anomalies, whose
     counterexample search (multisection rounds over the whole GPU) is timed
     too.  Not part of `value`; median of 5 calls after one warm-up."""
     out = {}
-    for tag, anom, seed in (("valid", 0.0, 0x5EED0004), ("invalid", 1.0, 1006)):
-        ops, off, _, n_inv = abi.synth(1, 5000, concurrency=50, p_info=0.2,
+    for tag, anom, seed in (("valid", 0.0, 0x5EED0004), ("invalid", 1.0, 1007)):
+        ops, off, _, n_inv = abi.synth(1, 5000, concurrency=50, p_info=0.2, info_frac=0.2,
                                        p_anomaly=anom, seed=seed)
         times, gap = [], []
         for _ in range(6):
@@ -281,7 +302,8 @@ def hot_key(ctx, abi):
         if tag == "invalid":
             out[tag]["fail_op"] = int(r["fail_op"][0])
     v = out["valid"]
-    return dict(v, workload="C4: 1 key x 5000 ops, concurrency 50, p_info 0.2 (host buffers)",
+    return dict(v, workload="C4: 1 key x 5000 ops, concurrency 50, 20 % (1000) crashed "
+                            "writes/CAS (host buffers)",
                 invalid=out["invalid"])
 
 
@@ -402,8 +424,8 @@ def model_leg(ctx, abi):
 
 def reduce_run(elapsed, n_ops, res, distributed, dev):
     """Whole-job numbers: the MAX of the ranks' timed-region wall times and
-    the SUM of their checked ops and verdict counts (weak scaling: every rank
-    checks its own batch)."""
+    the SUM of their checked ops and verdict counts (every rank checks its
+    own key range of the one batch, so the sums are the whole batch's)."""
     import torch
     import torch.distributed as dist
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -415,6 +437,16 @@ def reduce_run(elapsed, n_ops, res, distributed, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(counts)
     return float(t.item()), [int(v) for v in counts.tolist()]
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def cpu_baseline(args, ops, key_off, gpu_res):
@@ -441,6 +473,9 @@ def cpu_baseline(args, ops, key_off, gpu_res):
         "value": best[0],
         "unit": "ops/s",
         "cores": args.cpu_threads,
+        "host_nproc": os.cpu_count(),
+        "cpu_model": cpu_model(),
+        "cores_note": "threads used = this box's CPU share; host_nproc counts the whole machine",
         "kind": "port",
         "sample": "%d keys x %d ops of the same C2 workload (%d records), "
                   "oracle/%s restatement of knossos (faster of jit/wgl), %.1f s"

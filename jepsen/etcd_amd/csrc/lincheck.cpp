@@ -67,6 +67,10 @@ constexpr int kHbmCoop4MaxKeys = 4096;
 constexpr int kGapMaxWG = 1024;
 constexpr size_t kGapWsBytes = size_t(1) << 30;
 constexpr int kGapLdsFull = 48 << 10;
+// few keys (at most this many workgroups): occupancy does not matter, so a
+// whole-key decision may hold a large matching in LDS (gfx950: 160 KB per CU)
+constexpr int kGapLdsFew = 128 << 10;
+constexpr int64_t kGapFewKeys = 512;
 constexpr int64_t kGapSkelLdsMax = 78 << 10;  // two such workgroups per CU (160 KB)
 constexpr int kGapLdsProbe = 48 << 10;
 constexpr int kGapMaxRounds = 64;
@@ -313,11 +317,13 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     job.bisect = d.h_status->max_len < kGapProbeMinLen || 2 * n_jit > wg_cap;
     // LDS per workgroup: the longest key's skeleton (68 B per record) plus
     // 8 KB for its matching when that stays within kGapSkelLdsMax (two
-    // workgroups per CU); else room for the matching alone (56 B per record
-    // at worst), up to kGapLdsFull
+    // workgroups per CU); else room for the matching alone (80 B per record
+    // plus its class table at worst), up to kGapLdsFull, or kGapLdsFew when
+    // there are few keys
     const int64_t skel = 68 * gap_cap + (8 << 10);
+    const int64_t match_cap = n_jit <= kGapFewKeys ? kGapLdsFew : kGapLdsFull;
     job.lds_bytes = (int)(skel <= kGapSkelLdsMax ? skel
-                                                 : std::min<int64_t>(kGapLdsFull, 56 * gap_cap));
+                                                 : std::min<int64_t>(match_cap, 80 * gap_cap + 1040));
     // LC_GAP_LDS=0 (tests): keep every matching in the HBM workspace
     const char *lds_env = getenv("LC_GAP_LDS");
     const bool no_lds = lds_env && lds_env[0] == '0';

@@ -33,16 +33,17 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port,
                             rank=rank, world_size=world)
     ops, off, lab, _ = abi.synth(120, 150, concurrency=10, p_anomaly=0.25, seed=31)
-    a, b = D.shard(off, rank, world)
+    a, b = D.shard(off, rank, world, ops=ops)   # bench.py's C3 split
     sub, soff = D.slice_keys(ops, off, a, b)
     _, r = oracle.check(sub, soff, algo=oracle.JITC)   # stand-in for the GPU
     verd, fail = D.gather_results(r, (a, b), len(off) - 1)
     el, counts = bench.reduce_run(0.5 + rank, len(sub), r, world, torch.device("cpu"))
+    rows = D.gather_rows([rank, a, b, len(sub)])
     if rank == 0:
         _, full = oracle.check(ops, off, algo=oracle.JITC)
         out.put(((verd == full["verdict"]).all(), (fail == full["fail_op"]).all(),
                  D.merge_verdicts(verd), el, counts, int(off[-1]),
-                 int((full["verdict"] == 1).sum())))
+                 int((full["verdict"] == 1).sum()), rows))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -58,7 +59,10 @@ def test_two_rank_shard_gather_and_reduce():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ok_v, ok_f, merged, el, counts, n_ops, n_valid = res
+    ok_v, ok_f, merged, el, counts, n_ops, n_valid, rows = res
+    # the ranks' key ranges tile the batch, contiguously
+    assert rows[0][1] == 0 and rows[0][2] == rows[1][1] and rows[1][2] == 120
+    assert rows[0][3] + rows[1][3] == n_ops
     assert ok_v and ok_f
     assert merged is False            # the batch holds injected anomalies
     assert el == 1.5                  # max over ranks

@@ -11,8 +11,9 @@ import numpy as np  # noqa: E402
 from jepsen.etcd_amd import abi  # noqa: E402
 
 CFGS = {
-    "C4": dict(n_keys=1, ops_per_key=5000, concurrency=50, p_info=0.2, seed=0x5EED0004),
-    "C4x": dict(n_keys=1, ops_per_key=5000, concurrency=50, p_info=0.2, p_anomaly=1.0, seed=1006),
+    "C4": dict(n_keys=1, ops_per_key=5000, concurrency=50, p_info=0.2, info_frac=0.2, seed=0x5EED0004),
+    "C4x": dict(n_keys=1, ops_per_key=5000, concurrency=50, p_info=0.2, info_frac=0.2, p_anomaly=1.0, seed=1007),
+    "C4r1": dict(n_keys=1, ops_per_key=5000, concurrency=50, p_info=0.2, seed=0x5EED0004),
     "C5": dict(n_keys=1000, ops_per_key=200, concurrency=10, p_anomaly=0.1, seed=0x5EED0005),
     "C5big": dict(n_keys=10000, ops_per_key=200, concurrency=10, p_info=0.1, p_anomaly=0.1, seed=77),
     "C2info": dict(n_keys=10000, ops_per_key=1000, concurrency=20, p_info=0.05, seed=0x5EED0012),
