@@ -38,6 +38,8 @@
 
 #include "kernels.h"
 #include "records.h"
+#include "wave.h"
+#include "gapmatch.h"
 
 namespace lcdev {
 namespace {
@@ -61,28 +63,6 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
   return ((uint64_t)hi << 32) | lo;
 }
-// Number of set bits of m in lanes below this one (prefix-sum compaction).
-__device__ __forceinline__ int lanes_below(uint64_t m) {
-  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
-// Minimum of v over the 64 lanes as a wave-uniform (SGPR) value: four DPP
-// min steps inside each 16-lane row (quad_perm [1,0,3,2], quad_perm
-// [2,3,0,1], row_half_mirror, row_mirror), then the four row minima are read
-// with v_readlane and combined on the scalar unit.  No LDS round trip.
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-  v = umin(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
-  v = umin(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
-  v = umin(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));
-  v = umin(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));
-  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
-  const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
-  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
-  const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
-  return umin(umin(r0, r1), umin(r2, r3));
-}
-
 // Bitwise AND of a 64-bit value over the 64 lanes (wave-uniform result).
 __device__ __forceinline__ uint32_t wave_and_u32(uint32_t v) {
   v &= (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false);
@@ -1077,9 +1057,10 @@ __device__ __forceinline__ void fast_tier_handoff(int64_t key, int32_t *flags, K
 struct FastLds {
   uint32_t A[kFastMax + 4], B[kFastMax];  // 16-byte aligned rows (timing check)
   int Val[kFastMax];
-  uint16_t Own[kFastMax];
+  uint16_t Own[kFastMax + 4];  // 0xFFFF: no mutation placed (cleared with A/B)
   uint32_t wsum[kFastWaves];  // per wave: mutations placed | inel << 16 | bad << 17
   uint32_t wbad[kFastWaves];  // per wave: 1 if a CAS/read/timing condition failed
+  int wg[4 * kFastWaves];     // crash-light path: per-wave words (below)
 };
 
 // One thread's records of one key, as loaded (decoded only once they land).
@@ -1157,22 +1138,276 @@ __device__ __forceinline__ bool timing_fails(const FastLds &s, int M, int tid) {
           (int)(umax(ex, p2) > b.z) | (int)(umax(ex, p3) > b.w)) != 0;
 }
 
+// ---------------------------------------------------------------------------
+// Crash-light keys decided in place.  A key whose only obstacle to the
+// version order is a few crashed writes/CAS (a partition nemesis leaves a
+// few percent of them, bench.py's crash_leg) is the gap tier's case, but its
+// records are already in registers and its pinned positions already folded
+// into A / B / Val / Own: the workgroup finishes the gap tier's decision
+// here (gap_tier.hip, same procedure and same matching, gapmatch.h) instead
+// of handing the key over for a second record pass.
+//   * unheld positions below M = max(last pinned position + 1, last read
+//     version) are the gaps; Val of a gap holds its value requirement,
+//     claimed with atomicCAS by the reads of the version it writes and by a
+//     pinned CAS right after it (two different claims: invalid);
+//   * timing is the version order's own check over A / B (gap positions
+//     carry the read bounds), and a gap's deadline is min(B[k..M-1]);
+//   * the optional ops (crashed writes/CAS) and the gaps are compacted in
+//     call / position order into dynamic LDS and wave 0 runs the gap
+//     tier's matching over them.
+// A valid key is decided here (and its witness completed: the matched ops'
+// positions); anything else — invalid (the gap tier bisects for the fail
+// op), more than kFgMaxGaps gaps or kFgMaxOps optional ops, a crashed op
+// that carries a version, the branch budget — is handed over as before.
+constexpr int kFgMaxGaps = 48;
+constexpr int kFgMaxOps = 96;
+// dynamic LDS: the matching region at its largest (gapmatch.h layout without
+// the class table: 16 B + 5 ints per gap, 16 B + 7 ints per op), then the
+// optional ops' record indices and the branch stack (gap, value)
+constexpr int kFgMatchBytes = 36 * kFgMaxGaps + 44 * kFgMaxOps;
+constexpr int kFgLdsBytes = kFgMatchBytes + 4 * kFgMaxOps + 8 * kFgMaxGaps;
+
+// Exclusive suffix minimum over the workgroup's threads (those above this
+// one), with the wave totals through s.wg[8..11]; one barrier.
+__device__ __forceinline__ uint32_t fg_suffix_min_excl(uint32_t v, FastLds &s) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  uint32_t incl = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_down((int)incl, o);
+    if (lane + o < kWave) incl = umin(incl, y);
+  }
+  if (lane == 0) s.wg[8 + w] = (int)incl;
+  uint32_t excl = (uint32_t)__shfl_down((int)incl, 1);
+  if (lane == kWave - 1) excl = kNever;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kFastWaves; j++)
+    if (j > w) excl = umin(excl, (uint32_t)s.wg[8 + j]);
+  return excl;
+}
+
+// Exclusive prefix sum over the workgroup's threads, wave totals through
+// s.wg[12..15]; *total = the sum.  Shares the caller's next barrier: the
+// caller reads the result only after one.
+__device__ __forceinline__ int fg_prefix_wave(int v, FastLds &s) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == kWave - 1) s.wg[12 + w] = incl;
+  return incl - v;
+}
+
+// Returns true when the key was decided valid here; false: hand it over.
+// The records are read again (L2/MALL-hot: the workgroup loaded them just
+// before) rather than kept in registers across the branch: the version
+// order's pass 2 holds 4 x 48 B per thread, and keeping them live on this
+// path too would cost the kernel its 7-waves-per-SIMD occupancy.
+__device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops,
+                         const KParams &p, FastLds &s, lc_key_result *__restrict__ out,
+                         int32_t *__restrict__ wit, int32_t *__restrict__ kind) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  const int64_t base_idx = kops[0].call;
+  const int V0 = p.init_ver, init = p.init_val;
+  // unheld positions start with no value requirement
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int k = 4 * tid + j;
+    if (k < n && s.Own[k] == 0xFFFF) s.Val[k] = kAny;
+  }
+  __syncthreads();
+  // pass G1: duplicates, value claims, the extent M, optional ops per chunk
+  int maxpos = -1, maxread = 0, inv = 0, giveup = 0;
+  uint64_t optm[kPer];
+  auto claim = [&](int k, int v) {  // value v required at version V0+k+1 (k >= 0)
+    if (s.Own[k] != 0xFFFF) {
+      inv |= s.Val[k] != v;
+    } else {
+      const int old = atomicCAS(&s.Val[k], kAny, v);
+      inv |= (old != kAny) & (old != v);
+    }
+  };
+#pragma unroll 1  // one record in flight: this path must not raise the kernel's VGPR count
+  for (int u = 0; u < kPer; u++) {
+    const int r = tid + u * kFastThreads;
+    bool opt = false;
+    if (r < n) {
+      const Rec d = decode(load_raw(kops, r, n), base_idx);
+      if (d.f == LC_F_READ) {
+        if (d.ret != kNever && d.ver != -1) {  // (pass 1 handed [nil x] reads over)
+          const int k = d.ver - V0;
+          maxread = max(maxread, k);
+          if (d.val != -1) {
+            if (k == 0) inv |= d.val != init;
+            else claim(k - 1, d.val);
+          }
+        }
+      } else if (d.ret == kNever) {
+        opt = d.ver == -1;
+        giveup |= d.ver != -1;  // a crashed op pinned to a version: the gap tier's
+      } else {
+        const int pos = d.ver - V0 - 1;
+        maxpos = max(maxpos, pos);
+        inv |= s.Own[pos] != r;  // two mutations on one version
+        if (d.f == LC_F_CAS) {
+          if (pos == 0) inv |= d.exp != init;
+          else claim(pos - 1, d.exp);
+        }
+      }
+    }
+    optm[u] = __ballot(opt);
+  }
+  // per wave: extent, flags, optional ops per chunk
+  const uint32_t wmax = wave_max_u32((uint32_t)max(maxpos + 1, maxread));
+  const bool wflag = __ballot(inv | giveup) != 0;
+  if (lane == 0) {
+    s.wg[w] = (int)(wmax | (wflag ? 0x80000000u : 0u));
+#pragma unroll
+    for (int u = 0; u < kPer; u++)
+      reinterpret_cast<uint8_t *>(&s.wg[4 + w])[u] = (uint8_t)__popcll(optm[u]);
+  }
+  __syncthreads();
+  const int4 w0 = *reinterpret_cast<const int4 *>(&s.wg[0]);
+  if ((w0.x | w0.y | w0.z | w0.w) < 0) return false;  // invalid or not this path's
+  const int M = max(max(w0.x, w0.y), max(w0.z, w0.w));
+  // optional-op slots: chunk-major, then wave, then lane (= record order)
+  int n_opt = 0;
+#pragma unroll
+  for (int u = 0; u < kPer; u++)
+#pragma unroll
+    for (int j = 0; j < kFastWaves; j++) n_opt += reinterpret_cast<const uint8_t *>(&s.wg[4 + j])[u];
+  if (n_opt > kFgMaxOps) return false;
+  // deadlines: Uh[k] = min(B[k..M-1]) for this thread's positions 4t..4t+3
+  uint32_t bmin = kNever;
+  int gapc = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int k = 4 * tid + j;
+    bmin = umin(bmin, k < M ? s.B[k] : kNever);
+    gapc += (k < M) && s.Own[k] == 0xFFFF;
+  }
+  const int gpre = fg_prefix_wave(gapc, s);
+  const uint32_t after = fg_suffix_min_excl(bmin, s);
+  // (the barrier inside fg_suffix_min_excl also publishes s.wg[12..15])
+  int G = 0, gbase = gpre;
+#pragma unroll
+  for (int j = 0; j < kFastWaves; j++) {
+    G += s.wg[12 + j];
+    if (j < w) gbase += s.wg[12 + j];
+  }
+  // the timing verdict, gathered per wave (s.wbad is free on this path)
+  const bool tbad = __ballot(timing_fails(s, M, tid)) != 0;
+  if (lane == 0) s.wbad[w] = tbad;
+  if (G > kFgMaxGaps) return false;
+  // compact gaps and optional ops into the matching region (lds_dyn)
+  Cmp<true> c;
+  c.ws = nullptr;
+  c.G = G;
+  c.n_opt = n_opt;
+  c.cap = 0;
+  c.moff = 0;
+  int *opt_rec = reinterpret_cast<int *>(lds_dyn) + kFgMatchBytes / 4;
+  int *brPos = opt_rec + kFgMaxOps, *brVal = brPos + kFgMaxGaps;
+  {
+    // this thread's positions high to low: the suffix minimum runs down
+    uint32_t uh = after;
+    int gi = gbase + gapc;
+#pragma unroll
+    for (int j = 3; j >= 0; j--) {
+      const int k = 4 * tid + j;
+      uh = umin(uh, k < M ? s.B[k] : kNever);
+      if ((k < M) && s.Own[k] == 0xFFFF) {
+        gi--;
+        c.gaps()[gi] = make_int4((int)uh, s.Val[k], k == 0 ? init : s.Val[k - 1], k);
+        c.at(aMG, gi) = -1;
+      }
+    }
+  }
+  int obase = 0;
+#pragma unroll 1
+  for (int u = 0; u < kPer; u++) {
+    int my = obase;  // slots before this wave's ops of chunk u
+#pragma unroll
+    for (int j = 0; j < kFastWaves; j++) {
+      const int cnt = reinterpret_cast<const uint8_t *>(&s.wg[4 + j])[u];
+      my += j < w ? cnt : 0;
+      obase += cnt;
+    }
+    if ((optm[u] >> lane) & 1) {
+      const int o = my + lanes_below(optm[u]);
+      const Rec d = decode(load_raw(kops, tid + u * kFastThreads, n), base_idx);
+      c.ops()[o] = make_int4((int)d.call, d.val, d.f == LC_F_CAS ? d.exp : kAny, -1);
+      c.at(aMO, o) = -1;
+      c.at(aVis, o) = 0;
+      opt_rec[o] = tid + u * kFastThreads;
+    }
+  }
+  __syncthreads();
+  {
+    const uint4 tb = *reinterpret_cast<const uint4 *>(s.wbad);
+    if (tb.x | tb.y | tb.z | tb.w) return false;
+  }
+  if (G > n_opt) return false;  // invalid: the gap tier names the fail op
+  int res = GD_VALID;
+  int64_t nodes = 0;
+  if (G > 0 && w == 0) {
+    ClsSt cst;  // (generic matching: at most kFgMaxOps < kClsMinOps optional ops)
+    cst.K = 0;
+    res = match_branch_m<true, false>(c, G, n_opt, brPos, brVal, &nodes, cst);
+    if (lane == 0) s.wg[0] = res;
+    if (res == GD_VALID && wit)
+      for (int gi = lane; gi < G; gi += kWave) wit[opt_rec[c.at(aMG, gi)]] = c.gaps()[gi].w;
+  }
+  __syncthreads();
+  if (G > 0) res = s.wg[0];
+  if (res != GD_VALID) return false;
+  if (tid == 0) {
+    out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, nodes, G};
+    if (kind) kind[key] = LC_WITNESS_FULL;
+  }
+  return true;
+}
+
+// Where a key the workgroup does not decide goes: the version-order tier
+// flags it for the handoff compaction; the crash-light pass (LIGHT, over the
+// compacted list) appends it to the gap tier's list.  wit / kind: lc_aux.
+struct FastSinks {
+  int32_t *flags;
+  KStatus *status;
+  int32_t *h_handoff;
+  int32_t *pass;
+  int32_t *wit;
+  int32_t *kind;
+};
+
+template <bool LIGHT>
+__device__ __forceinline__ void fast_pass_on(int64_t key, const FastSinks &o, bool jit_only = false) {
+  if constexpr (LIGHT)
+    o.pass[atomicAdd(&o.status->n_gap2, 1)] = (int32_t)key;  // few: invalid / large keys
+  else
+    fast_tier_handoff(key, o.flags, o.status, o.h_handoff, jit_only);
+}
+
+
 // Decide one key (records in b when 0 < n64 <= kFastMax) or hand it over.
 // Three barriers: after the LDS init, after pass 1, before thread 0 reads
 // the per-wave verdicts.
+template <bool LIGHT>
 __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *__restrict__ kops,
                                          const FastRecs &b, const KParams &p, FastLds &s,
-                                         lc_key_result *__restrict__ out,
-                                         int32_t *__restrict__ flags,
-                                         KStatus *__restrict__ status,
-                                         int32_t *__restrict__ h_handoff) {
+                                         lc_key_result *__restrict__ out, const FastSinks &o,
+                                         int32_t *__restrict__ wit) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   if (n64 <= 0 || n64 > kFastMax) {
     if (tid == 0) {
       if (n64 == 0)
         out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 0};
       else
-        fast_tier_handoff(key, flags, status, h_handoff);
+        fast_pass_on<LIGHT>(key, o);
     }
     return;
   }
@@ -1194,6 +1429,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
   if (4 * tid <= n) {
     reinterpret_cast<uint4 *>(s.A)[tid] = make_uint4(0, 0, 0, 0);  // nothing constrains t_k from below
     reinterpret_cast<uint4 *>(s.B)[tid] = make_uint4(kNever, kNever, kNever, kNever);
+    reinterpret_cast<uint2 *>(s.Own)[tid] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
   }
   if (tid == 0) s.A[kFastMax] = 0;
   __syncthreads();
@@ -1258,8 +1494,14 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
   // 0..M-1 each held once (pass 2 checks both)
   const int M = (int)((ws.x & 0xFFFF) + (ws.y & 0xFFFF) + (ws.z & 0xFFFF) + (ws.w & 0xFFFF));
   if (wor >> 16) {  // ineligible or a version out of range: hand over
-    if (tid == 0)
-      fast_tier_handoff(key, flags, status, h_handoff, (wor >> 18) & 1);
+    // crash-light pass: crashed writes/CAS are the only obstacle
+    if constexpr (LIGHT)
+      if ((wor >> 16) == 1 && fast_gap(key, n, kops, p, s, out, wit, o.kind)) return;
+    if (tid == 0) fast_pass_on<LIGHT>(key, o, (wor >> 18) & 1);
+    return;
+  }
+  if constexpr (LIGHT) {  // eligible here too: the version order found it invalid
+    if (tid == 0) fast_pass_on<LIGHT>(key, o);
     return;
   }
   // pass 2: positions, duplicates, CAS expectations and read claims against
@@ -1294,7 +1536,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     if (!(wb.x | wb.y | wb.z | wb.w))
       out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
     else
-      fast_tier_handoff(key, flags, status, h_handoff);
+      fast_pass_on<LIGHT>(key, o);
   }
 }
 
@@ -1313,7 +1555,39 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
   const lc_op *kops = ops + (beg - key_off[0]);
   FastRecs r;
   if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
-  fast_key(key, end - beg, kops, r, p, s, out, flags, status, h_handoff);
+  const FastSinks o{flags, status, h_handoff, nullptr, nullptr, nullptr};
+  fast_key<false>(key, end - beg, kops, r, p, s, out, o, nullptr);
+}
+
+// Crash-light pass over the keys the version-order tier handed to the gap
+// tier (status->n_jit of them, written by the compaction launched just
+// before: no host round trip in between).  Same decision as the version-
+// order tier plus the in-place gap decision; what it cannot decide goes to
+// `pass` (status->n_gap2) for the gap tier.  Grid-stride over the list.
+// 4 waves per SIMD (at most 128 VGPRs): left alone the compiler takes 138
+// (3 waves); 4 has no VGPR spills and decides bench.py's crash_leg in
+// 0.24 ms against 0.29 ms (5 and 6 waves spill: 0.33 / 0.36 ms).
+#ifndef LC_LIGHT_WPE
+#define LC_LIGHT_WPE 4
+#endif
+#define LC_LIGHT_ATTR __attribute__((amdgpu_waves_per_eu(LC_LIGHT_WPE, 8)))
+__global__ __launch_bounds__(kFastThreads) LC_LIGHT_ATTR void gap_light_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
+    const int32_t *__restrict__ keys, const KParams p, lc_key_result *__restrict__ out,
+    const FastSinks o) {
+  __shared__ FastLds s;
+  const int32_t n_list = __hip_atomic_load(&o.status->n_jit, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+  for (int t = blockIdx.x; t < n_list; t += gridDim.x) {
+    const int64_t key = keys[t];
+    const int64_t beg = key_off[key], end = key_off[key + 1];
+    const lc_op *kops = ops + (beg - key_off[0]);
+    FastRecs r;
+    if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
+    fast_key<true>(key, end - beg, kops, r, p, s, out, o,
+                   o.wit ? o.wit + (beg - key_off[0]) : nullptr);
+    __syncthreads();  // the next key reuses the shared memory
+  }
 }
 
 // Workspace layout per wave: 3 regions of cap Cfg, 2 tables of 2*cap Cfg,
@@ -1520,6 +1794,20 @@ hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
   if (n_keys <= 0) return hipSuccess;
   hipLaunchKernelGGL(fast_tier_kernel, dim3((unsigned)n_keys), dim3(kFastThreads), 0,
                      stream, d_ops, d_key_off, p, d_out, d_flags, d_status, h_handoff);
+  return hipGetLastError();
+}
+
+hipError_t launch_gap_light(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
+                            int64_t max_keys, const KParams &p, lc_key_result *d_out,
+                            int32_t *d_pass, KStatus *d_status, int32_t *d_witness,
+                            int32_t *d_witness_kind, hipStream_t stream) {
+  if (max_keys <= 0) return hipSuccess;
+  const FastSinks o{nullptr, d_status, nullptr, d_pass, d_witness, d_witness_kind};
+  // the matching region is dynamic LDS; 7 workgroups per CU x 256 CUs stay
+  // resident, so a larger grid only adds workgroups that find no key
+  const int64_t wgs = std::min<int64_t>(max_keys, 7 * 256);
+  hipLaunchKernelGGL(gap_light_kernel, dim3((unsigned)wgs), dim3(kFastThreads),
+                     (unsigned)kFgLdsBytes, stream, d_ops, d_key_off, d_keys, p, d_out, o);
   return hipGetLastError();
 }
 

@@ -29,6 +29,7 @@ struct KStatus {
   int32_t n_open;       // gap tier: counterexample intervals still open after a round
   int32_t max_lds;      // gap tier: largest matching footprint (bytes) of a full decision
   int32_t any_handoff;  // fast tier: some key was handed over (read before the host store)
+  int32_t n_gap2;       // crash-light pass: keys it passes on to the gap tier
 };
 
 constexpr int kWave = 64;
@@ -56,6 +57,16 @@ hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_flags,
                             KStatus *d_status, int32_t *h_handoff, hipStream_t stream);
+// Crash-light pass (check_kernel.hip, "Crash-light keys"): over the
+// compacted gap-tier list d_keys (status->n_jit keys, at most max_keys), a
+// key whose only obstacle is a few crashed writes/CAS is decided valid in
+// place (the gap tier's procedure, one record pass), completing its witness
+// (d_witness / d_witness_kind may be null); the others go to d_pass
+// (status->n_gap2) for the gap tier.
+hipError_t launch_gap_light(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
+                            int64_t max_keys, const KParams &p, lc_key_result *d_out,
+                            int32_t *d_pass, KStatus *d_status, int32_t *d_witness,
+                            int32_t *d_witness_kind, hipStream_t stream);
 // With witness_kind, every handed-over key's kind is reset to
 // LC_WITNESS_NONE (a later tier that certifies it sets it again).
 hipError_t launch_handoff_compact(int32_t *d_flags, const int64_t *d_key_off, int64_t n_keys,

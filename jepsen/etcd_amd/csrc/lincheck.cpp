@@ -101,6 +101,9 @@ struct Dev {
   size_t flags_cap = 0;
   int32_t *d_jit2 = nullptr;           // keys the gap tier passes on
   size_t jit2_cap = 0;
+  int32_t *d_gap2 = nullptr;           // keys the crash-light pass leaves to the gap tier
+  size_t gap2_cap = 0;
+  hipEvent_t el = nullptr;             // after the crash-light pass
   int32_t *d_gws = nullptr;            // gap-tier workspace
   size_t gws_cap = 0;
   char *d_cex = nullptr;               // gap-tier counterexample intervals + probes
@@ -216,6 +219,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   if (!rc) rc = ensure(c, &d.d_ovf2, &d.ovf2_cap, sizeof(int32_t) * (size_t)n_keys);
   if (!rc) rc = ensure(c, &d.d_jit, &d.jit_cap, sizeof(int32_t) * (size_t)n_keys);
   if (!rc) rc = ensure(c, &d.d_jit2, &d.jit2_cap, sizeof(int32_t) * (size_t)n_keys);
+  if (!rc) rc = ensure(c, &d.d_gap2, &d.gap2_cap, sizeof(int32_t) * (size_t)n_keys);
   const bool flags_new = d.flags_cap < sizeof(int32_t) * (size_t)n_keys || !d.d_flags;
   if (!rc) rc = ensure(c, &d.d_flags, &d.flags_cap, sizeof(int32_t) * (size_t)n_keys);
   if (rc) return rc;
@@ -232,6 +236,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
   d.status_dirty = true;
   float ms = 0;
+  bool light = false;  // the crash-light pass ran (its time is in gap_ms)
   int64_t n_jit = n_keys;
   const int32_t *jit_list = nullptr;
   const bool want_wit = wo.wit && wo.kind;
@@ -250,32 +255,50 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.ef));
     d.fast_ms = ms;
     n_jit = 0;
+    jit_list = d.d_jit;
     if (__atomic_load_n(d.h_handoff, __ATOMIC_ACQUIRE)) {
       HIP_TRY(c, lcdev::launch_handoff_compact(d.d_flags, d_off, n_keys, gap_on ? 1 : 0, d.d_jit,
                                                d.d_jit2, d.d_status, want_wit ? wo.kind : nullptr,
                                                st));
+      // the crash-light pass reads the list and its length from the device:
+      // no host round trip between the compaction and it
+      if (gap_on) {
+        HIP_TRY(c, lcdev::launch_gap_light(d_ops, d_off, d.d_jit, n_keys, p, d_out, d.d_gap2,
+                                           d.d_status, want_wit ? wo.wit : nullptr,
+                                           want_wit ? wo.kind : nullptr, st));
+        HIP_TRY(c, hipEventRecord(d.el, st));
+      }
       HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                                 hipMemcpyDeviceToHost, st));
       HIP_TRY(c, hipStreamSynchronize(st));
-      n_jit = d.h_status->n_jit;
       n_direct = d.h_status->n_jit2;
+      if (gap_on) {
+        light = true;
+        HIP_TRY(c, hipEventElapsedTime(&ms, d.ef, d.el));
+        d.gap_ms = ms;
+        d.n_gap = d.h_status->n_jit;
+        n_jit = d.h_status->n_gap2;  // what the gap tier proper still has to decide
+        jit_list = d.d_gap2;
+      } else {
+        n_jit = d.h_status->n_jit;
+      }
     }
-    jit_list = d.d_jit;
   } else {
     HIP_TRY(c, hipEventRecord(d.ef, st));
   }
   if (n_jit == 0 && n_direct == 0) {
-    d.kernel_ms = d.fast_ms;
-    d.status_dirty = false;
+    d.kernel_ms = d.fast_ms + d.gap_ms;
+    // after a handoff d_status is not zero: the next call clears it (async)
+    d.status_dirty = light;
     return 0;
   }
-  hipEvent_t before_jit = d.ef;
+  hipEvent_t before_jit = light ? d.el : d.ef;
   const int64_t gap_cap = ((int64_t)d.h_status->max_len + 2 + 3) & ~int64_t(3);  // 16-B records
   const size_t gap_per_wg = lcdev::gap_tier_ws_bytes(1, gap_cap);
   if (gap_on && (n_jit == 0 || gap_per_wg > kGapWsBytes)) {
     // no gap-tier pass: its queue (if any) joins the direct keys for the JIT
     if (n_jit > 0)
-      HIP_TRY(c, hipMemcpyAsync(d.d_jit2 + n_direct, d.d_jit, sizeof(int32_t) * (size_t)n_jit,
+      HIP_TRY(c, hipMemcpyAsync(d.d_jit2 + n_direct, jit_list, sizeof(int32_t) * (size_t)n_jit,
                                 hipMemcpyDeviceToDevice, st));
     n_jit += n_direct;
     jit_list = d.d_jit2;
@@ -381,7 +404,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     HIP_TRY(c, hipStreamSynchronize(st));
     HIP_TRY(c, hipEventElapsedTime(&ms, d.ef, d.eg));
     d.gap_ms = ms;
-    d.n_gap = n_jit;
+    if (!light) d.n_gap = n_jit;
     n_jit = d.h_status->n_jit2;
     jit_list = d.d_jit2;
     before_jit = d.eg;
@@ -495,6 +518,7 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
           hipEventCreateWithFlags(&d.e2, kEventFlags) != hipSuccess ||
           hipEventCreateWithFlags(&d.ef, kEventFlags) != hipSuccess ||
           hipEventCreateWithFlags(&d.eg, kEventFlags) != hipSuccess ||
+          hipEventCreateWithFlags(&d.el, kEventFlags) != hipSuccess ||
           hipMalloc(reinterpret_cast<void **>(&d.d_status), sizeof(lcdev::KStatus)) != hipSuccess ||
           hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess ||
           hipHostMalloc(reinterpret_cast<void **>(&d.h_handoff), sizeof(int32_t),
@@ -542,6 +566,8 @@ void lc_close(lc_ctx *c) {
     if (d.d_wit) (void)hipFree(d.d_wit);
     if (d.d_kind) (void)hipFree(d.d_kind);
     if (d.eg) (void)hipEventDestroy(d.eg);
+    if (d.el) (void)hipEventDestroy(d.el);
+    if (d.d_gap2) (void)hipFree(d.d_gap2);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
   delete c;
