@@ -1442,12 +1442,13 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     const int r = tid + u * kFastThreads;
     // previous record's call: lane-1's record of the same u, or for lane 0
     // the scalar-loaded one
-    int64_t prev = __shfl_up(b.w[u].c.x, 1);
+    const Raw &bw = b.w[u];
+    int64_t prev = __shfl_up(bw.c.x, 1);
     if (lane == 0) prev = b.pc[u];
     bool placed = false;
     if (r < n) {
-      const Rec d = decode(b.w[u], base_idx);
-      if (d.bad || d.f > LC_F_CAS || (r > 0 && prev >= b.w[u].c.x)) {
+      const Rec d = decode(bw, base_idx);
+      if (d.bad || d.f > LC_F_CAS || (r > 0 && prev >= bw.c.x)) {
         inel = jit_only = 1;  // the JIT tier reports malformed / unknown :f
       } else if (d.f == LC_F_READ) {
         if (d.ret != kNever && !(d.ver == -1 && d.val == -1)) {  // else never constrains

@@ -1,0 +1,42 @@
+"""Dev probe: run one bench.py leg's workload N times (for rocprofv3 passes
+that must see only that leg's kernels).
+  python tools/leg.py crash|model|hot|hotx [reps]
+crash: C2 with 5 % crashed writes/CAS (gap_light_kernel / gap_tier_kernel)
+model: cas-register model, 1000 keys x 1000 ops, concurrency 20 (lds_tier,
+       hbm_coop_kernel<4>)
+hot / hotx: C4 at 20 % crashed, valid / invalid (gap_tier_kernel)"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+from jepsen.etcd_amd import abi  # noqa: E402
+
+leg = sys.argv[1]
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+if leg == "crash":
+    ops, off, _, _ = abi.synth(10000, 1000, concurrency=20, p_info=0.05, seed=0x5EED0012)
+elif leg == "model":
+    ops, off, _, _ = abi.synth(1000, 1000, concurrency=20, seed=7)
+    ops = ops.copy()
+    ops[:, 3] = abi.LC_NIL
+elif leg in ("hot", "hotx"):
+    ops, off, _, _ = abi.synth(1, 5000, concurrency=50, p_info=0.2, info_frac=0.2,
+                               p_anomaly=1.0 if leg == "hotx" else 0.0,
+                               seed=1007 if leg == "hotx" else 0x5EED0004)
+else:
+    raise SystemExit("unknown leg " + leg)
+with abi.Context(device_mask=1) as ctx:
+    for i in range(reps):
+        t = time.perf_counter()
+        _, r = ctx.check(ops, off)
+        s = ctx.stats()
+        print(json.dumps({"leg": leg, "rep": i, "wall_ms": (time.perf_counter() - t) * 1e3,
+                          "fast_ms": s["fast_kernel_ms"], "gap_ms": s["gap_kernel_ms"],
+                          "jit_ms": s["jit_kernel_ms"], "hbm_ms": s["hbm_kernel_ms"],
+                          "configs": int(r["configs_explored"].sum()),
+                          "verdicts": np.bincount(r["verdict"] + 1, minlength=3).tolist()}),
+              flush=True)
