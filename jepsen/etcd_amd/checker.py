@@ -21,13 +21,18 @@ since :unknown is truthy in Clojure).  Each key's map has checker/compose's
 shape, {"valid?", "linear": <the GPU verdict>, "timeline": ...}; with
 timeline_dir set, the timeline half renders <dir>/independent/<k>/
 timeline.html on the host (timeline.py), as jepsen's timeline/html would.
-Errors: a malformed history raises LcError (-EINVAL); jepsen's check-safe
-would turn an exception into {:valid? :unknown :error ...}, which
-`check_safe` reproduces.
+An invalid key's map also carries knossos's diagnostics (diagnostics.py):
+"previous-ok", and — from the witness of the prefix before the failing
+return (lc_aux) — "configs", "last-op" and "final-paths".
+
+Errors: a key with malformed records is "unknown" alone (cause
+"malformed"), as jepsen.independent would lose only that key; unusable
+arguments raise LcError, and jepsen's check-safe turns an exception into
+{:valid? :unknown :error ...}, which `check_safe` reproduces.
 """
 import os
 
-from . import abi, history as H, timeline as TL
+from . import abi, diagnostics as D, history as H, timeline as TL
 
 UNKNOWN = "unknown"
 
@@ -110,7 +115,7 @@ class RegisterChecker:
         init = H.MUTEX_FREE if m.name == "mutex" else (0 if m.value is not None else H.LC_NIL)
         o = abi.default_opts(self.max_configs_per_key, m.version, init,
                              time_budget_ms=self.time_budget_ms)
-        _, res = self._context().check(ops, key_off, o)
+        _, res, wit, kind = self._context().check(ops, key_off, o, witness=True)
         results = {}
         for i, k in enumerate(keys):
             r = res[i]
@@ -122,6 +127,12 @@ class RegisterChecker:
                 d = done[i][int(r["fail_op"])]
                 out["op"] = d["completion"] or d["invoke"]
                 out["fail-prefix-end"] = int(r["fail_prefix_end"])
+                w = None
+                if m.name == "versioned-register" and kind[i] == abi.LC_WITNESS_PREFIX:
+                    w = wit[key_off[i]:key_off[i + 1]]
+                out.update(D.invalid_analysis(done[i], int(r["fail_op"]),
+                                              int(r["fail_prefix_end"]), w,
+                                              init=(m.version, m.value)))
             elif v == UNKNOWN:
                 out["cause"] = abi.REASONS.get(int(r["reason"]), "?")
             results[k] = out

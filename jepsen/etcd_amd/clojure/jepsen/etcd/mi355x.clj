@@ -26,11 +26,18 @@
 
     :checker (jepsen.etcd.mi355x/checker)
 
+  An invalid key's :linear map carries knossos's diagnostics: :op,
+  :previous-ok and, from the witness of the prefix before the failing
+  return (lc_check_ex, lc_aux), one :configs entry, :last-op and
+  :final-paths (jepsen/etcd_amd/diagnostics.py restates the same).  A key
+  with malformed records is :unknown alone.
+
   Untested in the build container (no JVM there); the same contract is
   exercised from Python by tests/test_gpu.py::test_register_checker_end_to_end."
   (:require [jepsen.checker :as checker]
             [jepsen.checker.timeline :as timeline]
-            [jepsen.independent :as independent])
+            [jepsen.independent :as independent]
+            [knossos.model :as model])
   (:import (com.sun.jna Function Memory NativeLibrary Pointer)
            (com.sun.jna.ptr PointerByReference)))
 
@@ -57,21 +64,26 @@
 (defn- client-op? [op] (integer? (:process op)))
 
 (defn- subhistories
-  "{k [op ...]}: jepsen.independent's split of the client ops; tuple values
-  are unwrapped, non-tuple ops go to every key."
+  "{k [op ...]}: jepsen.independent's split of the client ops in one pass
+  over the history; tuple values are unwrapped, non-tuple ops go to every
+  key (in history order, interleaved with the key's own ops)."
   [history]
-  (let [ops  (filter client-op? history)
-        keys (->> ops (keep (fn [op] (let [v (:value op)]
-                                       (when (independent/tuple? v) (key v)))))
-                  distinct)]
-    (into (array-map)
-          (for [k keys]
-            [k (->> ops
-                    (keep (fn [op]
-                            (let [v (:value op)]
-                              (cond (not (independent/tuple? v)) op
-                                    (= k (key v)) (assoc op :value (val v))))))
-                    vec)]))))
+  (let [ops   (filterv client-op? history)
+        ;; first pass over the ops: the keys, in order of appearance
+        order (->> ops
+                   (keep (fn [op] (let [v (:value op)] (when (independent/tuple? v) (key v)))))
+                   distinct
+                   vec)
+        ;; second pass: route each op to its key (or to every key)
+        subs  (reduce (fn [m op]
+                        (let [v (:value op)]
+                          (if (independent/tuple? v)
+                            (assoc! m (key v) (conj! (get m (key v)) (assoc op :value (val v))))
+                            (reduce (fn [m k] (assoc! m k (conj! (get m k) op))) m order))))
+                      (transient (zipmap order (repeatedly #(transient []))))
+                      ops)
+        subs  (persistent! subs)]
+    (into (array-map) (for [k order] [k (persistent! (get subs k))]))))
 
 (defn- complete
   "knossos-style completion of one key: [{:op invoke-with-completed-value
@@ -141,44 +153,132 @@
             [f (intern v) LC_NIL ver call ret]))))))
 
 (defn- pack
-  "Packs all keys: returns [keys completed-per-key ^Memory ops ^Memory key-off]."
+  "Packs all keys: returns [keys completed-per-key ^Memory ops ^Memory key-off
+  n-records].  Records are filled into one long[] and written to the
+  off-heap buffer in a single bulk copy."
   [model subs]
   (let [keys  (vec (keys subs))
         done  (mapv (fn [k] (complete (get subs k))) keys)
-        n     (reduce + (map count done))
-        ops   (Memory. (max 1 (* op-bytes n)))
-        off   (Memory. (* 8 (inc (count keys))))]
+        n     (long (reduce + (map count done)))
+        arr   (long-array (* 6 n))
+        offs  (long-array (inc (count keys)))]
     (loop [ki 0, i 0]
-      (.setLong off (* 8 ki) i)
+      (aset offs ki i)
       (when (< ki (count keys))
         (let [intern (interner)
-              recs   (map (partial record model intern) (nth done ki))
-              i'     (reduce (fn [i r]
-                               (dotimes [j 6]
-                                 (.setLong ops (+ (* i op-bytes) (* 8 j)) (long (nth r j))))
-                               (inc i))
-                             i recs)]
+              i'     (reduce (fn [^long i r]
+                               (let [[f v e ver call ret] (record model intern r)
+                                     b (* 6 i)]
+                                 (aset arr b (long f)) (aset arr (+ b 1) (long v))
+                                 (aset arr (+ b 2) (long e)) (aset arr (+ b 3) (long ver))
+                                 (aset arr (+ b 4) (long call)) (aset arr (+ b 5) (long ret))
+                                 (inc i)))
+                             i (nth done ki))]
           (recur (inc ki) i'))))
-    [keys done ops off]))
+    (let [ops (Memory. (max 1 (* op-bytes n)))
+          off (Memory. (* 8 (inc (count keys))))]
+      (.write ops 0 arr 0 (alength arr))
+      (.write off 0 offs 0 (alength offs))
+      [keys done ops off n])))
+
+;; ---- knossos's invalid-analysis keys (diagnostics.py restates the same)
+
+(defn- vr-step
+  "VersionedRegister.step (register.clj:60-96) over [version value] state
+  and a completed op: the next state, or (model/inconsistent msg)."
+  [[version value :as state] op]
+  (let [[op-version op-value] (:value op)
+        version' (inc version)]
+    (case (:f op)
+      :write (if (and (some? op-version) (not= version' op-version))
+               (model/inconsistent (str "can't go from version " version " to " op-version))
+               [version' op-value])
+      :cas   (let [[v v'] op-value]
+               (cond (and (some? op-version) (not= version' op-version))
+                     (model/inconsistent (str "can't go from version " version " to " op-version))
+                     (not= value v)
+                     (model/inconsistent (str "can't CAS " value " from " v " to " v'))
+                     :else [version' v']))
+      :read  (cond (and (some? op-version) (not= version op-version))
+                   (model/inconsistent (str "can't read version " op-version " from version " version))
+                   (and (some? op-value) (not= value op-value))
+                   (model/inconsistent (str "can't read " op-value " from register " value))
+                   :else state)
+      (model/inconsistent (str "no step for " (:f op))))))
+
+(defn- model-map [s] (if (model/inconsistent? s) s {:version (first s) :value (second s)}))
+
+(defn- op-map [r] (if (not= LC_INF (:ret r)) (:completion r) (:op r)))
+
+(defn- invalid-analysis
+  ":previous-ok, and from the prefix witness (positions per record, or nil)
+  :configs [one configuration], :last-op and :final-paths."
+  [done fail-op fail-ret witness init]
+  (let [oks  (filter #(and (= :ok (:type (:completion %))) (< (:ret %) fail-ret)) done)
+        prev (when (seq oks) (:completion (apply max-key :ret oks)))
+        out  {:previous-ok prev}]
+    (if-not witness
+      out
+      (let [cut   (dec fail-ret)
+            muts  (->> (map-indexed vector witness) (filter #(>= (second %) 0))
+                       (sort-by second) (map first))
+            state (reduce (fn [s i] (if (model/inconsistent? s) s (vr-step s (:op (nth done i)))))
+                          init muts)]
+        (if (model/inconsistent? state)
+          out
+          (let [lin      (set muts)
+                freads   (->> (map-indexed vector done)
+                              (filter (fn [[_ r]] (and (= :read (:f (:op r))) (<= (:ret r) cut)
+                                                       (= (first (:value (:op r))) (first state)))))
+                              (map first))
+                last-i   (if (seq freads) (apply max-key #(:ret (nth done %)) freads) (last muts))
+                last-op  (when last-i (op-map (nth done last-i)))
+                pending  (->> (range (count done))
+                              (filter #(let [r (nth done %)]
+                                         (and (<= (:call r) cut) (not (lin %)) (> (:ret r) cut)))))
+                head     {:op last-op :model (model-map state)}
+                try-op   (fn [s i] (let [s' (vr-step s (:op (nth done i)))]
+                                     [s' {:op (op-map (nth done i)) :model (model-map s')}]))
+                direct   [head (second (try-op state fail-op))]
+                via      (for [i pending :when (not= i fail-op)
+                               :let [[s' mid] (try-op state i)]
+                               :when (or (model/inconsistent? s')
+                                         (model/inconsistent? (first (try-op s' fail-op))))]
+                           (if (model/inconsistent? s')
+                             [head mid]
+                             [head mid (second (try-op s' fail-op))]))]
+            (assoc out
+                   :configs     [{:model (model-map state) :last-op last-op
+                                  :pending (mapv #(:op (nth done %)) pending)}]
+                   :last-op     last-op
+                   :final-paths (vec (take 10 (cons direct via))))))))))
 
 (defn- merge-valid [vs]
   (cond (some false? vs)          false
         (some #{:unknown} vs)     :unknown
         :else                     true))
 
+(def ^:private reasons
+  {2 :config-budget 3 :window-overflow 4 :malformed 5 :unknown-f 7 :time-budget})
+
 (defn- check-keys
-  "One lc_check over subs {k [op ...]}: {k result-map}."
+  "One lc_check_ex over subs {k [op ...]}: {k result-map}.  Malformed keys
+  come back :unknown one by one; lc_check_ex fails (and this throws, for
+  check-safe) only on unusable arguments or a GPU error."
   [model max-configs-per-key time-budget-ms subs]
-  (let [[keys done ops off] (pack model subs)
+  (let [[keys done ops off n] (pack model subs)
         nk   (count keys)
         out  (Memory. (* result-bytes nk))
+        wit  (Memory. (max 4 (* 4 n)))
+        kind (Memory. (max 4 (* 4 nk)))
+        aux  (doto (Memory. 16) (.setPointer 0 wit) (.setPointer 8 kind))
         o    (doto (Memory. 40)
                (.setLong 0 0) (.setLong 8 (if (= model :mutex) 0 LC_NIL))
                (.setLong 16 max-configs-per-key)
                (.setLong 24 time-budget-ms) (.setLong 32 0))
         rc   (locking ctx
-               (.invokeInt (fun "lc_check")
-                           (object-array [@ctx ops off (long nk) o out])))]
+               (.invokeInt (fun "lc_check_ex")
+                           (object-array [@ctx ops off (long nk) o out aux])))]
     (when-not (zero? rc)
       (throw (ex-info "lc_check failed"
                       {:rc rc :error (.invoke (fun "lc_last_error")
@@ -189,14 +289,20 @@
                   verdict (.getInt out b)
                   reason  (.getInt out (+ b 4))
                   fail-op (.getLong out (+ b 8))
-                  v       (case verdict 1 true 0 false :unknown)]
+                  fail-at (.getLong out (+ b 16))
+                  v       (case verdict 1 true 0 false :unknown)
+                  d       (nth done ki)
+                  k0      (.getLong off (* 8 ki))
+                  witness (when (and (false? v) (= model :versioned-register)
+                                     (= 2 (.getInt kind (* 4 ki))))  ; LC_WITNESS_PREFIX
+                            (vec (.getIntArray wit (* 4 k0) (count d))))]
               [(nth keys ki)
                (cond-> {:valid?   v
                         :analyzer :mi355x
-                        :configs  (.getLong out (+ b 24))}
-                 (false? v)   (assoc :op (let [r (nth (nth done ki) fail-op)]
-                                           (or (:completion r) (:op r))))
-                 (= v :unknown) (assoc :error [:lincheck-reason reason]))])))))
+                        :configs-explored (.getLong out (+ b 24))}
+                 (false? v)     (merge {:op (op-map (nth d fail-op))}
+                                       (invalid-analysis d fail-op fail-at witness [0 nil]))
+                 (= v :unknown) (assoc :error [:lincheck-reason (reasons reason reason)]))])))))
 
 (defn linearizable
   "(checker/linearizable {:model m}) over the whole history, for the knossos

@@ -10,6 +10,7 @@ import pytest
 import oracle
 from jepsen.etcd_amd import abi, edn, history as H, synth
 from jepsen.etcd_amd.history import Tuple
+from helpers import GOLDEN
 
 
 def same_as_pack(hist, text=None, **kw):
@@ -180,3 +181,35 @@ def test_check_edn_end_to_end_gpu(tmp_path):
         rec = h.key_off[kk] + ref["fail_op"][kk]
         assert r["op"] == (h.op_text(rec, 1) or h.op_text(rec, 0))
     assert edn.render(result).startswith("{:valid? false")
+
+
+def _expected(path):
+    """{key: (valid, op_index or None)} from a make_edn.py expected file."""
+    import re
+    out = {}
+    for m in re.finditer(r"(\d+) \{:valid\? (\w+)(?: :op-index (\d+))?\}", open(path).read()):
+        out[int(m.group(1))] = (m.group(2) == "true", int(m.group(3)) if m.group(3) else None)
+    return out
+
+
+@pytest.mark.parametrize("name", ["kat", "c1", "tiny", "info", "c5"])
+def test_jvm_parity_kit_histories(name):
+    """The JVM parity kit (tests/golden/edn, tools/jvm_parity/parity.clj):
+    each exported Jepsen history, read back by this build's EDN reader,
+    splits into keys whose oracle verdicts and failing completions equal the
+    kit's expected file — so a JVM box running the reference's own checker
+    over the same file compares against the decisions the fixtures pin."""
+    import gzip
+    base = os.path.join(GOLDEN, "edn", name)
+    h = edn.read(gzip.open(base + ".edn.gz").read())
+    exp = _expected(base + ".expected.edn")
+    assert len(h.keys) == len(exp)
+    _, r = oracle.check(h.ops, h.key_off, algo=oracle.JITC, n_threads=8, max_configs=1 << 22)
+    for i, ktext in enumerate(h.keys):
+        valid, op_index = exp[int(ktext)]
+        if r["verdict"][i] == -1:
+            continue  # beyond the oracle's budget (info fixture)
+        assert r["verdict"][i] == (1 if valid else 0), ktext
+        if not valid:
+            assert r["fail_prefix_end"][i] == op_index, ktext
+    assert (r["verdict"] != -1).mean() > 0.9

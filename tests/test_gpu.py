@@ -428,6 +428,11 @@ def test_register_checker_end_to_end(tmp_path):
     for k in bad:
         r = res["results"][k]
         assert r["valid?"] is False and r["linear"]["op"]["type"] == "ok"
+        # knossos's diagnostics, from the prefix witness (diagnostics.py)
+        lin = r["linear"]
+        assert lin["previous-ok"]["index"] < lin["fail-prefix-end"]
+        assert lin["configs"] and lin["last-op"] == lin["configs"][0]["last-op"]
+        assert all("inconsistent" in p[-1]["model"] for p in lin["final-paths"])
         page = open(r["timeline"]["file"]).read()  # independent/<k>/timeline.html
         assert 'cex"' in page and os.path.dirname(r["timeline"]["file"]).endswith("/%d" % k)
     assert res["results"][0]["timeline"]["valid?"] is True
