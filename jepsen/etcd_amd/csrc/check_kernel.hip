@@ -44,6 +44,26 @@
 namespace lcdev {
 namespace {
 
+#ifdef HBM_PROFILE
+// dev only: per-workgroup counters of the cooperative expansion (wave 0 of
+// workgroups 0..3): levels, rounds, insert probe iterations, configurations,
+// and clocks in candidate generation / inserts / barriers
+__device__ unsigned long long g_hprof[4][16];
+// per log2(max set of a return): returns, ticks, LDS-mode returns, configs (all workgroups)
+__device__ unsigned long long g_hhist[20][4];
+__device__ unsigned int g_hdone;
+__device__ unsigned long long g_hp2[16];
+#define HP2(i, v) \
+  do { if (blockIdx.x < 64 && (threadIdx.x & 63) == 0) atomicAdd(&g_hp2[i], (unsigned long long)(v)); } while (0)
+#define HTICK(x) const uint64_t x = wall_clock64()
+#define HPROF(i, v) \
+  do { if (blockIdx.x < 4 && threadIdx.x == 0) g_hprof[blockIdx.x][i] += (v); } while (0)
+#else
+#define HPROF(i, v) do { } while (0)
+#define HP2(i, v) do { } while (0)
+#define HTICK(x) do { } while (0)
+#endif
+
 struct Cfg {
   uint64_t mask;  // bit t: the op in window slot t is linearized
   uint64_t sv;    // (uint32 version << 32) | uint32 value-id (NIL = 0xFFFFFFFF)
@@ -61,6 +81,11 @@ __device__ __forceinline__ int rl32(int v, int l) {
 __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
   return ((uint64_t)hi << 32) | lo;
 }
 // Bitwise AND of a 64-bit value over the 64 lanes (wave-uniform result).
@@ -153,14 +178,22 @@ struct CoopShared {
   int cmd;
   int rF, rR, rW, nF;
   uint64_t bs, muts, reads, crashed;
-  uint32_t epoch;
-  int nR, nW, head, lo, hi, go, status;
+  uint32_t epoch, tmask;
+  union {  // set sizes; a round's appends to both reserve with one atomic
+    struct { int nR, nW; };
+    unsigned long long nRW;
+  };
+  int head, lo, hi, go, status;
+  int lds;  // this attempt keeps its tables and sets in LDS (CoopTab)
+  uint32_t lepoch;  // its LDS epoch (16 bits)
+  int lclear;       // the LDS epoch wrapped: clear the tags first
   unsigned long long explored;
   long long budget;
   SlotLds slots;
 };
 
 struct HbmStore {
+  static constexpr int kLT = 0;  // no LDS tables (CoopStore has them)
   SlotLds *sl;    // slot staging (LDS)
   CoopShared *coop = nullptr;  // set in the cooperative kernel
   int nwaves = 1;
@@ -168,8 +201,33 @@ struct HbmStore {
   Cfg *tabs;      // 2 tables (roles R, W) of 2*cap entries
   uint32_t *tags; // 2 tag arrays of 2*cap
   int cap;         // configurations per region
-  uint32_t tmask;  // table entries - 1 (power of two, >= 7)
+  uint32_t tmask;  // table entries - 1 (power of two, >= 7), this return's size
+  uint32_t tmask_full;  // the workspace's table size - 1 (2 * cap entries)
+  int hint = 0;    // largest R / W set of this key's returns so far
   uint32_t epoch;
+  // Table size of a return (adaptive, round 2).  The sets of one return are
+  // usually far smaller than the workspace's capacity, and a table sized for
+  // the capacity spreads them over 512 KB per role: every probe missed L2
+  // and the Infinity Cache (~2 GB of tables over 1,000 keys).  A return
+  // starts with 4x the larger of its frontier and the key's largest set so
+  // far (at least `floor` entries); a role that fills past `lim` aborts the
+  // return, which is redone with a 4x table (the expansion is deterministic
+  // up to order, so R, the explored count and the verdict are unchanged).
+  __device__ __forceinline__ uint32_t pick_tmask(int nF, uint32_t floor) const {
+    const uint32_t need = (uint32_t)max(4 * max(nF, hint), (int)floor);
+    uint32_t t = 8;
+    while (t < need && t <= tmask_full) t <<= 1;
+    return min(t - 1, tmask_full);
+  }
+  __device__ __forceinline__ uint32_t grow_tmask() const {
+    return min(((tmask + 1) << 2) - 1, tmask_full);
+  }
+  // Entries a role may hold before the return aborts: half the table less
+  // one round of inserts of every wave (each wave checks after its round),
+  // so a probe always finds a free entry; the full table holds `cap`.
+  __device__ __forceinline__ int lim(int nwaves) const {
+    return tmask == tmask_full ? cap : min(cap, (int)((tmask + 1) / 2) - kWave * nwaves);
+  }
   __device__ __forceinline__ Cfg *reg(int r) const { return base + (size_t)r * cap; }
   __device__ __forceinline__ Cfg *tab(int role) const { return tabs + (size_t)role * (tmask + 1); }
   __device__ __forceinline__ uint32_t *tag(int role) const { return tags + (size_t)role * (tmask + 1); }
@@ -213,6 +271,8 @@ struct HbmStore {
   // that lost a race re-reads the same entry next round, after the winner's
   // store has been fenced, so equal configurations inserted together are
   // kept once.  Returns 1 (inserted), 0 (already there), per lane.
+  // (role may differ per lane: the R and W inserts of a round run together,
+  // so a round costs one chain of dependent table round trips, not two)
   __device__ __forceinline__ int insert_lanes(int role, const Cfg &c, bool want) {
     uint32_t h = (hash(c.mask, c.sv) & tmask) & ~7u;
     int res = 0;
@@ -258,11 +318,12 @@ struct HbmStore {
       h = (h + 1) & tmask;
     }
   }
-  __device__ __forceinline__ int insert_lanes_coop(int role, const Cfg &c, bool want) {
+  __device__ __forceinline__ int insert_lanes_coop(int role, const Cfg &c, bool want) {  // (role per lane)
     uint32_t h = (hash(c.mask, c.sv) & tmask) & ~7u;
     int res = 0;
     bool pend = want;
     while (__ballot(pend)) {
+      HPROF(2, 1);
       if (pend) {
         const uint32_t t = __hip_atomic_load(&tag(role)[h], __ATOMIC_ACQUIRE,
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -320,6 +381,145 @@ struct HbmStore {
     return -1;
   }
 };
+
+// LDS tables of the cooperative tier (round 2).  Most returns of a key on
+// the HBM tiers have small R / W sets (model leg: 75 configurations on
+// average) but many BFS levels, and each level's inserts are a chain of
+// dependent table round trips: in HBM (tag load, CAS, entry store, release)
+// one probe took ~1.4 us.  A return whose frontier fits runs its expansion
+// with both tables and both sets in LDS (R is also appended to the global
+// region the event loop reads); one whose sets outgrow kLim is redone with
+// the HBM tables (status -3, as for the adaptive HBM size), so R, the
+// explored count and the verdict do not depend on it.
+// A table entry is 4 bytes, (epoch << 16) | index into the role's set, so
+// the LDS holds kLim = 5/16 of the table size per set (load <= 31%): 640
+// configurations in 36 KB with 4-wave workgroups, four of them per CU.
+constexpr uint32_t kIdxBusy = 0xFFFFu;  // claimed, index not yet published
+constexpr uint32_t kIdxOvf = 0xFFFEu;   // claimed past kLim (the return is redone)
+template <int LT>
+struct CoopTab {
+  static constexpr int kLim = LT * 5 / 16;  // configurations per set
+  static_assert(kLim < (int)kIdxOvf, "set index must fit 16 bits");
+  uint32_t tag[2][LT];  // (epoch << 16) | index, per role
+  Cfg set[2][kLim];     // R and W of this return
+};
+template <int LT>
+__device__ __forceinline__ CoopTab<LT> &coop_tab() {
+  __shared__ CoopTab<LT> t;
+  return t;
+}
+template <int LT>
+struct CoopStore : HbmStore {
+  static constexpr int kLT = LT;
+  int last = 0;           // the previous return's larger set
+  uint32_t lepoch = 0;    // LDS table epoch (16 bits; 0 is never current)
+};
+
+// LDS-only fences: the tables are workgroup-private, so publishing an entry
+// waits for LDS (lgkmcnt) only, not for the wave's global R appends.
+__device__ __forceinline__ void lds_release() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+}
+__device__ __forceinline__ void lds_acquire() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+__device__ __forceinline__ void lds_barrier() {
+  lds_release();
+  __builtin_amdgcn_s_barrier();
+  lds_acquire();
+}
+__device__ __forceinline__ uint32_t lds_tag_load(uint32_t *p) {
+  const uint32_t t = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  lds_acquire();
+  return t;
+}
+__device__ __forceinline__ void lds_tag_publish(uint32_t *p, uint32_t v) {
+  lds_release();
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Lane-parallel dedup insert into the LDS tables (each lane its own role):
+// a stale entry is claimed as (epoch, kIdxBusy) with CAS; the lanes that won
+// this round reserve their set indices together (one packed atomic on
+// C.nRW), store the configuration (R also to the global region rR) and
+// publish (epoch, index).  A busy entry is re-read next round; its owner
+// publishes within the round it claimed it, so no wave waits on another
+// wave's unfinished loop.  A lane that probed LT/4 entries, or whose index
+// is past kLim, sets ovf.  Returns 1 (inserted) or 0 (already there).
+template <int LT>
+__device__ __forceinline__ int lds_insert_lanes(CoopTab<LT> &T, CoopShared &C, HbmStore &st,
+                                                int rR, int role, const Cfg &c, bool want,
+                                                uint32_t eb, bool &ovf, int lane) {
+  uint32_t h = HbmStore::hash(c.mask, c.sv) & (LT - 1);
+  int res = 0, probes = 0;
+  bool pend = want;
+  while (__ballot(pend)) {
+    bool won = false;
+    if (pend) {
+      const uint32_t t = lds_tag_load(&T.tag[role][h]);
+      if ((t & 0xFFFF0000u) == eb) {
+        const uint32_t ix = t & 0xFFFFu;
+        if (ix < kIdxOvf) {
+          const Cfg e = T.set[role][ix];
+          if (e.mask == c.mask && e.sv == c.sv) {
+            pend = false;  // already there
+          } else {
+            h = (h + 1) & (LT - 1);
+            if (++probes >= LT / 4) {
+              ovf = true;
+              pend = false;
+            }
+          }
+        } else if (ix == kIdxOvf) {
+          ovf = true;
+          pend = false;
+        }  // kIdxBusy: re-read next round
+      } else {
+        won = atomicCAS(&T.tag[role][h], t, eb | kIdxBusy) == t;
+      }
+    }
+    const uint64_t wR = __ballot(won && role == ROLE_R), wW = __ballot(won && role == ROLE_W);
+    if (wR | wW) {
+      unsigned long long a = 0;
+      if (lane == 0)
+        a = atomicAdd(&C.nRW, (unsigned long long)__popcll(wR) | ((unsigned long long)__popcll(wW) << 32));
+      const int aR = uni((int)a), aW = uni((int)(a >> 32));
+      if (won) {
+        const int ix = role == ROLE_R ? aR + lanes_below(wR) : aW + lanes_below(wW);
+        uint32_t pub = eb | kIdxOvf;
+        if (ix < CoopTab<LT>::kLim) {
+          T.set[role][ix] = c;
+          if (role == ROLE_R) st.reg(rR)[ix] = c;
+          pub = eb | (uint32_t)ix;
+        } else {
+          ovf = true;
+        }
+        lds_tag_publish(&T.tag[role][h], pub);
+        res = 1;
+        pend = false;
+      }
+    }
+  }
+  return res;
+}
+// Claim an entry for a configuration known distinct whose set index ix is
+// already reserved (the split of F); its set entry is stored by the caller.
+template <int LT>
+__device__ __forceinline__ void lds_claim_lane(CoopTab<LT> &T, int role, const Cfg &c, int ix,
+                                               uint32_t eb, bool &ovf) {
+  uint32_t h = HbmStore::hash(c.mask, c.sv) & (LT - 1);
+  lds_release();  // the set entry before its tag
+  for (int probes = 0; probes < LT / 4;) {
+    const uint32_t t = lds_tag_load(&T.tag[role][h]);
+    if ((t & 0xFFFF0000u) != eb) {
+      if (atomicCAS(&T.tag[role][h], t, eb | (uint32_t)ix) == t) return;
+      continue;  // lost the race for this entry: re-read it
+    }
+    h = (h + 1) & (LT - 1);
+    probes++;
+  }
+  ovf = true;
+}
 
 // ------------------------------------------------------------ the search
 
@@ -430,6 +630,7 @@ __device__ __forceinline__ int general_return(Store &st, const Slot &sl, const M
   return nR;
 }
 
+
 __device__ __forceinline__ void coop_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_s_barrier();
@@ -439,12 +640,32 @@ __device__ __forceinline__ void coop_barrier() {
 // One wave's share of a cooperative expansion (every wave of the workgroup
 // calls it; the parameters are in C).  Barrier count is uniform: one after
 // the split, two per BFS level.
+template <int LT>
 __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
   const int nw = st.nwaves;
   st.epoch = C.epoch;
-  const uint64_t bs = C.bs, muts = C.muts, reads = C.reads, crashed = C.crashed;
+  st.tmask = C.tmask;
+  CoopTab<LT> &T = coop_tab<LT>();
+  const bool lds = C.lds;  // uniform over the workgroup
+  const int lim = lds ? CoopTab<LT>::kLim : st.lim(nw);
+  const uint32_t eb = C.lepoch << 16;  // LDS tables' epoch
+  bool ovf = false;
+  if (lds && C.lclear) {  // the 16-bit LDS epoch wrapped: clear the tags
+    uint32_t *tg = &T.tag[0][0];
+    for (int i = wave * kWave + lane; i < 2 * LT; i += nw * kWave) tg[i] = 0;
+    lds_barrier();
+  }
+  const uint64_t bs = C.bs, crashed = C.crashed;
+  const uint64_t muts = rfl64(C.muts), reads = rfl64(C.reads);  // scalar loops below
   const int rF = C.rF, rR = C.rR, rW = C.rW, nF = C.nF;
   const SlotLds &L = C.slots;
+  // Lane t holds slot t's precondition, value and class bit: the candidate
+  // and read-closure loops run over slots uniformly and read them with
+  // v_readlane (no dependent LDS load per slot and lane).
+  HTICK(hx0);
+  const int4 spre = L.pre[lane];
+  const int sval = L.val[lane];
+  const uint64_t spbit = L.pbit[lane];
   // split F into R (x linearized, its bit dropped) and W
   for (int j0 = wave * kWave; j0 < nF; j0 += nw * kWave) {
     const int j = j0 + lane;
@@ -461,20 +682,50 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
     }
     bR = __builtin_amdgcn_readfirstlane(bR);
     bW = __builtin_amdgcn_readfirstlane(bW);
-    if (has) st.claim_unique_lane(ROLE_R, rR, bR + lanes_below(mh), Cfg{c.mask & ~bs, c.sv});
-    if (lacks) st.claim_unique_lane(ROLE_W, rW, bW + lanes_below(ml), c);
+    if (lds) {  // nF <= kLim: both sets fit
+      if (has) {
+        const Cfg rc{c.mask & ~bs, c.sv};
+        const int ix = bR + lanes_below(mh);
+        st.reg(rR)[ix] = rc;
+        T.set[ROLE_R][ix] = rc;
+        lds_claim_lane(T, ROLE_R, rc, ix, eb, ovf);
+      }
+      if (lacks) {
+        const int ix = bW + lanes_below(ml);
+        T.set[ROLE_W][ix] = c;
+        lds_claim_lane(T, ROLE_W, c, ix, eb, ovf);
+      }
+    } else {
+      if (has) st.claim_unique_lane(ROLE_R, rR, bR + lanes_below(mh), Cfg{c.mask & ~bs, c.sv});
+      if (lacks) st.claim_unique_lane(ROLE_W, rW, bW + lanes_below(ml), c);
+    }
   }
+  if (__ballot(ovf) && lane == 0) atomicMin(&C.status, -3);
+  HTICK(hx1);
+  if (lds) HP2(0, hx1 - hx0);
   // Level bounds and the go flag are written by wave 0 between two barriers,
   // while no wave appends, so every wave reads the same values.
-  coop_barrier();
+#ifdef HBM_PROFILE
+  const uint64_t ts0 = wall_clock64();
+#endif
+  if (lds) lds_barrier(); else coop_barrier();
+#ifdef HBM_PROFILE
+  HPROF(10, wall_clock64() - ts0);
+#endif
   if (wave == 0 && lane == 0) {
     C.lo = 0;
     C.hi = C.nW;
     C.head = 0;
     C.go = C.hi > 0 && C.status == 0;
   }
-  coop_barrier();
+  if (lds) lds_barrier(); else coop_barrier();
+  HTICK(hx2);
+  if (lds) HP2(1, hx2 - hx1);
+  if (lds) HP2(9, 1);
   while (C.go) {
+    HPROF(0, 1);
+    HTICK(hl0);
+    if (lds) HP2(3, 1);
     const int lo = C.lo, hi = C.hi;
     // this level: W[lo, hi) in batches of 64 claimed from C.head
     for (;;) {
@@ -485,103 +736,193 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
         break;
       const int j = b + lane;
       const bool act = j < hi;
-      const Cfg c = st.get(rW, act ? j : b);
+#ifdef HBM_PROFILE
+      const uint64_t tc0 = wall_clock64();
+#endif
+      HTICK(hb0);
+      const Cfg c = lds ? T.set[ROLE_W][act ? j : b] : st.get(rW, act ? j : b);
       const int cver = sv_ver(c.sv), cval = sv_val(c.sv);
       uint64_t cand = 0;
-      if (act) {
-        uint64_t m = muts & ~c.mask;
-        while (m) {
-          const int t = __builtin_ctzll(m);
-          m &= m - 1;
-          const int4 pr = L.pre[t];
-          if (pre_ok(pr.x, pr.y, pr.z, pr.w, cver, cval) &&
-              (!((crashed >> t) & 1) || (L.pbit[t] & ~c.mask) == 0))
-            cand |= 1ull << t;
-        }
+      for (uint64_t m = muts; m; m &= m - 1) {  // uniform over pending mutations
+        const int t = __builtin_ctzll(m);
+        bool ok = pre_ok(rl32(spre.x, t), rl32(spre.y, t), rl32(spre.z, t), rl32(spre.w, t), cver, cval);
+        if ((crashed >> t) & 1) ok = ok && (rl64(spbit, t) & ~c.mask) == 0;
+        if (ok) cand |= 1ull << t;
       }
+      cand &= act ? ~c.mask : 0ull;
+      unsigned long long exw = 0;  // this batch's successors (one atomic per batch)
+      HTICK(hb1);
+      if (lds) HP2(12, hb1 - hb0);
+#ifdef HBM_PROFILE
+      HPROF(5, wall_clock64() - tc0);
+#endif
       for (;;) {
         const bool has = cand != 0;
         const uint64_t hb = __ballot(has);
         if (!hb) break;
-        Cfg nc{0, 0};
-        bool toR = false;
-        if (has) {
-          const int t = __builtin_ctzll(cand);
-          cand &= cand - 1;
-          const int nver = cver + 1, nval = L.val[t];
-          uint64_t nm = c.mask | (1ull << t);
-          uint64_t r = reads & ~nm;
-          while (r) {
-            const int u = __builtin_ctzll(r);
-            r &= r - 1;
-            const int4 pr = L.pre[u];
-            if (pre_ok(pr.x, pr.y, pr.z, pr.w, nver, nval)) nm |= 1ull << u;
+        HPROF(1, 1);
+        HPROF(3, __popcll(hb));
+        exw += __popcll(hb);
+        const int t = has ? __builtin_ctzll(cand) : 0;
+        cand &= cand - 1;
+        const int nver = cver + 1, nval = __shfl(sval, t);
+        uint64_t nm = c.mask | (1ull << t);
+        for (uint64_t r = reads; r; r &= r - 1) {  // eager read closure, uniform over reads
+          const int u = __builtin_ctzll(r);
+          if (pre_ok(rl32(spre.x, u), rl32(spre.y, u), rl32(spre.z, u), rl32(spre.w, u), nver, nval))
+            nm |= 1ull << u;
+        }
+        const bool toR = (nm & bs) != 0;
+        const Cfg nc{toR ? nm & ~bs : nm, pack_sv(nver, nval)};
+#ifdef HBM_PROFILE
+        const uint64_t ti0 = wall_clock64();
+#endif
+        if (lds) {  // inserts, set indices and appends in one pass
+          lds_insert_lanes(T, C, st, rR, toR ? ROLE_R : ROLE_W, nc, has, eb, ovf, lane);
+          if (__ballot(ovf)) {
+            if (lane == 0) atomicMin(&C.status, -3);
+            break;
           }
-          toR = (nm & bs) != 0;
-          nc = Cfg{toR ? nm & ~bs : nm, pack_sv(nver, nval)};
+          continue;
         }
-        const int insR = st.insert_lanes_coop(ROLE_R, nc, has && toR);
-        const int insW = st.insert_lanes_coop(ROLE_W, nc, has && !toR);
+        const int ins = st.insert_lanes_coop(toR ? ROLE_R : ROLE_W, nc, has);
+#ifdef HBM_PROFILE
+        HPROF(6, wall_clock64() - ti0);
+        if (lds) HPROF(14, wall_clock64() - ti0);
+        if (lds) HP2(4, wall_clock64() - ti0);
+        if (lds) HP2(5, 1);
+        if (lds) HPROF(15, 1);
+#endif
+        const bool insR = ins && toR, insW = ins && !toR;
         const uint64_t bR = __ballot(insR), bW = __ballot(insW);
-        int aR = 0, aW = 0;
-        unsigned long long ex = 0;
-        if (lane == 0) {
-          aR = bR ? atomicAdd(&C.nR, __popcll(bR)) : 0;
-          aW = bW ? atomicAdd(&C.nW, __popcll(bW)) : 0;
-          ex = atomicAdd(&C.explored, (unsigned long long)__popcll(hb)) + __popcll(hb);
-        }
-        aR = __builtin_amdgcn_readfirstlane(aR);
-        aW = __builtin_amdgcn_readfirstlane(aW);
-        const bool fullR = aR + __popcll(bR) > st.cap, fullW = aW + __popcll(bW) > st.cap;
+        unsigned long long aRW = 0;
+        if (lane == 0 && (bR | bW))
+          aRW = atomicAdd(&C.nRW, (unsigned long long)__popcll(bR) |
+                                      ((unsigned long long)__popcll(bW) << 32));
+        const int aR = uni((int)aRW), aW = uni((int)(aRW >> 32));
+        const bool fullR = aR + __popcll(bR) > lim, fullW = aW + __popcll(bW) > lim;
+        const bool full = fullR || fullW;
         if (insR && !fullR) st.reg(rR)[aR + lanes_below(bR)] = nc;
         if (insW && !fullW) st.reg(rW)[aW + lanes_below(bW)] = nc;
-        if (lane == 0) {
-          if (fullR || fullW) atomicMin(&C.status, -1);
-          else if ((long long)ex > C.budget && C.status == 0) atomicMin(&C.status, -2);
+        // -3: this return's tables are too small (redone larger / in HBM);
+        // -1: the workspace is full (next tier)
+        if (full) {
+          if (lane == 0) atomicMin(&C.status, lim < st.cap ? -3 : -1);
+          break;
         }
-        if (fullR || fullW) break;
       }
+      if (lane == 0 && exw) {
+        const unsigned long long ex = atomicAdd(&C.explored, exw) + exw;
+        if ((long long)ex > C.budget && C.status == 0) atomicMin(&C.status, -2);
+      }
+      HTICK(hb2);
+      if (lds) HP2(10, hb2 - hb0);
+      if (lds) HP2(13, hb2 - hb1);
+      if (lds) HP2(11, 1);
     }
-    coop_barrier();  // the level's appends are done
+#ifdef HBM_PROFILE
+    const uint64_t tb0 = wall_clock64();
+#endif
+    HTICK(hl1);
+    if (lds) HP2(2, hl1 - hl0);
+    if (lds) lds_barrier(); else coop_barrier();  // the level's appends are done
+    HTICK(hl2);
+    if (lds) HP2(6, hl2 - hl1);
+#ifdef HBM_PROFILE
+    HPROF(7, wall_clock64() - tb0);
+#endif
     if (wave == 0 && lane == 0) {
       C.lo = hi;
       C.hi = C.nW;
       C.head = 0;
       C.go = C.lo < C.hi && C.status == 0;
     }
-    coop_barrier();
+    if (lds) lds_barrier(); else coop_barrier();
+    HTICK(hl3);
+    if (lds) HP2(7, hl3 - hl2);
   }
+  HTICK(hx3);
+  if (lds) coop_barrier();  // the global R appends, for wave 0 and the next split
+  HTICK(hx4);
+  if (lds) HP2(8, hx4 - hx3);
 }
 
 // Wave 0's side of a cooperative return: publish, expand with the others.
-__device__ int coop_return(HbmStore &st, const Slot &sl, const Masks &mk, int s, int rF, int rR,
+template <int LT>
+__device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, int s, int rF, int rR,
                            int rW, int nF, const KParams &p, KeyOut &o, int lane) {
   CoopShared &C = *st.coop;
-  st.begin_return();
   C.slots.pre[lane] = make_int4(sl.nv, sl.nvm, sl.nl, sl.nlm);
   C.slots.val[lane] = sl.val;
   C.slots.pbit[lane] = sl.pbit;
-  if (lane == 0) {
-    C.cmd = kCoopExpand;
-    C.rF = rF;
-    C.rR = rR;
-    C.rW = rW;
-    C.nF = nF;
-    C.bs = 1ull << s;
-    C.muts = mk.occ & ~mk.rdm;
-    C.reads = mk.occ & mk.rdm;
-    C.crashed = mk.crashed;
-    C.epoch = st.epoch;
-    C.nR = 0;
-    C.nW = 0;
-    C.status = 0;
-    C.explored = (unsigned long long)o.explored;
-    C.budget = (long long)p.budget;
+  // LDS tables first when this frontier and the previous return's sets fit
+  constexpr int kLim = CoopTab<LT>::kLim;
+  bool lds = nF <= kLim && st.last <= kLim;
+  const uint32_t floor = max(1024u, 256u * (uint32_t)st.nwaves);
+  if (!lds) st.tmask = st.pick_tmask(nF, floor);
+#ifdef HBM_PROFILE
+  const uint64_t tr0 = wall_clock64();
+  HPROF(4, 1);
+  HPROF(11, nF);
+#endif
+  for (;;) {
+    st.begin_return();  // a fresh epoch per attempt: the aborted one's entries are stale
+    int lclear = 0;
+    if (lds) {
+      st.lepoch = (st.lepoch + 1) & 0xFFFFu;
+      if (st.lepoch == 0) {
+        st.lepoch = 1;
+        lclear = 1;
+      }
+    }
+    if (lane == 0) {
+      C.cmd = kCoopExpand;
+      C.rF = rF;
+      C.rR = rR;
+      C.rW = rW;
+      C.nF = nF;
+      C.bs = 1ull << s;
+      C.muts = mk.occ & ~mk.rdm;
+      C.reads = mk.occ & mk.rdm;
+      C.crashed = mk.crashed;
+      C.epoch = st.epoch;
+      C.tmask = st.tmask;
+      C.lds = lds;
+      C.lclear = lclear;
+      C.lepoch = st.lepoch;
+      C.nR = 0;
+      C.nW = 0;
+      C.status = 0;
+      C.explored = (unsigned long long)o.explored;
+      C.budget = (long long)p.budget;
+    }
+    coop_barrier();  // the workers' start barrier
+    coop_expand<LT>(st, C, lane, 0);
+    if (C.status != -3) break;
+    HPROF(12, 1);
+    if (lds) {
+      lds = false;
+      st.tmask = st.pick_tmask(max(nF, kLim), floor);
+    } else {
+      st.tmask = st.grow_tmask();
+    }
   }
-  coop_barrier();  // the workers' start barrier
-  coop_expand(st, C, lane, 0);
+#ifdef HBM_PROFILE
+  HPROF(8, wall_clock64() - tr0);
+  if (lane == 0 && C.status == 0) {
+    const int mx = max(C.nR, C.nW);
+    const int bkt = min(19, 32 - __builtin_clz((unsigned)max(mx, 1)));
+    atomicAdd(&g_hhist[bkt][0], 1ull);
+    atomicAdd(&g_hhist[bkt][1], (unsigned long long)(wall_clock64() - tr0));
+    atomicAdd(&g_hhist[bkt][2], (unsigned long long)lds);
+    atomicAdd(&g_hhist[bkt][3], (unsigned long long)(C.explored - (unsigned long long)o.explored));
+  }
+#endif
+  if (C.status < 0) return C.status;
   o.explored = (int64_t)C.explored;
-  return C.status < 0 ? C.status : C.nR;
+  st.last = max(C.nR, C.nW);
+  if (!lds) st.hint = max(st.hint, st.last);
+  return C.nR;
 }
 
 // HBM tier: the same expansion as general_return, lane-parallel.  The
@@ -592,12 +933,34 @@ __device__ int coop_return(HbmStore &st, const Slot &sl, const Masks &mk, int s,
 // (insert_lanes) and appended to the regions by ballot prefix.  Every W
 // configuration is still expanded exactly once, so R, the explored count and
 // the verdicts equal the serial expansion's; only the order differs.
-__device__ __forceinline__ int general_return_par(HbmStore &st, const Slot &sl, const Masks &mk,
+__device__ __forceinline__ int general_return_par_try(HbmStore &st, const Slot &sl,
+                                                      const Masks &mk, int s, int rF, int rR,
+                                                      int rW, int nF, const KParams &p, KeyOut &o,
+                                                      int lane);
+template <class S>
+__device__ __forceinline__ int general_return_par(S &st, const Slot &sl, const Masks &mk,
                                                   int s, int rF, int rR, int rW, int nF,
                                                   const KParams &p, KeyOut &o, int lane) {
-  if (st.coop) return coop_return(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
+  if constexpr (S::kLT > 0) return coop_return<S::kLT>(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
+  st.tmask = st.pick_tmask(nF, 1024u);
+  const int64_t explored0 = o.explored;
+  for (;;) {
+    const int r = general_return_par_try(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
+    if (r != -3) return r;
+    o.explored = explored0;
+    st.tmask = st.grow_tmask();
+  }
+}
+
+// One attempt of general_return_par with this return's table size: -3 when
+// a role outgrows it (the caller redoes the return with a larger table).
+__device__ __forceinline__ int general_return_par_try(HbmStore &st, const Slot &sl,
+                                                      const Masks &mk, int s, int rF, int rR,
+                                                      int rW, int nF, const KParams &p, KeyOut &o,
+                                                      int lane) {
   const uint64_t bs = 1ull << s;
   st.begin_return();
+  const int lim = st.lim(1);
   SlotLds &L = *st.sl;
   L.pre[lane] = make_int4(sl.nv, sl.nvm, sl.nl, sl.nlm);
   L.val[lane] = sl.val;
@@ -660,11 +1023,11 @@ __device__ __forceinline__ int general_return_par(HbmStore &st, const Slot &sl, 
         nc = Cfg{toR ? nm & ~bs : nm, pack_sv(nver, nval)};
       }
       o.explored += __popcll(hb);
-      // dedup into R and W (two rounds of inserts, one per role)
-      const int insR = st.insert_lanes(ROLE_R, nc, has && toR);
-      const int insW = st.insert_lanes(ROLE_W, nc, has && !toR);
+      // dedup into R or W, both roles in one round of inserts
+      const int ins = st.insert_lanes(toR ? ROLE_R : ROLE_W, nc, has);
+      const bool insR = ins && toR, insW = ins && !toR;
       const uint64_t bR = __ballot(insR), bW = __ballot(insW);
-      if (nR + __popcll(bR) > st.cap || nW + __popcll(bW) > st.cap) return -1;
+      if (nR + __popcll(bR) > lim || nW + __popcll(bW) > lim) return lim < st.cap ? -3 : -1;
       if (insR) st.reg(rR)[nR + lanes_below(bR)] = nc;
       if (insW) st.reg(rW)[nW + lanes_below(bW)] = nc;
       nR += __popcll(bR);
@@ -674,6 +1037,7 @@ __device__ __forceinline__ int general_return_par(HbmStore &st, const Slot &sl, 
     }
     head += taken;  // entries appended meanwhile are taken by a later batch
   }
+  st.hint = max(st.hint, max(nR, nW));
   return nR;
 }
 
@@ -885,7 +1249,7 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
         return;
       }
       int r;
-      if constexpr (std::is_same<Store, HbmStore>::value)
+      if constexpr (std::is_base_of<HbmStore, Store>::value)
         r = general_return_par(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
       else
         r = general_return(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
@@ -1612,7 +1976,7 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
   st.tabs = st.base + 3 * cap;
   st.tags = reinterpret_cast<uint32_t *>(st.tabs + 4 * cap);
   st.cap = (int)cap;
-  st.tmask = (uint32_t)(2 * cap - 1);
+  st.tmask = st.tmask_full = (uint32_t)(2 * cap - 1);
   // Tags are zeroed by the host before the launch; epochs start at 1.
   st.epoch = 0;
   const int64_t key_base = key_off[0];
@@ -1620,6 +1984,7 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
     const int64_t key = keys[li];
     const int64_t beg = key_off[key], end = key_off[key + 1];
     KeyOut o;
+    st.hint = 0;  // table-size hint: per key
     check_key(ops + (beg - key_base), (int)(end - beg), p, st, o, lane);
     if (o.reason == LC_REASON_FRONTIER_LDS) {
       if (last_tier) {
@@ -1709,9 +2074,15 @@ __global__ __launch_bounds__(NW * kWave) void hbm_coop_kernel(
     const int64_t cap, int32_t *__restrict__ ovf_out, int32_t *__restrict__ n_ovf_out,
     const int last_tier) {
   __shared__ CoopShared C;
+  constexpr int LT = NW >= 16 ? 4096 : 2048;  // LDS table entries per role
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  {  // LDS tags start stale (epochs start at 1)
+    uint32_t *tg = &coop_tab<LT>().tag[0][0];
+    for (int i = threadIdx.x; i < 2 * LT; i += NW * kWave) tg[i] = 0;
+    __syncthreads();
+  }
   char *w = ws + (size_t)blockIdx.x * hbm_wave_bytes(cap);
-  HbmStore st;
+  CoopStore<LT> st;
   st.sl = &C.slots;
   st.coop = &C;
   st.nwaves = NW;
@@ -1719,7 +2090,7 @@ __global__ __launch_bounds__(NW * kWave) void hbm_coop_kernel(
   st.tabs = st.base + 3 * cap;
   st.tags = reinterpret_cast<uint32_t *>(st.tabs + 4 * cap);
   st.cap = (int)cap;
-  st.tmask = (uint32_t)(2 * cap - 1);
+  st.tmask = st.tmask_full = (uint32_t)(2 * cap - 1);
   st.epoch = 0;  // tags zeroed by the host; epochs start at 1
   if (wave == 0) {
     const int64_t key_base = key_off[0];
@@ -1727,7 +2098,16 @@ __global__ __launch_bounds__(NW * kWave) void hbm_coop_kernel(
       const int64_t key = keys[li];
       const int64_t beg = key_off[key], end = key_off[key + 1];
       KeyOut o;
+      st.hint = 0;  // table-size hints: per key
+      st.last = 0;
+#ifdef HBM_PROFILE
+      const uint64_t tk0 = wall_clock64();
+#endif
       check_key(ops + (beg - key_base), (int)(end - beg), p, st, o, lane);
+#ifdef HBM_PROFILE
+      HPROF(9, wall_clock64() - tk0);
+      HPROF(13, o.explored);
+#endif
       if (o.reason == LC_REASON_FRONTIER_LDS) {
         if (last_tier)
           o.reason = LC_REASON_CONFIG_BUDGET;
@@ -1737,12 +2117,35 @@ __global__ __launch_bounds__(NW * kWave) void hbm_coop_kernel(
       if (lane == 0) write_result(&out[key], o);
     }
     if (lane == 0) C.cmd = kCoopExit;
+#ifdef HBM_PROFILE
+    __threadfence();
+    if (lane == 0 && atomicAdd(&g_hdone, 1u) == gridDim.x - 1)
+    {
+      if (lane == 0 && g_hdone == gridDim.x)
+        printf("hp2 lds: split %llu bar0 %llu levels %llu level-work %llu rounds %llu insert %llu "
+               "bar1 %llu bar2 %llu endbar %llu expands %llu | batches %llu batch %llu cand %llu rounds %llu\n", g_hp2[0], g_hp2[1], g_hp2[3], g_hp2[2],
+               g_hp2[5], g_hp2[4], g_hp2[6], g_hp2[7], g_hp2[8], g_hp2[9], g_hp2[11], g_hp2[10], g_hp2[12], g_hp2[13]);
+    }
+    if (lane == 0 && g_hdone == gridDim.x)
+      for (int b = 0; b < 20; b++)
+        if (g_hhist[b][0])
+          printf("hist set<2^%d: returns %llu ticks %llu lds %llu configs %llu\n", b, g_hhist[b][0],
+                 g_hhist[b][1], g_hhist[b][2], g_hhist[b][3]);
+    if (blockIdx.x < 2 && lane == 0)
+      printf("hbm coop wg %d: levels %llu rounds %llu insert-iters %llu configs %llu cyc: cand %llu insert %llu barrier %llu"
+             " | returns %llu sumF %llu retries %llu explored %llu ticks: key %llu return %llu split %llu | lds rounds %llu insert %llu\n",
+             (int)blockIdx.x, g_hprof[blockIdx.x][0], g_hprof[blockIdx.x][1], g_hprof[blockIdx.x][2],
+             g_hprof[blockIdx.x][3], g_hprof[blockIdx.x][5], g_hprof[blockIdx.x][6], g_hprof[blockIdx.x][7],
+             g_hprof[blockIdx.x][4], g_hprof[blockIdx.x][11], g_hprof[blockIdx.x][12], g_hprof[blockIdx.x][13],
+             g_hprof[blockIdx.x][9], g_hprof[blockIdx.x][8], g_hprof[blockIdx.x][10],
+             g_hprof[blockIdx.x][15], g_hprof[blockIdx.x][14]);
+#endif
     coop_barrier();
   } else {
     for (;;) {
       coop_barrier();
       if (C.cmd == kCoopExit) break;
-      coop_expand(st, C, lane, wave);
+      coop_expand<LT>(st, C, lane, wave);
     }
   }
 }
