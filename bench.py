@@ -412,12 +412,18 @@ def model_leg(ctx, abi):
         times.append((time.perf_counter() - t0) * 1e3)
         st.append(ctx.stats())
     t = float(np.median(times[1:]))
+    hbm_ms = float(np.median([x["hbm_kernel_ms"] for x in st[1:]]))
+    explored = int(r["configs_explored"].sum())
     return {"workload": "cas-register model: 1000 keys x 1000 ops, concurrency 20 (host buffers)",
             "call_ms": t, "ops_per_s": int(off[-1]) / (t * 1e-3),
             "jit_kernel_ms": float(np.median([x["jit_kernel_ms"] for x in st[1:]])),
-            "hbm_kernel_ms": float(np.median([x["hbm_kernel_ms"] for x in st[1:]])),
+            "hbm_kernel_ms": hbm_ms,
             "hbm_keys": int(st[-1]["n_hbm_keys"]),
-            "configs_explored": int(r["configs_explored"].sum()),
+            "configs_explored": explored,
+            # probe throughput: every configuration explored is one dedup probe
+            # (most in LDS tables since round 2; HBM bytes per probe from the
+            # PMC pass, profiles/r02/pmc_model_hbm_coop4.json)
+            "probes_per_s": explored / (hbm_ms * 1e-3) if hbm_ms > 0 else None,
             "max_frontier": int(r["max_frontier"].max()),
             "valid": int((r["verdict"] == 1).sum()), "unknown": int((r["verdict"] == -1).sum())}
 

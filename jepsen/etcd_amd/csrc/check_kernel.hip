@@ -45,23 +45,11 @@ namespace lcdev {
 namespace {
 
 #ifdef HBM_PROFILE
-// dev only: per-workgroup counters of the cooperative expansion (wave 0 of
-// workgroups 0..3): levels, rounds, insert probe iterations, configurations,
-// and clocks in candidate generation / inserts / barriers
-__device__ unsigned long long g_hprof[4][16];
-// per log2(max set of a return): returns, ticks, LDS-mode returns, configs (all workgroups)
+// Dev only (tools/build_variants.sh NAME -DHBM_PROFILE): per cooperative
+// return, by log2 of its larger set: returns, device ticks (100 MHz), LDS-
+// mode returns, configurations explored; printed by the last workgroup.
 __device__ unsigned long long g_hhist[20][4];
 __device__ unsigned int g_hdone;
-__device__ unsigned long long g_hp2[16];
-#define HP2(i, v) \
-  do { if (blockIdx.x < 64 && (threadIdx.x & 63) == 0) atomicAdd(&g_hp2[i], (unsigned long long)(v)); } while (0)
-#define HTICK(x) const uint64_t x = wall_clock64()
-#define HPROF(i, v) \
-  do { if (blockIdx.x < 4 && threadIdx.x == 0) g_hprof[blockIdx.x][i] += (v); } while (0)
-#else
-#define HPROF(i, v) do { } while (0)
-#define HP2(i, v) do { } while (0)
-#define HTICK(x) do { } while (0)
 #endif
 
 struct Cfg {
@@ -158,8 +146,9 @@ struct LdsStore {
 // valid when their epoch tag equals the current return's epoch, so a table is
 // "cleared" by bumping the epoch.  One wave owns one workspace.  Probing is
 // linear from the start of the hashed bucket, whole buckets at a time.
-// Per-return copy of the window's slots in LDS, so each lane can test any
-// slot against its own configuration (HBM tier's lane-parallel expansion).
+// Per-return copy of the window's slots in LDS for the cooperative tier's
+// worker waves (each loads slot `lane` into registers and tests slots with
+// ballots / v_readlane, see legal_by_state).
 struct SlotLds {
   int4 pre[kWave];      // (nv, nvm, nl, nlm)
   int val[kWave];
@@ -184,6 +173,7 @@ struct CoopShared {
     unsigned long long nRW;
   };
   int head, lo, hi, go, status;
+  unsigned long long qword;  // LDS work queue: claimed head (low), expanding waves (high)
   int lds;  // this attempt keeps its tables and sets in LDS (CoopTab)
   uint32_t lepoch;  // its LDS epoch (16 bits)
   int lclear;       // the LDS epoch wrapped: clear the tags first
@@ -194,7 +184,6 @@ struct CoopShared {
 
 struct HbmStore {
   static constexpr int kLT = 0;  // no LDS tables (CoopStore has them)
-  SlotLds *sl;    // slot staging (LDS)
   CoopShared *coop = nullptr;  // set in the cooperative kernel
   int nwaves = 1;
   Cfg *base;      // 3 regions of cap configurations, contiguous
@@ -323,7 +312,6 @@ struct HbmStore {
     int res = 0;
     bool pend = want;
     while (__ballot(pend)) {
-      HPROF(2, 1);
       if (pend) {
         const uint32_t t = __hip_atomic_load(&tag(role)[h], __ATOMIC_ACQUIRE,
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -394,6 +382,7 @@ struct HbmStore {
 // A table entry is 4 bytes, (epoch << 16) | index into the role's set, so
 // the LDS holds kLim = 5/16 of the table size per set (load <= 31%): 640
 // configurations in 36 KB with 4-wave workgroups, four of them per CU.
+constexpr int kSpinMax = 1 << 22;       // queue waits (s_sleep 1 each) before giving up
 constexpr uint32_t kIdxBusy = 0xFFFFu;  // claimed, index not yet published
 constexpr uint32_t kIdxOvf = 0xFFFEu;   // claimed past kLim (the return is redone)
 template <int LT>
@@ -402,6 +391,7 @@ struct CoopTab {
   static_assert(kLim < (int)kIdxOvf, "set index must fit 16 bits");
   uint32_t tag[2][LT];  // (epoch << 16) | index, per role
   Cfg set[2][kLim];     // R and W of this return
+  uint16_t wrdy[kLim];  // W entry written (its epoch): the work queue's readiness
 };
 template <int LT>
 __device__ __forceinline__ CoopTab<LT> &coop_tab() {
@@ -487,7 +477,8 @@ __device__ __forceinline__ int lds_insert_lanes(CoopTab<LT> &T, CoopShared &C, H
       if (won) {
         const int ix = role == ROLE_R ? aR + lanes_below(wR) : aW + lanes_below(wW);
         uint32_t pub = eb | kIdxOvf;
-        if (ix < CoopTab<LT>::kLim) {
+        const bool fits = ix < CoopTab<LT>::kLim;
+        if (fits) {
           T.set[role][ix] = c;
           if (role == ROLE_R) st.reg(rR)[ix] = c;
           pub = eb | (uint32_t)ix;
@@ -495,6 +486,8 @@ __device__ __forceinline__ int lds_insert_lanes(CoopTab<LT> &T, CoopShared &C, H
           ovf = true;
         }
         lds_tag_publish(&T.tag[role][h], pub);
+        if (fits && role == ROLE_W)  // queue readiness, after the release above
+          __hip_atomic_store(&T.wrdy[ix], (uint16_t)(eb >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         res = 1;
         pend = false;
       }
@@ -637,6 +630,25 @@ __device__ __forceinline__ void coop_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// Per lane, the slots (lane t holds slot t's precondition in spre) legal in
+// the lane's state (ver, val): one ballot per distinct state among the
+// lanes, which share few states (a batch's configurations differ mostly in
+// which ops they linearized), instead of a test per slot and lane.
+__device__ __forceinline__ uint64_t legal_by_state(const int4 &spre, int ver, int val, bool act) {
+  uint64_t legal = 0;
+  bool todo = act;
+  for (uint64_t pend = __ballot(todo); pend; pend = __ballot(todo)) {
+    const int l = __builtin_ctzll(pend);
+    const int sver = rl32(ver, l), sval = rl32(val, l);
+    const uint64_t m = __ballot(pre_ok(spre.x, spre.y, spre.z, spre.w, sver, sval));
+    if (todo && ver == sver && val == sval) {
+      legal = m;
+      todo = false;
+    }
+  }
+  return legal;
+}
+
 // One wave's share of a cooperative expansion (every wave of the workgroup
 // calls it; the parameters are in C).  Barrier count is uniform: one after
 // the split, two per BFS level.
@@ -653,6 +665,7 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
   if (lds && C.lclear) {  // the 16-bit LDS epoch wrapped: clear the tags
     uint32_t *tg = &T.tag[0][0];
     for (int i = wave * kWave + lane; i < 2 * LT; i += nw * kWave) tg[i] = 0;
+    for (int i = wave * kWave + lane; i < CoopTab<LT>::kLim; i += nw * kWave) T.wrdy[i] = 0;
     lds_barrier();
   }
   const uint64_t bs = C.bs, crashed = C.crashed;
@@ -662,7 +675,6 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
   // Lane t holds slot t's precondition, value and class bit: the candidate
   // and read-closure loops run over slots uniformly and read them with
   // v_readlane (no dependent LDS load per slot and lane).
-  HTICK(hx0);
   const int4 spre = L.pre[lane];
   const int sval = L.val[lane];
   const uint64_t spbit = L.pbit[lane];
@@ -693,7 +705,8 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
       if (lacks) {
         const int ix = bW + lanes_below(ml);
         T.set[ROLE_W][ix] = c;
-        lds_claim_lane(T, ROLE_W, c, ix, eb, ovf);
+        lds_claim_lane(T, ROLE_W, c, ix, eb, ovf);  // (releases the entry first)
+        __hip_atomic_store(&T.wrdy[ix], (uint16_t)(eb >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     } else {
       if (has) st.claim_unique_lane(ROLE_R, rR, bR + lanes_below(mh), Cfg{c.mask & ~bs, c.sv});
@@ -701,82 +714,121 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
     }
   }
   if (__ballot(ovf) && lane == 0) atomicMin(&C.status, -3);
-  HTICK(hx1);
-  if (lds) HP2(0, hx1 - hx0);
-  // Level bounds and the go flag are written by wave 0 between two barriers,
-  // while no wave appends, so every wave reads the same values.
-#ifdef HBM_PROFILE
-  const uint64_t ts0 = wall_clock64();
-#endif
-  if (lds) lds_barrier(); else coop_barrier();
-#ifdef HBM_PROFILE
-  HPROF(10, wall_clock64() - ts0);
-#endif
-  if (wave == 0 && lane == 0) {
-    C.lo = 0;
-    C.hi = C.nW;
-    C.head = 0;
-    C.go = C.hi > 0 && C.status == 0;
+  if (lds) {
+    // LDS: W is a work queue.  The split's claims must all be in the tables
+    // before any successor is deduplicated against them: one barrier.
+    lds_barrier();
+  } else {
+    // HBM: level-synchronous.  Level bounds and the go flag are written by
+    // wave 0 between two barriers, while no wave appends, so every wave
+    // reads the same values.
+    coop_barrier();
+    if (wave == 0 && lane == 0) {
+      C.lo = 0;
+      C.hi = C.nW;
+      C.head = 0;
+      C.go = C.hi > 0 && C.status == 0;
+    }
+    coop_barrier();
   }
-  if (lds) lds_barrier(); else coop_barrier();
-  HTICK(hx2);
-  if (lds) HP2(1, hx2 - hx1);
-  if (lds) HP2(9, 1);
-  while (C.go) {
-    HPROF(0, 1);
-    HTICK(hl0);
-    if (lds) HP2(3, 1);
-    const int lo = C.lo, hi = C.hi;
-    // this level: W[lo, hi) in batches of 64 claimed from C.head
-    for (;;) {
-      int b = 0;
-      if (lane == 0) b = atomicAdd(&C.head, kWave);
-      b = __builtin_amdgcn_readfirstlane(b) + lo;
-      if (b >= hi || __hip_atomic_load(&C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-        break;
-      const int j = b + lane;
-      const bool act = j < hi;
-#ifdef HBM_PROFILE
-      const uint64_t tc0 = wall_clock64();
-#endif
-      HTICK(hb0);
-      const Cfg c = lds ? T.set[ROLE_W][act ? j : b] : st.get(rW, act ? j : b);
-      const int cver = sv_ver(c.sv), cval = sv_val(c.sv);
-      uint64_t cand = 0;
-      for (uint64_t m = muts; m; m &= m - 1) {  // uniform over pending mutations
-        const int t = __builtin_ctzll(m);
-        bool ok = pre_ok(rl32(spre.x, t), rl32(spre.y, t), rl32(spre.z, t), rl32(spre.w, t), cver, cval);
-        if ((crashed >> t) & 1) ok = ok && (rl64(spbit, t) & ~c.mask) == 0;
-        if (ok) cand |= 1ull << t;
+  const uint32_t ep16 = eb >> 16;
+  for (;;) {
+    int lo = 0, hi = 0;
+    if (!lds) {
+      if (!C.go) break;
+      lo = C.lo;
+      hi = C.hi;
+    }
+    for (;;) {  // batches of up to 64 W configurations
+      int b = 0, k = 0;
+      if (lds) {
+        // Queue claim: (head, active) packed in one word, so a wave that
+        // finds the queue empty leaves only when no wave is expanding (a
+        // wave that still expands re-reads the queue after its appends).
+        if (lane == 0) {
+          for (int spin = 0;; spin++) {
+            if (spin == kSpinMax) atomicMin(&C.status, -3);  // safety net: redone in HBM
+            if (__hip_atomic_load(&C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+              k = -1;
+              break;
+            }
+            const unsigned long long q =
+                __hip_atomic_load(&C.qword, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int h = (int)(uint32_t)q;
+            const int n = min(__hip_atomic_load(&C.nW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
+                              CoopTab<LT>::kLim);
+            if (h < n) {
+              const int kk = min(kWave, n - h);
+              if (atomicCAS(&C.qword, q, q + (unsigned long long)kk + (1ull << 32)) == q) {
+                b = h;
+                k = kk;
+                break;
+              }
+              continue;
+            }
+            if ((q >> 32) == 0) {  // nothing queued, nobody expanding
+              k = -1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        k = uni(k);
+        b = uni(b);
+        if (k < 0) break;
+      } else {
+        if (lane == 0) b = atomicAdd(&C.head, kWave);
+        b = uni(b) + lo;
+        if (b >= hi || __hip_atomic_load(&C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+          break;
+        k = min(kWave, hi - b);
       }
-      cand &= act ? ~c.mask : 0ull;
+      const int j = b + lane;
+      const bool act = lane < k;
+      Cfg c;
+      if (lds) {
+        // entries reserved by a wave still in its round: wait for their flag
+        if (act)
+          for (int spin = 0; __hip_atomic_load(&T.wrdy[j], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP) != ep16; spin++) {
+            if (spin == kSpinMax) {  // safety net (a writer is always mid-round): redone in HBM
+              ovf = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        if (__ballot(ovf)) {
+          if (lane == 0) {
+            atomicMin(&C.status, -3);
+            atomicAdd(&C.qword, ~0ull << 32);
+          }
+          break;
+        }
+        lds_acquire();
+        c = T.set[ROLE_W][act ? j : b];
+      } else {
+        c = st.get(rW, act ? j : b);
+      }
+      const int cver = sv_ver(c.sv), cval = sv_val(c.sv);
+      uint64_t cand = legal_by_state(spre, cver, cval, act) & muts & ~c.mask;
+      // a crashed op only if it is the earliest unlinearized of its class
+      for (uint64_t m = muts & crashed; m; m &= m - 1) {
+        const int t = __builtin_ctzll(m);
+        if (rl64(spbit, t) & ~c.mask) cand &= ~(1ull << t);
+      }
       unsigned long long exw = 0;  // this batch's successors (one atomic per batch)
-      HTICK(hb1);
-      if (lds) HP2(12, hb1 - hb0);
-#ifdef HBM_PROFILE
-      HPROF(5, wall_clock64() - tc0);
-#endif
       for (;;) {
         const bool has = cand != 0;
         const uint64_t hb = __ballot(has);
         if (!hb) break;
-        HPROF(1, 1);
-        HPROF(3, __popcll(hb));
         exw += __popcll(hb);
         const int t = has ? __builtin_ctzll(cand) : 0;
         cand &= cand - 1;
         const int nver = cver + 1, nval = __shfl(sval, t);
         uint64_t nm = c.mask | (1ull << t);
-        for (uint64_t r = reads; r; r &= r - 1) {  // eager read closure, uniform over reads
-          const int u = __builtin_ctzll(r);
-          if (pre_ok(rl32(spre.x, u), rl32(spre.y, u), rl32(spre.z, u), rl32(spre.w, u), nver, nval))
-            nm |= 1ull << u;
-        }
+        nm |= legal_by_state(spre, nver, nval, has) & reads;  // eager read closure
         const bool toR = (nm & bs) != 0;
         const Cfg nc{toR ? nm & ~bs : nm, pack_sv(nver, nval)};
-#ifdef HBM_PROFILE
-        const uint64_t ti0 = wall_clock64();
-#endif
         if (lds) {  // inserts, set indices and appends in one pass
           lds_insert_lanes(T, C, st, rR, toR ? ROLE_R : ROLE_W, nc, has, eb, ovf, lane);
           if (__ballot(ovf)) {
@@ -786,13 +838,6 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
           continue;
         }
         const int ins = st.insert_lanes_coop(toR ? ROLE_R : ROLE_W, nc, has);
-#ifdef HBM_PROFILE
-        HPROF(6, wall_clock64() - ti0);
-        if (lds) HPROF(14, wall_clock64() - ti0);
-        if (lds) HP2(4, wall_clock64() - ti0);
-        if (lds) HP2(5, 1);
-        if (lds) HPROF(15, 1);
-#endif
         const bool insR = ins && toR, insW = ins && !toR;
         const uint64_t bR = __ballot(insR), bW = __ballot(insW);
         unsigned long long aRW = 0;
@@ -815,36 +860,19 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
         const unsigned long long ex = atomicAdd(&C.explored, exw) + exw;
         if ((long long)ex > C.budget && C.status == 0) atomicMin(&C.status, -2);
       }
-      HTICK(hb2);
-      if (lds) HP2(10, hb2 - hb0);
-      if (lds) HP2(13, hb2 - hb1);
-      if (lds) HP2(11, 1);
+      if (lds && lane == 0) atomicAdd(&C.qword, ~0ull << 32);  // active - 1, after the appends
     }
-#ifdef HBM_PROFILE
-    const uint64_t tb0 = wall_clock64();
-#endif
-    HTICK(hl1);
-    if (lds) HP2(2, hl1 - hl0);
-    if (lds) lds_barrier(); else coop_barrier();  // the level's appends are done
-    HTICK(hl2);
-    if (lds) HP2(6, hl2 - hl1);
-#ifdef HBM_PROFILE
-    HPROF(7, wall_clock64() - tb0);
-#endif
+    if (lds) break;
+    coop_barrier();  // the level's appends are done
     if (wave == 0 && lane == 0) {
       C.lo = hi;
       C.hi = C.nW;
       C.head = 0;
       C.go = C.lo < C.hi && C.status == 0;
     }
-    if (lds) lds_barrier(); else coop_barrier();
-    HTICK(hl3);
-    if (lds) HP2(7, hl3 - hl2);
+    coop_barrier();
   }
-  HTICK(hx3);
   if (lds) coop_barrier();  // the global R appends, for wave 0 and the next split
-  HTICK(hx4);
-  if (lds) HP2(8, hx4 - hx3);
 }
 
 // Wave 0's side of a cooperative return: publish, expand with the others.
@@ -862,8 +890,6 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
   if (!lds) st.tmask = st.pick_tmask(nF, floor);
 #ifdef HBM_PROFILE
   const uint64_t tr0 = wall_clock64();
-  HPROF(4, 1);
-  HPROF(11, nF);
 #endif
   for (;;) {
     st.begin_return();  // a fresh epoch per attempt: the aborted one's entries are stale
@@ -888,6 +914,7 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
       C.epoch = st.epoch;
       C.tmask = st.tmask;
       C.lds = lds;
+      C.qword = 0;
       C.lclear = lclear;
       C.lepoch = st.lepoch;
       C.nR = 0;
@@ -899,7 +926,6 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
     coop_barrier();  // the workers' start barrier
     coop_expand<LT>(st, C, lane, 0);
     if (C.status != -3) break;
-    HPROF(12, 1);
     if (lds) {
       lds = false;
       st.tmask = st.pick_tmask(max(nF, kLim), floor);
@@ -908,7 +934,6 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
     }
   }
 #ifdef HBM_PROFILE
-  HPROF(8, wall_clock64() - tr0);
   if (lane == 0 && C.status == 0) {
     const int mx = max(C.nR, C.nW);
     const int bkt = min(19, 32 - __builtin_clz((unsigned)max(mx, 1)));
@@ -961,10 +986,6 @@ __device__ __forceinline__ int general_return_par_try(HbmStore &st, const Slot &
   const uint64_t bs = 1ull << s;
   st.begin_return();
   const int lim = st.lim(1);
-  SlotLds &L = *st.sl;
-  L.pre[lane] = make_int4(sl.nv, sl.nvm, sl.nl, sl.nlm);
-  L.val[lane] = sl.val;
-  L.pbit[lane] = sl.pbit;
   int nR = 0, nW = 0;
   for (int j0 = 0; j0 < nF; j0 += kWave) {  // split F into R and W, as serially
     const int j = j0 + lane;
@@ -981,6 +1002,7 @@ __device__ __forceinline__ int general_return_par_try(HbmStore &st, const Slot &
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const uint64_t muts = mk.occ & ~mk.rdm, reads = mk.occ & mk.rdm;
+  const int4 spre = make_int4(sl.nv, sl.nvm, sl.nl, sl.nlm);  // lane t: slot t
   for (int head = 0; head < nW;) {
     const int j = head + lane;
     const bool act = j < nW;  // this batch: W[head, min(head + 64, nW)) as of now
@@ -989,39 +1011,22 @@ __device__ __forceinline__ int general_return_par_try(HbmStore &st, const Slot &
     const int cver = sv_ver(c.sv), cval = sv_val(c.sv);
     // candidates: legal pending mutations; a crashed one only if it is the
     // earliest unlinearized member of its class
-    uint64_t cand = 0;
-    if (act) {
-      uint64_t m = muts & ~c.mask;
-      while (m) {
-        const int t = __builtin_ctzll(m);
-        m &= m - 1;
-        const int4 pr = L.pre[t];
-        if (pre_ok(pr.x, pr.y, pr.z, pr.w, cver, cval) &&
-            (!((mk.crashed >> t) & 1) || (L.pbit[t] & ~c.mask) == 0))
-          cand |= 1ull << t;
-      }
+    uint64_t cand = legal_by_state(spre, cver, cval, act) & muts & ~c.mask;
+    for (uint64_t m = muts & mk.crashed; m; m &= m - 1) {
+      const int t = __builtin_ctzll(m);
+      if (rl64(sl.pbit, t) & ~c.mask) cand &= ~(1ull << t);
     }
     for (;;) {
       const bool has = cand != 0;
       const uint64_t hb = __ballot(has);
       if (!hb) break;
-      Cfg nc{0, 0};
-      bool toR = false;
-      if (has) {
-        const int t = __builtin_ctzll(cand);
-        cand &= cand - 1;
-        const int nver = cver + 1, nval = L.val[t];
-        uint64_t nm = c.mask | (1ull << t);
-        uint64_t r = reads & ~nm;  // eager read closure at the successor
-        while (r) {
-          const int u = __builtin_ctzll(r);
-          r &= r - 1;
-          const int4 pr = L.pre[u];
-          if (pre_ok(pr.x, pr.y, pr.z, pr.w, nver, nval)) nm |= 1ull << u;
-        }
-        toR = (nm & bs) != 0;
-        nc = Cfg{toR ? nm & ~bs : nm, pack_sv(nver, nval)};
-      }
+      const int t = has ? __builtin_ctzll(cand) : 0;
+      cand &= cand - 1;
+      const int nver = cver + 1, nval = __shfl(sl.val, t);
+      uint64_t nm = c.mask | (1ull << t);
+      nm |= legal_by_state(spre, nver, nval, has) & reads;  // eager read closure
+      const bool toR = (nm & bs) != 0;
+      const Cfg nc{toR ? nm & ~bs : nm, pack_sv(nver, nval)};
       o.explored += __popcll(hb);
       // dedup into R or W, both roles in one round of inserts
       const int ins = st.insert_lanes(toR ? ROLE_R : ROLE_W, nc, has);
@@ -1969,9 +1974,7 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
     const int last_tier) {
   const int lane = threadIdx.x;
   char *w = ws + (size_t)blockIdx.x * hbm_wave_bytes(cap);
-  __shared__ SlotLds slots;
   HbmStore st;
-  st.sl = &slots;
   st.base = reinterpret_cast<Cfg *>(w);
   st.tabs = st.base + 3 * cap;
   st.tags = reinterpret_cast<uint32_t *>(st.tabs + 4 * cap);
@@ -2067,7 +2070,7 @@ __global__ __launch_bounds__(kCompactThreads) void handoff_compact_kernel(
 // the higher-capacity tiers).  Wave 0 runs the event loop; waves 1..NW-1
 // serve its expansions until told to exit.
 template <int NW>
-__global__ __launch_bounds__(NW * kWave) void hbm_coop_kernel(
+__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4))) void hbm_coop_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
     const int32_t *__restrict__ keys, const int32_t n_list,
     const KParams p, lc_key_result *__restrict__ out, char *__restrict__ ws,
@@ -2076,14 +2079,14 @@ __global__ __launch_bounds__(NW * kWave) void hbm_coop_kernel(
   __shared__ CoopShared C;
   constexpr int LT = NW >= 16 ? 4096 : 2048;  // LDS table entries per role
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  {  // LDS tags start stale (epochs start at 1)
+  {  // LDS tags and W flags start stale (epochs start at 1)
     uint32_t *tg = &coop_tab<LT>().tag[0][0];
     for (int i = threadIdx.x; i < 2 * LT; i += NW * kWave) tg[i] = 0;
+    for (int i = threadIdx.x; i < CoopTab<LT>::kLim; i += NW * kWave) coop_tab<LT>().wrdy[i] = 0;
     __syncthreads();
   }
   char *w = ws + (size_t)blockIdx.x * hbm_wave_bytes(cap);
   CoopStore<LT> st;
-  st.sl = &C.slots;
   st.coop = &C;
   st.nwaves = NW;
   st.base = reinterpret_cast<Cfg *>(w);
@@ -2100,14 +2103,7 @@ __global__ __launch_bounds__(NW * kWave) void hbm_coop_kernel(
       KeyOut o;
       st.hint = 0;  // table-size hints: per key
       st.last = 0;
-#ifdef HBM_PROFILE
-      const uint64_t tk0 = wall_clock64();
-#endif
       check_key(ops + (beg - key_base), (int)(end - beg), p, st, o, lane);
-#ifdef HBM_PROFILE
-      HPROF(9, wall_clock64() - tk0);
-      HPROF(13, o.explored);
-#endif
       if (o.reason == LC_REASON_FRONTIER_LDS) {
         if (last_tier)
           o.reason = LC_REASON_CONFIG_BUDGET;
@@ -2120,25 +2116,10 @@ __global__ __launch_bounds__(NW * kWave) void hbm_coop_kernel(
 #ifdef HBM_PROFILE
     __threadfence();
     if (lane == 0 && atomicAdd(&g_hdone, 1u) == gridDim.x - 1)
-    {
-      if (lane == 0 && g_hdone == gridDim.x)
-        printf("hp2 lds: split %llu bar0 %llu levels %llu level-work %llu rounds %llu insert %llu "
-               "bar1 %llu bar2 %llu endbar %llu expands %llu | batches %llu batch %llu cand %llu rounds %llu\n", g_hp2[0], g_hp2[1], g_hp2[3], g_hp2[2],
-               g_hp2[5], g_hp2[4], g_hp2[6], g_hp2[7], g_hp2[8], g_hp2[9], g_hp2[11], g_hp2[10], g_hp2[12], g_hp2[13]);
-    }
-    if (lane == 0 && g_hdone == gridDim.x)
       for (int b = 0; b < 20; b++)
         if (g_hhist[b][0])
-          printf("hist set<2^%d: returns %llu ticks %llu lds %llu configs %llu\n", b, g_hhist[b][0],
+          printf("set<2^%d: returns %llu ticks %llu lds %llu configs %llu\n", b, g_hhist[b][0],
                  g_hhist[b][1], g_hhist[b][2], g_hhist[b][3]);
-    if (blockIdx.x < 2 && lane == 0)
-      printf("hbm coop wg %d: levels %llu rounds %llu insert-iters %llu configs %llu cyc: cand %llu insert %llu barrier %llu"
-             " | returns %llu sumF %llu retries %llu explored %llu ticks: key %llu return %llu split %llu | lds rounds %llu insert %llu\n",
-             (int)blockIdx.x, g_hprof[blockIdx.x][0], g_hprof[blockIdx.x][1], g_hprof[blockIdx.x][2],
-             g_hprof[blockIdx.x][3], g_hprof[blockIdx.x][5], g_hprof[blockIdx.x][6], g_hprof[blockIdx.x][7],
-             g_hprof[blockIdx.x][4], g_hprof[blockIdx.x][11], g_hprof[blockIdx.x][12], g_hprof[blockIdx.x][13],
-             g_hprof[blockIdx.x][9], g_hprof[blockIdx.x][8], g_hprof[blockIdx.x][10],
-             g_hprof[blockIdx.x][15], g_hprof[blockIdx.x][14]);
 #endif
     coop_barrier();
   } else {
