@@ -59,7 +59,7 @@ def parse():
                     help="timed region only (no CPU baseline, no hot-key leg): "
                          "for rocprofv3 runs whose per-kernel averages must "
                          "match the bench line")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "traffic_fast_tier.json"))
     return ap.parse_args()
 
 
@@ -205,8 +205,8 @@ def main():
             "kernel_ms": dom_ms,
             "algorithmic_bytes_per_launch": algo_bytes,
             "algorithmic_bytes": "48 B/op record read + 40 B/key result (DESIGN.md §6)",
-            "traffic_source": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch, profiles/"
-                              + os.path.basename(args.traffic_json),
+            "traffic_source": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch, "
+                              + os.path.relpath(args.traffic_json, ROOT),
             "l2_hit_rate": l2_hit,
         },
         "tiers": {"fast_kernel_ms": fast_ms, "gap_kernel_ms": gap_ms, "jit_kernel_ms": jit_ms,
