@@ -32,7 +32,7 @@ arguments raise LcError, and jepsen's check-safe turns an exception into
 """
 import os
 
-from . import abi, diagnostics as D, history as H, timeline as TL
+from . import abi, diagnostics as D, history as H, linear_svg as LS, timeline as TL
 
 UNKNOWN = "unknown"
 
@@ -139,7 +139,13 @@ class RegisterChecker:
         if not self.independent:
             return results[None]
         subs = H.split_by_key(H.index_history(history)) if self.timeline_dir else None
-        for k, lin in results.items():
+        for i, (k, lin) in enumerate(results.items()):
+            if self.timeline_dir and lin["valid?"] is False and "final-paths" in lin:
+                # jepsen's checker/linearizable renders a failed analysis
+                # into the key's directory as linear.svg
+                lin["linear-svg"] = LS.write(
+                    os.path.join(self.timeline_dir, "independent", str(k), "linear.svg"),
+                    done[i], lin, title="key %s" % (k,))
             results[k] = self._composed(k, lin, subs)
         return {"valid?": _merge_valid(r["valid?"] for r in results.values()),
                 "results": results,

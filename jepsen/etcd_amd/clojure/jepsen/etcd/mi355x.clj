@@ -318,14 +318,29 @@
           {:valid? true :analyzer :mi355x}
           (get (check-keys model max-configs-per-key time-budget-ms {nil ops}) nil))))))
 
+(defn- render-linear!
+  "What jepsen's checker/linearizable does with a failed analysis: knossos's
+  own renderer draws it into the key's directory as linear.svg.  A rendering
+  error is swallowed (jepsen only warns); it never changes the verdict."
+  [test subdir sub linear]
+  (when (and (false? (:valid? linear)) (seq (:final-paths linear)))
+    (try
+      (let [render! (requiring-resolve 'knossos.linear.report/render-analysis!)
+            path!   (requiring-resolve 'jepsen.store/path!)
+            ^java.io.File f (path! test subdir "linear.svg")]
+        (render! sub linear (.getCanonicalPath f)))
+      (catch Throwable _ nil))))
+
 (defn- composed
   "checker/compose's per-key map (register.clj:109-112): the GPU's :linear
   result beside jepsen's own timeline/html, which renders into the key's
-  independent/ subdirectory as jepsen.independent/checker would direct it."
+  independent/ subdirectory as jepsen.independent/checker would direct it
+  (plus linear.svg for an invalid key, as checker/linearizable writes it)."
   [test opts k sub linear timeline?]
   (if-not timeline?
     {:valid? (:valid? linear) :linear linear}
     (let [subdir (concat (:subdirectory opts) ["independent" k])
+          _      (render-linear! test subdir sub linear)
           tl     (checker/check-safe (timeline/html) test sub
                                      {:subdirectory subdir :history-key k})]
       {:valid?   (merge-valid [(:valid? linear) (:valid? tl)])

@@ -81,3 +81,41 @@ def test_analysis_on_synthetic_anomalies():
             assert "inconsistent" in path[-1]["model"]
             assert all("inconsistent" not in s["model"] for s in path[:-1])
     assert n_inv >= 10
+
+
+def test_linear_svg_draws_the_failure(tmp_path):
+    """linear.svg (jepsen/etcd_amd/linear_svg.py, the restated knossos
+    render-analysis! figure): one bar per op the analysis names, the failing
+    op drawn as the failure, every final path ending in a red inconsistent
+    step labelled with the model's message; valid XML."""
+    import xml.etree.ElementTree as ET
+    from jepsen.etcd_amd import linear_svg as LS
+    hist, labels = synth.jepsen_history(20, 120, concurrency=8, p_info=0.1,
+                                        p_anomaly=0.8, seed=23)
+    keys, ops, off, done = H.pack(hist)
+    drawn = 0
+    for k in range(len(keys)):
+        recs = [tuple(r) for r in ops[off[k]:off[k + 1]].tolist()]
+        if gm.decide(recs) != 0:
+            continue
+        fo, at = gm.first_failure(recs)
+        v, w = gm.decide(recs, cutoff=at - 1, witness=True)
+        a = D.invalid_analysis(done[k], fo, at, np.array(w))
+        d = done[k][fo]
+        a["op"] = d["completion"] or d["invoke"]
+        path = LS.write(str(tmp_path / ("k%d" % k) / "linear.svg"), done[k], a, title="key %d" % k)
+        root = ET.parse(path).getroot()
+        ns = "{http://www.w3.org/2000/svg}"
+        rects = root.findall(ns + "rect")
+        rec = {id(r[f]): i for i, r in enumerate(done[k]) for f in ("invoke", "completion")
+               if r.get(f) is not None}
+        want = {rec[id(x)] for x in [a["previous-ok"], a["op"]] + a["configs"][0]["pending"]
+                + [s["op"] for p in a["final-paths"] for s in p] if x is not None}
+        assert len(rects) == len(want)
+        assert [r.get("class") for r in rects].count("fail") == 1
+        bad = [t.text for t in root.findall(ns + "text") if t.get("class") == "badmodel"]
+        ends = [p[-1]["model"]["inconsistent"] for p in a["final-paths"]
+                if "inconsistent" in p[-1]["model"]]
+        assert sorted(bad) == sorted(ends) and ends
+        drawn += 1
+    assert drawn >= 3
