@@ -435,6 +435,9 @@ def test_register_checker_end_to_end(tmp_path):
         assert all("inconsistent" in p[-1]["model"] for p in lin["final-paths"])
         page = open(r["timeline"]["file"]).read()  # independent/<k>/timeline.html
         assert 'cex"' in page and os.path.dirname(r["timeline"]["file"]).endswith("/%d" % k)
+        svg = open(lin["linear-svg"]).read()  # independent/<k>/linear.svg
+        assert 'class="fail"' in svg and os.path.dirname(lin["linear-svg"]) == \
+            os.path.dirname(r["timeline"]["file"])
     assert res["results"][0]["timeline"]["valid?"] is True
     assert C.check_safe(chk, {}, [{"type": "invoke", "process": 0, "value": None}]) == \
         {"valid?": True, "results": {}, "failures": []}
