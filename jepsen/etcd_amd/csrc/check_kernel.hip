@@ -382,6 +382,10 @@ struct HbmStore {
 // A table entry is 4 bytes, (epoch << 16) | index into the role's set, so
 // the LDS holds kLim = 5/16 of the table size per set (load <= 31%): 640
 // configurations in 36 KB with 4-wave workgroups, four of them per CU.
+#ifndef LC_LEPOCH_MASK
+#define LC_LEPOCH_MASK 0xFFFFu  // tests build a variant with 0x3 to wrap every 3 returns
+#endif
+constexpr uint32_t kLepochMask = LC_LEPOCH_MASK;
 constexpr int kSpinMax = 1 << 22;       // queue waits (s_sleep 1 each) before giving up
 constexpr uint32_t kIdxBusy = 0xFFFFu;  // claimed, index not yet published
 constexpr uint32_t kIdxOvf = 0xFFFEu;   // claimed past kLim (the return is redone)
@@ -895,7 +899,7 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
     st.begin_return();  // a fresh epoch per attempt: the aborted one's entries are stale
     int lclear = 0;
     if (lds) {
-      st.lepoch = (st.lepoch + 1) & 0xFFFFu;
+      st.lepoch = (st.lepoch + 1) & kLepochMask;
       if (st.lepoch == 0) {
         st.lepoch = 1;
         lclear = 1;
