@@ -166,7 +166,7 @@ constexpr uint32_t kBusy = 0x80000000u;  // table tag: claimed, configuration be
 struct CoopShared {
   int cmd;
   int rF, rR, rW, nF;
-  uint64_t bs, muts, reads, crashed;
+  uint64_t bs, muts, reads, ordered;  // ordered: slots with class predecessors (pbit)
   uint32_t epoch, tmask;
   union {  // set sizes; a round's appends to both reserve with one atomic
     struct { int nR, nW; };
@@ -522,19 +522,20 @@ __device__ __forceinline__ void lds_claim_lane(CoopTab<LT> &T, int role, const C
 
 // Per-lane record of the window slot this lane holds (valid when the lane's
 // bit is set in `occ`).  Slot kinds are uniform 64-bit masks (occ, rdm =
-// reads, crashed, latest); the per-lane fields are the precondition, the
-// value a mutation writes, the class fields for crashed-op symmetry, the
-// return index and the op index.
-//   pbit  for a crashed write/CAS: one-hot slot of the previously called
-//         crashed op of the same class (f, value, expected, version), or 0.
-//         Such ops are interchangeable (the completion never came), so only
-//         the earliest-called unlinearized member of a class is a candidate:
-//         an exact symmetry reduction (oracle ORACLE_FLAG_CRASH_SYMMETRY,
-//         checked against the faithful search in tests/).
+// reads, crashed); the per-lane fields are the precondition, the value a
+// mutation writes, the class fields, the return index and the op index.
+//   pbit  for a write/CAS: the pending slots of its class (equal f, value,
+//         expected, version) with an earlier deadline (return index;
+//         crashed = never, ties by call order).  Equal ops have equal
+//         preconditions and effects, so linearizing the earliest-deadline
+//         one first dominates (an exchange argument: oracle.c,
+//         ORACLE_FLAG_DEADLINE_ORDER; crashed ops alone is the round-1
+//         CRASH_SYMMETRY): a slot is a candidate only when its pbit slots
+//         are linearized.  Checked against the faithful search in tests/.
 struct Slot {
   int nv, nvm, nl, nlm;   // precondition
   int val;                // value written (mutations)
-  int f, exp, ver;        // class fields (crashed ops)
+  int f, exp, ver;        // class fields
   int idx;                // op index within the key
   uint32_t ret;           // kNever: free or crashed (never returns)
   uint64_t pbit;
@@ -544,7 +545,6 @@ struct Masks {
   uint64_t occ;      // occupied slots
   uint64_t rdm;      // slots holding reads
   uint64_t crashed;  // slots holding crashed writes/CAS
-  uint64_t latest;   // crashed slots that are the latest of their class
 };
 
 __device__ __forceinline__ uint64_t legal_ballot(const Slot &sl, int ver, int val) {
@@ -556,7 +556,7 @@ __device__ __forceinline__ uint64_t legal_ballot(const Slot &sl, int ver, int va
 __device__ __forceinline__ uint64_t mutation_candidates(const Slot &sl, const Masks &mk,
                                                         uint64_t cm, int ver, int val) {
   uint64_t cand = legal_ballot(sl, ver, val) & mk.occ & ~mk.rdm & ~cm;
-  if (cand & mk.crashed) cand &= __ballot((sl.pbit & ~cm) == 0);
+  cand &= __ballot((sl.pbit & ~cm) == 0);  // deadline order within a class
   return cand;
 }
 // Eager read closure at a successor state: pending reads legal there.
@@ -573,7 +573,6 @@ __device__ __forceinline__ void retire(Slot &sl, Masks &mk, uint64_t rb, int lan
   mk.occ &= ~rb;
   mk.rdm &= ~rb;
   mk.crashed &= ~rb;
-  mk.latest &= ~rb;
   if ((rb >> lane) & 1) sl.ret = kNever;
   sl.pbit &= ~rb;
 }
@@ -672,7 +671,7 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
     for (int i = wave * kWave + lane; i < CoopTab<LT>::kLim; i += nw * kWave) T.wrdy[i] = 0;
     lds_barrier();
   }
-  const uint64_t bs = C.bs, crashed = C.crashed;
+  const uint64_t bs = C.bs, ordered = C.ordered;
   const uint64_t muts = rfl64(C.muts), reads = rfl64(C.reads);  // scalar loops below
   const int rF = C.rF, rR = C.rR, rW = C.rW, nF = C.nF;
   const SlotLds &L = C.slots;
@@ -815,8 +814,8 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
       }
       const int cver = sv_ver(c.sv), cval = sv_val(c.sv);
       uint64_t cand = legal_by_state(spre, cver, cval, act) & muts & ~c.mask;
-      // a crashed op only if it is the earliest unlinearized of its class
-      for (uint64_t m = muts & crashed; m; m &= m - 1) {
+      // an op only if its class predecessors (deadline order) are linearized
+      for (uint64_t m = muts & ordered; m; m &= m - 1) {
         const int t = __builtin_ctzll(m);
         if (rl64(spbit, t) & ~c.mask) cand &= ~(1ull << t);
       }
@@ -887,6 +886,7 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
   C.slots.pre[lane] = make_int4(sl.nv, sl.nvm, sl.nl, sl.nlm);
   C.slots.val[lane] = sl.val;
   C.slots.pbit[lane] = sl.pbit;
+  const uint64_t ordered = __ballot(sl.pbit != 0);  // (a ballot: outside the lane-0 block)
   // LDS tables first when this frontier and the previous return's sets fit
   constexpr int kLim = CoopTab<LT>::kLim;
   bool lds = nF <= kLim && st.last <= kLim;
@@ -914,7 +914,7 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
       C.bs = 1ull << s;
       C.muts = mk.occ & ~mk.rdm;
       C.reads = mk.occ & mk.rdm;
-      C.crashed = mk.crashed;
+      C.ordered = ordered;
       C.epoch = st.epoch;
       C.tmask = st.tmask;
       C.lds = lds;
@@ -1007,6 +1007,7 @@ __device__ __forceinline__ int general_return_par_try(HbmStore &st, const Slot &
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const uint64_t muts = mk.occ & ~mk.rdm, reads = mk.occ & mk.rdm;
   const int4 spre = make_int4(sl.nv, sl.nvm, sl.nl, sl.nlm);  // lane t: slot t
+  const uint64_t ordered = __ballot(sl.pbit != 0);
   for (int head = 0; head < nW;) {
     const int j = head + lane;
     const bool act = j < nW;  // this batch: W[head, min(head + 64, nW)) as of now
@@ -1016,7 +1017,7 @@ __device__ __forceinline__ int general_return_par_try(HbmStore &st, const Slot &
     // candidates: legal pending mutations; a crashed one only if it is the
     // earliest unlinearized member of its class
     uint64_t cand = legal_by_state(spre, cver, cval, act) & muts & ~c.mask;
-    for (uint64_t m = muts & mk.crashed; m; m &= m - 1) {
+    for (uint64_t m = muts & ordered; m; m &= m - 1) {
       const int t = __builtin_ctzll(m);
       if (rl64(sl.pbit, t) & ~c.mask) cand &= ~(1ull << t);
     }
@@ -1098,7 +1099,7 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
   int rF = 0, rR = 1, rW = 2, nF = 1;
 
   Slot sl{0, 0, 0, 0, -1, 0, -1, -1, -1, kNever, 0ull};
-  Masks mk{0, 0, 0, 0};
+  Masks mk{0, 0, 0};
 
   const int64_t base_idx = kops[0].call;  // scalar load (key is wave-uniform)
   const uint64_t t0 = p.time_ticks ? wall_clock64() : 0;
@@ -1143,11 +1144,16 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
         const int nl = rl32(cur.nl, li), nlm = rl32(cur.nlm, li);
         const uint32_t ret = (uint32_t)rl32((int)cur.ret, li);
         uint64_t pbit = 0;
-        if (ret == kNever) {  // crashed write/CAS (crashed reads were skipped)
-          pbit = __ballot(sl.f == f && sl.val == val && sl.exp == ex && sl.ver == ver) &
-                 mk.crashed & mk.latest;
-          mk.latest = (mk.latest & ~pbit) | bs;
-          mk.crashed |= bs;
+        if (f != LC_F_READ) {
+          // Deadline order (oracle ORACLE_FLAG_DEADLINE_ORDER): within a
+          // class of equal writes/CAS (f, value, expected, version), an op
+          // may be linearized only after the pending members with earlier
+          // deadlines (return index; crashed = never, ties by call order).
+          const uint64_t cls = __ballot(sl.f == f && sl.val == val && sl.exp == ex && sl.ver == ver) &
+                               mk.occ & ~mk.rdm;
+          pbit = cls & __ballot(sl.ret <= ret);  // before s (equal: both crashed, called first)
+          if (((cls & ~pbit) >> lane) & 1) sl.pbit |= bs;  // the later ones wait for s
+          if (ret == kNever) mk.crashed |= bs;
         }
         if (lane == s) {
           sl.nv = nv;

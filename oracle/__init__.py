@@ -19,7 +19,9 @@ JIT, WGL = 0, 1
 READ_CLOSURE = 0x100
 CRASH_SYMMETRY = 0x200
 RETIRE = 0x400
-JITC = JIT | READ_CLOSURE | CRASH_SYMMETRY | RETIRE
+DEADLINE_ORDER = 0x800
+# the reductions the GPU's search tiers apply (DEADLINE_ORDER since round 2)
+JITC = JIT | READ_CLOSURE | CRASH_SYMMETRY | RETIRE | DEADLINE_ORDER
 
 RESULT_DTYPE = np.dtype([
     ("verdict", "<i4"), ("reason", "<i4"), ("fail_op", "<i8"),

@@ -239,6 +239,20 @@ static event *build_events(const lc_op *o, int64_t n, int64_t *ne) {
  *                 interchangeable once called (their version is always nil:
  *                 the completion never arrived), so only the earliest-called
  *                 unlinearized member of such a class may be linearized next.
+ *  DEADLINE_ORDER writes/CAS with equal (f, value, expected, version) have the
+ *                 same precondition and effect, so among the pending members
+ *                 of such a class only the one with the earliest deadline
+ *                 (return index; crashed = never, ties by call) may be
+ *                 linearized next.  Exchange argument: if a and b are both
+ *                 pending, ret(a) <= ret(b), and a linearization puts b at p
+ *                 and a later at q <= ret(a), swapping them keeps every op
+ *                 within its interval (p >= now >= call(a), q <= ret(a) <=
+ *                 ret(b)) and every state unchanged; a crashed b may also
+ *                 stay unlinearized.  So the configuration that took a
+ *                 dominates the one that took b.  This generalises
+ *                 CRASH_SYMMETRY (crashed ops: equal deadlines) to :ok ops,
+ *                 which matters for version-less models, where equal writes
+ *                 are common (round 2).
  *  RETIRE         an op linearized in every configuration is done for good:
  *                 a crashed op has no return, and an :ok op's return would
  *                 keep every configuration unchanged (JIT keeps the configs
@@ -282,6 +296,7 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
   const int closure = (reduce & ORACLE_FLAG_READ_CLOSURE) != 0;
   const int symmetry = (reduce & ORACLE_FLAG_CRASH_SYMMETRY) != 0;
   const int retire = (reduce & ORACLE_FLAG_RETIRE) != 0;
+  const int deadline = (reduce & ORACLE_FLAG_DEADLINE_ORDER) != 0;
   result_init(res);
   if (n == 0) return;
   int64_t ne = 0;
@@ -310,8 +325,10 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
   uint64_t *crashed = (uint64_t *)calloc((size_t)bw, sizeof(uint64_t));
   uint64_t *all = (uint64_t *)calloc((size_t)bw, sizeof(uint64_t));
   uint64_t *tmp = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)nw);
+  /* DEADLINE_ORDER: per slot, the same-class slots to linearize before it */
+  uint64_t *before = (uint64_t *)calloc((size_t)(bw * 64) * (size_t)bw, sizeof(uint64_t));
   cset F, R, V;
-  int ok = slot_of && slot_op && pred && latest && occ && crashed && all && tmp;
+  int ok = slot_of && slot_op && pred && latest && occ && crashed && all && tmp && before;
   ok = ok && cset_init(&F, nw) == 0 && cset_init(&R, nw) == 0 &&
        cset_init(&V, nw) == 0;
   if (!ok) {
@@ -340,6 +357,19 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
       slot_op[s] = x;
       pred[s] = -1;
       latest[s] = 0;
+      if (deadline && o[x].f != LC_F_READ) {
+        uint64_t *bs_row = before + (size_t)s * (size_t)bw;
+        memset(bs_row, 0, sizeof(uint64_t) * (size_t)bw);
+        for (int u = 0; u < bw * 64; u++) {
+          if (u == s || !BIT(occ, u)) continue;
+          const lc_op *ou = &o[slot_op[u]];
+          if (ou->f == LC_F_READ || !same_class(ou, &o[x])) continue;
+          if (ou->ret <= o[x].ret) /* earlier deadline (equal: both crashed, u called first) */
+            bs_row[u >> 6] |= 1ULL << (u & 63);
+          else
+            before[(size_t)u * (size_t)bw + (size_t)(s >> 6)] |= 1ULL << (s & 63);
+        }
+      }
       if (is_crashed_mutation(&o[x])) {
         crashed[s >> 6] |= 1ULL << (s & 63);
         if (symmetry) {
@@ -393,6 +423,12 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
           const int t = w * 64 + b;
           c = cset_get(&V, h);
           if (symmetry && pred[t] >= 0 && !BIT(c, pred[t])) continue;
+          if (deadline) {
+            const uint64_t *row = before + (size_t)t * (size_t)bw;
+            int blocked = 0;
+            for (int w2 = 0; w2 < bw; w2++) blocked |= (row[w2] & ~c[w2]) != 0;
+            if (blocked) continue;
+          }
           int64_t nv, nval;
           const int st = oracle_step((int64_t)c[bw], (int64_t)c[bw + 1],
                                      &o[slot_op[t]], &nv, &nval);
@@ -430,6 +466,8 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
     F = R;
     R = t;
     occ[wx] &= ~bx;
+    if (deadline) /* x is linearized in every configuration from here on */
+      for (int u = 0; u < bw * 64; u++) before[(size_t)u * (size_t)bw + (size_t)wx] &= ~bx;
     if ((int64_t)F.n > res->max_frontier) res->max_frontier = (int64_t)F.n;
     if (F.n == 0) {
       res->verdict = LC_INVALID;
@@ -466,6 +504,9 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
           occ[w] &= ~all[w];
           crashed[w] &= ~all[w];
         }
+        if (deadline)
+          for (int u = 0; u < bw * 64; u++)
+            for (int w = 0; w < bw; w++) before[(size_t)u * (size_t)bw + (size_t)w] &= ~all[w];
       }
     }
   }
@@ -482,6 +523,7 @@ done:
   free(crashed);
   free(all);
   free(tmp);
+  free(before);
   free(ev);
 }
 

@@ -30,6 +30,7 @@ extern "C" {
 #define ORACLE_FLAG_READ_CLOSURE   0x100
 #define ORACLE_FLAG_CRASH_SYMMETRY 0x200
 #define ORACLE_FLAG_RETIRE         0x400
+#define ORACLE_FLAG_DEADLINE_ORDER 0x800
 
 /* Check every key with the chosen algorithm on n_threads host threads.
  * Same record format, options and result struct as lc_check().

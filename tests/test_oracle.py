@@ -79,7 +79,7 @@ def test_golden_fixtures(name):
             assert (r["fail_op"] == z["fail_op"]).all()
 
 
-@pytest.mark.parametrize("mode", ["READ_CLOSURE", "CRASH_SYMMETRY", "RETIRE", "ALL"])
+@pytest.mark.parametrize("mode", ["READ_CLOSURE", "CRASH_SYMMETRY", "RETIRE", "DEADLINE_ORDER", "ALL"])
 @pytest.mark.parametrize("p_info,seed", [(0.05, 99), (0.15, 7)])
 def test_reductions_are_exact_on_synthetic(mode, p_info, seed):
     """Each exact reduction (oracle.c) agrees with the faithful knossos.linear
@@ -153,3 +153,24 @@ def test_version_order_decision_matches_search():
     for k in KATS:
         d = fastpath_ref.decide([tuple(r) for r in k["ops"]])
         assert d is None or d == (1 if k["valid"] else 0), k["name"]
+
+
+@pytest.mark.parametrize("conc,seed", [(6, 3), (10, 5), (14, 8)])
+def test_deadline_order_exact_version_less(conc, seed):
+    """DEADLINE_ORDER matters where equal writes/CAS are common: version-less
+    keys (the cas-register model).  Verdict and canonical fail op equal the
+    faithful search on every key both decide, with fewer configurations."""
+    ops, off, _, _ = abi.synth(80, 120, concurrency=conc, p_info=0.03, p_anomaly=0.0, seed=seed)
+    ops = ops.copy()
+    ops[:, 3] = -1
+    rng = np.random.default_rng(seed)  # a few reads of a value nothing wrote
+    reads = np.nonzero((ops[:, 0] == 0) & (ops[:, 5] != INF))[0]
+    ops[rng.choice(reads, 12, replace=False), 1] = 999
+    _, j = oracle.check(ops, off, algo=oracle.JIT, n_threads=4, max_configs=400000)
+    _, d = oracle.check(ops, off, algo=oracle.JIT | oracle.DEADLINE_ORDER, n_threads=4,
+                        max_configs=400000)
+    known = (j["verdict"] != -1) & (d["verdict"] != -1)
+    assert known.mean() > 0.8 and (j["verdict"][known] == 0).any()
+    assert (j["verdict"][known] == d["verdict"][known]).all()
+    assert (j["fail_op"][known] == d["fail_op"][known]).all()
+    assert d["configs_explored"][known].sum() < j["configs_explored"][known].sum()
