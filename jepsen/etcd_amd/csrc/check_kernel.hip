@@ -1981,7 +1981,7 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
     const int32_t *__restrict__ keys, const int32_t n_list,
     const KParams p, lc_key_result *__restrict__ out, char *__restrict__ ws,
     const int64_t cap, int32_t *__restrict__ ovf_out, int32_t *__restrict__ n_ovf_out,
-    const int last_tier) {
+    int32_t *__restrict__ n_malformed, const int last_tier) {
   const int lane = threadIdx.x;
   char *w = ws + (size_t)blockIdx.x * hbm_wave_bytes(cap);
   HbmStore st;
@@ -2006,7 +2006,10 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
         ovf_out[atomicAdd(n_ovf_out, 1)] = (int32_t)key;  // next, larger tier
       }
     }
-    if (lane == 0) write_result(&out[key], o);
+    if (lane == 0) {
+      if (o.reason == LC_REASON_MALFORMED) atomicAdd(n_malformed, 1);
+      write_result(&out[key], o);
+    }
   }
 }
 
@@ -2085,7 +2088,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
     const int32_t *__restrict__ keys, const int32_t n_list,
     const KParams p, lc_key_result *__restrict__ out, char *__restrict__ ws,
     const int64_t cap, int32_t *__restrict__ ovf_out, int32_t *__restrict__ n_ovf_out,
-    const int last_tier) {
+    int32_t *__restrict__ n_malformed, const int last_tier) {
   __shared__ CoopShared C;
   constexpr int LT = NW >= 16 ? 4096 : 2048;  // LDS table entries per role
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
@@ -2120,7 +2123,10 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         else if (lane == 0)
           ovf_out[atomicAdd(n_ovf_out, 1)] = (int32_t)key;
       }
-      if (lane == 0) write_result(&out[key], o);
+      if (lane == 0) {
+        if (o.reason == LC_REASON_MALFORMED) atomicAdd(n_malformed, 1);
+        write_result(&out[key], o);
+      }
     }
     if (lane == 0) C.cmd = kCoopExit;
 #ifdef HBM_PROFILE
@@ -2225,16 +2231,17 @@ size_t hbm_tier_ws_bytes(int n_waves, int64_t cap) {
 hipError_t launch_hbm_coop(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
                            int32_t n_list, const KParams &p, lc_key_result *d_out, void *d_ws,
                            int n_wg, int64_t cap, int32_t *d_ovf_out, int32_t *d_n_ovf_out,
-                           int last_tier, int waves_per_key, hipStream_t stream) {
+                           int32_t *d_malformed, int last_tier, int waves_per_key,
+                           hipStream_t stream) {
   if (n_list <= 0) return hipSuccess;
   if (waves_per_key >= 16)
     hipLaunchKernelGGL(hbm_coop_kernel<16>, dim3((unsigned)n_wg), dim3(16 * kWave), 0, stream,
                        d_ops, d_key_off, d_keys, n_list, p, d_out, static_cast<char *>(d_ws), cap,
-                       d_ovf_out, d_n_ovf_out, last_tier);
+                       d_ovf_out, d_n_ovf_out, d_malformed, last_tier);
   else
     hipLaunchKernelGGL(hbm_coop_kernel<4>, dim3((unsigned)n_wg), dim3(4 * kWave), 0, stream,
                        d_ops, d_key_off, d_keys, n_list, p, d_out, static_cast<char *>(d_ws), cap,
-                       d_ovf_out, d_n_ovf_out, last_tier);
+                       d_ovf_out, d_n_ovf_out, d_malformed, last_tier);
   return hipGetLastError();
 }
 
@@ -2242,12 +2249,12 @@ hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
                            const int32_t *d_keys,
                            int32_t n_list, const KParams &p, lc_key_result *d_out,
                            void *d_ws, int n_waves, int64_t cap,
-                           int32_t *d_ovf_out, int32_t *d_n_ovf_out, int last_tier,
-                           hipStream_t stream) {
+                           int32_t *d_ovf_out, int32_t *d_n_ovf_out, int32_t *d_malformed,
+                           int last_tier, hipStream_t stream) {
   if (n_list <= 0) return hipSuccess;
   hipLaunchKernelGGL(hbm_tier_kernel, dim3((unsigned)n_waves), dim3(kWave), 0,
                      stream, d_ops, d_key_off, d_keys, n_list, p,
-                     d_out, static_cast<char *>(d_ws), cap, d_ovf_out, d_n_ovf_out,
+                     d_out, static_cast<char *>(d_ws), cap, d_ovf_out, d_n_ovf_out, d_malformed,
                      last_tier);
   return hipGetLastError();
 }

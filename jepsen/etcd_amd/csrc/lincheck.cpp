@@ -60,6 +60,7 @@ constexpr int kHbmWaves[kHbmTiers] = {2048, 128, 16};
 // 1 on 10,000 (331 vs 355 ms with 4).
 constexpr int kHbmCoop16MaxKeys = 512;
 constexpr int kHbmCoop4MaxKeys = 4096;
+constexpr int kJitDirectMaxKeys = 1024;  // 4 cooperative workgroups per CU x 256 CUs
 // Gap tier: at most this many workgroups, and this much workspace (each
 // workgroup needs 92 B per record of the longest key handed over).  Dynamic
 // LDS for the matching arrays: up to kGapLdsFull per workgroup for whole-key
@@ -410,7 +411,25 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     before_jit = d.eg;
   }
   d.n_jit = n_jit;
-  if (n_jit == 0) {
+  // Few keys for the frontier search (at most kJitDirectMaxKeys: one 4-wave
+  // workgroup per key, all resident at once) go straight to the cooperative
+  // tier, whose LDS tables serve small frontiers and whose hash tables keep
+  // large ones; the LDS tier's one-wave-per-key pass would be redone for
+  // every key that outgrows it.  Measured (tools/jit_direct_ab.py, version-
+  // less batches): 1,000 x 1,000 at concurrency 20 19.4 -> 15.0 ms,
+  // 1,000 x 200 2.4 -> 1.8 ms, 64 x 1,000 10.1 -> 6.5 ms; but 4,000 x 100
+  // 1.0 -> 3.0 ms, where the LDS tier's four keys per workgroup win.
+  // LC_JIT_DIRECT=0 (A/B) keeps the LDS tier first.
+  const char *direct_env = getenv("LC_JIT_DIRECT");
+  // (not with LC_FLAG_NO_FAST_PATH, whose JIT list is implicit: every key)
+  const bool direct = !(direct_env && direct_env[0] == '0') && n_jit > 0 && jit_list &&
+                      n_jit <= kJitDirectMaxKeys && !(flags & LC_FLAG_NO_HBM_RETRY);
+  if (direct) {
+    HIP_TRY(c, hipMemcpyAsync(d.d_ovf, jit_list, sizeof(int32_t) * (size_t)n_jit,
+                              hipMemcpyDeviceToDevice, st));
+    HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, before_jit));
+    d.kernel_ms = ms;
+  } else if (n_jit == 0) {
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, before_jit));
     d.kernel_ms = ms;
   } else {
@@ -427,7 +446,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     d.kernel_ms = ms;
   }
   d.malformed = d.h_status->malformed;
-  const int32_t n_ovf = d.h_status->n_overflow;
+  const int32_t n_ovf = direct ? (int32_t)n_jit : d.h_status->n_overflow;
   d.n_hbm = n_ovf;
   if (n_ovf > 0 && !(flags & LC_FLAG_NO_HBM_RETRY)) {
     int32_t n_list = n_ovf;
@@ -454,11 +473,13 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       const int last = tier == kHbmTiers - 1;
       if (coop)
         HIP_TRY(c, lcdev::launch_hbm_coop(d_ops, d_off, list, n_list, p, d_out, d.d_ws, waves,
-                                          kHbmCap[tier], next, &d.d_status->n_overflow2, last, wpk, st));
+                                          kHbmCap[tier], next, &d.d_status->n_overflow2,
+                                          &d.d_status->malformed, last, wpk, st));
       else
         HIP_TRY(c, lcdev::launch_hbm_tier(d_ops, d_off, list, n_list, p,
                                           d_out, d.d_ws, waves, kHbmCap[tier], next,
-                                          &d.d_status->n_overflow2, last, st));
+                                          &d.d_status->n_overflow2, &d.d_status->malformed,
+                                          last, st));
       HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                                 hipMemcpyDeviceToHost, st));
       HIP_TRY(c, hipStreamSynchronize(st));
@@ -469,6 +490,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     HIP_TRY(c, hipStreamSynchronize(st));
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e1, d.e2));
     d.hbm_ms = ms;
+    d.malformed = d.h_status->malformed;  // (keys sent straight here report it)
   }
   HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
   HIP_TRY(c, hipStreamSynchronize(st));

@@ -126,17 +126,26 @@ def test_long_key(ctx):
     assert (g["verdict"] == 1).all()
 
 
-def test_hbm_tier_resolves_lds_overflow(ctx):
+def test_hbm_tier_resolves_lds_overflow(ctx, monkeypatch):
+    """LDS tier first (LC_JIT_DIRECT=0): exactly the keys that outgrow it go
+    on to the HBM tier; and by default (at most 1,024 frontier-search keys go
+    straight to the cooperative tier) the same verdicts and fail ops."""
     z = np.load(os.path.join(GOLDEN, "info.npz"))
     nogap = abi.LC_FLAG_NO_GAP_TIER  # crash-heavy keys reach the JIT search
     o = abi.default_opts(flags=abi.LC_FLAG_NO_HBM_RETRY | nogap)
     _, lds_only = ctx.check(z["ops"], z["key_off"], o)
     spilled = lds_only["reason"] == 6
     assert spilled.any()
+    monkeypatch.setenv("LC_JIT_DIRECT", "0")
     _, full = ctx.check(z["ops"], z["key_off"], abi.default_opts(flags=nogap))
     assert ctx.stats()["n_hbm_keys"] == spilled.sum()
     assert (full["verdict"] == z["verdict"]).all()
     assert (full["fail_op"] == z["fail_op"]).all()
+    monkeypatch.delenv("LC_JIT_DIRECT")
+    _, direct = ctx.check(z["ops"], z["key_off"], abi.default_opts(flags=nogap))
+    assert ctx.stats()["n_hbm_keys"] == ctx.stats()["n_jit_keys"] > spilled.sum()
+    for f in ("verdict", "fail_op", "fail_prefix_end", "max_frontier", "configs_explored"):
+        assert (direct[f] == full[f]).all(), f
 
 
 @pytest.mark.parametrize("mode", ["0", "4", "16"])
