@@ -96,7 +96,8 @@ hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
 
 // HBM tier: re-runs the listed keys with configuration sets in global memory
 // (open-addressed hash tables, 128-byte buckets).  ws is a workspace of
-// hbm_tier_ws_bytes(n_waves, cap) bytes (zeroed by the caller); cap =
+// hbm_tier_ws_bytes(n_waves, cap) bytes (no initial contents: each
+// workgroup zeroes its tag arrays at launch); cap =
 // configurations per set.  Keys that overflow again are appended to
 // d_ovf_out (count *d_n_ovf_out) unless last_tier, where they become
 // LC_REASON_CONFIG_BUDGET (:unknown).

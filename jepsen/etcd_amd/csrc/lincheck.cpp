@@ -58,7 +58,7 @@ constexpr int kHbmWaves[kHbmTiers] = {2048, 128, 16};
 // DESIGN.md §4): 16 wins on 512 crash-heavy keys (4.9 s vs 13.1 s with 4,
 // 40 s with 1), 4 on 1000-2000 version-less keys (71 vs 113 vs 119 ms),
 // 1 on 10,000 (331 vs 355 ms with 4).
-constexpr int kHbmCoop16MaxKeys = 512;
+constexpr int kHbmCoop16MaxKeys = 256;  // one 16-wave workgroup per CU (tools/coop_width_ab.py)
 constexpr int kHbmCoop4MaxKeys = 4096;
 constexpr int kJitDirectMaxKeys = 1024;  // 4 cooperative workgroups per CU x 256 CUs
 // Gap tier: at most this many workgroups, and this much workspace (each
@@ -468,7 +468,6 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       const size_t ws = lcdev::hbm_tier_ws_bytes(waves, kHbmCap[tier]);
       rc = ensure(c, reinterpret_cast<char **>(&d.d_ws), &d.ws_cap, ws);
       if (rc) return rc;
-      HIP_TRY(c, hipMemsetAsync(d.d_ws, 0, ws, st));
       HIP_TRY(c, hipMemsetAsync(&d.d_status->n_overflow2, 0, sizeof(int32_t), st));
       const int last = tier == kHbmTiers - 1;
       if (coop)
