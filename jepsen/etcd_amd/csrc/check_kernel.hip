@@ -1586,7 +1586,10 @@ __device__ __forceinline__ int fg_prefix_wave(int v, FastLds &s) {
 // before) rather than kept in registers across the branch: the version
 // order's pass 2 holds 4 x 48 B per thread, and keeping them live on this
 // path too would cost the kernel its 7-waves-per-SIMD occupancy.
-__device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops,
+#ifndef LC_FG_REGS
+#define LC_FG_REGS 1  // decode the records from pass 1's registers (0: re-read them)
+#endif
+__device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, const FastRecs &b,
                          const KParams &p, FastLds &s, lc_key_result *__restrict__ out,
                          int32_t *__restrict__ wit, int32_t *__restrict__ kind) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
@@ -1610,12 +1613,20 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops,
       inv |= (old != kAny) & (old != v);
     }
   };
-#pragma unroll 1  // one record in flight: this path must not raise the kernel's VGPR count
+#if LC_FG_REGS
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
   for (int u = 0; u < kPer; u++) {
     const int r = tid + u * kFastThreads;
     bool opt = false;
     if (r < n) {
+#if LC_FG_REGS
+      const Rec d = decode(b.w[u], base_idx);
+#else
       const Rec d = decode(load_raw(kops, r, n), base_idx);
+#endif
       if (d.f == LC_F_READ) {
         if (d.ret != kNever && d.ver != -1) {  // (pass 1 handed [nil x] reads over)
           const int k = d.ver - V0;
@@ -1707,7 +1718,11 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops,
     }
   }
   int obase = 0;
+#if LC_FG_REGS
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
   for (int u = 0; u < kPer; u++) {
     int my = obase;  // slots before this wave's ops of chunk u
 #pragma unroll
@@ -1718,7 +1733,11 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops,
     }
     if ((optm[u] >> lane) & 1) {
       const int o = my + lanes_below(optm[u]);
+#if LC_FG_REGS
+      const Rec d = decode(b.w[u], base_idx);
+#else
       const Rec d = decode(load_raw(kops, tid + u * kFastThreads, n), base_idx);
+#endif
       c.ops()[o] = make_int4((int)d.call, d.val, d.f == LC_F_CAS ? d.exp : kAny, -1);
       c.at(aMO, o) = -1;
       c.at(aVis, o) = 0;
@@ -1876,7 +1895,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
   if (wor >> 16) {  // ineligible or a version out of range: hand over
     // crash-light pass: crashed writes/CAS are the only obstacle
     if constexpr (LIGHT)
-      if ((wor >> 16) == 1 && fast_gap(key, n, kops, p, s, out, wit, o.kind)) return;
+      if ((wor >> 16) == 1 && fast_gap(key, n, kops, b, p, s, out, wit, o.kind)) return;
     if (tid == 0) fast_pass_on<LIGHT>(key, o, (wor >> 18) & 1);
     return;
   }
