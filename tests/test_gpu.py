@@ -334,6 +334,33 @@ def test_gap_tier_hbm_fallback_agrees(ctx, seed, anom, monkeypatch):
             assert (a[f] == b[f]).all(), f
 
 
+def test_handoff_is_never_missed(ctx):
+    """The version-order tier's handoff flag (host-coherent memory, read after
+    an event sync recorded without a system fence; the kernel fences after its
+    store) must be seen on every call: alternate a clean batch with a
+    same-shaped crash-heavy one holding invalid keys, device-resident with one
+    output buffer, so a missed handoff would leave the clean batch's verdicts
+    in place for the crashed keys."""
+    import torch
+    dev = torch.device("cuda:0")
+    clean = abi.synth(2000, 200, concurrency=10, seed=41)[:2]
+    crash = abi.synth(2000, 200, concurrency=10, p_info=0.1, p_anomaly=0.3, seed=42)[:2]
+    want = [ctx.check(o, f)[1] for o, f in (clean, crash)]
+    assert (want[1]["verdict"] == 0).any() and (want[0]["verdict"] == 1).all()
+    bufs = [(torch.from_numpy(o).to(dev), torch.from_numpy(f).to(dev)) for o, f in (clean, crash)]
+    out = torch.zeros(2000 * abi.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    for i in range(40):
+        k = i % 2
+        d_ops, d_off = bufs[k]
+        ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), 2000, out.data_ptr(),
+                         stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        got = np.frombuffer(out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
+        for f in ("verdict", "fail_op"):
+            assert (got[f] == want[k][f]).all(), (i, f)
+
+
 def test_gap_tier_repeatable(ctx):
     """Same batch, same answers, call after call: the gap tier's decisions
     within one workgroup follow each other without extra barriers, so a
