@@ -49,6 +49,8 @@ namespace {
 // return, by log2 of its larger set: returns, device ticks (100 MHz), LDS-
 // mode returns, configurations explored; printed by the last workgroup.
 __device__ unsigned long long g_hhist[20][4];
+// per workgroup: ticks in LDS-mode returns, in HBM-mode returns (incl. failed LDS attempts), whole keys
+__device__ unsigned long long g_hwg[4096][3];
 __device__ unsigned int g_hdone;
 #endif
 
@@ -946,6 +948,9 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
     atomicAdd(&g_hhist[bkt][2], (unsigned long long)lds);
     atomicAdd(&g_hhist[bkt][3], (unsigned long long)(C.explored - (unsigned long long)o.explored));
   }
+  if (lane == 0 && blockIdx.x < 4096) {
+    g_hwg[blockIdx.x][lds ? 0 : 1] += wall_clock64() - tr0;
+  }
 #endif
   if (C.status < 0) return C.status;
   o.explored = (int64_t)C.explored;
@@ -1750,6 +1755,10 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, con
     if (tb.x | tb.y | tb.z | tb.w) return false;
   }
   if (G > n_opt) return false;  // invalid: the gap tier names the fail op
+#ifdef LC_FG_NOMATCH  // dev timing only: everything but the matching
+  if (tid == 0) out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, G};
+  return true;
+#endif
   int res = GD_VALID;
   int64_t nodes = 0;
   if (G > 0 && w == 0) {
@@ -2146,7 +2155,13 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
       KeyOut o;
       st.hint = 0;  // table-size hints: per key
       st.last = 0;
+#ifdef HBM_PROFILE
+      const uint64_t tk0 = wall_clock64();
+#endif
       check_key(ops + (beg - key_base), (int)(end - beg), p, st, o, lane);
+#ifdef HBM_PROFILE
+      if (lane == 0 && blockIdx.x < 4096) g_hwg[blockIdx.x][2] += wall_clock64() - tk0;
+#endif
       if (o.reason == LC_REASON_FRONTIER_LDS) {
         if (last_tier)
           o.reason = LC_REASON_CONFIG_BUDGET;
@@ -2166,6 +2181,19 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         if (g_hhist[b][0])
           printf("set<2^%d: returns %llu ticks %llu lds %llu configs %llu\n", b, g_hhist[b][0],
                  g_hhist[b][1], g_hhist[b][2], g_hhist[b][3]);
+    if (lane == 0 && g_hdone == gridDim.x) {
+      unsigned long long sum = 0;
+      for (unsigned i = 0; i < gridDim.x && i < 4096; i++) sum += g_hwg[i][2];
+      printf("workgroups %u mean key ticks %llu\n", gridDim.x, sum / gridDim.x);
+      for (int t = 0; t < 6; t++) {
+        unsigned best = 0;
+        for (unsigned i = 0; i < gridDim.x && i < 4096; i++)
+          if (g_hwg[i][2] > g_hwg[best][2]) best = i;
+        printf("  slow wg %u: key %llu lds-returns %llu hbm-returns %llu\n", best, g_hwg[best][2],
+               g_hwg[best][0], g_hwg[best][1]);
+        g_hwg[best][2] = 0;
+      }
+    }
 #endif
     coop_barrier();
   } else {
