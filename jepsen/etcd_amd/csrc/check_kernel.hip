@@ -2019,7 +2019,7 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
     const int32_t *__restrict__ keys, const int32_t n_list,
     const KParams p, lc_key_result *__restrict__ out, char *__restrict__ ws,
     const int64_t cap, int32_t *__restrict__ ovf_out, int32_t *__restrict__ n_ovf_out,
-    int32_t *__restrict__ n_malformed, const int last_tier) {
+    int32_t *__restrict__ n_malformed, int32_t *__restrict__ next, const int last_tier) {
   const int lane = threadIdx.x;
   char *w = ws + (size_t)blockIdx.x * hbm_wave_bytes(cap);
   HbmStore st;
@@ -2031,7 +2031,11 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
   hbm_zero_tags(st.tags, cap);
   st.epoch = 0;  // epochs start at 1
   const int64_t key_base = key_off[0];
-  for (int li = blockIdx.x; li < n_list; li += gridDim.x) {
+  for (;;) {  // list entries claimed one at a time (next: zero at launch)
+    int li = 0;
+    if (lane == 0) li = atomicAdd(next, 1);
+    li = uni(li);
+    if (li >= n_list) break;
     const int64_t key = keys[li];
     const int64_t beg = key_off[key], end = key_off[key + 1];
     KeyOut o;
@@ -2126,7 +2130,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
     const int32_t *__restrict__ keys, const int32_t n_list,
     const KParams p, lc_key_result *__restrict__ out, char *__restrict__ ws,
     const int64_t cap, int32_t *__restrict__ ovf_out, int32_t *__restrict__ n_ovf_out,
-    int32_t *__restrict__ n_malformed, const int last_tier) {
+    int32_t *__restrict__ n_malformed, int32_t *__restrict__ next, const int last_tier) {
   __shared__ CoopShared C;
   constexpr int LT = NW >= 16 ? 4096 : 2048;  // LDS table entries per role
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
@@ -2149,7 +2153,11 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
   st.epoch = 0;  // epochs start at 1
   if (wave == 0) {
     const int64_t key_base = key_off[0];
-    for (int li = blockIdx.x; li < n_list; li += gridDim.x) {
+    for (;;) {  // list entries claimed one at a time (next: zero at launch)
+      int li = 0;
+      if (lane == 0) li = atomicAdd(next, 1);
+      li = uni(li);
+      if (li >= n_list) break;
       const int64_t key = keys[li];
       const int64_t beg = key_off[key], end = key_off[key + 1];
       KeyOut o;
@@ -2290,17 +2298,17 @@ size_t hbm_tier_ws_bytes(int n_waves, int64_t cap) {
 hipError_t launch_hbm_coop(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
                            int32_t n_list, const KParams &p, lc_key_result *d_out, void *d_ws,
                            int n_wg, int64_t cap, int32_t *d_ovf_out, int32_t *d_n_ovf_out,
-                           int32_t *d_malformed, int last_tier, int waves_per_key,
-                           hipStream_t stream) {
+                           int32_t *d_malformed, int32_t *d_next, int last_tier,
+                           int waves_per_key, hipStream_t stream) {
   if (n_list <= 0) return hipSuccess;
   if (waves_per_key >= 16)
     hipLaunchKernelGGL(hbm_coop_kernel<16>, dim3((unsigned)n_wg), dim3(16 * kWave), 0, stream,
                        d_ops, d_key_off, d_keys, n_list, p, d_out, static_cast<char *>(d_ws), cap,
-                       d_ovf_out, d_n_ovf_out, d_malformed, last_tier);
+                       d_ovf_out, d_n_ovf_out, d_malformed, d_next, last_tier);
   else
     hipLaunchKernelGGL(hbm_coop_kernel<4>, dim3((unsigned)n_wg), dim3(4 * kWave), 0, stream,
                        d_ops, d_key_off, d_keys, n_list, p, d_out, static_cast<char *>(d_ws), cap,
-                       d_ovf_out, d_n_ovf_out, d_malformed, last_tier);
+                       d_ovf_out, d_n_ovf_out, d_malformed, d_next, last_tier);
   return hipGetLastError();
 }
 
@@ -2309,12 +2317,12 @@ hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
                            int32_t n_list, const KParams &p, lc_key_result *d_out,
                            void *d_ws, int n_waves, int64_t cap,
                            int32_t *d_ovf_out, int32_t *d_n_ovf_out, int32_t *d_malformed,
-                           int last_tier, hipStream_t stream) {
+                           int32_t *d_next, int last_tier, hipStream_t stream) {
   if (n_list <= 0) return hipSuccess;
   hipLaunchKernelGGL(hbm_tier_kernel, dim3((unsigned)n_waves), dim3(kWave), 0,
                      stream, d_ops, d_key_off, d_keys, n_list, p,
                      d_out, static_cast<char *>(d_ws), cap, d_ovf_out, d_n_ovf_out, d_malformed,
-                     last_tier);
+                     d_next, last_tier);
   return hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ struct KStatus {
   int32_t max_lds;      // gap tier: largest matching footprint (bytes) of a full decision
   int32_t any_handoff;  // fast tier: some key was handed over (read before the host store)
   int32_t n_gap2;       // crash-light pass: keys it passes on to the gap tier
+  int32_t hbm_next;     // HBM tiers: next list entry to claim (zeroed before each launch)
 };
 
 constexpr int kWave = 64;
@@ -108,18 +109,20 @@ size_t hbm_tier_ws_bytes(int n_waves, int64_t cap);
 // hbm_tier_ws_bytes(n_wg, cap).
 // Both HBM launches count the keys they find malformed in *d_malformed (the
 // first frontier-search tier a key reaches reports it: the LDS tier, or the
-// HBM tier when few keys skip the LDS tier).
+// HBM tier when few keys skip the LDS tier).  Workgroups claim list entries
+// from *d_next (zero at launch), so a workgroup that drew quick keys takes
+// more of them.
 hipError_t launch_hbm_coop(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
                            int32_t n_list, const KParams &p, lc_key_result *d_out, void *d_ws,
                            int n_wg, int64_t cap, int32_t *d_ovf_out, int32_t *d_n_ovf_out,
-                           int32_t *d_malformed, int last_tier, int waves_per_key,
-                           hipStream_t stream);
+                           int32_t *d_malformed, int32_t *d_next, int last_tier,
+                           int waves_per_key, hipStream_t stream);
 hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
                            const int32_t *d_keys,
                            int32_t n_list, const KParams &p, lc_key_result *d_out,
                            void *d_ws, int n_waves, int64_t cap,
                            int32_t *d_ovf_out, int32_t *d_n_ovf_out, int32_t *d_malformed,
-                           int last_tier, hipStream_t stream);
+                           int32_t *d_next, int last_tier, hipStream_t stream);
 
 // Gap tier (gap_tier.hip): version-pinned keys with crashed writes/CAS are
 // decided by matching gaps to optional ops; keys it cannot decide are

@@ -59,7 +59,8 @@ constexpr int kHbmWaves[kHbmTiers] = {2048, 128, 16};
 // 40 s with 1), 4 on 1000-2000 version-less keys (71 vs 113 vs 119 ms),
 // 1 on 10,000 (331 vs 355 ms with 4).
 constexpr int kHbmCoop16MaxKeys = 256;  // one 16-wave workgroup per CU (tools/coop_width_ab.py)
-constexpr int kHbmCoop4MaxKeys = 4096;
+constexpr int kHbmCoop16Resident = 256;   // 16-wave workgroups resident: one per CU
+constexpr int kHbmCoop4Resident = 1024;   // 4-wave workgroups: four per CU (LDS tables)
 constexpr int kJitDirectMaxKeys = 1024;  // 4 cooperative workgroups per CU x 256 CUs
 // Gap tier: at most this many workgroups, and this much workspace (each
 // workgroup needs 92 B per record of the longest key handed over).  Dynamic
@@ -454,31 +455,35 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     HIP_TRY(c, hipEventRecord(d.e1, st));
     // LC_HBM_COOP (test/A-B knob): 0 one wavefront per key throughout,
     // 4 / 16 a workgroup of that many wavefronts per key throughout; default:
-    // 16 for short lists, 4 for medium ones, 1 once a wavefront per key
-    // already fills the SIMDs.
+    // 16 for at most 256 keys (one workgroup per CU), else 4.  (Round 1 used
+    // one wavefront per key beyond 4,096 keys; with the LDS tables the
+    // 4-wave workgroups win there too: version-less 10,000 x 1,000 at
+    // concurrency 20, HBM tier 128 -> 98 ms, tools/hbm_width_large.py.)
     const char *coop_env = getenv("LC_HBM_COOP");
     const int coop_mode = coop_env ? atoi(coop_env) : 1;
     for (int tier = 0; tier < kHbmTiers && n_list > 0; tier++) {
-      int wpk = coop_mode == 1 ? (n_list <= kHbmCoop16MaxKeys  ? 16
-                                  : n_list <= kHbmCoop4MaxKeys ? 4
-                                                               : 0)
-                               : coop_mode;
+      int wpk = coop_mode == 1 ? (n_list <= kHbmCoop16MaxKeys ? 16 : 4) : coop_mode;
       const bool coop = wpk == 4 || wpk == 16;
-      const int waves = std::min<int>(kHbmWaves[tier], n_list);
+      // workgroups: at most the resident ones (keys are claimed dynamically)
+      const int resident = wpk == 16 ? kHbmCoop16Resident : wpk == 4 ? kHbmCoop4Resident
+                                                                       : kHbmWaves[tier];
+      const int waves = std::min<int>(std::min(kHbmWaves[tier], resident), n_list);
       const size_t ws = lcdev::hbm_tier_ws_bytes(waves, kHbmCap[tier]);
       rc = ensure(c, reinterpret_cast<char **>(&d.d_ws), &d.ws_cap, ws);
       if (rc) return rc;
       HIP_TRY(c, hipMemsetAsync(&d.d_status->n_overflow2, 0, sizeof(int32_t), st));
+      HIP_TRY(c, hipMemsetAsync(&d.d_status->hbm_next, 0, sizeof(int32_t), st));
       const int last = tier == kHbmTiers - 1;
       if (coop)
         HIP_TRY(c, lcdev::launch_hbm_coop(d_ops, d_off, list, n_list, p, d_out, d.d_ws, waves,
                                           kHbmCap[tier], next, &d.d_status->n_overflow2,
-                                          &d.d_status->malformed, last, wpk, st));
+                                          &d.d_status->malformed, &d.d_status->hbm_next, last,
+                                          wpk, st));
       else
         HIP_TRY(c, lcdev::launch_hbm_tier(d_ops, d_off, list, n_list, p,
                                           d_out, d.d_ws, waves, kHbmCap[tier], next,
                                           &d.d_status->n_overflow2, &d.d_status->malformed,
-                                          last, st));
+                                          &d.d_status->hbm_next, last, st));
       HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                                 hipMemcpyDeviceToHost, st));
       HIP_TRY(c, hipStreamSynchronize(st));
