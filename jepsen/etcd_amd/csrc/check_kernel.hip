@@ -2132,7 +2132,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
     const int64_t cap, int32_t *__restrict__ ovf_out, int32_t *__restrict__ n_ovf_out,
     int32_t *__restrict__ n_malformed, int32_t *__restrict__ next, const int last_tier) {
   __shared__ CoopShared C;
-  constexpr int LT = NW >= 16 ? 4096 : 2048;  // LDS table entries per role
+  constexpr int LT = NW >= 8 ? 4096 : 2048;  // LDS table entries per role
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   {  // LDS tags and W flags start stale (epochs start at 1)
     uint32_t *tg = &coop_tab<LT>().tag[0][0];
@@ -2301,7 +2301,11 @@ hipError_t launch_hbm_coop(const lc_op *d_ops, const int64_t *d_key_off, const i
                            int32_t *d_malformed, int32_t *d_next, int last_tier,
                            int waves_per_key, hipStream_t stream) {
   if (n_list <= 0) return hipSuccess;
-  if (waves_per_key >= 16)
+  if (waves_per_key == 8)  // (A/B: LC_HBM_COOP=8)
+    hipLaunchKernelGGL(hbm_coop_kernel<8>, dim3((unsigned)n_wg), dim3(8 * kWave), 0, stream,
+                       d_ops, d_key_off, d_keys, n_list, p, d_out, static_cast<char *>(d_ws), cap,
+                       d_ovf_out, d_n_ovf_out, d_malformed, d_next, last_tier);
+  else if (waves_per_key >= 16)
     hipLaunchKernelGGL(hbm_coop_kernel<16>, dim3((unsigned)n_wg), dim3(16 * kWave), 0, stream,
                        d_ops, d_key_off, d_keys, n_list, p, d_out, static_cast<char *>(d_ws), cap,
                        d_ovf_out, d_n_ovf_out, d_malformed, d_next, last_tier);

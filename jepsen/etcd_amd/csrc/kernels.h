@@ -103,7 +103,7 @@ hipError_t launch_lds_tier(const lc_op *d_ops, const int64_t *d_key_off,
 // d_ovf_out (count *d_n_ovf_out) unless last_tier, where they become
 // LC_REASON_CONFIG_BUDGET (:unknown).
 size_t hbm_tier_ws_bytes(int n_waves, int64_t cap);
-// Cooperative variant: one workgroup of waves_per_key (4 or 16) wavefronts
+// Cooperative variant: one workgroup of waves_per_key (4, 8 or 16) wavefronts
 // per key, its waves expanding the key's frontier together (for short key
 // lists, where a wavefront per key leaves SIMDs idle).  Workspace:
 // hbm_tier_ws_bytes(n_wg, cap).

@@ -58,7 +58,13 @@ constexpr int kHbmWaves[kHbmTiers] = {2048, 128, 16};
 // DESIGN.md §4): 16 wins on 512 crash-heavy keys (4.9 s vs 13.1 s with 4,
 // 40 s with 1), 4 on 1000-2000 version-less keys (71 vs 113 vs 119 ms),
 // 1 on 10,000 (331 vs 355 ms with 4).
-constexpr int kHbmCoop16MaxKeys = 256;  // one 16-wave workgroup per CU (tools/coop_width_ab.py)
+// 8-wave workgroups (two per CU) up to 512 keys, 4-wave ones beyond: version-
+// less 1,000-op keys at concurrency 20 (tools/coop8_ab.py), HBM tier ms:
+//   keys        64    256    400    512    700   1000
+//   4 waves   11.6   11.8   12.0   12.1   12.7   13.5
+//   8 waves    9.1    9.1    9.2    9.4   15.3   18.0
+//   16 waves   9.0    9.1   14.6   16.4   21.6   30.0
+constexpr int kHbmCoop8MaxKeys = 512;
 constexpr int kHbmCoop16Resident = 256;   // 16-wave workgroups resident: one per CU
 constexpr int kHbmCoop4Resident = 1024;   // 4-wave workgroups: four per CU (LDS tables)
 constexpr int kJitDirectMaxKeys = 1024;  // 4 cooperative workgroups per CU x 256 CUs
@@ -455,18 +461,18 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     HIP_TRY(c, hipEventRecord(d.e1, st));
     // LC_HBM_COOP (test/A-B knob): 0 one wavefront per key throughout,
     // 4 / 16 a workgroup of that many wavefronts per key throughout; default:
-    // 16 for at most 256 keys (one workgroup per CU), else 4.  (Round 1 used
+    // 8 for at most 512 keys (two workgroups per CU), else 4.  (Round 1 used
     // one wavefront per key beyond 4,096 keys; with the LDS tables the
     // 4-wave workgroups win there too: version-less 10,000 x 1,000 at
     // concurrency 20, HBM tier 128 -> 98 ms, tools/hbm_width_large.py.)
     const char *coop_env = getenv("LC_HBM_COOP");
     const int coop_mode = coop_env ? atoi(coop_env) : 1;
     for (int tier = 0; tier < kHbmTiers && n_list > 0; tier++) {
-      int wpk = coop_mode == 1 ? (n_list <= kHbmCoop16MaxKeys ? 16 : 4) : coop_mode;
-      const bool coop = wpk == 4 || wpk == 16;
+      int wpk = coop_mode == 1 ? (n_list <= kHbmCoop8MaxKeys ? 8 : 4) : coop_mode;
+      const bool coop = wpk == 4 || wpk == 8 || wpk == 16;
       // workgroups: at most the resident ones (keys are claimed dynamically)
-      const int resident = wpk == 16 ? kHbmCoop16Resident : wpk == 4 ? kHbmCoop4Resident
-                                                                       : kHbmWaves[tier];
+      const int resident = wpk == 16 ? kHbmCoop16Resident : wpk == 8 ? 512
+                           : wpk == 4 ? kHbmCoop4Resident : kHbmWaves[tier];
       const int waves = std::min<int>(std::min(kHbmWaves[tier], resident), n_list);
       const size_t ws = lcdev::hbm_tier_ws_bytes(waves, kHbmCap[tier]);
       rc = ensure(c, reinterpret_cast<char **>(&d.d_ws), &d.ws_cap, ws);

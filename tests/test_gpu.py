@@ -148,7 +148,7 @@ def test_hbm_tier_resolves_lds_overflow(ctx, monkeypatch):
         assert (direct[f] == full[f]).all(), f
 
 
-@pytest.mark.parametrize("mode", ["0", "4", "16"])
+@pytest.mark.parametrize("mode", ["0", "4", "8", "16"])
 def test_hbm_tier_cooperative_agrees(ctx, mode, monkeypatch):
     """The HBM tier with one wavefront per key (LC_HBM_COOP=0) and with a
     workgroup of 4 or 16 wavefronts per key reaches the same configuration sets: same
