@@ -178,6 +178,7 @@ struct CoopShared {
   unsigned long long qword;  // LDS work queue: claimed head (low), expanding waves (high)
   int lds;  // this attempt keeps its tables and sets in LDS (CoopTab)
   uint32_t lepoch;  // its LDS epoch (16 bits)
+  int kw;           // LDS mode: W's versions are kw + popc(mask & muts) (set by the split)
   int lclear;       // the LDS epoch wrapped: clear the tags first
   unsigned long long explored;
   long long budget;
@@ -393,11 +394,17 @@ constexpr uint32_t kIdxBusy = 0xFFFFu;  // claimed, index not yet published
 constexpr uint32_t kIdxOvf = 0xFFFEu;   // claimed past kLim (the return is redone)
 template <int LT>
 struct CoopTab {
-  static constexpr int kLim = LT * 5 / 16;  // configurations per set
+  // configurations per set: 12 B each (below) plus a 2-byte flag, with the
+  // tables at <= 42 % load: 864 in 38 KB (4-wave), 1,728 in 76 KB (8-wave)
+  static constexpr int kLim = LT * 27 / 64;
   static_assert(kLim < (int)kIdxOvf, "set index must fit 16 bits");
-  uint32_t tag[2][LT];  // (epoch << 16) | index, per role
-  Cfg set[2][kLim];     // R and W of this return
-  uint16_t wrdy[kLim];  // W entry written (its epoch): the work queue's readiness
+  uint32_t tag[2][LT];      // (epoch << 16) | index, per role
+  // R and W of this return as (linearized set, value): within one return and
+  // role the version follows from the set (every configuration has freed the
+  // same mutation slots), so it is not stored; W's is kw + popc(mask & muts)
+  uint64_t smask[2][kLim];
+  int32_t sval[2][kLim];
+  uint16_t wrdy[kLim];      // W entry written (its epoch): the work queue's readiness
 };
 template <int LT>
 __device__ __forceinline__ CoopTab<LT> &coop_tab() {
@@ -456,8 +463,8 @@ __device__ __forceinline__ int lds_insert_lanes(CoopTab<LT> &T, CoopShared &C, H
       if ((t & 0xFFFF0000u) == eb) {
         const uint32_t ix = t & 0xFFFFu;
         if (ix < kIdxOvf) {
-          const Cfg e = T.set[role][ix];
-          if (e.mask == c.mask && e.sv == c.sv) {
+          // (mask, value) decide: the version follows from the mask (CoopTab)
+          if (T.smask[role][ix] == c.mask && T.sval[role][ix] == sv_val(c.sv)) {
             pend = false;  // already there
           } else {
             h = (h + 1) & (LT - 1);
@@ -485,7 +492,8 @@ __device__ __forceinline__ int lds_insert_lanes(CoopTab<LT> &T, CoopShared &C, H
         uint32_t pub = eb | kIdxOvf;
         const bool fits = ix < CoopTab<LT>::kLim;
         if (fits) {
-          T.set[role][ix] = c;
+          T.smask[role][ix] = c.mask;
+          T.sval[role][ix] = sv_val(c.sv);
           if (role == ROLE_R) st.reg(rR)[ix] = c;
           pub = eb | (uint32_t)ix;
         } else {
@@ -689,6 +697,7 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
     const bool v = j < nF;
     Cfg c{0, 0};
     if (v) c = st.get(rF, j);
+    if (lds && j == 0) C.kw = sv_ver(c.sv) - __popcll(c.mask & muts);  // (any F config gives it)
     const bool has = v && (c.mask & bs);
     const bool lacks = v && !(c.mask & bs);
     const uint64_t mh = __ballot(has), ml = __ballot(lacks);
@@ -704,12 +713,14 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
         const Cfg rc{c.mask & ~bs, c.sv};
         const int ix = bR + lanes_below(mh);
         st.reg(rR)[ix] = rc;
-        T.set[ROLE_R][ix] = rc;
+        T.smask[ROLE_R][ix] = rc.mask;
+        T.sval[ROLE_R][ix] = sv_val(rc.sv);
         lds_claim_lane(T, ROLE_R, rc, ix, eb, ovf);
       }
       if (lacks) {
         const int ix = bW + lanes_below(ml);
-        T.set[ROLE_W][ix] = c;
+        T.smask[ROLE_W][ix] = c.mask;
+        T.sval[ROLE_W][ix] = sv_val(c.sv);
         lds_claim_lane(T, ROLE_W, c, ix, eb, ovf);  // (releases the entry first)
         __hip_atomic_store(&T.wrdy[ix], (uint16_t)(eb >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -737,6 +748,7 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
     coop_barrier();
   }
   const uint32_t ep16 = eb >> 16;
+  const int kw = lds ? C.kw : 0;  // (written in the split, before the barrier above)
   for (;;) {
     int lo = 0, hi = 0;
     if (!lds) {
@@ -810,7 +822,9 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
           break;
         }
         lds_acquire();
-        c = T.set[ROLE_W][act ? j : b];
+        const int jj = act ? j : b;
+        c.mask = T.smask[ROLE_W][jj];
+        c.sv = pack_sv(kw + __popcll(c.mask & muts), T.sval[ROLE_W][jj]);
       } else {
         c = st.get(rW, act ? j : b);
       }
