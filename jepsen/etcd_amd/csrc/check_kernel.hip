@@ -382,9 +382,9 @@ struct HbmStore {
 // region the event loop reads); one whose sets outgrow kLim is redone with
 // the HBM tables (status -3, as for the adaptive HBM size), so R, the
 // explored count and the verdict do not depend on it.
-// A table entry is 4 bytes, (epoch << 16) | index into the role's set, so
-// the LDS holds kLim = 5/16 of the table size per set (load <= 31%): 640
-// configurations in 36 KB with 4-wave workgroups, four of them per CU.
+// A table entry is 4 bytes, (epoch << 16) | index into the role's set; the
+// sets hold 12-byte configurations (CoopTab), so a 4-wave workgroup fits 864
+// per set in its 40 KB (four per CU) and an 8-wave one 1,728 in 80 KB.
 #ifndef LC_LEPOCH_MASK
 #define LC_LEPOCH_MASK 0xFFFFu  // tests build a variant with 0x3 to wrap every 3 returns
 #endif
