@@ -487,7 +487,30 @@ def cpu_baseline(args, ops, key_off, gpu_res):
                   "oracle/%s restatement of knossos (faster of jit/wgl), %.1f s"
                   % (k, args.ops_per_key, len(sub_ops), best[1], best[2]),
         "verdict_mismatches_vs_gpu": mism,
+        "model_leg": cpu_model_leg(args),
     }
+
+
+def cpu_model_leg(args, n_keys=200):
+    """The model leg's workload (version-less, 1,000 ops, concurrency 20) on
+    the CPU: the oracle's JIT with the same exact reductions as the GPU's
+    search (oracle.JITC), on the first n_keys keys, same threads.  Compare
+    with model_leg.ops_per_s (whole 1,000-key batch, host buffers)."""
+    import oracle
+    from jepsen.etcd_amd import abi
+    ops, off, _, _ = abi.synth(1000, 1000, concurrency=20, seed=7)
+    ops = ops.copy()
+    ops[:, 3] = abi.LC_NIL
+    sub_ops, sub_off = ops[: off[n_keys]], off[: n_keys + 1]
+    t0 = time.perf_counter()
+    _, r = oracle.check(sub_ops, sub_off, algo=oracle.JITC, n_threads=args.cpu_threads,
+                        max_configs=1 << 24)
+    dt = time.perf_counter() - t0
+    return {"value": len(sub_ops) / dt, "unit": "ops/s", "cores": args.cpu_threads,
+            "kind": "port",
+            "sample": "%d keys x 1000 ops of the model leg's workload, oracle JITC (knossos.linear "
+                      "restated with the GPU's exact reductions), %.2f s" % (n_keys, dt),
+            "configs_explored": int(r["configs_explored"].sum())}
 
 
 if __name__ == "__main__":
