@@ -72,6 +72,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for a 1-GPU box (never set by the driver): every rank on
+    # device LC_BENCH_DEVICE, process group LC_BENCH_BACKEND (gloo) instead of
+    # RCCL, which refuses two ranks on one GPU
+    if os.environ.get("LC_BENCH_DEVICE"):
+        local = int(os.environ["LC_BENCH_DEVICE"])
+    backend = os.environ.get("LC_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     # under torchrun (even with one rank) the RCCL group carries the timing
     # barrier and the max/sum reductions
@@ -83,7 +89,10 @@ def main():
         saved = os.dup(1)
         os.dup2(2, 1)
         try:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(backend)
             dist.barrier()
         finally:
             sys.stdout.flush()
@@ -221,7 +230,7 @@ def main():
         line["c1_leg"] = c1_leg(ctx, abi)
         line["host_leg"] = host_leg(ctx, abi, ops, key_off, n_inv)
         line["hot_key"] = hot_key(ctx, abi)
-        line["search_leg"] = search_leg(ctx, abi, d_ops, d_off, d_out, args, stream, n_ops)
+        line["search_leg"] = search_leg(ctx, abi, d_ops, d_off, d_out, my_keys, stream, n_ops)
         line["mixed_leg"] = mixed_leg(ctx, abi, dev, stream)
         line["model_leg"] = model_leg(ctx, abi)
         line["crash_leg"] = crash_leg(ctx, abi, dev, stream)
@@ -307,17 +316,18 @@ def hot_key(ctx, abi):
                 invalid=out["invalid"])
 
 
-def search_leg(ctx, abi, d_ops, d_off, d_out, args, stream, n_ops):
-    """The same resident C2 batch with the version-order and gap tiers off
-    (LC_FLAG_NO_FAST_PATH): every key goes through the JIT frontier search
-    (lds_tier_kernel).  Not part of `value`; shows the search kernel's rate."""
+def search_leg(ctx, abi, d_ops, d_off, d_out, n_keys, stream, n_ops):
+    """The same resident C2 batch (this rank's key range) with the
+    version-order and gap tiers off (LC_FLAG_NO_FAST_PATH): every key goes
+    through the JIT frontier search (lds_tier_kernel).  Not part of `value`;
+    shows the search kernel's rate."""
     import torch
     opts = abi.default_opts(flags=abi.LC_FLAG_NO_FAST_PATH)
     ms, wall = [], []
     for i in range(4):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), args.keys, d_out.data_ptr(),
+        ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), n_keys, d_out.data_ptr(),
                          stream=stream.cuda_stream, opts=opts)
         wall.append(time.perf_counter() - t0)
         ms.append(ctx.stats()["jit_kernel_ms"])
