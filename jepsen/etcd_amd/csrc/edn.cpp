@@ -1,13 +1,14 @@
 // edn.cpp — Jepsen history.edn -> packed lc_op records (include/lincheck_edn.h).
 //
-// Host code (no HIP).  Three stages:
-//  1. a single-threaded structural scan finds the top-level forms (strings,
-//     character literals, comments and brackets only: no values are built);
-//  2. the forms are parsed on n_threads threads into compact op summaries
-//     (type, f, process, index and the parts of :value the register model
-//     reads, with EDN-equality identities for keys and values);
+// Host code (no HIP).  Three stages, each on n_threads threads:
+//  1. a structural scan finds the top-level forms (strings, character
+//     literals, comments and brackets only: no values are built), on pieces
+//     cut at newlines and stitched into the serial scan's result;
+//  2. the forms are parsed into compact op summaries (type, f, process, index
+//     and the parts of :value the register model reads, with EDN-equality
+//     identities for keys and values);
 //  3. the per-key split (jepsen.independent, register.clj:108), knossos
-//     history completion and per-key value interning, keys in parallel.
+//     history completion and per-key value interning.
 // The rules are those of jepsen/etcd_amd/history.py; tests/test_edn.py holds
 // the two to the same records on generated and hand-written histories.
 #include "../../../include/lincheck_edn.h"
@@ -20,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -138,6 +140,100 @@ struct Scanner {
   }
 };
 
+using Spans = std::vector<std::pair<size_t, size_t>>;
+
+// Top-level forms of text[p, e) that start before cend, from p (which must be
+// a top-level position).  Returns the position after the last form's
+// trailing whitespace (>= cend or e), or the error position.
+size_t scan_run(const char *text, size_t p, size_t cend, size_t e, Spans &forms,
+                const char *&err, size_t &err_at) {
+  Scanner sc{text, e, p};
+  for (;;) {
+    sc.ws();
+    if (sc.p >= e || sc.p >= cend) return sc.p;
+    const size_t b = sc.p;
+    if (!sc.form()) {
+      err = sc.err, err_at = sc.err_at;
+      return sc.p;
+    }
+    forms.emplace_back(b, sc.p);
+  }
+}
+
+// The top-level forms of text[b, e), on up to T threads, equal to one serial
+// scan's.  The range is cut after newlines and each piece is scanned as if it
+// began at top level (Jepsen writes one op per line, so it nearly always
+// does).  A stitch pass walks the pieces in order from the true scan's
+// position: a piece whose speculative forms include that position is right
+// from there on (the scan is a function of the position alone); one that does
+// not (a string or collection spans the cut) is rescanned serially.
+bool scan_forms(const char *text, size_t b, size_t e, int T, Spans &forms, const char *&err,
+                size_t &err_at) {
+  const size_t len = e > b ? e - b : 0;
+  const char *mp = getenv("LC_EDN_MIN_PIECE");  // bytes per piece (tests cut small pieces)
+  const size_t min_piece = std::max<size_t>(1, mp ? (size_t)atoll(mp) : (size_t)1 << 20);
+  T = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(T, 1), len / min_piece));
+  if (T == 1) {
+    scan_run(text, b, e, e, forms, err, err_at);
+    return !err;
+  }
+  struct Piece {
+    size_t beg, end, last = 0, err_at = 0;
+    Spans forms;
+    const char *err = nullptr;
+  };
+  std::vector<Piece> pc(T);
+  for (int t = 0; t < T; t++) {
+    size_t c = b + len * t / T;
+    if (t) {
+      const void *nl = memchr(text + c, '\n', e - c);
+      c = nl ? (size_t)((const char *)nl - text) + 1 : e;
+      c = std::max(c, pc[t - 1].beg);
+    }
+    pc[t].beg = c;
+  }
+  for (int t = 0; t < T; t++) pc[t].end = t + 1 < T ? pc[t + 1].beg : e;
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; t++)
+      th.emplace_back([&, t] {
+        Piece &x = pc[t];
+        x.forms.reserve((x.end - x.beg) / 48);
+        x.last = scan_run(text, x.beg, x.end, e, x.forms, x.err, x.err_at);
+      });
+    Piece &x = pc[0];
+    x.last = scan_run(text, x.beg, x.end, e, x.forms, x.err, x.err_at);
+    for (auto &y : th) y.join();
+  }
+  size_t total = 0;
+  for (auto &x : pc) total += x.forms.size();
+  forms.reserve(total);
+  size_t pos = b;  // a position of the true scan, at top level
+  for (int t = 0; t < T; t++) {
+    Piece &x = pc[t];
+    if (pos >= x.end) continue;  // a form of an earlier piece covers this one
+    Scanner sc{text, e, pos};
+    sc.ws();
+    pos = sc.p;
+    if (pos >= e) break;
+    if (pos >= x.end) continue;
+    auto it = std::lower_bound(x.forms.begin(), x.forms.end(), std::make_pair(pos, (size_t)0));
+    if (it != x.forms.end() && it->first == pos) {  // in step with the true scan
+      forms.insert(forms.end(), it, x.forms.end());
+      if (x.err) {
+        err = x.err, err_at = x.err_at;
+        return false;
+      }
+      pos = x.last;
+    } else {
+      pos = scan_run(text, pos, x.end, e, forms, err, err_at);
+      if (err) return false;
+    }
+    Spans().swap(x.forms);
+  }
+  return true;
+}
+
 // ----------------------------------------------------------------- parse
 enum NT : uint8_t {
   N_NIL, N_BOOL, N_INT, N_BIG, N_FLOAT, N_DEC, N_RATIO, N_STR, N_CHAR, N_KW, N_SYM,
@@ -207,6 +303,18 @@ struct Parser {
     return true;
   }
   bool number(size_t b, size_t e, uint32_t &out) {
+    {  // the common case, a plain decimal that fits: what strtoll below would give
+      size_t q = b + (s[b] == '+' || s[b] == '-');
+      if (e > q && e - q <= 18) {
+        int64_t v = 0;
+        size_t r = q;
+        while (r < e && s[r] >= '0' && s[r] <= '9') v = v * 10 + (s[r++] - '0');
+        if (r == e) {
+          out = add(N_INT, b, e, s[b] == '-' ? -v : v);
+          return true;
+        }
+      }
+    }
     const std::string t(s + b, e - b);
     if (t.find('/') != std::string::npos) {
       out = add(N_RATIO, b, e);
@@ -430,7 +538,39 @@ struct alignas(128) Chunk {  // one per parse thread: no false sharing of the ve
   std::string pool;
   const char *err = nullptr;
   size_t err_at = 0;
+  // the chunk's view of the per-key split: per op, a chunk-local key id
+  // (-1 not a client op, -2 a client op without a tuple); per local key, its
+  // canonical text and the op where it first appears
+  std::vector<int32_t> kid;
+  std::vector<std::string_view> lkey;
+  std::vector<uint32_t> lfirst;
+  bool shared = false;
 };
+
+// Local key ids in order of first appearance within the chunk.
+void local_keys(Chunk &c, bool independent) {
+  c.kid.resize(c.ops.size());
+  std::unordered_map<std::string_view, int32_t> ids;
+  for (size_t i = 0; i < c.ops.size(); i++) {
+    const POp &o = c.ops[i];
+    if (!o.client) {
+      c.kid[i] = -1;
+    } else if (independent && !o.tuple) {
+      c.kid[i] = -2;
+      c.shared = true;
+    } else {  // not independent: every client op is the one key ""
+      const std::string_view k = independent ? std::string_view(c.pool.data() + o.key.off, o.key.len)
+                                             : std::string_view();
+      auto it = ids.find(k);
+      if (it == ids.end()) {
+        it = ids.emplace(k, (int32_t)c.lkey.size()).first;
+        c.lkey.push_back(k);
+        c.lfirst.push_back((uint32_t)i);
+      }
+      c.kid[i] = it->second;
+    }
+  }
+}
 
 void put_val(const Parser &ps, uint32_t id, std::string &pool, Val &v) {
   const Node &x = ps.nodes[id];
@@ -537,16 +677,16 @@ struct lc_edn_history {
 namespace {
 
 struct Interner {
-  std::unordered_map<std::string, int32_t> ids;
+  std::unordered_map<std::string_view, int32_t> ids;  // views into the chunks' pools
   std::vector<std::string> *shown;
   const char *text;
   int64_t operator()(const std::vector<Chunk> &ch, const POp &o, const Val &v) {
     if (v.nil) return LC_NIL;
-    std::string k(ch[o.thread].pool, v.off, v.len);
+    const std::string_view k(ch[o.thread].pool.data() + v.off, v.len);
     auto it = ids.find(k);
     if (it != ids.end()) return it->second;
     const int32_t id = (int32_t)shown->size();
-    ids.emplace(std::move(k), id);
+    ids.emplace(k, id);
     shown->emplace_back(text + v.beg, v.end - v.beg);
     return id;
   }
@@ -577,32 +717,40 @@ int lc_edn_parse(const char *text, size_t len, int64_t flags, int n_threads,
     t_last = t;
   };
   // 1. top-level forms (inside a single wrapping vector, if that is the file)
+  const int T0 = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
   Scanner sc{text, len};
   sc.ws();
   size_t stop = len;
+  Spans forms;
+  const char *serr = nullptr;
+  size_t serr_at = 0;
+  bool scanned = false;
   if (sc.p < len && text[sc.p] == '[') {
-    Scanner probe{text, len, sc.p};
-    if (!probe.form()) return fail(probe.err, probe.err_at);
-    probe.ws();
-    if (probe.p == len) {  // one vector holding the ops
-      sc.p++;
-      stop = probe.p - 1;
-      while (stop > sc.p && text[stop] != ']') stop--;
+    size_t last = len;
+    while (last > sc.p && is_ws(text[last - 1])) last--;
+    // the common wrapped file, "[op op ...]": scan the inside directly
+    if (last > sc.p + 1 && text[last - 1] == ']' &&
+        scan_forms(text, sc.p + 1, last - 1, T0, forms, serr, serr_at) &&
+        (forms.empty() || forms.back().second <= last - 1)) {
+      scanned = true;
+    } else {
+      forms.clear();
+      serr = nullptr;
+      Scanner probe{text, len, sc.p};
+      if (!probe.form()) return fail(probe.err, probe.err_at);
+      probe.ws();
+      if (probe.p == len) {  // one vector holding the ops
+        sc.p++;
+        stop = probe.p - 1;
+        while (stop > sc.p && text[stop] != ']') stop--;
+      }
     }
   }
-  std::vector<std::pair<size_t, size_t>> forms;
-  for (;;) {
-    sc.n = stop;
-    sc.ws();
-    if (sc.p >= stop) break;
-    const size_t b = sc.p;
-    if (!sc.form()) return fail(sc.err, sc.err_at);
-    forms.emplace_back(b, sc.p);
-  }
+  if (!scanned && !scan_forms(text, sc.p, stop, T0, forms, serr, serr_at))
+    return fail(serr, serr_at);
   lap("scan");
   // 2. parse forms in parallel
-  int T = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
-  T = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, forms.size() / 4096 + 1));
+  int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)T0, forms.size() / 4096 + 1));
   std::vector<Chunk> ch(T);
   {
     std::vector<std::thread> th;
@@ -612,6 +760,7 @@ int lc_edn_parse(const char *text, size_t len, int64_t flags, int n_threads,
         const auto a = std::chrono::steady_clock::now();
         parse_chunk(text, forms, f0, f1, independent, model == LC_EDN_VERSIONED_REGISTER,
                     (uint32_t)t, ch[t]);
+        if (!ch[t].err) local_keys(ch[t], independent);
         if (timing)
           fprintf(stderr, "  thread %d: %zu forms %.1f ms\n", t, f1 - f0,
                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count());
@@ -623,63 +772,88 @@ int lc_edn_parse(const char *text, size_t len, int64_t flags, int n_threads,
   for (auto &c : ch)
     if (c.err) return fail(c.err, c.err_at);
   lap("parse");
-  // 3. keys in order of first appearance (client ops with a tuple value)
+  // 3. keys in order of first appearance (client ops with a tuple value): the
+  // chunks' local keys are merged in chunk order, then every chunk scatters
+  // its ops into flat per-key lists, file order within a key
+  auto par = [](int n, auto fn) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < n; t++) th.emplace_back(fn, t);
+    fn(0);
+    for (auto &x : th) x.join();
+  };
   auto *h = new lc_edn_history();
   h->text = text;
   h->n_events = (int64_t)forms.size();
-  std::unordered_map<std::string, int32_t> key_ids;
-  std::vector<std::vector<std::pair<int32_t, int32_t>>> sub;  // per key: (chunk, op)
-  if (!independent) {
-    h->keys.push_back("nil");
-    sub.emplace_back();
-  }
   std::vector<int64_t> first_pos(T + 1, 0);
   for (int t = 0; t < T; t++) first_pos[t + 1] = first_pos[t] + (int64_t)ch[t].ops.size();
+  std::vector<std::vector<int32_t>> gid(T);  // per chunk: local key -> key
   bool any_shared = false;
-  for (int t = 0; t < T; t++) {
-    for (size_t i = 0; i < ch[t].ops.size(); i++) {
-      const POp &o = ch[t].ops[i];
-      if (!o.client) continue;
-      if (!independent) {
-        sub[0].emplace_back(t, (int32_t)i);
-        continue;
+  {
+    std::unordered_map<std::string_view, int32_t> key_ids;
+    if (!independent) {
+      key_ids.emplace(std::string_view(), 0);
+      h->keys.push_back("nil");
+    }
+    for (int t = 0; t < T; t++) {
+      any_shared |= ch[t].shared;
+      gid[t].resize(ch[t].lkey.size());
+      for (size_t l = 0; l < ch[t].lkey.size(); l++) {
+        auto it = key_ids.find(ch[t].lkey[l]);
+        if (it == key_ids.end()) {
+          it = key_ids.emplace(ch[t].lkey[l], (int32_t)h->keys.size()).first;
+          const POp &o = ch[t].ops[ch[t].lfirst[l]];
+          h->keys.emplace_back(text + o.key.beg, o.key.end - o.key.beg);
+        }
+        gid[t][l] = it->second;
       }
-      if (!o.tuple) {
-        any_shared = true;
-        continue;
-      }
-      std::string k(ch[t].pool, o.key.off, o.key.len);
-      auto it = key_ids.find(k);
-      int32_t kid;
-      if (it == key_ids.end()) {
-        kid = (int32_t)h->keys.size();
-        key_ids.emplace(std::move(k), kid);
-        h->keys.emplace_back(text + o.key.beg, o.key.end - o.key.beg);
-        sub.emplace_back();
-      } else {
-        kid = it->second;
-      }
-      sub[kid].emplace_back(t, (int32_t)i);
     }
   }
-  if (any_shared) {  // rare: re-walk in file order, adding non-tuple client ops to every key
-    for (auto &s : sub) s.clear();
+  const size_t K = h->keys.size();
+  std::vector<int64_t> sub_off(K + 1, 0);
+  std::vector<std::pair<int32_t, int32_t>> sub;  // (chunk, op), key-major
+  if (!any_shared) {
+    std::vector<int64_t> at((size_t)T * K, 0);  // per chunk and key: count, then write position
+    par(T, [&](int t) {
+      int64_t *c = at.data() + (size_t)t * K;
+      for (const int32_t l : ch[t].kid)
+        if (l >= 0) c[gid[t][l]]++;
+    });
+    int64_t run = 0;
+    for (size_t k = 0; k < K; k++) {
+      sub_off[k] = run;
+      for (int t = 0; t < T; t++) {
+        const int64_t c = at[(size_t)t * K + k];
+        at[(size_t)t * K + k] = run;
+        run += c;
+      }
+    }
+    sub_off[K] = run;
+    sub.resize((size_t)run);
+    par(T, [&](int t) {
+      int64_t *w = at.data() + (size_t)t * K;
+      const auto &kid = ch[t].kid;
+      for (size_t i = 0; i < kid.size(); i++)
+        if (kid[i] >= 0) sub[(size_t)w[gid[t][kid[i]]]++] = {t, (int32_t)i};
+    });
+  } else {  // rare: non-tuple client ops go to every key, in file order
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> lists(K);
     for (int t = 0; t < T; t++) {
-      for (size_t i = 0; i < ch[t].ops.size(); i++) {
-        const POp &o = ch[t].ops[i];
-        if (!o.client) continue;
-        if (o.tuple) {
-          std::string k(ch[t].pool, o.key.off, o.key.len);
-          sub[key_ids[k]].emplace_back(t, (int32_t)i);
-        } else {
-          for (auto &s : sub) s.emplace_back(t, (int32_t)i);
+      for (size_t i = 0; i < ch[t].kid.size(); i++) {
+        const int32_t l = ch[t].kid[i];
+        if (l >= 0) {
+          lists[gid[t][l]].emplace_back(t, (int32_t)i);
+        } else if (l == -2) {
+          for (auto &s : lists) s.emplace_back(t, (int32_t)i);
         }
       }
+    }
+    for (size_t k = 0; k < K; k++) {
+      sub_off[k + 1] = sub_off[k] + (int64_t)lists[k].size();
+      sub.insert(sub.end(), lists[k].begin(), lists[k].end());
     }
   }
   lap("split");
   // 4. per key: completion + packing, keys in parallel
-  const size_t K = h->keys.size();
   struct KeyOut {
     std::vector<lc_op> recs;
     std::vector<std::pair<size_t, size_t>> inv, comp;
@@ -695,7 +869,8 @@ int lc_edn_parse(const char *text, size_t len, int64_t flags, int n_threads,
       };
       std::vector<R> rs;
       std::unordered_map<int64_t, int32_t> pending;
-      for (const auto &e : sub[k]) {
+      for (int64_t j = sub_off[k]; j < sub_off[k + 1]; j++) {
+        const auto &e = sub[(size_t)j];
         const POp &o = ch[e.first].ops[e.second];
         const int64_t idx = o.has_index ? o.index : first_pos[e.first] + e.second;
         if (o.type == 0) {
@@ -754,24 +929,25 @@ int lc_edn_parse(const char *text, size_t len, int64_t flags, int n_threads,
       }
     }
   };
-  {
-    const int KT = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, K / 64 + 1));
-    std::vector<std::thread> th;
-    for (int t = 0; t < KT; t++) th.emplace_back(do_keys, K * t / KT, K * (t + 1) / KT);
-    for (auto &x : th) x.join();
-  }
+  const int KT = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, K / 64 + 1));
+  par(KT, [&](int t) { do_keys(K * t / KT, K * (t + 1) / KT); });
   lap("complete");
   h->key_off.assign(K + 1, 0);
   for (size_t k = 0; k < K; k++) h->key_off[k + 1] = h->key_off[k] + (int64_t)ko[k].recs.size();
-  h->ops.reserve((size_t)h->key_off[K]);
+  h->ops.resize((size_t)h->key_off[K]);
+  h->inv.resize((size_t)h->key_off[K]);
+  h->comp.resize((size_t)h->key_off[K]);
   h->values.resize(K);
-  for (size_t k = 0; k < K; k++) {
-    h->ops.insert(h->ops.end(), ko[k].recs.begin(), ko[k].recs.end());
-    h->inv.insert(h->inv.end(), ko[k].inv.begin(), ko[k].inv.end());
-    h->comp.insert(h->comp.end(), ko[k].comp.begin(), ko[k].comp.end());
-    h->values[k] = std::move(ko[k].values);
-    ko[k] = KeyOut();
-  }
+  par(KT, [&](int t) {
+    for (size_t k = K * t / KT; k < K * (t + 1) / KT; k++) {
+      const size_t o = (size_t)h->key_off[k];
+      std::copy(ko[k].recs.begin(), ko[k].recs.end(), h->ops.begin() + o);
+      std::copy(ko[k].inv.begin(), ko[k].inv.end(), h->inv.begin() + o);
+      std::copy(ko[k].comp.begin(), ko[k].comp.end(), h->comp.begin() + o);
+      h->values[k] = std::move(ko[k].values);
+      ko[k] = KeyOut();
+    }
+  });
   lap("gather");
   *out = h;
   return 0;

@@ -69,8 +69,8 @@ class EdnHistory:
         if isinstance(text, bytes):
             ptr = ctypes.c_char_p(text)  # no copy
         else:
-            self._buf = (ctypes.c_char * len(text)).from_buffer(text)
-            ptr = ctypes.cast(self._buf, ctypes.c_char_p)
+            self._buf = np.frombuffer(text, dtype=np.uint8)  # read-only views too
+            ptr = ctypes.cast(self._buf.ctypes.data, ctypes.c_char_p)
         h = ctypes.c_void_p()
         err = ctypes.create_string_buffer(256)
         rc = L.lc_edn_parse(ptr, len(text),
@@ -115,7 +115,10 @@ def read(src, independent=True, n_threads=0, model="versioned-register"):
             size = os.fstat(fh.fileno()).st_size
             if size == 0:
                 return EdnHistory(b"", independent, n_threads, model)
-            mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_COPY)
+            # read-only and prefaulted: first-touch faults from the parse
+            # threads would cost more than the scan itself
+            mm = mmap.mmap(fh.fileno(), 0, flags=mmap.MAP_SHARED | getattr(mmap, "MAP_POPULATE", 0),
+                           prot=mmap.PROT_READ)
         return EdnHistory(mm, independent, n_threads, model)
     if isinstance(src, str):
         src = src.encode()

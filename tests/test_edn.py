@@ -213,3 +213,55 @@ def test_jvm_parity_kit_histories(name):
         if not valid:
             assert r["fail_prefix_end"][i] == op_index, ktext
     assert (r["verdict"] != -1).mean() > 0.9
+
+
+def _awkward(hist):
+    """to_edn with forms, strings and comments that span lines and hold brackets."""
+    out = []
+    for i, line in enumerate(edn.to_edn(hist).splitlines()):
+        if i % 7 == 3:
+            line = line.replace(", ", ",\n  ")  # one op map over several lines
+        if i % 11 == 5:
+            out.append('{:type :info, :f :log, :process :nemesis, :value "a\n] } ) [\n \\"{"}')
+        if i % 13 == 2:
+            out.append("; ] a comment [ {")
+        if i % 17 == 9:
+            out.append("#_ {:type :invoke,\n :process 0}")
+        out.append(line)
+    return "\n".join(out) + "\n"
+
+
+@pytest.mark.parametrize("wrapped", [False, True])
+def test_parallel_scan_equals_the_serial_scan(monkeypatch, wrapped):
+    """The scan cuts the file at newlines and stitches the pieces (edn.cpp
+    scan_forms); with pieces of a few hundred bytes nearly every cut falls
+    inside a multi-line form or string, and the result must still be the
+    serial scan's: same records, spans and event count."""
+    hist, _ = synth.jepsen_history(30, 200, concurrency=10, p_info=0.05, p_anomaly=0.2, seed=31)
+    text = _awkward(hist)
+    if wrapped:
+        text = "[" + text + "]\n"
+    a = edn.read(text, n_threads=1)
+    monkeypatch.setenv("LC_EDN_MIN_PIECE", "300")
+    for t in (2, 8, 64):
+        b = edn.read(text, n_threads=t)
+        assert b.n_events == a.n_events and b.keys == a.keys
+        assert (b.ops == a.ops).all() and (b.key_off == a.key_off).all()
+        for rec in range(0, len(a.ops), 97):
+            assert b.op_text(rec, 0) == a.op_text(rec, 0) and b.op_text(rec, 1) == a.op_text(rec, 1)
+    assert a.n_events == len(hist) + len(range(5, len(hist), 11))  # + the :log ops
+
+
+def test_parallel_scan_reports_the_first_error(monkeypatch):
+    hist, _ = synth.jepsen_history(10, 200, seed=32)
+    lines = _awkward(hist).splitlines()
+    lines[len(lines) // 3] += ")"
+    lines[2 * len(lines) // 3] = '{:a "unterminated'
+    text = "\n".join(lines)
+    with pytest.raises(abi.LcError) as e1:
+        edn.read(text, n_threads=1)
+    monkeypatch.setenv("LC_EDN_MIN_PIECE", "300")
+    for t in (2, 8, 64):
+        with pytest.raises(abi.LcError) as e2:
+            edn.read(text, n_threads=t)
+        assert str(e2.value) == str(e1.value)
