@@ -1,0 +1,114 @@
+/*
+ * lincheck_fx.h — frontier exchange: ONE oversized key's JIT frontier search
+ * spread over a whole GPU, and over several GPUs by hash ownership.
+ *
+ * SURVEY.md §8(e), "the one exception": a key too large for one workgroup of
+ * the HBM tier (lincheck.h) — a version-less model (cas-register, register,
+ * mutex: lock.clj:244) with a long, highly concurrent history, where knossos'
+ * search (knossos.linear, called through checker/linearizable at
+ * register.clj:110-111) holds frontiers of 10^5..10^7 configurations.
+ *
+ * The search is knossos.linear's (Lowe's JIT linearization) with the exact
+ * reductions of the other tiers (eager read closure, deadline order,
+ * retirement: DESIGN.md §4), restated by the oracle as JITC; on every key
+ * the verdict, the canonical fail op, the configurations explored and the
+ * largest frontier equal the oracle's.  A return's expansion is level-
+ * synchronous over the whole device: every wave takes configurations of the
+ * current level, generates their successors (lane = window slot) and
+ * inserts them into open-addressed device tables.
+ *
+ * Over n ranks each configuration is owned by hash(configuration) mod n (a
+ * Zobrist hash over every op it has linearized, retired ones included, so
+ * retirement never moves a configuration).  While the frontier holds more
+ * than `part_above` configurations it is partitioned: each rank expands the
+ * configurations it owns and sends every successor to its owner (counts
+ * first, then payload: an all-to-all-v), and a small sum-reduction per level
+ * detects the end of the level.  Below `repl_below` the frontier is
+ * gathered back and every rank holds (and expands) all of it, with no
+ * traffic.
+ *
+ * The collectives are the caller's: `lc_fx_transport` is three callbacks
+ * (jepsen/etcd_amd/fx.py implements them with torch.distributed — RCCL
+ * over xGMI with device buffers under "nccl", host-staged under "gloo").
+ * With transport == NULL and virtual_ranks = k the library runs k ranks as
+ * threads on one device with an in-process transport (device copies), so the
+ * partitioned path is testable on one GPU.
+ *
+ * Plain C types only.
+ */
+#ifndef LINCHECK_FX_H
+#define LINCHECK_FX_H
+
+#include <stdint.h>
+
+#include "lincheck.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LC_FX_SUM 0
+#define LC_FX_MAX 1
+
+/* Collectives over the ranks of one search.  Every callback is called by
+ * every rank in the same order; each returns 0 or a negative error.
+ *  exchange_counts  send[j] = entries this rank sends to rank j; fills
+ *                   recv[j] = entries rank j sends to this rank (n_ranks each).
+ *  alltoallv        d_send (device memory) holds this rank's entries grouped
+ *                   by destination rank, send_counts[j] of them for rank j;
+ *                   writes the entries received, grouped by source rank, to
+ *                   d_recv (device, room for the sum of recv_counts).
+ *  allreduce        in-place element-wise reduction (LC_FX_SUM / LC_FX_MAX)
+ *                   of n int64 values in host memory. */
+typedef struct lc_fx_transport {
+  void *user;
+  int32_t rank;
+  int32_t n_ranks;
+  int (*exchange_counts)(void *user, const int64_t *send, int64_t *recv);
+  int (*alltoallv)(void *user, const void *d_send, const int64_t *send_counts,
+                   void *d_recv, const int64_t *recv_counts, int64_t entry_bytes);
+  int (*allreduce)(void *user, int64_t *vals, int32_t n, int32_t op);
+} lc_fx_transport;
+
+typedef struct lc_fx_params {
+  int32_t device;         /* HIP device ordinal */
+  int32_t virtual_ranks;  /* transport == NULL: ranks run as threads on `device` (>= 1) */
+  int64_t part_above;     /* partition while the frontier exceeds this (< 0: default 65536) */
+  int64_t repl_below;     /* replicate again below this (< 0: default part_above / 4) */
+  int64_t table_log2;     /* log2 of each dedup table's entries (0: from the budget) */
+} lc_fx_params;
+
+typedef struct lc_fx_stats {
+  double  total_ms;         /* host wall time of the last lc_fx_check */
+  int64_t returns;          /* :ok returns whose frontier was expanded */
+  int64_t levels;           /* BFS levels run (replicated + partitioned) */
+  int64_t part_returns;     /* returns expanded with the frontier partitioned */
+  int64_t part_levels;      /* levels run partitioned (one exchange each) */
+  int64_t sent_configs;     /* configurations this rank sent to other ranks */
+  int64_t gathers;          /* partitioned -> replicated switches */
+  int64_t max_local_frontier; /* largest frontier share held by this rank */
+} lc_fx_stats;
+
+typedef struct lc_fx lc_fx;
+
+/* Open an engine.  transport == NULL: params->virtual_ranks in-process ranks.
+ * Returns 0, -EINVAL, -ENODEV, -ENOMEM or -EIO (text in lc_fx_last_error). */
+int lc_fx_open(const lc_fx_params *params, const lc_fx_transport *transport, lc_fx **out);
+
+/* Decide one key: ops[0..n) are its records (lincheck.h layout, host memory,
+ * sorted by call).  Every rank calls it with the same key.  `out` gets the
+ * same result lc_check gives (verdict, reason, fail_op, fail_prefix_end,
+ * configs_explored, max_frontier), identical on every rank.  Keys with more
+ * than LC_MAX_WINDOW open ops are :unknown (LC_REASON_WINDOW_OVERFLOW). */
+int lc_fx_check(lc_fx *fx, const lc_op *ops, int64_t n, const lc_opts *opts,
+                lc_key_result *out);
+
+int lc_fx_last_stats(lc_fx *fx, lc_fx_stats *out);   /* rank 0's (or this rank's) */
+const char *lc_fx_last_error(lc_fx *fx);
+void lc_fx_close(lc_fx *fx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LINCHECK_FX_H */

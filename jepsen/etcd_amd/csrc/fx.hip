@@ -1,0 +1,1150 @@
+// fx.hip — frontier exchange: one oversized key's JIT frontier search over a
+// whole GPU, and over several ranks by hash ownership (include/lincheck_fx.h,
+// DESIGN.md §7).
+//
+// The search is knossos.linear's (the JIT linearization behind
+// checker/linearizable, register.clj:110-111) with the exact reductions the
+// other tiers use (eager read closure, deadline order, retirement), restated
+// by oracle.c's check_key_jit under JITC; this file keeps its structure:
+// events in history order; a call takes a window slot (the lowest free one);
+// an :ok return of x expands every configuration lacking x until x is
+// linearized (level-synchronous here, oracle.c:416-463), the configurations
+// that linearized x become the frontier, and ops linearized in every
+// configuration retire (oracle.c:479-511).  The model step is
+// register.clj:60-96 in precondition form (records.h):
+//     legal(ver, val) <=> (((ver ^ nv) & nvm) | ((val ^ nl) & nlm)) == 0.
+//
+// Device layout (per rank):
+//   F, R, V lists   16-B configurations (mask over the 64 window slots,
+//                   int32 version, int32 value id); F is the frontier, R the
+//                   configurations that linearized x, V the worklist whose
+//                   levels are ranges [lo, hi) of the list
+//   R and V tables  open-addressed dedup sets: 16-B keys plus an 8-B tag
+//                   (epoch << 32 | fingerprint; fingerprint 0 = being
+//                   written), epoch bumped per return so nothing is cleared
+//   candidate regions (partitioned mode) one per owner rank
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../../include/lincheck_fx.h"
+
+namespace {
+
+constexpr int kW = 64;
+constexpr int32_t kFieldMax = 0x7FFFFFFE;
+constexpr int kMaxProbe = 1 << 12;     // table probes per insert before giving up (overflow)
+constexpr int kMaxSpin = 1 << 22;      // loop iterations per insert, busy waits included
+constexpr int kExpandWG = 1024;        // expand grid: 4 waves per workgroup
+constexpr int kFlatWG = 1024;          // thread-per-configuration kernels
+
+struct Cfg {
+  uint64_t mask;
+  uint32_t ver;
+  uint32_t val;
+};
+static_assert(sizeof(Cfg) == 16, "16-byte configuration");
+
+struct Slot {
+  int32_t nv, nvm, nl, nlm;  // precondition
+  int32_t value;             // effect of a write/CAS: the new value
+  int32_t pad;
+  uint64_t before;           // deadline order: same-class slots to linearize first
+  uint64_t zob;              // Zobrist word of the op (0 for reads)
+};
+
+struct Win {
+  uint64_t occ;    // occupied slots
+  uint64_t reads;  // slots holding reads (never candidates: closed eagerly)
+  uint64_t xbit;   // slot of the returning op
+  uint64_t kzob;   // Zobrist words of every retired mutation, xor-ed
+  int32_t rank, n_ranks;
+  int32_t pad[2];
+  Slot s[kW];
+};
+
+struct Ctr {
+  unsigned long long nR, nV;    // list sizes
+  unsigned long long lo, hi;    // current level of V
+  unsigned long long explored;  // successors generated (cumulative)
+  unsigned long long levels;    // non-empty levels (cumulative)
+  unsigned long long andmask;   // AND of R's masks
+  unsigned long long overflow;  // a list or table ran out of room
+  unsigned long long nsel;      // filter output
+  unsigned long long pad[7];
+  unsigned long long cand[64];  // partitioned: candidates per owner rank
+};
+
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+__device__ inline uint64_t cfg_hash(const Cfg &c) {
+  return mix64(c.mask ^ mix64(((uint64_t)c.ver << 32) | c.val));
+}
+
+__device__ inline bool legal(const Slot &s, uint32_t ver, uint32_t val) {
+  return ((((int32_t)ver ^ s.nv) & s.nvm) | (((int32_t)val ^ s.nl) & s.nlm)) == 0;
+}
+
+// Owner rank: a Zobrist hash over the mutations the configuration has
+// linearized, retired ones included (kzob), and its state.  Retirement clears
+// a bit in every configuration and folds the op's word into kzob, so owners
+// never move; reads carry no word, so read closure never moves them either.
+__device__ inline uint32_t owner_of(const Cfg &c, const Win &w) {
+  uint64_t z = w.kzob, m = c.mask;
+  while (m) {
+    const int b = __builtin_ctzll(m);
+    m &= m - 1;
+    z ^= w.s[b].zob;
+  }
+  z ^= mix64(((uint64_t)c.ver << 32) | c.val);
+  return (uint32_t)(mix64(z) % (uint64_t)w.n_ranks);
+}
+
+// Insert into an open-addressed table.  1: new, 0: present, -1: no room.
+// The winner of a stale tag writes the key and publishes the tag inside the
+// loop body (not after a divergent loop exit), so a lane of the same wave
+// spinning on the busy tag sees it on its next iteration.
+__device__ int tab_insert(unsigned long long *tags, Cfg *keys, uint64_t tmask, uint32_t epoch,
+                          const Cfg &c) {
+  const uint64_t h = cfg_hash(c);
+  const uint32_t fp = (uint32_t)(h >> 32) | 1u;
+  const unsigned long long busy = (unsigned long long)epoch << 32;
+  const unsigned long long pub = busy | fp;
+  uint64_t i = h & tmask;
+  int res = -1, probes = 0;
+  bool done = false;
+  for (int it = 0; !done && it < kMaxSpin; it++) {
+    unsigned long long t = __hip_atomic_load(&tags[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(t >> 32) != epoch) {
+      unsigned long long expct = t;
+      if (__hip_atomic_compare_exchange_strong(&tags[i], &expct, busy, __ATOMIC_ACQ_REL,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        keys[i] = c;
+        __hip_atomic_store(&tags[i], pub, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        res = 1;
+        done = true;
+      }
+    } else if ((uint32_t)t == fp) {
+      const Cfg k = keys[i];
+      if (k.mask == c.mask && k.ver == c.ver && k.val == c.val) {
+        res = 0;
+        done = true;
+      } else {
+        i = (i + 1) & tmask;
+        done = ++probes >= kMaxProbe;
+      }
+    } else if ((uint32_t)t != 0) {
+      i = (i + 1) & tmask;
+      done = ++probes >= kMaxProbe;
+    }
+    // (uint32_t)t == 0: being written by another lane; read it again
+  }
+  return res;
+}
+
+struct Tabs {
+  unsigned long long *tagR, *tagV;
+  Cfg *keyR, *keyV;
+  Cfg *listR, *listV;
+  uint64_t tmask;
+  unsigned long long list_cap;
+};
+
+// Wave-aggregated append of the lanes in `take` (each with its own c).
+__device__ inline void wave_append(bool take, const Cfg &c, Cfg *list, unsigned long long *count,
+                                   unsigned long long cap, unsigned long long *overflow) {
+  const uint64_t m = __ballot(take);
+  if (!m) return;
+  const int lane = __lane_id();
+  const int leader = __builtin_ctzll(m);
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(m));
+  base = __shfl(base, leader);
+  if (take) {
+    const unsigned long long pos = base + __popcll(m & ((1ULL << lane) - 1));
+    if (pos < cap) list[pos] = c;
+    else atomicOr(overflow, 1ULL);
+  }
+}
+
+// Insert successors (or split frontier configurations): those that
+// linearized x (xbit) go to R with x's bit cleared, the others to V.
+__device__ inline void insert_rv(bool have, Cfg c, uint64_t xbit, const Tabs &t, uint32_t epoch,
+                                 Ctr *ctr) {
+  bool toR = have && (c.mask & xbit);
+  if (toR) c.mask &= ~xbit;
+  int r = -1;
+  if (have) r = tab_insert(toR ? t.tagR : t.tagV, toR ? t.keyR : t.keyV, t.tmask, epoch, c);
+  if (have && r < 0) atomicOr(&ctr->overflow, 1ULL);
+  wave_append(r == 1 && toR, c, t.listR, &ctr->nR, t.list_cap, &ctr->overflow);
+  wave_append(r == 1 && !toR, c, t.listV, &ctr->nV, t.list_cap, &ctr->overflow);
+}
+
+__global__ __launch_bounds__(256) void fx_insert_kernel(const Cfg *__restrict__ in, int64_t n,
+                                                        const Win *__restrict__ win, Tabs t,
+                                                        uint32_t epoch, Ctr *ctr) {
+  const uint64_t xbit = win->xbit;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x; b < n; b += stride) {
+    const int64_t i = b + threadIdx.x;
+    const bool have = i < n;
+    Cfg c{};
+    if (have) c = in[i];
+    insert_rv(have, c, xbit, t, epoch, ctr);
+  }
+}
+
+__global__ void fx_mark_kernel(Ctr *ctr) {
+  ctr->lo = ctr->hi;
+  ctr->hi = ctr->nV;
+  if (ctr->hi > ctr->lo) ctr->levels++;
+}
+
+// One level of the expansion: every wave takes configurations of V[lo, hi)
+// (from ctr when range == nullptr) one at a time, lane t tests window slot t
+// (pending, not a read, its deadline-order predecessors linearized, legal),
+// builds the successor with its eager read closure, and either inserts it
+// (replicated mode) or appends it to its owner's candidate region
+// (partitioned mode: cand != nullptr).
+__global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ gwin, Tabs t,
+                                                        uint32_t epoch, Ctr *ctr, int64_t lo_arg,
+                                                        int64_t hi_arg, Cfg *cbuf,
+                                                        unsigned long long cand_cap) {
+  __shared__ Win w;
+  {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(gwin);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(&w);
+    for (int i = threadIdx.x; i < (int)(sizeof(Win) / 4); i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  int64_t lo, hi;
+  if (lo_arg < 0) {
+    lo = (int64_t)ctr->lo;
+    hi = (int64_t)ctr->hi;
+  } else {
+    lo = lo_arg;
+    hi = hi_arg;
+  }
+  const int lane = __lane_id();
+  const Slot me = w.s[lane];
+  const uint64_t bit = 1ULL << lane;
+  const uint64_t muts = w.occ & ~w.reads;
+  const uint64_t reads = w.occ & w.reads;
+  const bool is_mut = (muts & bit) != 0;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kW;
+  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kW;
+  unsigned long long explored = 0;
+  for (int64_t i = lo + wave; i < hi; i += nwaves) {
+    const Cfg c = t.listV[i];
+    const bool cand = is_mut && !(c.mask & bit) && !(me.before & ~c.mask) && legal(me, c.ver, c.val);
+    Cfg s = c;
+    if (cand) {
+      s.mask |= bit;
+      s.ver = c.ver + 1;
+      s.val = (uint32_t)me.value;
+      uint64_t pr = reads & ~s.mask;
+      while (pr) {
+        const int b = __builtin_ctzll(pr);
+        pr &= pr - 1;
+        if (legal(w.s[b], s.ver, s.val)) s.mask |= 1ULL << b;
+      }
+    }
+    explored += __popcll(__ballot(cand));
+    if (!cand_cap) {
+      insert_rv(cand, s, w.xbit, t, epoch, ctr);
+    } else {
+      // append to the owner's region; one atomic per distinct owner in the wave
+      const uint32_t own = cand ? owner_of(s, w) : 0xFFFFFFFFu;
+      uint64_t pend = __ballot(cand);
+      while (pend) {
+        const uint32_t o = __shfl(own, __builtin_ctzll(pend));
+        const bool mine = cand && own == o;
+        const uint64_t m = __ballot(mine);
+        pend &= ~m;
+        wave_append(mine, s, cbuf + (size_t)o * cand_cap, &ctr->cand[o], cand_cap, &ctr->overflow);
+      }
+    }
+  }
+  if (lane == 0 && explored) atomicAdd(&ctr->explored, explored);
+}
+
+__device__ inline unsigned long long wave_and(unsigned long long v) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, off), hi = __shfl_xor((uint32_t)(v >> 32), off);
+    v &= ((unsigned long long)hi << 32) | lo;
+  }
+  return v;
+}
+
+// AND of the masks of list[0 .. *n) into ctr->andmask (retirement).
+__global__ __launch_bounds__(256) void fx_and_kernel(const Cfg *__restrict__ list,
+                                                     const unsigned long long *n, Ctr *ctr) {
+  const int64_t cnt = (int64_t)*n;
+  unsigned long long a = ~0ULL;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt;
+       i += (int64_t)gridDim.x * blockDim.x)
+    a &= list[i].mask;
+  a = wave_and(a);
+  if (__lane_id() == 0 && a != ~0ULL) atomicAnd(&ctr->andmask, a);
+}
+
+__global__ __launch_bounds__(256) void fx_clear_kernel(Cfg *list, int64_t n, uint64_t bits) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    list[i].mask &= ~bits;
+}
+
+// A read is called: linearize it at once wherever it is legal (closure).
+__global__ __launch_bounds__(256) void fx_close_read_kernel(Cfg *list, int64_t n, uint64_t bit,
+                                                            Slot s) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    Cfg c = list[i];
+    if (legal(s, c.ver, c.val)) list[i].mask = c.mask | bit;
+  }
+}
+
+// Keep the configurations this rank owns (replicated -> partitioned).
+__global__ __launch_bounds__(256) void fx_filter_kernel(const Cfg *__restrict__ in, int64_t n,
+                                                        const Win *__restrict__ gwin, Cfg *out,
+                                                        unsigned long long cap, Ctr *ctr) {
+  __shared__ Win w;
+  {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(gwin);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(&w);
+    for (int i = threadIdx.x; i < (int)(sizeof(Win) / 4); i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x; b < n; b += stride) {
+    const int64_t i = b + threadIdx.x;
+    Cfg c{};
+    bool keep = false;
+    if (i < n) {
+      c = in[i];
+      keep = owner_of(c, w) == (uint32_t)w.rank;
+    }
+    wave_append(keep, c, out, &ctr->nsel, cap, &ctr->overflow);
+  }
+}
+
+__global__ void fx_reset_kernel(Ctr *ctr) {
+  ctr->nR = ctr->nV = ctr->lo = ctr->hi = 0;
+  ctr->andmask = ~0ULL;
+  ctr->nsel = 0;
+  for (int i = 0; i < 64; i++) ctr->cand[i] = 0;
+}
+
+// ------------------------------------------------------------ host side
+
+uint64_t splitmix(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+
+int32_t clamp_ver(int64_t v) { return (v < -1 || v > kFieldMax) ? kFieldMax : (int32_t)v; }
+
+// In-process transport: k ranks as threads on one device.
+struct Hub {
+  int P;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool aborted = false;
+  std::vector<int64_t> counts;            // P x P
+  std::vector<const char *> sendp;
+  std::vector<const int64_t *> sendc;
+  std::vector<int64_t> red;               // P x n
+  explicit Hub(int p) : P(p), counts((size_t)p * p), sendp(p), sendc(p) {}
+  int barrier() {
+    std::unique_lock<std::mutex> g(mu);
+    if (aborted) return -ECANCELED;
+    const uint64_t my = gen;
+    if (++arrived == P) {
+      arrived = 0;
+      gen++;
+      cv.notify_all();
+    } else {
+      cv.wait(g, [&] { return gen != my || aborted; });
+    }
+    return aborted ? -ECANCELED : 0;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> g(mu);
+    aborted = true;
+    cv.notify_all();
+  }
+};
+
+struct HubRank {
+  Hub *hub;
+  int rank;
+};
+
+int hub_exchange_counts(void *u, const int64_t *send, int64_t *recv) {
+  HubRank *r = static_cast<HubRank *>(u);
+  Hub *h = r->hub;
+  for (int j = 0; j < h->P; j++) h->counts[(size_t)r->rank * h->P + j] = send[j];
+  int e = h->barrier();
+  if (e) return e;
+  for (int j = 0; j < h->P; j++) recv[j] = h->counts[(size_t)j * h->P + r->rank];
+  return h->barrier();
+}
+
+int hub_alltoallv(void *u, const void *d_send, const int64_t *send_counts, void *d_recv,
+                  const int64_t *recv_counts, int64_t bytes) {
+  HubRank *r = static_cast<HubRank *>(u);
+  Hub *h = r->hub;
+  h->sendp[r->rank] = static_cast<const char *>(d_send);
+  h->sendc[r->rank] = send_counts;
+  int e = h->barrier();
+  if (e) return e;
+  char *dst = static_cast<char *>(d_recv);
+  for (int j = 0; j < h->P; j++) {
+    int64_t off = 0;
+    for (int k = 0; k < r->rank; k++) off += h->sendc[j][k];
+    const int64_t cnt = h->sendc[j][r->rank];
+    if (cnt != recv_counts[j]) {
+      h->abort();
+      return -EPROTO;
+    }
+    if (cnt && hipMemcpy(dst, h->sendp[j] + off * bytes, (size_t)(cnt * bytes),
+                         hipMemcpyDeviceToDevice) != hipSuccess) {
+      h->abort();
+      return -EIO;
+    }
+    dst += cnt * bytes;
+  }
+  // a device-to-device hipMemcpy may return before the copy has run: the
+  // engine reads d_recv on its own stream next
+  if (hipStreamSynchronize(nullptr) != hipSuccess) {
+    h->abort();
+    return -EIO;
+  }
+  return h->barrier();
+}
+
+int hub_allreduce(void *u, int64_t *vals, int32_t n, int32_t op) {
+  HubRank *r = static_cast<HubRank *>(u);
+  Hub *h = r->hub;
+  {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->red.size() < (size_t)h->P * n) h->red.resize((size_t)h->P * n);
+  }
+  int e = h->barrier();
+  if (e) return e;
+  std::memcpy(&h->red[(size_t)r->rank * n], vals, sizeof(int64_t) * n);
+  e = h->barrier();
+  if (e) return e;
+  for (int i = 0; i < n; i++) {
+    int64_t a = h->red[i];
+    for (int j = 1; j < h->P; j++) {
+      const int64_t b = h->red[(size_t)j * n + i];
+      a = op == LC_FX_MAX ? std::max(a, b) : a + b;
+    }
+    vals[i] = a;
+  }
+  return h->barrier();
+}
+
+#define FX_TRY(expr)                                                          \
+  do {                                                                        \
+    hipError_t e_ = (expr);                                                   \
+    if (e_ != hipSuccess) {                                                   \
+      err = std::string(#expr) + ": " + hipGetErrorString(e_);                \
+      return -EIO;                                                            \
+    }                                                                         \
+  } while (0)
+
+#define FX_COLL(expr)                                                         \
+  do {                                                                        \
+    int e_ = (expr);                                                          \
+    if (e_ != 0) {                                                            \
+      err = std::string("collective failed: ") + #expr + " -> " + std::to_string(e_); \
+      return e_ < 0 ? e_ : -EIO;                                              \
+    }                                                                         \
+  } while (0)
+
+struct Rank {
+  int dev = 0;
+  int rank = 0, P = 1;
+  lc_fx_transport tr{};
+  int64_t part_above = 65536, repl_below = 16384;
+  int table_log2 = 0;
+  hipStream_t st = nullptr;
+  std::string err;
+  lc_fx_stats stats{};
+
+  // device state
+  Cfg *F = nullptr, *Rl = nullptr, *Vl = nullptr, *tmp = nullptr;
+  unsigned long long list_cap = 0;
+  unsigned long long *tagR = nullptr, *tagV = nullptr;
+  Cfg *keyR = nullptr, *keyV = nullptr;
+  uint64_t tmask = 0;
+  Win *dWin = nullptr, *hWin = nullptr;
+  Ctr *dCtr = nullptr, *hCtr = nullptr;
+  Cfg *cand = nullptr;
+  unsigned long long cand_cap = 0;  // per owner region
+  Cfg *sendb = nullptr, *recvb = nullptr;
+  size_t send_cap = 0, recv_cap = 0;
+  uint32_t epoch = 0;
+
+  ~Rank() { release(); }
+
+  void release() {
+    for (void *p : {(void *)F, (void *)Rl, (void *)Vl, (void *)tmp, (void *)tagR, (void *)tagV,
+                    (void *)keyR, (void *)keyV, (void *)dWin, (void *)dCtr, (void *)cand,
+                    (void *)sendb, (void *)recvb})
+      if (p) (void)hipFree(p);
+    F = Rl = Vl = tmp = keyR = keyV = cand = sendb = recvb = nullptr;
+    tagR = tagV = nullptr;
+    dWin = nullptr;
+    dCtr = nullptr;
+    if (hWin) (void)hipHostFree(hWin);
+    if (hCtr) (void)hipHostFree(hCtr);
+    hWin = nullptr;
+    hCtr = nullptr;
+    list_cap = 0;
+    if (st) (void)hipStreamDestroy(st);
+    st = nullptr;
+  }
+
+  int open() {
+    FX_TRY(hipSetDevice(dev));
+    FX_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    FX_TRY(hipMalloc(&dWin, sizeof(Win)));
+    FX_TRY(hipMalloc(&dCtr, sizeof(Ctr)));
+    FX_TRY(hipHostMalloc(&hWin, sizeof(Win), hipHostMallocDefault));
+    FX_TRY(hipHostMalloc(&hCtr, sizeof(Ctr), hipHostMallocDefault));
+    std::memset(hWin, 0, sizeof(Win));
+    return 0;
+  }
+
+  // Lists and tables for a budget of `budget` configurations.
+  int reserve(int64_t budget) {
+    unsigned long long need = (unsigned long long)budget + 1;
+    int lg = table_log2;
+    if (lg <= 0) {
+      lg = 10;
+      while ((1ULL << lg) < 2 * need) lg++;
+    }
+    const uint64_t tcap = 1ULL << lg;
+    if (list_cap >= need && tmask + 1 == tcap) return 0;
+    for (void *p : {(void *)F, (void *)Rl, (void *)Vl, (void *)tmp, (void *)tagR, (void *)tagV,
+                    (void *)keyR, (void *)keyV})
+      if (p) (void)hipFree(p);
+    FX_TRY(hipMalloc(&F, need * sizeof(Cfg)));
+    FX_TRY(hipMalloc(&Rl, need * sizeof(Cfg)));
+    FX_TRY(hipMalloc(&Vl, need * sizeof(Cfg)));
+    FX_TRY(hipMalloc(&tmp, need * sizeof(Cfg)));
+    FX_TRY(hipMalloc(&tagR, tcap * 8));
+    FX_TRY(hipMalloc(&tagV, tcap * 8));
+    FX_TRY(hipMalloc(&keyR, tcap * sizeof(Cfg)));
+    FX_TRY(hipMalloc(&keyV, tcap * sizeof(Cfg)));
+    FX_TRY(hipMemsetAsync(tagR, 0, tcap * 8, st));
+    FX_TRY(hipMemsetAsync(tagV, 0, tcap * 8, st));
+    list_cap = need;
+    tmask = tcap - 1;
+    epoch = 0;
+    if (P > 1 && !cand) {
+      cand_cap = 1ULL << 21;  // per owner: a chunk of cand_cap / 64 configurations
+      FX_TRY(hipMalloc(&cand, (size_t)P * cand_cap * sizeof(Cfg)));
+    }
+    return 0;
+  }
+
+  int ensure_buf(Cfg **p, size_t *cap, size_t n) {
+    if (*cap >= n && *p) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    size_t c = std::max<size_t>(n, 1 << 16);
+    FX_TRY(hipMalloc(p, c * sizeof(Cfg)));
+    *cap = c;
+    return 0;
+  }
+
+  Tabs tabs() const {
+    Tabs t;
+    t.tagR = tagR;
+    t.tagV = tagV;
+    t.keyR = keyR;
+    t.keyV = keyV;
+    t.listR = Rl;
+    t.listV = Vl;
+    t.tmask = tmask;
+    t.list_cap = list_cap;
+    return t;
+  }
+
+  int sync_ctr() {
+    FX_TRY(hipMemcpyAsync(hCtr, dCtr, sizeof(Ctr), hipMemcpyDeviceToHost, st));
+    FX_TRY(hipStreamSynchronize(st));
+    return 0;
+  }
+
+  static int grid_for(int64_t n) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(kFlatWG, (n + 255) / 256));
+  }
+
+  // Send `n` configurations at `src` (device) to every rank as a group, or
+  // count-first all-to-all of the per-owner candidate regions.
+  int gather_all(int64_t nF, int64_t *nOut) {
+    std::vector<int64_t> sc(P, nF), rc(P, 0);
+    if (int e = ensure_buf(&sendb, &send_cap, (size_t)std::max<int64_t>(nF * P, 1))) return e;
+    for (int j = 0; j < P; j++)
+      if (nF)
+        FX_TRY(hipMemcpyAsync(sendb + (size_t)j * nF, F, nF * sizeof(Cfg), hipMemcpyDeviceToDevice, st));
+    FX_TRY(hipStreamSynchronize(st));
+    FX_COLL(tr.exchange_counts(tr.user, sc.data(), rc.data()));
+    int64_t tot = 0;
+    for (int j = 0; j < P; j++) tot += rc[j];
+    if ((unsigned long long)tot > list_cap) {
+      err = "gathered frontier exceeds the list capacity";
+      return -ENOMEM;
+    }
+    FX_COLL(tr.alltoallv(tr.user, sendb, sc.data(), F, rc.data(), sizeof(Cfg)));
+    *nOut = tot;
+    stats.gathers++;
+    return 0;
+  }
+
+  // One partitioned level chunk: candidates of V[a, b) to their owners.
+  int part_chunk(int64_t a, int64_t b) {
+    FX_TRY(hipMemsetAsync(dCtr->cand, 0, sizeof(unsigned long long) * P, st));
+    if (b > a) {
+      const int g = (int)std::max<int64_t>(1, std::min<int64_t>(kExpandWG, (b - a + 3) / 4));
+      fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tabs(), epoch, dCtr, a, b, cand, cand_cap);
+      FX_TRY(hipGetLastError());
+    }
+    if (int e = sync_ctr()) return e;
+    std::vector<int64_t> sc(P), rc(P);
+    int64_t tot_send = 0;
+    for (int j = 0; j < P; j++) {
+      const unsigned long long c = std::min<unsigned long long>(hCtr->cand[j], cand_cap);
+      sc[j] = j == rank ? 0 : (int64_t)c;
+      tot_send += sc[j];
+    }
+    // own candidates are inserted directly
+    const int64_t self = (int64_t)std::min<unsigned long long>(hCtr->cand[rank], cand_cap);
+    if (self) {
+      fx_insert_kernel<<<grid_for(self), 256, 0, st>>>(cand + (size_t)rank * cand_cap, self, dWin,
+                                                      tabs(), epoch, dCtr);
+      FX_TRY(hipGetLastError());
+    }
+    if (int e = ensure_buf(&sendb, &send_cap, (size_t)std::max<int64_t>(tot_send, 1))) return e;
+    int64_t off = 0;
+    for (int j = 0; j < P; j++) {
+      if (sc[j])
+        FX_TRY(hipMemcpyAsync(sendb + off, cand + (size_t)j * cand_cap, sc[j] * sizeof(Cfg),
+                              hipMemcpyDeviceToDevice, st));
+      off += sc[j];
+    }
+    FX_TRY(hipStreamSynchronize(st));
+    FX_COLL(tr.exchange_counts(tr.user, sc.data(), rc.data()));
+    int64_t tot = 0;
+    for (int j = 0; j < P; j++) tot += rc[j];
+    if (int e = ensure_buf(&recvb, &recv_cap, (size_t)std::max<int64_t>(tot, 1))) return e;
+    FX_COLL(tr.alltoallv(tr.user, sendb, sc.data(), recvb, rc.data(), sizeof(Cfg)));
+    stats.sent_configs += tot_send;
+    if (tot) {
+      fx_insert_kernel<<<grid_for(tot), 256, 0, st>>>(recvb, tot, dWin, tabs(), epoch, dCtr);
+      FX_TRY(hipGetLastError());
+    }
+    return 0;
+  }
+
+  int check(const lc_op *o, int64_t n, const lc_opts *opts, lc_key_result *res);
+};
+
+bool same_class(const lc_op &a, const lc_op &b) {
+  return a.f == b.f && a.value == b.value && a.expected == b.expected && a.version == b.version;
+}
+
+struct Ev {
+  int64_t idx;
+  int32_t is_ret;
+  int32_t op;
+};
+
+void result_init(lc_key_result *r) {
+  r->verdict = LC_VALID;
+  r->reason = LC_REASON_NONE;
+  r->fail_op = -1;
+  r->fail_prefix_end = -1;
+  r->configs_explored = 0;
+  r->max_frontier = 0;
+}
+
+void result_unknown(lc_key_result *r, int reason) {
+  r->verdict = LC_UNKNOWN;
+  r->reason = reason;
+  r->fail_op = -1;
+  r->fail_prefix_end = -1;
+}
+
+int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result *res) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::memset(&stats, 0, sizeof(stats));
+  lc_opts opts;
+  if (opts_in) {
+    opts = *opts_in;
+  } else {
+    opts.init_version = 0;
+    opts.init_value = LC_NIL;
+    opts.max_configs_per_key = 0;
+    opts.time_budget_ms = 0;
+    opts.flags = 0;
+  }
+  if (opts.init_version < 0 || opts.init_version > kFieldMax || opts.init_value < -1 ||
+      opts.init_value > kFieldMax) {
+    err = "lc_opts: init_version/init_value out of int32 range";
+    return -EINVAL;
+  }
+  result_init(res);
+  if (n == 0) return 0;
+  // Per-key validity (lc_check's rules): malformed -> :unknown reason 4,
+  // an unknown :f -> reason 5 (register.clj:63 throws).
+  for (int64_t i = 0; i < n; i++) {
+    const lc_op &a = o[i];
+    if (a.call < 0 || a.ret <= a.call || (i > 0 && a.call <= o[i - 1].call) || a.value < -1 ||
+        a.value > kFieldMax || a.expected < -1 || a.expected > kFieldMax) {
+      result_unknown(res, LC_REASON_MALFORMED);
+      return 0;
+    }
+  }
+  for (int64_t i = 0; i < n; i++)
+    if (o[i].f != LC_F_READ && o[i].f != LC_F_WRITE && o[i].f != LC_F_CAS) {
+      result_unknown(res, LC_REASON_UNKNOWN_F);
+      return 0;
+    }
+  const int64_t budget = opts.max_configs_per_key > 0 ? opts.max_configs_per_key : (int64_t)1 << 24;
+  if (int e = reserve(budget)) return e;
+
+  std::vector<Ev> ev;
+  ev.reserve((size_t)(2 * n));
+  for (int64_t i = 0; i < n; i++) {
+    ev.push_back({o[i].call, 0, (int32_t)i});
+    if (o[i].ret != LC_INF) ev.push_back({o[i].ret, 1, (int32_t)i});
+  }
+  std::sort(ev.begin(), ev.end(), [](const Ev &a, const Ev &b) {
+    if (a.idx != b.idx) return a.idx < b.idx;
+    if (a.is_ret != b.is_ret) return a.is_ret < b.is_ret;
+    return a.op < b.op;
+  });
+
+  std::vector<int32_t> slot_of((size_t)n, -1);
+  int32_t slot_op[kW];
+  uint64_t before[kW] = {0};
+  uint64_t occ = 0, reads = 0, kzob = 0;
+  Win &w = *hWin;
+  std::memset(&w, 0, sizeof(Win));
+  w.rank = rank;
+  w.n_ranks = P;
+
+  // F = {(init state, nothing linearized)}
+  Cfg init{0, (uint32_t)opts.init_version, (uint32_t)(int32_t)opts.init_value};
+  FX_TRY(hipMemcpyAsync(F, &init, sizeof(Cfg), hipMemcpyHostToDevice, st));
+  FX_TRY(hipMemsetAsync(dCtr, 0, sizeof(Ctr), st));
+  FX_TRY(hipStreamSynchronize(st));
+  int64_t nF = 1, nFglobal = 1;
+  bool part = false;
+  int64_t max_frontier = 1;
+  int64_t explored_repl = 0, explored_part = 0;
+  unsigned long long explored_seen = 0;
+  int spec_levels = 4;
+  const bool timed = opts.time_budget_ms > 0;
+  bool decided = false;
+  const bool debug = getenv("LC_FX_DEBUG") != nullptr;
+
+  auto slot_pre = [&](const lc_op &a, Slot &s) {
+    const int32_t ver = clamp_ver(a.version);
+    const int32_t vchk = ver != -1 ? -1 : 0;
+    if (a.f == LC_F_READ) {
+      s.nv = ver;
+      s.nvm = vchk;
+      s.nl = (int32_t)a.value;
+      s.nlm = a.value != LC_NIL ? -1 : 0;
+      s.value = 0;
+    } else {
+      s.nv = ver - 1;
+      s.nvm = vchk;
+      s.nl = (int32_t)a.expected;
+      s.nlm = a.f == LC_F_CAS ? -1 : 0;
+      s.value = (int32_t)a.value;
+    }
+  };
+
+  for (size_t e = 0; e < ev.size() && !decided; e++) {
+    const int32_t x = ev[e].op;
+    const lc_op &ox = o[x];
+    if (!ev[e].is_ret) {
+      // trivial reads (crashed, or [nil nil]) never constrain: no slot
+      if (ox.f == LC_F_READ && (ox.ret == LC_INF || (ox.version == LC_NIL && ox.value == LC_NIL)))
+        continue;
+      if (occ == ~0ULL) {
+        result_unknown(res, LC_REASON_WINDOW_OVERFLOW);
+        decided = true;
+        break;
+      }
+      const int s = __builtin_ctzll(~occ);
+      const uint64_t sb = 1ULL << s;
+      occ |= sb;
+      slot_of[x] = s;
+      slot_op[s] = x;
+      before[s] = 0;
+      Slot &sl = w.s[s];
+      std::memset(&sl, 0, sizeof(Slot));
+      slot_pre(ox, sl);
+      if (ox.f == LC_F_READ) {
+        reads |= sb;
+        sl.zob = 0;
+        // closure: the new read is linearized wherever it is legal now
+        if (nF) {
+          fx_close_read_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, sb, sl);
+          FX_TRY(hipGetLastError());
+        }
+      } else {
+        reads &= ~sb;
+        sl.zob = splitmix(0xF0F0ULL + (uint64_t)x) | 1;
+        for (int u = 0; u < kW; u++) {
+          if (u == s || !((occ >> u) & 1) || ((reads >> u) & 1)) continue;
+          if (!same_class(o[slot_op[u]], ox)) continue;
+          if (o[slot_op[u]].ret <= ox.ret) before[s] |= 1ULL << u;
+          else before[u] |= sb;
+        }
+      }
+      continue;
+    }
+    if (slot_of[x] < 0) continue;  // trivial read, or retired
+    const int sx = slot_of[x];
+    const uint64_t xb = 1ULL << sx;
+    // the window as the device sees it during this return
+    w.occ = occ;
+    w.reads = reads;
+    w.xbit = xb;
+    w.kzob = kzob;
+    for (int u = 0; u < kW; u++) w.s[u].before = before[u];
+    FX_TRY(hipMemcpyAsync(dWin, &w, sizeof(Win), hipMemcpyHostToDevice, st));
+    // mode switches (several ranks only)
+    if (P > 1 && !part && nFglobal > part_above) {
+      FX_TRY(hipMemsetAsync(&dCtr->nsel, 0, sizeof(unsigned long long), st));
+      fx_filter_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, dWin, tmp, list_cap, dCtr);
+      FX_TRY(hipGetLastError());
+      if (int er = sync_ctr()) return er;
+      std::swap(F, tmp);
+      nF = (int64_t)hCtr->nsel;
+      part = true;
+    } else if (P > 1 && part && nFglobal < repl_below) {
+      int64_t tot = 0;
+      if (int er = gather_all(nF, &tot)) return er;
+      nF = tot;
+      part = false;
+    }
+    epoch++;
+    stats.returns++;
+    fx_reset_kernel<<<1, 1, 0, st>>>(dCtr);
+    if (nF) {
+      fx_insert_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, dWin, tabs(), epoch, dCtr);
+      FX_TRY(hipGetLastError());
+    }
+    int64_t nRg = 0;   // global size of R after this return
+    bool over = false, timeout = false;
+    if (!part) {
+      // replicated: speculative batches of levels, one sync per batch
+      for (;;) {
+        for (int l = 0; l < spec_levels; l++) {
+          fx_mark_kernel<<<1, 1, 0, st>>>(dCtr);
+          fx_expand_kernel<<<kExpandWG, 256, 0, st>>>(dWin, tabs(), epoch, dCtr, -1, -1, nullptr, 0);
+        }
+        fx_and_kernel<<<kFlatWG, 256, 0, st>>>(Rl, &dCtr->nR, dCtr);
+        FX_TRY(hipGetLastError());
+        if (int er = sync_ctr()) return er;
+        if (hCtr->overflow || (int64_t)(hCtr->nR + hCtr->nV) > budget) {
+          over = true;
+          break;
+        }
+        if (hCtr->hi == hCtr->nV) break;  // the last level found nothing new
+        FX_TRY(hipMemsetAsync(&dCtr->andmask, 0xFF, sizeof(unsigned long long), st));
+        spec_levels = std::min(spec_levels * 2, 64);
+      }
+      const unsigned long long ex = hCtr->explored;
+      explored_repl += (int64_t)(ex - explored_seen);
+      explored_seen = ex;
+      nRg = (int64_t)hCtr->nR;
+      if (timed) timeout = std::chrono::duration<double, std::milli>(
+                               std::chrono::steady_clock::now() - t0).count() > (double)opts.time_budget_ms;
+      if (P > 1 && timed) {
+        int64_t v[1] = {timeout ? 1 : 0};
+        FX_COLL(tr.allreduce(tr.user, v, 1, LC_FX_SUM));
+        timeout = v[0] > 0;
+      }
+    } else {
+      // partitioned: every level is chunks of (expand, exchange, insert)
+      stats.part_returns++;
+      if (int er = sync_ctr()) return er;
+      int64_t lvl_lo = 0, lvl_hi = (int64_t)hCtr->nV, pos = 0;
+      const int64_t chunk = (int64_t)(cand_cap / kW);
+      for (;;) {
+        const int64_t a = pos, b = std::min(lvl_hi, pos + chunk);
+        pos = b;
+        if (int er = part_chunk(a, b)) return er;
+        if (int er = sync_ctr()) return er;
+        if (timed) timeout = std::chrono::duration<double, std::milli>(
+                                 std::chrono::steady_clock::now() - t0).count() > (double)opts.time_budget_ms;
+        int64_t v[5] = {pos < lvl_hi ? 1 : 0, (int64_t)hCtr->nV - lvl_hi,
+                        (int64_t)(hCtr->nR + hCtr->nV), (int64_t)hCtr->overflow ? 1 : 0,
+                        timeout ? 1 : 0};
+        FX_COLL(tr.allreduce(tr.user, v, 5, LC_FX_SUM));
+        if (v[3] || v[2] > budget) {
+          over = true;
+          break;
+        }
+        if (v[4]) {
+          timeout = true;
+          break;
+        }
+        if (v[0]) continue;  // some rank has more of this level
+        stats.part_levels++;
+        if (v[1] == 0) break;  // no rank found anything new
+        lvl_lo = lvl_hi;
+        lvl_hi = (int64_t)hCtr->nV;
+        pos = lvl_lo;
+      }
+      (void)lvl_lo;
+      if (!over && !timeout) {
+        fx_and_kernel<<<kFlatWG, 256, 0, st>>>(Rl, &dCtr->nR, dCtr);
+        FX_TRY(hipGetLastError());
+      }
+      if (int er = sync_ctr()) return er;
+      explored_part += (int64_t)(hCtr->explored - explored_seen);
+      explored_seen = hCtr->explored;
+      // global |R| and the global AND (bit b set everywhere <=> no rank lacks it)
+      int64_t v[1 + kW];
+      v[0] = (int64_t)hCtr->nR;
+      for (int b = 0; b < kW; b++) v[1 + b] = ((hCtr->andmask >> b) & 1) ? 0 : 1;
+      FX_COLL(tr.allreduce(tr.user, v, 1 + kW, LC_FX_SUM));
+      nRg = v[0];
+      unsigned long long gand = 0;
+      for (int b = 0; b < kW; b++)
+        if (!v[1 + b]) gand |= 1ULL << b;
+      hCtr->andmask = gand;
+    }
+    if (over) {
+      result_unknown(res, LC_REASON_CONFIG_BUDGET);
+      decided = true;
+      break;
+    }
+    if (timeout) {
+      result_unknown(res, LC_REASON_TIME_BUDGET);
+      decided = true;
+      break;
+    }
+    // F := R
+    std::swap(F, Rl);
+    nF = (int64_t)hCtr->nR;
+    nFglobal = nRg;
+    stats.max_local_frontier = std::max<int64_t>(stats.max_local_frontier, nF);
+    occ &= ~xb;
+    reads &= ~xb;
+    kzob ^= w.s[sx].zob;
+    for (int u = 0; u < kW; u++) before[u] &= ~xb;
+    max_frontier = std::max(max_frontier, nFglobal);
+    if (nFglobal == 0) {
+      res->verdict = LC_INVALID;
+      res->reason = LC_REASON_NONLINEARIZABLE;
+      res->fail_op = x;
+      res->fail_prefix_end = ox.ret;
+      decided = true;
+      break;
+    }
+    // retirement: ops linearized in every configuration free their slots
+    const uint64_t all = occ & hCtr->andmask;
+    if (debug)
+      fprintf(stderr, "fx r%d ret x=%d slot=%d part=%d nF=%lld nFg=%lld nV=%llu expl=%llu and=%llx occ=%llx\n",
+              rank, x, sx, (int)part, (long long)nF, (long long)nFglobal, hCtr->nV, hCtr->explored,
+              hCtr->andmask, (unsigned long long)occ);
+    if (all) {
+      if (nF) {
+        fx_clear_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, all);
+        FX_TRY(hipGetLastError());
+      }
+      for (int u = 0; u < kW; u++) {
+        if (!((all >> u) & 1)) continue;
+        slot_of[slot_op[u]] = -1;  // its return (if any) is now a no-op
+        kzob ^= w.s[u].zob;
+      }
+      occ &= ~all;
+      reads &= ~all;
+      for (int u = 0; u < kW; u++) before[u] &= ~all;
+    }
+  }
+  // every rank reports the same totals
+  int64_t tot_part = explored_part;
+  if (P > 1) {
+    int64_t v[1] = {explored_part};
+    FX_COLL(tr.allreduce(tr.user, v, 1, LC_FX_SUM));
+    tot_part = v[0];
+  }
+  res->configs_explored = 1 + explored_repl + tot_part;
+  res->max_frontier = max_frontier;
+  FX_TRY(hipStreamSynchronize(st));
+  stats.levels = (int64_t)hCtr->levels + stats.part_levels;
+  stats.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return 0;
+}
+
+}  // namespace
+
+struct lc_fx {
+  lc_fx_params params{};
+  bool virt = false;
+  std::vector<Rank *> ranks;    // virtual: P of them; real: one
+  std::unique_ptr<Hub> hub;
+  std::vector<HubRank> hub_ranks;
+  std::string err;
+  lc_fx_stats stats{};
+};
+
+extern "C" {
+
+int lc_fx_open(const lc_fx_params *params, const lc_fx_transport *transport, lc_fx **out) {
+  if (!params || !out) return -EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -ENODEV;
+  if (params->device < 0 || params->device >= ndev) return -ENODEV;
+  lc_fx *fx = new lc_fx();
+  fx->params = *params;
+  int P = 1;
+  if (transport) {
+    if (transport->n_ranks < 1 || transport->n_ranks > 64 || transport->rank < 0 ||
+        transport->rank >= transport->n_ranks || !transport->exchange_counts ||
+        !transport->alltoallv || !transport->allreduce) {
+      delete fx;
+      return -EINVAL;
+    }
+    P = transport->n_ranks;
+  } else {
+    P = std::max(1, params->virtual_ranks);
+    if (P > 64) {
+      delete fx;
+      return -EINVAL;
+    }
+    fx->virt = true;
+    fx->hub.reset(new Hub(P));
+    fx->hub_ranks.resize(P);
+  }
+  const int nr = transport ? 1 : P;
+  for (int i = 0; i < nr; i++) {
+    Rank *r = new Rank();
+    r->dev = params->device;
+    r->P = P;
+    if (transport) {
+      r->tr = *transport;
+      r->rank = transport->rank;
+    } else {
+      r->rank = i;
+      fx->hub_ranks[i] = HubRank{fx->hub.get(), i};
+      r->tr.user = &fx->hub_ranks[i];
+      r->tr.rank = i;
+      r->tr.n_ranks = P;
+      r->tr.exchange_counts = hub_exchange_counts;
+      r->tr.alltoallv = hub_alltoallv;
+      r->tr.allreduce = hub_allreduce;
+    }
+    if (params->part_above >= 0) r->part_above = params->part_above;
+    r->repl_below = params->repl_below >= 0 ? params->repl_below : r->part_above / 4;
+    r->table_log2 = (int)params->table_log2;
+    fx->ranks.push_back(r);
+    if (int e = r->open()) {
+      fx->err = r->err;
+      lc_fx_close(fx);
+      return e;
+    }
+  }
+  *out = fx;
+  return 0;
+}
+
+int lc_fx_check(lc_fx *fx, const lc_op *ops, int64_t n, const lc_opts *opts, lc_key_result *out) {
+  if (!fx || !out || n < 0 || (n > 0 && !ops)) return -EINVAL;
+  if (!fx->virt) {
+    Rank *r = fx->ranks[0];
+    (void)hipSetDevice(r->dev);
+    const int e = r->check(ops, n, opts, out);
+    fx->stats = r->stats;
+    if (e) fx->err = r->err;
+    return e;
+  }
+  const int P = (int)fx->ranks.size();
+  fx->hub.reset(new Hub(P));
+  for (int i = 0; i < P; i++) fx->hub_ranks[i].hub = fx->hub.get();
+  std::vector<lc_key_result> res(P);
+  std::vector<int> rc(P, 0);
+  std::vector<std::thread> th;
+  for (int i = 0; i < P; i++)
+    th.emplace_back([&, i] {
+      (void)hipSetDevice(fx->ranks[i]->dev);
+      rc[i] = fx->ranks[i]->check(ops, n, opts, &res[i]);
+      if (rc[i]) fx->hub->abort();
+    });
+  for (auto &t : th) t.join();
+  for (int i = 0; i < P; i++)
+    if (rc[i] && rc[i] != -ECANCELED) {
+      fx->err = fx->ranks[i]->err;
+      return rc[i];
+    }
+  for (int i = 0; i < P; i++)
+    if (rc[i]) {
+      fx->err = fx->ranks[i]->err;
+      return rc[i];
+    }
+  for (int i = 1; i < P; i++)
+    if (std::memcmp(&res[i], &res[0], sizeof(lc_key_result)) != 0) {
+      fx->err = "ranks disagree on the result";
+      return -EPROTO;
+    }
+  *out = res[0];
+  fx->stats = fx->ranks[0]->stats;
+  return 0;
+}
+
+int lc_fx_last_stats(lc_fx *fx, lc_fx_stats *out) {
+  if (!fx || !out) return -EINVAL;
+  *out = fx->stats;
+  return 0;
+}
+
+const char *lc_fx_last_error(lc_fx *fx) { return fx ? fx->err.c_str() : "null lc_fx"; }
+
+void lc_fx_close(lc_fx *fx) {
+  if (!fx) return;
+  for (Rank *r : fx->ranks) {
+    (void)hipSetDevice(r->dev);
+    delete r;
+  }
+  delete fx;
+}
+
+}  // extern "C"

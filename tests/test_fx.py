@@ -1,0 +1,184 @@
+"""Frontier exchange (include/lincheck_fx.h): one key's JIT search over the
+whole GPU, partitioned over ranks by hash ownership.
+
+The oracle's JITC mode (oracle.c check_key_jit with the GPU's exact
+reductions) runs the same search serially, so every field of every decided
+key must match it exactly: verdict, canonical fail op, configurations
+explored and largest frontier.  Forcing the partitioned mode
+(part_above=0) on small keys runs every level through the all-to-all-v
+exchange; a middle threshold switches between the replicated and the
+partitioned frontier back and forth.  The multi-process test drives the
+engine through torch.distributed (gloo, two ranks sharing the card) — the
+transport an 8-GPU node uses under RCCL."""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+
+import oracle
+from helpers import FREE, pack_keys, random_casreg, random_mutex, random_tiny
+from jepsen.etcd_amd import abi
+
+FIELDS = ("verdict", "reason", "fail_op", "fail_prefix_end", "configs_explored", "max_frontier")
+
+
+def _keys(seed, n_each=60):
+    """(records, init_value) per key: cas-register, mutex and register keys,
+    tiny to mid-sized, crashes and anomalies included."""
+    rng = random.Random(seed)
+    keys = []
+    for _ in range(n_each):
+        keys.append((random_casreg(rng, rng.randrange(1, 60), p_info=0.1), -1))
+        keys.append((random_mutex(rng, rng.randrange(1, 60), p_info=0.1), FREE))
+        keys.append((random_tiny(rng, rng.randrange(1, 30)), -1))
+    # synthetic version-less keys with real frontiers (concurrency 8-12)
+    for i, conc in enumerate((8, 10, 12)):
+        ops, off, _, _ = abi.synth(4, 300, concurrency=conc, p_info=0.01, p_anomaly=0.5,
+                                   seed=seed * 7 + i)
+        ops = ops.copy()
+        ops[:, 3] = -1
+        for k in range(4):
+            keys.append((ops[off[k]:off[k + 1]].tolist(), -1))
+    return keys
+
+
+def _oracle(recs, init_value):
+    ops, off = pack_keys([recs])
+    _, r = oracle.check(ops, off, algo=oracle.JITC, init_value=init_value)
+    return r[0]
+
+
+def _compare(got, want, tag):
+    if want["reason"] == abi.LC_REASON_CONFIG_BUDGET:
+        return  # the oracle's own budget; not a parity case
+    for f in FIELDS:
+        assert int(got[f]) == int(want[f]), (tag, f, int(got[f]), int(want[f]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,part_above", [(1, -1), (3, 0), (2, 6), (4, 0)])
+def test_fx_matches_oracle_jitc(ranks, part_above):
+    from jepsen.etcd_amd.fx import FrontierExchange
+    keys = _keys(0xF00 + ranks * 10 + max(part_above, 0))
+    n_window = 0
+    with FrontierExchange(device=0, virtual_ranks=ranks, part_above=part_above,
+                          table_log2=18) as fx:
+        for i, (recs, init) in enumerate(keys):
+            want = _oracle(recs, init)
+            got = fx.check(np.array(recs, dtype=np.int64).reshape(-1, 6),
+                           abi.default_opts(init_value=init))
+            if got["reason"] == abi.LC_REASON_WINDOW_OVERFLOW:
+                n_window += 1  # > 64 open ops: the oracle's window is unbounded
+                continue
+            _compare(got, want, (ranks, part_above, i))
+        st = fx.stats()
+    assert n_window <= len(keys) // 20
+    if ranks > 1 and part_above == 0:
+        assert st["part_returns"] > 0
+
+
+@pytest.mark.gpu
+def test_fx_partition_switches_and_exchanges():
+    """A key whose frontier crosses the thresholds both ways: replicated ->
+    partitioned (filter by owner) -> replicated (gather), same result as one
+    rank, with configurations actually sent between ranks."""
+    from jepsen.etcd_amd.fx import FrontierExchange
+    ops, off, _, _ = abi.synth(1, 600, concurrency=14, p_info=0.005, seed=0xFACE)
+    ops = ops.copy()
+    ops[:, 3] = -1
+    with FrontierExchange(device=0, virtual_ranks=1) as fx:
+        one = fx.check(ops)
+    want = _oracle(ops.tolist(), -1)
+    _compare(one, want, "one rank")
+    assert one["max_frontier"] > 40
+    with FrontierExchange(device=0, virtual_ranks=3, part_above=30, repl_below=10,
+                          table_log2=18) as fx:
+        got = fx.check(ops)
+        st = fx.stats()
+    _compare(got, want, "three ranks")
+    assert st["part_returns"] > 0 and st["gathers"] > 0 and st["sent_configs"] > 0
+
+
+@pytest.mark.gpu
+def test_fx_budget_window_and_errors():
+    from jepsen.etcd_amd.fx import FrontierExchange
+    ops, off, _, _ = abi.synth(1, 400, concurrency=16, p_info=0.02, seed=0xB0B)
+    ops = ops.copy()
+    ops[:, 3] = -1
+    with FrontierExchange(device=0, virtual_ranks=2, part_above=0, table_log2=16) as fx:
+        r = fx.check(ops, abi.default_opts(max_configs_per_key=50))
+        assert r["verdict"] == -1 and r["reason"] == abi.LC_REASON_CONFIG_BUDGET
+        # 70 writes open at once: more than LC_MAX_WINDOW slots
+        recs = [[1, i % 3, -1, -1, i, 1000 + i] for i in range(70)]
+        r = fx.check(np.array(recs, dtype=np.int64))
+        assert r["verdict"] == -1 and r["reason"] == abi.LC_REASON_WINDOW_OVERFLOW
+        bad = np.array([[1, 0, -1, -1, 5, 3]], dtype=np.int64)  # ret < call
+        assert fx.check(bad)["reason"] == abi.LC_REASON_MALFORMED
+        unk = np.array([[7, 0, -1, -1, 0, 1]], dtype=np.int64)
+        assert fx.check(unk)["reason"] == abi.LC_REASON_UNKNOWN_F
+        empty = fx.check(np.zeros((0, 6), dtype=np.int64))
+        assert empty["verdict"] == 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, keys, q):
+    import torch.distributed as dist
+    from jepsen.etcd_amd.fx import FrontierExchange
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                            world_size=world)
+    try:
+        out = []
+        fx = FrontierExchange(device=0, group=dist.group.WORLD, part_above=4, repl_below=2)
+        for recs in keys:
+            r = fx.check(np.array(recs, dtype=np.int64).reshape(-1, 6))
+            out.append([int(r[f]) for f in FIELDS])
+        st = fx.stats()
+        fx.close()
+        q.put((rank, out, st))
+    except Exception as e:  # reported by the parent
+        q.put((rank, repr(e), None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_fx_two_processes_over_torch_distributed():
+    """Two ranks (processes) on one card, collectives over gloo through
+    TorchTransport: equal results on both ranks, equal to the oracle."""
+    import torch.multiprocessing as mp
+    rng = random.Random(0xD15)
+    keys = [random_casreg(rng, rng.randrange(5, 50), p_info=0.1) for _ in range(12)]
+    ops, off, _, _ = abi.synth(2, 250, concurrency=10, p_info=0.01, p_anomaly=0.5, seed=0xD16)
+    ops = ops.copy()
+    ops[:, 3] = -1
+    keys += [ops[off[k]:off[k + 1]].tolist() for k in range(2)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, keys, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        rank, out, st = q.get(timeout=240)
+        assert st is not None, out
+        res[rank] = (out, st)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] == res[1][0]
+    assert res[0][1]["part_returns"] > 0 and res[0][1]["sent_configs"] + res[1][1]["sent_configs"] > 0
+    for recs, got in zip(keys, res[0][0]):
+        want = _oracle(recs, -1)
+        if got[1] == abi.LC_REASON_WINDOW_OVERFLOW:
+            continue
+        _compare(dict(zip(FIELDS, got)), want, "two processes")

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(abi.LIB_PATH)
     names = []
-    for h in ("lincheck.h", "lincheck_synth.h", "lincheck_edn.h"):
+    for h in ("lincheck.h", "lincheck_synth.h", "lincheck_edn.h", "lincheck_fx.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         names += re.findall(r"^\s*(?:const\s+)?\w+\s+\**(lc_\w+)\s*\(", src, re.M)
     assert set(names) == {
@@ -27,7 +27,8 @@ def test_library_exports_every_declared_symbol():
         "lc_check_ex", "lc_check_device_ex", "lc_key_cost", "lc_build_id",
         "lc_synth_register", "lc_synth_key", "lc_edn_parse", "lc_edn_n_keys", "lc_edn_n_ops",
         "lc_edn_n_events", "lc_edn_ops", "lc_edn_key_off", "lc_edn_key", "lc_edn_op_text",
-        "lc_edn_value", "lc_edn_free"}
+        "lc_edn_value", "lc_edn_free", "lc_fx_open", "lc_fx_check", "lc_fx_last_stats",
+        "lc_fx_last_error", "lc_fx_close"}
     for n in names:
         assert hasattr(lib, n), n
     assert abi.lib().lc_abi_version() == 2
@@ -39,6 +40,10 @@ def test_struct_sizes():
     assert ctypes.sizeof(abi.LcSynthParams) == 56
     assert ctypes.sizeof(abi.LcStats) == 104
     assert ctypes.sizeof(abi.LcAux) == 16
+    from jepsen.etcd_amd import fx
+    assert ctypes.sizeof(fx.LcFxParams) == 32
+    assert ctypes.sizeof(fx.LcFxTransport) == 40
+    assert ctypes.sizeof(fx.LcFxStats) == 64
 
 
 def test_library_built_from_this_tree():
@@ -55,6 +60,9 @@ def test_open_without_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(abi.LcError):
         abi.Context(0)
+    from jepsen.etcd_amd import fx
+    with pytest.raises(abi.LcError):
+        fx.FrontierExchange(device=0)
 
 
 def test_synth_deterministic_and_exact():
