@@ -87,6 +87,8 @@ typedef struct lc_fx_stats {
   int64_t sent_configs;     /* configurations this rank sent to other ranks */
   int64_t gathers;          /* partitioned -> replicated switches */
   int64_t max_local_frontier; /* largest frontier share held by this rank */
+  int64_t redos;            /* returns redone with a larger dedup table */
+  int64_t wide_returns;     /* returns on 16-byte-key tables (a slot >= 58 open, or > 63 values) */
 } lc_fx_stats;
 
 typedef struct lc_fx lc_fx;

@@ -36,6 +36,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../../include/lincheck_fx.h"
@@ -46,8 +47,13 @@ constexpr int kW = 64;
 constexpr int32_t kFieldMax = 0x7FFFFFFE;
 constexpr int kMaxProbe = 1 << 12;     // table probes per insert before giving up (overflow)
 constexpr int kMaxSpin = 1 << 22;      // loop iterations per insert, busy waits included
-constexpr int kExpandWG = 1024;        // expand grid: 4 waves per workgroup
+constexpr int kExpandWG = 2048;        // expand grid (most): 4 waves per workgroup
 constexpr int kFlatWG = 1024;          // thread-per-configuration kernels
+// replicated returns run whole in one workgroup while the frontier, the last
+// return's work and every level stay this small
+constexpr int64_t kSmallF = 256;
+constexpr int64_t kSmallWork = 2048;
+constexpr unsigned long long kSmallLevel = 1024;
 
 struct Cfg {
   uint64_t mask;
@@ -80,9 +86,10 @@ struct Ctr {
   unsigned long long explored;  // successors generated (cumulative)
   unsigned long long levels;    // non-empty levels (cumulative)
   unsigned long long andmask;   // AND of R's masks
-  unsigned long long overflow;  // a list or table ran out of room
+  unsigned long long overflow;  // a list ran out of room (the budget)
   unsigned long long nsel;      // filter output
-  unsigned long long pad[7];
+  unsigned long long tfull;     // a table probe ran too long: redo the return with a larger table
+  unsigned long long pad[6];
   unsigned long long cand[64];  // partitioned: candidates per owner rank
 };
 
@@ -166,7 +173,38 @@ struct Tabs {
   Cfg *listR, *listV;
   uint64_t tmask;
   unsigned long long list_cap;
+  int compact;  // one-word keys (ctab_insert) instead of tag + 16-B key
 };
+
+// Compact tables.  Within one return every configuration has linearized the
+// retired mutations plus those its mask names, so its version is
+// V0 + (retired mutations) + popcount(mask & mutation slots): a function of
+// the mask.  The state reduces to the value, which the host interns per key
+// to a dense id.  With every occupied slot below kCompactSlots and at most
+// 63 value ids, (mask, value id) packs into one 64-bit word, and a table
+// entry is that word: insertion is one device-scope atomicCAS per probe
+// (EMPTY -> word; the value returned says new, present, or occupied by
+// another word), with no key payload, tag or fence.  Tables are reset to
+// EMPTY (all ones: value id 63 is never used) before each return.
+constexpr int kCompactSlots = 58;
+constexpr unsigned long long kEmpty = ~0ULL;
+
+__device__ inline int ctab_insert(unsigned long long *tab, uint64_t tmask, const Cfg &c) {
+  const unsigned long long word = c.mask | ((unsigned long long)c.val << kCompactSlots);
+  uint64_t i = mix64(word) & tmask;
+  for (int probes = 0; probes < kMaxProbe; probes++) {
+    const unsigned long long old = atomicCAS(&tab[i], kEmpty, word);
+    if (old == kEmpty) return 1;
+    if (old == word) return 0;
+    i = (i + 1) & tmask;
+  }
+  return -1;
+}
+
+__device__ inline int any_insert(const Tabs &t, bool toR, uint32_t epoch, const Cfg &c) {
+  if (t.compact) return ctab_insert(toR ? t.tagR : t.tagV, t.tmask, c);
+  return tab_insert(toR ? t.tagR : t.tagV, toR ? t.keyR : t.keyV, t.tmask, epoch, c);
+}
 
 // Wave-aggregated append of the lanes in `take` (each with its own c).
 __device__ inline void wave_append(bool take, const Cfg &c, Cfg *list, unsigned long long *count,
@@ -192,8 +230,8 @@ __device__ inline void insert_rv(bool have, Cfg c, uint64_t xbit, const Tabs &t,
   bool toR = have && (c.mask & xbit);
   if (toR) c.mask &= ~xbit;
   int r = -1;
-  if (have) r = tab_insert(toR ? t.tagR : t.tagV, toR ? t.keyR : t.keyV, t.tmask, epoch, c);
-  if (have && r < 0) atomicOr(&ctr->overflow, 1ULL);
+  if (have) r = any_insert(t, toR, epoch, c);
+  if (have && r < 0) atomicOr(&ctr->tfull, 1ULL);
   wave_append(r == 1 && toR, c, t.listR, &ctr->nR, t.list_cap, &ctr->overflow);
   wave_append(r == 1 && !toR, c, t.listV, &ctr->nV, t.list_cap, &ctr->overflow);
 }
@@ -219,38 +257,45 @@ __global__ void fx_mark_kernel(Ctr *ctr) {
 }
 
 // One level of the expansion: every wave takes configurations of V[lo, hi)
-// (from ctr when range == nullptr) one at a time, lane t tests window slot t
-// (pending, not a read, its deadline-order predecessors linearized, legal),
-// builds the successor with its eager read closure, and either inserts it
-// (replicated mode) or appends it to its owner's candidate region
-// (partitioned mode: cand != nullptr).
-__global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ gwin, Tabs t,
-                                                        uint32_t epoch, Ctr *ctr, int64_t lo_arg,
-                                                        int64_t hi_arg, Cfg *cbuf,
-                                                        unsigned long long cand_cap) {
-  __shared__ Win w;
-  {
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(gwin);
-    uint32_t *dst = reinterpret_cast<uint32_t *>(&w);
-    for (int i = threadIdx.x; i < (int)(sizeof(Win) / 4); i += blockDim.x) dst[i] = src[i];
-  }
-  __syncthreads();
-  int64_t lo, hi;
-  if (lo_arg < 0) {
-    lo = (int64_t)ctr->lo;
-    hi = (int64_t)ctr->hi;
-  } else {
-    lo = lo_arg;
-    hi = hi_arg;
-  }
+// one at a time, lane t tests window slot t (pending, not a read, its
+// deadline-order predecessors linearized, legal), builds the successor with
+// its eager read closure, and either inserts it (replicated mode) or appends
+// it to its owner's candidate region (partitioned mode: cand_cap != 0).
+// Per-wave LDS staging of new list entries (replicated mode): one atomic per
+// flush of up to kStage entries instead of one per configuration expanded —
+// the list counters are the only same-address atomics of a level.
+constexpr int kStage = 192;
+struct Stage {
+  Cfg r[kStage];
+  Cfg v[kStage];
+};
+
+__device__ inline void stage_flush(Cfg *buf, int &n, Cfg *list, unsigned long long *count,
+                                   unsigned long long cap, unsigned long long *overflow) {
+  if (!n) return;
+  __builtin_amdgcn_wave_barrier();
   const int lane = __lane_id();
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(count, (unsigned long long)n);
+  base = __shfl(base, 0);
+  for (int j = lane; j < n; j += kW) {
+    if (base + j < cap) list[base + j] = buf[j];
+    else atomicOr(overflow, 1ULL);
+  }
+  __builtin_amdgcn_wave_barrier();
+  n = 0;
+}
+
+__device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch, Ctr *ctr,
+                                    int64_t lo, int64_t hi, int64_t wave, int64_t nwaves,
+                                    Cfg *cbuf, unsigned long long cand_cap, Stage *stg) {
+  const int lane = __lane_id();
+  int nr = 0, nv = 0;  // staged entries (wave-uniform)
   const Slot me = w.s[lane];
   const uint64_t bit = 1ULL << lane;
   const uint64_t muts = w.occ & ~w.reads;
   const uint64_t reads = w.occ & w.reads;
   const bool is_mut = (muts & bit) != 0;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kW;
-  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kW;
   unsigned long long explored = 0;
   for (int64_t i = lo + wave; i < hi; i += nwaves) {
     const Cfg c = t.listV[i];
@@ -269,7 +314,19 @@ __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ 
     }
     explored += __popcll(__ballot(cand));
     if (!cand_cap) {
-      insert_rv(cand, s, w.xbit, t, epoch, ctr);
+      const bool toR = cand && (s.mask & w.xbit);
+      if (toR) s.mask &= ~w.xbit;
+      int r = -1;
+      if (cand) r = any_insert(t, toR, epoch, s);
+      if (cand && r < 0) atomicOr(&ctr->tfull, 1ULL);
+      const uint64_t below = (1ULL << lane) - 1;
+      const uint64_t mR = __ballot(r == 1 && toR), mV = __ballot(r == 1 && !toR);
+      if (r == 1 && toR) stg->r[nr + __popcll(mR & below)] = s;
+      if (r == 1 && !toR) stg->v[nv + __popcll(mV & below)] = s;
+      nr += __popcll(mR);
+      nv += __popcll(mV);
+      if (nr > kStage - kW) stage_flush(stg->r, nr, t.listR, &ctr->nR, t.list_cap, &ctr->overflow);
+      if (nv > kStage - kW) stage_flush(stg->v, nv, t.listV, &ctr->nV, t.list_cap, &ctr->overflow);
     } else {
       // append to the owner's region; one atomic per distinct owner in the wave
       const uint32_t own = cand ? owner_of(s, w) : 0xFFFFFFFFu;
@@ -283,7 +340,98 @@ __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ 
       }
     }
   }
+  if (!cand_cap) {
+    stage_flush(stg->r, nr, t.listR, &ctr->nR, t.list_cap, &ctr->overflow);
+    stage_flush(stg->v, nv, t.listV, &ctr->nV, t.list_cap, &ctr->overflow);
+  }
   if (lane == 0 && explored) atomicAdd(&ctr->explored, explored);
+}
+
+__device__ inline void load_win(Win &w, const Win *gwin) {
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(gwin);
+  uint32_t *dst = reinterpret_cast<uint32_t *>(&w);
+  for (int i = threadIdx.x; i < (int)(sizeof(Win) / 4); i += blockDim.x) dst[i] = src[i];
+}
+
+// A level over the grid: V[ctr->lo, ctr->hi) (lo_arg < 0) or [lo_arg, hi_arg).
+// Workgroups past the level's end leave before staging the window, so the
+// speculative launches of the replicated mode cost little when empty.
+__global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ gwin, Tabs t,
+                                                        uint32_t epoch, Ctr *ctr, int64_t lo_arg,
+                                                        int64_t hi_arg, Cfg *cbuf,
+                                                        unsigned long long cand_cap) {
+  int64_t lo, hi;
+  if (lo_arg < 0) {
+    lo = (int64_t)ctr->lo;
+    hi = (int64_t)ctr->hi;
+  } else {
+    lo = lo_arg;
+    hi = hi_arg;
+  }
+  if (lo + (int64_t)blockIdx.x * (blockDim.x / kW) >= hi) return;
+  __shared__ Win w;
+  __shared__ Stage stg[4];
+  load_win(w, gwin);
+  __syncthreads();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kW;
+  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kW;
+  expand_range(w, t, epoch, ctr, lo, hi, wave, nwaves, cbuf, cand_cap, &stg[threadIdx.x / kW]);
+}
+
+__device__ inline unsigned long long wave_and(unsigned long long v);
+
+// A whole return in one workgroup while the frontier is small (replicated
+// mode): split F, then levels separated by barriers, then the AND for
+// retirement — one launch instead of a launch pair per level.  A level
+// larger than `cutoff` is left to the grid (ctr->lo/hi stay at the last
+// level expanded, the protocol fx_mark_kernel continues from).
+__global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restrict__ F, int64_t nF,
+                                                              const Win *__restrict__ gwin, Tabs t,
+                                                              uint32_t epoch, Ctr *ctr,
+                                                              unsigned long long cutoff) {
+  __shared__ Win w;
+  __shared__ Stage stg[4];
+  __shared__ long long s_lo, s_hi;
+  __shared__ int s_go;
+  load_win(w, gwin);
+  __syncthreads();
+  for (int64_t b = 0; b < nF; b += blockDim.x) {
+    const int64_t i = b + threadIdx.x;
+    const bool have = i < nF;
+    Cfg c{};
+    if (have) c = F[i];
+    insert_rv(have, c, w.xbit, t, epoch, ctr);
+  }
+  const int64_t wave = threadIdx.x / kW;
+  const int64_t nwaves = blockDim.x / kW;
+  for (;;) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long nV =
+          __hip_atomic_load(&ctr->nV, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long hi = ctr->hi;
+      int go = 0;
+      if (nV > hi && nV - hi <= cutoff) {
+        ctr->lo = hi;
+        ctr->hi = nV;
+        ctr->levels++;
+        go = 1;
+      }
+      s_lo = (long long)hi;
+      s_hi = (long long)nV;
+      s_go = go;
+    }
+    __syncthreads();
+    if (!s_go) break;
+    expand_range(w, t, epoch, ctr, s_lo, s_hi, wave, nwaves, nullptr, 0, &stg[threadIdx.x / kW]);
+  }
+  // retirement AND over R (meaningful when the return finished here)
+  const int64_t nR =
+      (int64_t)__hip_atomic_load(&ctr->nR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long a = ~0ULL;
+  for (int64_t i = threadIdx.x; i < nR; i += blockDim.x) a &= t.listR[i].mask;
+  a = wave_and(a);
+  if (__lane_id() == 0 && a != ~0ULL) atomicAnd(&ctr->andmask, a);
 }
 
 __device__ inline unsigned long long wave_and(unsigned long long v) {
@@ -327,11 +475,7 @@ __global__ __launch_bounds__(256) void fx_filter_kernel(const Cfg *__restrict__ 
                                                         const Win *__restrict__ gwin, Cfg *out,
                                                         unsigned long long cap, Ctr *ctr) {
   __shared__ Win w;
-  {
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(gwin);
-    uint32_t *dst = reinterpret_cast<uint32_t *>(&w);
-    for (int i = threadIdx.x; i < (int)(sizeof(Win) / 4); i += blockDim.x) dst[i] = src[i];
-  }
+  load_win(w, gwin);
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x; b < n; b += stride) {
@@ -346,10 +490,14 @@ __global__ __launch_bounds__(256) void fx_filter_kernel(const Cfg *__restrict__ 
   }
 }
 
-__global__ void fx_reset_kernel(Ctr *ctr) {
+// Start (or redo) a return: empty R and V, explored back to its value
+// before the return.
+__global__ void fx_reset_kernel(Ctr *ctr, unsigned long long explored) {
   ctr->nR = ctr->nV = ctr->lo = ctr->hi = 0;
   ctr->andmask = ~0ULL;
   ctr->nsel = 0;
+  ctr->tfull = 0;
+  ctr->explored = explored;
   for (int i = 0; i < 64; i++) ctr->cand[i] = 0;
 }
 
@@ -584,15 +732,16 @@ struct Rank {
     return 0;
   }
 
-  Tabs tabs() const {
+  Tabs tabs(int lg, int compact) const {
     Tabs t;
+    t.compact = compact;
     t.tagR = tagR;
     t.tagV = tagV;
     t.keyR = keyR;
     t.keyV = keyV;
     t.listR = Rl;
     t.listV = Vl;
-    t.tmask = tmask;
+    t.tmask = std::min<uint64_t>(tmask, (1ULL << lg) - 1);
     t.list_cap = list_cap;
     return t;
   }
@@ -630,11 +779,11 @@ struct Rank {
   }
 
   // One partitioned level chunk: candidates of V[a, b) to their owners.
-  int part_chunk(int64_t a, int64_t b) {
+  int part_chunk(int64_t a, int64_t b, const Tabs &tb) {
     FX_TRY(hipMemsetAsync(dCtr->cand, 0, sizeof(unsigned long long) * P, st));
     if (b > a) {
       const int g = (int)std::max<int64_t>(1, std::min<int64_t>(kExpandWG, (b - a + 3) / 4));
-      fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tabs(), epoch, dCtr, a, b, cand, cand_cap);
+      fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tb, epoch, dCtr, a, b, cand, cand_cap);
       FX_TRY(hipGetLastError());
     }
     if (int e = sync_ctr()) return e;
@@ -649,7 +798,7 @@ struct Rank {
     const int64_t self = (int64_t)std::min<unsigned long long>(hCtr->cand[rank], cand_cap);
     if (self) {
       fx_insert_kernel<<<grid_for(self), 256, 0, st>>>(cand + (size_t)rank * cand_cap, self, dWin,
-                                                      tabs(), epoch, dCtr);
+                                                      tb, epoch, dCtr);
       FX_TRY(hipGetLastError());
     }
     if (int e = ensure_buf(&sendb, &send_cap, (size_t)std::max<int64_t>(tot_send, 1))) return e;
@@ -668,7 +817,7 @@ struct Rank {
     FX_COLL(tr.alltoallv(tr.user, sendb, sc.data(), recvb, rc.data(), sizeof(Cfg)));
     stats.sent_configs += tot_send;
     if (tot) {
-      fx_insert_kernel<<<grid_for(tot), 256, 0, st>>>(recvb, tot, dWin, tabs(), epoch, dCtr);
+      fx_insert_kernel<<<grid_for(tot), 256, 0, st>>>(recvb, tot, dWin, tb, epoch, dCtr);
       FX_TRY(hipGetLastError());
     }
     return 0;
@@ -762,8 +911,27 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   w.rank = rank;
   w.n_ranks = P;
 
+  // Values are interned per key to dense ids (nil first): the model only
+  // compares them for equality (register.clj:77,92), and the compact tables
+  // pack the id beside the mask.
+  std::unordered_map<int64_t, int32_t> vids;
+  auto vid = [&](int64_t v) {
+    auto it = vids.find(v);
+    if (it != vids.end()) return it->second;
+    const int32_t k = (int32_t)vids.size();
+    vids.emplace(v, k);
+    return k;
+  };
+  vid(LC_NIL);
+  vid(opts.init_value);
+  for (int64_t i = 0; i < n; i++) {
+    if (o[i].f != LC_F_READ || o[i].value != LC_NIL) vid(o[i].value);
+    if (o[i].f == LC_F_CAS) vid(o[i].expected);
+  }
+  const int64_t n_vals = (int64_t)vids.size();
+
   // F = {(init state, nothing linearized)}
-  Cfg init{0, (uint32_t)opts.init_version, (uint32_t)(int32_t)opts.init_value};
+  Cfg init{0, (uint32_t)opts.init_version, (uint32_t)vid(opts.init_value)};
   FX_TRY(hipMemcpyAsync(F, &init, sizeof(Cfg), hipMemcpyHostToDevice, st));
   FX_TRY(hipMemsetAsync(dCtr, 0, sizeof(Ctr), st));
   FX_TRY(hipStreamSynchronize(st));
@@ -773,6 +941,10 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   int64_t explored_repl = 0, explored_part = 0;
   unsigned long long explored_seen = 0;
   int spec_levels = 4;
+  int64_t levels_seen = 0, last_work = 0;
+  bool tags_dirty = true;
+  const int tlog_full = __builtin_ctzll(tmask + 1);
+  int tlog = 12;
   const bool timed = opts.time_budget_ms > 0;
   bool decided = false;
   const bool debug = getenv("LC_FX_DEBUG") != nullptr;
@@ -783,15 +955,15 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     if (a.f == LC_F_READ) {
       s.nv = ver;
       s.nvm = vchk;
-      s.nl = (int32_t)a.value;
+      s.nl = a.value != LC_NIL ? vid(a.value) : 0;
       s.nlm = a.value != LC_NIL ? -1 : 0;
       s.value = 0;
     } else {
       s.nv = ver - 1;
       s.nvm = vchk;
-      s.nl = (int32_t)a.expected;
+      s.nl = a.f == LC_F_CAS ? vid(a.expected) : 0;
       s.nlm = a.f == LC_F_CAS ? -1 : 0;
-      s.value = (int32_t)a.value;
+      s.value = vid(a.value);
     }
   };
 
@@ -861,61 +1033,112 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       nF = tot;
       part = false;
     }
-    epoch++;
     stats.returns++;
-    fx_reset_kernel<<<1, 1, 0, st>>>(dCtr);
-    if (nF) {
-      fx_insert_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, dWin, tabs(), epoch, dCtr);
-      FX_TRY(hipGetLastError());
-    }
+    const int compact = (occ >> kCompactSlots) == 0 && n_vals <= 63;
+    if (!compact) stats.wide_returns++;
     int64_t nRg = 0;   // global size of R after this return
     bool over = false, timeout = false;
-    if (!part) {
-      // replicated: speculative batches of levels, one sync per batch
-      for (;;) {
-        for (int l = 0; l < spec_levels; l++) {
-          fx_mark_kernel<<<1, 1, 0, st>>>(dCtr);
-          fx_expand_kernel<<<kExpandWG, 256, 0, st>>>(dWin, tabs(), epoch, dCtr, -1, -1, nullptr, 0);
-        }
-        fx_and_kernel<<<kFlatWG, 256, 0, st>>>(Rl, &dCtr->nR, dCtr);
-        FX_TRY(hipGetLastError());
-        if (int er = sync_ctr()) return er;
-        if (hCtr->overflow || (int64_t)(hCtr->nR + hCtr->nV) > budget) {
-          over = true;
-          break;
-        }
-        if (hCtr->hi == hCtr->nV) break;  // the last level found nothing new
-        FX_TRY(hipMemsetAsync(&dCtr->andmask, 0xFF, sizeof(unsigned long long), st));
-        spec_levels = std::min(spec_levels * 2, 64);
+    // Dedup tables: a power-of-two prefix sized from the work this return is
+    // likely to hold (the frontier, and the last return's R + V), so small
+    // returns probe lines that stay in L2; a probe chain that runs too long
+    // (tfull) redoes the return with a 4x larger prefix.
+    {
+      const int64_t guess = std::max<int64_t>(nF, last_work) * 4;
+      tlog = 12;
+      while (tlog < tlog_full && (1LL << tlog) < guess) tlog++;
+    }
+    for (int attempt = 0;; attempt++) {
+      const Tabs tb = tabs(tlog, compact);
+      epoch++;
+      if (compact) {
+        // one-word tables start EMPTY; the prefix this attempt uses
+        FX_TRY(hipMemsetAsync(tagR, 0xFF, (size_t)8 << tlog, st));
+        FX_TRY(hipMemsetAsync(tagV, 0xFF, (size_t)8 << tlog, st));
+        tags_dirty = true;
+      } else if (tags_dirty) {
+        // back to epoch tags after compact returns: no stale word may look live
+        FX_TRY(hipMemsetAsync(tagR, 0, (tmask + 1) * 8, st));
+        FX_TRY(hipMemsetAsync(tagV, 0, (tmask + 1) * 8, st));
+        tags_dirty = false;
       }
-      const unsigned long long ex = hCtr->explored;
-      explored_repl += (int64_t)(ex - explored_seen);
-      explored_seen = ex;
-      nRg = (int64_t)hCtr->nR;
-      if (timed) timeout = std::chrono::duration<double, std::milli>(
-                               std::chrono::steady_clock::now() - t0).count() > (double)opts.time_budget_ms;
-      if (P > 1 && timed) {
-        int64_t v[1] = {timeout ? 1 : 0};
-        FX_COLL(tr.allreduce(tr.user, v, 1, LC_FX_SUM));
-        timeout = v[0] > 0;
+      fx_reset_kernel<<<1, 1, 0, st>>>(dCtr, explored_seen);
+      bool tfull = false;
+      if (!part) {
+        // replicated: a small return runs whole in one workgroup; otherwise
+        // (or for what it leaves) speculative batches of levels over the
+        // grid, one sync per batch
+        bool small = nF <= kSmallF && last_work <= kSmallWork;
+        if (small) {
+          fx_small_return_kernel<<<1, 256, 0, st>>>(F, nF, dWin, tb, epoch, dCtr, kSmallLevel);
+          FX_TRY(hipGetLastError());
+          if (int er = sync_ctr()) return er;
+        } else if (nF) {
+          fx_insert_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, dWin, tb, epoch, dCtr);
+          FX_TRY(hipGetLastError());
+        }
+        const int g = (int)std::max<int64_t>(16, std::min<int64_t>(kExpandWG, (std::max(nF, last_work) + 3) / 4));
+        for (int batch = 0; !(small && batch == 0 && hCtr->hi == hCtr->nV); batch++) {
+          if (small && batch == 0 && (hCtr->tfull || hCtr->overflow)) break;
+          FX_TRY(hipMemsetAsync(&dCtr->andmask, 0xFF, sizeof(unsigned long long), st));
+          for (int l = 0; l < spec_levels; l++) {
+            fx_mark_kernel<<<1, 1, 0, st>>>(dCtr);
+            fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tb, epoch, dCtr, -1, -1, nullptr, 0);
+          }
+          fx_and_kernel<<<grid_for((int64_t)std::max(nF, last_work)), 256, 0, st>>>(Rl, &dCtr->nR, dCtr);
+          FX_TRY(hipGetLastError());
+          if (int er = sync_ctr()) return er;
+          if (hCtr->tfull || hCtr->overflow || (int64_t)(hCtr->nR + hCtr->nV) > budget) break;
+          if (hCtr->hi == hCtr->nV) break;  // the last level found nothing new
+          spec_levels = std::min(spec_levels * 2, 64);
+        }
+        if (hCtr->tfull && tlog < tlog_full) {
+          tlog = std::min(tlog + 2, tlog_full);
+          stats.redos++;
+          continue;
+        }
+        if (hCtr->tfull || hCtr->overflow || (int64_t)(hCtr->nR + hCtr->nV) > budget) over = true;
+        // next return: as many speculative levels as this one needed, plus one
+        const int64_t used = (int64_t)hCtr->levels - levels_seen;
+        levels_seen = (int64_t)hCtr->levels;
+        spec_levels = (int)std::max<int64_t>(2, std::min<int64_t>(64, used + 1));
+        const unsigned long long ex = hCtr->explored;
+        explored_repl += (int64_t)(ex - explored_seen);
+        explored_seen = ex;
+        nRg = (int64_t)hCtr->nR;
+        last_work = (int64_t)(hCtr->nR + hCtr->nV);
+        if (timed) timeout = std::chrono::duration<double, std::milli>(
+                                 std::chrono::steady_clock::now() - t0).count() > (double)opts.time_budget_ms;
+        if (P > 1 && timed) {
+          int64_t v[1] = {timeout ? 1 : 0};
+          FX_COLL(tr.allreduce(tr.user, v, 1, LC_FX_SUM));
+          timeout = v[0] > 0;
+        }
+        break;
       }
-    } else {
       // partitioned: every level is chunks of (expand, exchange, insert)
-      stats.part_returns++;
+      if (attempt == 0) stats.part_returns++;
+      if (nF) {
+        fx_insert_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, dWin, tb, epoch, dCtr);
+        FX_TRY(hipGetLastError());
+      }
       if (int er = sync_ctr()) return er;
       int64_t lvl_lo = 0, lvl_hi = (int64_t)hCtr->nV, pos = 0;
       const int64_t chunk = (int64_t)(cand_cap / kW);
       for (;;) {
         const int64_t a = pos, b = std::min(lvl_hi, pos + chunk);
         pos = b;
-        if (int er = part_chunk(a, b)) return er;
+        if (int er = part_chunk(a, b, tb)) return er;
         if (int er = sync_ctr()) return er;
         if (timed) timeout = std::chrono::duration<double, std::milli>(
                                  std::chrono::steady_clock::now() - t0).count() > (double)opts.time_budget_ms;
-        int64_t v[5] = {pos < lvl_hi ? 1 : 0, (int64_t)hCtr->nV - lvl_hi,
+        int64_t v[6] = {pos < lvl_hi ? 1 : 0, (int64_t)hCtr->nV - lvl_hi,
                         (int64_t)(hCtr->nR + hCtr->nV), (int64_t)hCtr->overflow ? 1 : 0,
-                        timeout ? 1 : 0};
-        FX_COLL(tr.allreduce(tr.user, v, 5, LC_FX_SUM));
+                        timeout ? 1 : 0, (int64_t)hCtr->tfull ? 1 : 0};
+        FX_COLL(tr.allreduce(tr.user, v, 6, LC_FX_SUM));
+        if (v[5]) {  // some rank's table is too small: every rank redoes the return
+          tfull = true;
+          break;
+        }
         if (v[3] || v[2] > budget) {
           over = true;
           break;
@@ -932,13 +1155,24 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         pos = lvl_lo;
       }
       (void)lvl_lo;
+      if (tfull) {
+        if (hCtr->tfull && tlog < tlog_full) tlog = std::min(tlog + 2, tlog_full);
+        int64_t v[1] = {hCtr->tfull && tlog >= tlog_full ? 1 : 0};  // full size and still full
+        FX_COLL(tr.allreduce(tr.user, v, 1, LC_FX_SUM));
+        if (!v[0]) {
+          stats.redos++;
+          continue;
+        }
+        over = true;
+      }
       if (!over && !timeout) {
-        fx_and_kernel<<<kFlatWG, 256, 0, st>>>(Rl, &dCtr->nR, dCtr);
+        fx_and_kernel<<<grid_for(nF), 256, 0, st>>>(Rl, &dCtr->nR, dCtr);
         FX_TRY(hipGetLastError());
       }
       if (int er = sync_ctr()) return er;
       explored_part += (int64_t)(hCtr->explored - explored_seen);
       explored_seen = hCtr->explored;
+      last_work = (int64_t)(hCtr->nR + hCtr->nV);
       // global |R| and the global AND (bit b set everywhere <=> no rank lacks it)
       int64_t v[1 + kW];
       v[0] = (int64_t)hCtr->nR;
@@ -949,6 +1183,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       for (int b = 0; b < kW; b++)
         if (!v[1 + b]) gand |= 1ULL << b;
       hCtr->andmask = gand;
+      break;
     }
     if (over) {
       result_unknown(res, LC_REASON_CONFIG_BUDGET);

@@ -50,7 +50,8 @@ class LcFxStats(ctypes.Structure):
     _fields_ = [("total_ms", ctypes.c_double), ("returns", ctypes.c_int64),
                 ("levels", ctypes.c_int64), ("part_returns", ctypes.c_int64),
                 ("part_levels", ctypes.c_int64), ("sent_configs", ctypes.c_int64),
-                ("gathers", ctypes.c_int64), ("max_local_frontier", ctypes.c_int64)]
+                ("gathers", ctypes.c_int64), ("max_local_frontier", ctypes.c_int64),
+                ("redos", ctypes.c_int64), ("wide_returns", ctypes.c_int64)]
 
 
 _bound = False

@@ -43,7 +43,7 @@ def test_struct_sizes():
     from jepsen.etcd_amd import fx
     assert ctypes.sizeof(fx.LcFxParams) == 32
     assert ctypes.sizeof(fx.LcFxTransport) == 40
-    assert ctypes.sizeof(fx.LcFxStats) == 64
+    assert ctypes.sizeof(fx.LcFxStats) == 80
 
 
 def test_library_built_from_this_tree():
