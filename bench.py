@@ -234,6 +234,7 @@ def main():
         line["mixed_leg"] = mixed_leg(ctx, abi, dev, stream)
         line["model_leg"] = model_leg(ctx, abi)
         line["crash_leg"] = crash_leg(ctx, abi, dev, stream)
+        line["oversized_key"] = oversized_key(ctx, abi)
 
     if rank == 0 and world == 1 and not (args.no_cpu_baseline or args.bare):
         line["cpu_baseline"] = cpu_baseline(args, ops, key_off, res)
@@ -438,6 +439,44 @@ def model_leg(ctx, abi):
             "valid": int((r["verdict"] == 1).sum()), "unknown": int((r["verdict"] == -1).sum())}
 
 
+def oversized_key_ops(abi):
+    """One version-less key (cas-register model) of 2,000 ops at concurrency
+    50: frontiers of up to 115,648 configurations, 72 M explored."""
+    ops, off, _, _ = abi.synth(1, 2000, concurrency=50, seed=0x5EED0004)
+    ops = ops.copy()
+    ops[:, 3] = abi.LC_NIL
+    return ops, off
+
+
+def oversized_key(ctx, abi):
+    """SURVEY §8(e)'s one exception: a single key too large for one
+    workgroup.  The frontier exchange (include/lincheck_fx.h) runs its JIT
+    search over the whole GPU; lc_check's tiers give the same key one
+    cooperative workgroup and its configuration budget.  Not part of `value`."""
+    from jepsen.etcd_amd.fx import FrontierExchange
+    ops, off = oversized_key_ops(abi)
+    with FrontierExchange(device=0) as fx:
+        fx.check(ops)  # warm-up (table allocation)
+        times = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            r = fx.check(ops)
+            times.append((time.perf_counter() - t0) * 1e3)
+        st = fx.stats()
+    t = min(times)
+    t0 = time.perf_counter()
+    _, rt = ctx.check(ops, off)
+    tiers_ms = (time.perf_counter() - t0) * 1e3
+    return {"workload": "1 key x 2000 ops, concurrency 50, cas-register model (no versions; host buffers)",
+            "fx_ms": t, "verdict": int(r["verdict"]), "configs_explored": int(r["configs_explored"]),
+            "max_frontier": int(r["max_frontier"]),
+            "configs_per_s": int(r["configs_explored"]) / (t * 1e-3),
+            "returns": st["returns"], "levels": st["levels"], "redos": st["redos"],
+            "tiers": {"call_ms": tiers_ms, "verdict": int(rt["verdict"][0]),
+                      "reason": abi.REASONS.get(int(rt["reason"][0])),
+                      "configs_explored": int(rt["configs_explored"][0])}}
+
+
 def reduce_run(elapsed, n_ops, res, distributed, dev):
     """Whole-job numbers: the MAX of the ranks' timed-region wall times and
     the SUM of their checked ops and verdict counts (every rank checks its
@@ -498,7 +537,24 @@ def cpu_baseline(args, ops, key_off, gpu_res):
                   % (k, args.ops_per_key, len(sub_ops), best[1], best[2]),
         "verdict_mismatches_vs_gpu": mism,
         "model_leg": cpu_model_leg(args),
+        "oversized_key": cpu_oversized_key(),
     }
+
+
+def cpu_oversized_key():
+    """The oversized key on one host thread: the oracle's JIT with the GPU's
+    exact reductions (oracle.JITC) — one key's search is sequential, in the
+    oracle as in knossos.  Compare with oversized_key.fx_ms."""
+    import oracle
+    from jepsen.etcd_amd import abi
+    ops, off = oversized_key_ops(abi)
+    t0 = time.perf_counter()
+    _, r = oracle.check(ops, off, algo=oracle.JITC, n_threads=1, max_configs=1 << 24)
+    dt = time.perf_counter() - t0
+    return {"value": int(r["configs_explored"][0]) / dt, "unit": "configs/s", "cores": 1,
+            "kind": "port", "ms": dt * 1e3, "verdict": int(r["verdict"][0]),
+            "sample": "the whole oversized key (2000 ops), oracle JITC, %.1f s" % dt,
+            "configs_explored": int(r["configs_explored"][0])}
 
 
 def cpu_model_leg(args, n_keys=200):

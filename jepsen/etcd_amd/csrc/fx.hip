@@ -174,7 +174,24 @@ struct Tabs {
   uint64_t tmask;
   unsigned long long list_cap;
   int compact;  // one-word keys (ctab_insert) instead of tag + 16-B key
+  unsigned long long *exp;  // explored, sharded over kExpShards lines (summed by fx_and_kernel)
 };
+
+// The explored counter is added to by every wave of every level: one
+// same-address atomic per wave serialised (~8k per level); 64 shards on
+// lines of their own, summed once per batch.
+constexpr int kExpShards = 64;
+constexpr int kExpStride = 16;  // u64 per shard: 128 B
+
+__device__ inline unsigned long long wave_sum_shards(unsigned long long *exp) {
+  unsigned long long v =
+      __hip_atomic_load(&exp[__lane_id() * kExpStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, off), hi = __shfl_xor((uint32_t)(v >> 32), off);
+    v += ((unsigned long long)hi << 32) | lo;
+  }
+  return v;
+}
 
 // Compact tables.  Within one return every configuration has linearized the
 // retired mutations plus those its mask names, so its version is
@@ -189,9 +206,10 @@ struct Tabs {
 constexpr int kCompactSlots = 58;
 constexpr unsigned long long kEmpty = ~0ULL;
 
-__device__ inline int ctab_insert(unsigned long long *tab, uint64_t tmask, const Cfg &c) {
+__device__ inline int ctab_insert(unsigned long long *tab, uint64_t tmask, const Cfg &c,
+                                  uint64_t start = ~0ULL) {
   const unsigned long long word = c.mask | ((unsigned long long)c.val << kCompactSlots);
-  uint64_t i = mix64(word) & tmask;
+  uint64_t i = (start == ~0ULL ? mix64(word) : start) & tmask;
   for (int probes = 0; probes < kMaxProbe; probes++) {
     const unsigned long long old = atomicCAS(&tab[i], kEmpty, word);
     if (old == kEmpty) return 1;
@@ -264,7 +282,7 @@ __global__ void fx_mark_kernel(Ctr *ctr) {
 // Per-wave LDS staging of new list entries (replicated mode): one atomic per
 // flush of up to kStage entries instead of one per configuration expanded —
 // the list counters are the only same-address atomics of a level.
-constexpr int kStage = 192;
+constexpr int kStage = 128;
 struct Stage {
   Cfg r[kStage];
   Cfg v[kStage];
@@ -286,9 +304,93 @@ __device__ inline void stage_flush(Cfg *buf, int &n, Cfg *list, unsigned long lo
   n = 0;
 }
 
+__device__ inline void stage_put(bool isnew, bool toR, const Cfg &c, Stage *stg, int &nr, int &nv,
+                                 const Tabs &t, Ctr *ctr) {
+  const uint64_t below = (1ULL << __lane_id()) - 1;
+  const uint64_t mR = __ballot(isnew && toR), mV = __ballot(isnew && !toR);
+  if (isnew && toR) stg->r[nr + __popcll(mR & below)] = c;
+  if (isnew && !toR) stg->v[nv + __popcll(mV & below)] = c;
+  nr += __popcll(mR);
+  nv += __popcll(mV);
+  if (nr > kStage - kW) stage_flush(stg->r, nr, t.listR, &ctr->nR, t.list_cap, &ctr->overflow);
+  if (nv > kStage - kW) stage_flush(stg->v, nv, t.listV, &ctr->nV, t.list_cap, &ctr->overflow);
+}
+
+// End of a level: the workgroup's waves reserve their staged entries with one
+// atomic per list for the whole workgroup (the list counters and the
+// explored shards are the level's only same-address atomics), then each wave
+// writes its own.  Every wave of the workgroup must call it.
+struct WgFlush {
+  int n[4][2];
+  unsigned long long base[2];
+  unsigned long long explored[4];
+};
+
+__device__ inline void wg_flush(WgFlush *wf, Stage *stg, int nr, int nv, unsigned long long explored,
+                                const Tabs &t, Ctr *ctr) {
+  const int w = threadIdx.x / kW, lane = __lane_id();
+  if (lane == 0) {
+    wf->n[w][0] = nr;
+    wf->n[w][1] = nv;
+    wf->explored[w] = explored;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x / kW;
+    unsigned long long tr = 0, tv = 0, te = 0;
+    for (int k = 0; k < nw; k++) {
+      tr += wf->n[k][0];
+      tv += wf->n[k][1];
+      te += wf->explored[k];
+    }
+    wf->base[0] = tr ? atomicAdd(&ctr->nR, tr) : 0;
+    wf->base[1] = tv ? atomicAdd(&ctr->nV, tv) : 0;
+    if (te) atomicAdd(&t.exp[(blockIdx.x % kExpShards) * kExpStride], te);
+  }
+  __syncthreads();
+  unsigned long long br = wf->base[0], bv = wf->base[1];
+  for (int k = 0; k < w; k++) {
+    br += wf->n[k][0];
+    bv += wf->n[k][1];
+  }
+  for (int j = lane; j < nr; j += kW) {
+    if (br + j < t.list_cap) t.listR[br + j] = stg->r[j];
+    else atomicOr(&ctr->overflow, 1ULL);
+  }
+  for (int j = lane; j < nv; j += kW) {
+    if (bv + j < t.list_cap) t.listV[bv + j] = stg->v[j];
+    else atomicOr(&ctr->overflow, 1ULL);
+  }
+}
+
+// Compact insert of two words with their first probes in flight together.
+__device__ inline void ctab_insert2(const Tabs &t, bool a, bool toRa, const Cfg &ca, int &ra,
+                                    bool b, bool toRb, const Cfg &cb, int &rb) {
+  unsigned long long *ta = toRa ? t.tagR : t.tagV, *tb = toRb ? t.tagR : t.tagV;
+  const unsigned long long wa = ca.mask | ((unsigned long long)ca.val << kCompactSlots);
+  const unsigned long long wb = cb.mask | ((unsigned long long)cb.val << kCompactSlots);
+  const uint64_t ia = mix64(wa) & t.tmask, ib = mix64(wb) & t.tmask;
+  unsigned long long oa = 0, ob = 0;
+  if (a) oa = atomicCAS(&ta[ia], kEmpty, wa);
+  if (b) ob = atomicCAS(&tb[ib], kEmpty, wb);
+  ra = rb = -2;  // -2: not inserted
+  if (a) ra = oa == kEmpty ? 1 : oa == wa ? 0 : ctab_insert(ta, t.tmask, ca, ia + 1);
+  if (b) rb = ob == kEmpty ? 1 : ob == wb ? 0 : ctab_insert(tb, t.tmask, cb, ib + 1);
+}
+
+// One level of the expansion: every wave takes configurations of V[lo, hi)
+// (two at a time in replicated mode, their table probes in flight
+// together), lane t tests window slot t (pending, not a read, its
+// deadline-order predecessors linearized, legal), builds the successor with
+// its eager read closure, and either inserts it (replicated mode) or appends
+// it to its owner's candidate region (partitioned mode: cand_cap != 0).
+// Read closure: the reads a successor's state makes legal are, for reads
+// without a version, fixed by the value this lane's op writes (rv_me, once
+// per launch); only reads that name a version are tested per successor.
 __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch, Ctr *ctr,
                                     int64_t lo, int64_t hi, int64_t wave, int64_t nwaves,
-                                    Cfg *cbuf, unsigned long long cand_cap, Stage *stg) {
+                                    Cfg *cbuf, unsigned long long cand_cap, Stage *stg,
+                                    WgFlush *wf) {
   const int lane = __lane_id();
   int nr = 0, nv = 0;  // staged entries (wave-uniform)
   const Slot me = w.s[lane];
@@ -296,38 +398,69 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
   const uint64_t muts = w.occ & ~w.reads;
   const uint64_t reads = w.occ & w.reads;
   const bool is_mut = (muts & bit) != 0;
-  unsigned long long explored = 0;
-  for (int64_t i = lo + wave; i < hi; i += nwaves) {
-    const Cfg c = t.listV[i];
-    const bool cand = is_mut && !(c.mask & bit) && !(me.before & ~c.mask) && legal(me, c.ver, c.val);
-    Cfg s = c;
+  uint64_t rv_me = 0, vreads = 0;
+  for (uint64_t pr = reads; pr;) {
+    const int b = __builtin_ctzll(pr);
+    pr &= pr - 1;
+    const Slot &r = w.s[b];
+    if (r.nvm) vreads |= 1ULL << b;
+    else if (!r.nlm || r.nl == me.value) rv_me |= 1ULL << b;
+  }
+  auto succ = [&](const Cfg &c, bool &cand, Cfg &s) {
+    cand = is_mut && !(c.mask & bit) && !(me.before & ~c.mask) && legal(me, c.ver, c.val);
+    s = c;
     if (cand) {
-      s.mask |= bit;
+      s.mask |= bit | rv_me;
       s.ver = c.ver + 1;
       s.val = (uint32_t)me.value;
-      uint64_t pr = reads & ~s.mask;
+      uint64_t pr = vreads & ~s.mask;
       while (pr) {
         const int b = __builtin_ctzll(pr);
         pr &= pr - 1;
         if (legal(w.s[b], s.ver, s.val)) s.mask |= 1ULL << b;
       }
     }
-    explored += __popcll(__ballot(cand));
-    if (!cand_cap) {
-      const bool toR = cand && (s.mask & w.xbit);
-      if (toR) s.mask &= ~w.xbit;
-      int r = -1;
-      if (cand) r = any_insert(t, toR, epoch, s);
-      if (cand && r < 0) atomicOr(&ctr->tfull, 1ULL);
-      const uint64_t below = (1ULL << lane) - 1;
-      const uint64_t mR = __ballot(r == 1 && toR), mV = __ballot(r == 1 && !toR);
-      if (r == 1 && toR) stg->r[nr + __popcll(mR & below)] = s;
-      if (r == 1 && !toR) stg->v[nv + __popcll(mV & below)] = s;
-      nr += __popcll(mR);
-      nv += __popcll(mV);
-      if (nr > kStage - kW) stage_flush(stg->r, nr, t.listR, &ctr->nR, t.list_cap, &ctr->overflow);
-      if (nv > kStage - kW) stage_flush(stg->v, nv, t.listV, &ctr->nV, t.list_cap, &ctr->overflow);
-    } else {
+  };
+  unsigned long long explored = 0;
+  if (!cand_cap) {
+    // the next pair's loads are issued before this pair's probes
+    Cfg nA{}, nB{};
+    if (lo + wave < hi) nA = t.listV[lo + wave];
+    if (lo + wave + nwaves < hi) nB = t.listV[lo + wave + nwaves];
+    for (int64_t i = lo + wave; i < hi; i += 2 * nwaves) {
+      const int64_t j = i + nwaves;
+      const bool hasB = j < hi;
+      const Cfg cA = nA;
+      const Cfg cB = hasB ? nB : cA;
+      if (i + 2 * nwaves < hi) nA = t.listV[i + 2 * nwaves];
+      if (j + 2 * nwaves < hi) nB = t.listV[j + 2 * nwaves];
+      bool kA, kB;
+      Cfg sA, sB;
+      succ(cA, kA, sA);
+      succ(cB, kB, sB);
+      kB = kB && hasB;
+      explored += __popcll(__ballot(kA)) + __popcll(__ballot(kB));
+      const bool rA = kA && (sA.mask & w.xbit), rB = kB && (sB.mask & w.xbit);
+      if (rA) sA.mask &= ~w.xbit;
+      if (rB) sB.mask &= ~w.xbit;
+      int xA = -2, xB = -2;
+      if (t.compact) {
+        ctab_insert2(t, kA, rA, sA, xA, kB, rB, sB, xB);
+      } else {
+        if (kA) xA = any_insert(t, rA, epoch, sA);
+        if (kB) xB = any_insert(t, rB, epoch, sB);
+      }
+      if (xA == -1 || xB == -1) atomicOr(&ctr->tfull, 1ULL);
+      stage_put(xA == 1, rA, sA, stg, nr, nv, t, ctr);
+      stage_put(xB == 1, rB, sB, stg, nr, nv, t, ctr);
+    }
+  } else {
+    for (int64_t i = lo + wave; i < hi; i += nwaves) {
+      const Cfg c = t.listV[i];
+      bool cand;
+      Cfg s;
+      succ(c, cand, s);
+      explored += __popcll(__ballot(cand));
       // append to the owner's region; one atomic per distinct owner in the wave
       const uint32_t own = cand ? owner_of(s, w) : 0xFFFFFFFFu;
       uint64_t pend = __ballot(cand);
@@ -340,11 +473,7 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
       }
     }
   }
-  if (!cand_cap) {
-    stage_flush(stg->r, nr, t.listR, &ctr->nR, t.list_cap, &ctr->overflow);
-    stage_flush(stg->v, nv, t.listV, &ctr->nV, t.list_cap, &ctr->overflow);
-  }
-  if (lane == 0 && explored) atomicAdd(&ctr->explored, explored);
+  wg_flush(wf, stg, nr, nv, explored, t, ctr);
 }
 
 __device__ inline void load_win(Win &w, const Win *gwin) {
@@ -371,11 +500,12 @@ __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ 
   if (lo + (int64_t)blockIdx.x * (blockDim.x / kW) >= hi) return;
   __shared__ Win w;
   __shared__ Stage stg[4];
+  __shared__ WgFlush wf;
   load_win(w, gwin);
   __syncthreads();
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kW;
   const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kW;
-  expand_range(w, t, epoch, ctr, lo, hi, wave, nwaves, cbuf, cand_cap, &stg[threadIdx.x / kW]);
+  expand_range(w, t, epoch, ctr, lo, hi, wave, nwaves, cbuf, cand_cap, &stg[threadIdx.x / kW], &wf);
 }
 
 __device__ inline unsigned long long wave_and(unsigned long long v);
@@ -391,6 +521,7 @@ __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restr
                                                               unsigned long long cutoff) {
   __shared__ Win w;
   __shared__ Stage stg[4];
+  __shared__ WgFlush wf;
   __shared__ long long s_lo, s_hi;
   __shared__ int s_go;
   load_win(w, gwin);
@@ -423,7 +554,7 @@ __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restr
     }
     __syncthreads();
     if (!s_go) break;
-    expand_range(w, t, epoch, ctr, s_lo, s_hi, wave, nwaves, nullptr, 0, &stg[threadIdx.x / kW]);
+    expand_range(w, t, epoch, ctr, s_lo, s_hi, wave, nwaves, nullptr, 0, &stg[threadIdx.x / kW], &wf);
   }
   // retirement AND over R (meaningful when the return finished here)
   const int64_t nR =
@@ -432,6 +563,11 @@ __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restr
   for (int64_t i = threadIdx.x; i < nR; i += blockDim.x) a &= t.listR[i].mask;
   a = wave_and(a);
   if (__lane_id() == 0 && a != ~0ULL) atomicAnd(&ctr->andmask, a);
+  __syncthreads();
+  if (threadIdx.x < kW) {
+    const unsigned long long e = wave_sum_shards(t.exp);
+    if (threadIdx.x == 0) ctr->explored = e;
+  }
 }
 
 __device__ inline unsigned long long wave_and(unsigned long long v) {
@@ -444,7 +580,12 @@ __device__ inline unsigned long long wave_and(unsigned long long v) {
 
 // AND of the masks of list[0 .. *n) into ctr->andmask (retirement).
 __global__ __launch_bounds__(256) void fx_and_kernel(const Cfg *__restrict__ list,
-                                                     const unsigned long long *n, Ctr *ctr) {
+                                                     const unsigned long long *n, Ctr *ctr,
+                                                     unsigned long long *exp) {
+  if (blockIdx.x == 0 && threadIdx.x < kW) {
+    const unsigned long long e = wave_sum_shards(exp);
+    if (threadIdx.x == 0) ctr->explored = e;
+  }
   const int64_t cnt = (int64_t)*n;
   unsigned long long a = ~0ULL;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt;
@@ -492,7 +633,8 @@ __global__ __launch_bounds__(256) void fx_filter_kernel(const Cfg *__restrict__ 
 
 // Start (or redo) a return: empty R and V, explored back to its value
 // before the return.
-__global__ void fx_reset_kernel(Ctr *ctr, unsigned long long explored) {
+__global__ void fx_reset_kernel(Ctr *ctr, unsigned long long explored, unsigned long long *exp) {
+  for (int i = 0; i < kExpShards; i++) exp[i * kExpStride] = i ? 0 : explored;
   ctr->nR = ctr->nV = ctr->lo = ctr->hi = 0;
   ctr->andmask = ~0ULL;
   ctr->nsel = 0;
@@ -652,6 +794,7 @@ struct Rank {
   uint64_t tmask = 0;
   Win *dWin = nullptr, *hWin = nullptr;
   Ctr *dCtr = nullptr, *hCtr = nullptr;
+  unsigned long long *dExp = nullptr;  // explored shards
   Cfg *cand = nullptr;
   unsigned long long cand_cap = 0;  // per owner region
   Cfg *sendb = nullptr, *recvb = nullptr;
@@ -662,13 +805,14 @@ struct Rank {
 
   void release() {
     for (void *p : {(void *)F, (void *)Rl, (void *)Vl, (void *)tmp, (void *)tagR, (void *)tagV,
-                    (void *)keyR, (void *)keyV, (void *)dWin, (void *)dCtr, (void *)cand,
+                    (void *)keyR, (void *)keyV, (void *)dWin, (void *)dCtr, (void *)dExp, (void *)cand,
                     (void *)sendb, (void *)recvb})
       if (p) (void)hipFree(p);
     F = Rl = Vl = tmp = keyR = keyV = cand = sendb = recvb = nullptr;
     tagR = tagV = nullptr;
     dWin = nullptr;
     dCtr = nullptr;
+    dExp = nullptr;
     if (hWin) (void)hipHostFree(hWin);
     if (hCtr) (void)hipHostFree(hCtr);
     hWin = nullptr;
@@ -683,6 +827,8 @@ struct Rank {
     FX_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     FX_TRY(hipMalloc(&dWin, sizeof(Win)));
     FX_TRY(hipMalloc(&dCtr, sizeof(Ctr)));
+    FX_TRY(hipMalloc(&dExp, sizeof(unsigned long long) * kExpShards * kExpStride));
+    FX_TRY(hipMemset(dExp, 0, sizeof(unsigned long long) * kExpShards * kExpStride));
     FX_TRY(hipHostMalloc(&hWin, sizeof(Win), hipHostMallocDefault));
     FX_TRY(hipHostMalloc(&hCtr, sizeof(Ctr), hipHostMallocDefault));
     std::memset(hWin, 0, sizeof(Win));
@@ -743,6 +889,7 @@ struct Rank {
     t.listV = Vl;
     t.tmask = std::min<uint64_t>(tmask, (1ULL << lg) - 1);
     t.list_cap = list_cap;
+    t.exp = dExp;
     return t;
   }
 
@@ -1061,7 +1208,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         FX_TRY(hipMemsetAsync(tagV, 0, (tmask + 1) * 8, st));
         tags_dirty = false;
       }
-      fx_reset_kernel<<<1, 1, 0, st>>>(dCtr, explored_seen);
+      fx_reset_kernel<<<1, 1, 0, st>>>(dCtr, explored_seen, dExp);
       bool tfull = false;
       if (!part) {
         // replicated: a small return runs whole in one workgroup; otherwise
@@ -1084,7 +1231,8 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
             fx_mark_kernel<<<1, 1, 0, st>>>(dCtr);
             fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tb, epoch, dCtr, -1, -1, nullptr, 0);
           }
-          fx_and_kernel<<<grid_for((int64_t)std::max(nF, last_work)), 256, 0, st>>>(Rl, &dCtr->nR, dCtr);
+          fx_and_kernel<<<grid_for((int64_t)std::max(nF, last_work)), 256, 0, st>>>(Rl, &dCtr->nR,
+                                                                                     dCtr, dExp);
           FX_TRY(hipGetLastError());
           if (int er = sync_ctr()) return er;
           if (hCtr->tfull || hCtr->overflow || (int64_t)(hCtr->nR + hCtr->nV) > budget) break;
@@ -1166,7 +1314,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         over = true;
       }
       if (!over && !timeout) {
-        fx_and_kernel<<<grid_for(nF), 256, 0, st>>>(Rl, &dCtr->nR, dCtr);
+        fx_and_kernel<<<grid_for(nF), 256, 0, st>>>(Rl, &dCtr->nR, dCtr, dExp);
         FX_TRY(hipGetLastError());
       }
       if (int er = sync_ctr()) return er;
