@@ -39,6 +39,7 @@ LC_REASON_UNKNOWN_F = 5
 LC_FLAG_NO_HBM_RETRY = 1
 LC_FLAG_NO_FAST_PATH = 2
 LC_FLAG_NO_GAP_TIER = 4
+LC_FLAG_WHOLE_GPU = 8
 LC_WITNESS_NONE, LC_WITNESS_FULL, LC_WITNESS_PREFIX = 0, 1, 2
 
 # lc_op: 6 x int64 (f, value, expected, version, call, ret); arrays are (n, 6).

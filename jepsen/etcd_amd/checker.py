@@ -90,13 +90,16 @@ class RegisterChecker:
     result is then one key's map (no :results)."""
 
     def __init__(self, model=None, device_mask=0, max_configs_per_key=0, independent=True,
-                 timeline_dir=None, time_budget_ms=0):
+                 timeline_dir=None, time_budget_ms=0, whole_gpu=False):
         self.model = model or VersionedRegister(0, None)
         self.device_mask = device_mask
         self.max_configs_per_key = max_configs_per_key
         self.independent = independent
         self.timeline_dir = timeline_dir
         self.time_budget_ms = time_budget_ms
+        # a key one workgroup's search leaves :unknown at the configuration
+        # budget is searched again over the whole GPU (LC_FLAG_WHOLE_GPU)
+        self.whole_gpu = whole_gpu
         self._ctx = None
 
     def _context(self):
@@ -114,6 +117,7 @@ class RegisterChecker:
         # starts free (id MUTEX_FREE)
         init = H.MUTEX_FREE if m.name == "mutex" else (0 if m.value is not None else H.LC_NIL)
         o = abi.default_opts(self.max_configs_per_key, m.version, init,
+                             flags=abi.LC_FLAG_WHOLE_GPU if self.whole_gpu else 0,
                              time_budget_ms=self.time_budget_ms)
         _, res, wit, kind = self._context().check(ops, key_off, o, witness=True)
         results = {}

@@ -42,6 +42,7 @@
            (com.sun.jna.ptr PointerByReference)))
 
 (def ^:const LC_NIL -1)
+(def ^:const LC_FLAG_WHOLE_GPU 8)  ; include/lincheck.h
 (def ^:const LC_INF Long/MAX_VALUE)
 (def ^:const op-bytes 48)
 (def ^:const result-bytes 40)
@@ -265,7 +266,7 @@
   "One lc_check_ex over subs {k [op ...]}: {k result-map}.  Malformed keys
   come back :unknown one by one; lc_check_ex fails (and this throws, for
   check-safe) only on unusable arguments or a GPU error."
-  [model max-configs-per-key time-budget-ms subs]
+  [model max-configs-per-key time-budget-ms flags subs]
   (let [[keys done ops off n] (pack model subs)
         nk   (count keys)
         out  (Memory. (* result-bytes nk))
@@ -275,7 +276,7 @@
         o    (doto (Memory. 40)
                (.setLong 0 0) (.setLong 8 (if (= model :mutex) 0 LC_NIL))
                (.setLong 16 max-configs-per-key)
-               (.setLong 24 time-budget-ms) (.setLong 32 0))
+               (.setLong 24 time-budget-ms) (.setLong 32 flags))
         rc   (locking ctx
                (.invokeInt (fun "lc_check_ex")
                            (object-array [@ctx ops off (long nk) o out aux])))]
@@ -309,14 +310,15 @@
   models this library packs: opts :model one of :versioned-register,
   :cas-register, :register, :mutex.  The lock workload's checker
   (lock.clj:243-244) becomes (linearizable {:model :mutex})."
-  [{:keys [model max-configs-per-key time-budget-ms]
+  [{:keys [model max-configs-per-key time-budget-ms whole-gpu?]
     :or {model :versioned-register max-configs-per-key 0 time-budget-ms 0}}]
   (reify checker/Checker
     (check [_ test history _opts]
       (let [ops (filterv client-op? history)]
         (if (empty? ops)
           {:valid? true :analyzer :mi355x}
-          (get (check-keys model max-configs-per-key time-budget-ms {nil ops}) nil))))))
+          (get (check-keys model max-configs-per-key time-budget-ms
+                           (if whole-gpu? LC_FLAG_WHOLE_GPU 0) {nil ops}) nil))))))
 
 (defn- render-linear!
   "What jepsen's checker/linearizable does with a failed analysis: knossos's
@@ -352,16 +354,19 @@
   :model (default :versioned-register, register.clj:111), :timeline?
   (default true: keep register.clj:112's timeline/html per key),
   :time-budget-ms (0 = none: a key whose frontier search runs longer is
-  :unknown, as knossos's aborts are)."
+  :unknown, as knossos's aborts are), :whole-gpu? (a key one workgroup's
+  search leaves :unknown at the configuration budget is searched again over
+  the whole GPU: LC_FLAG_WHOLE_GPU, include/lincheck_fx.h)."
   ([] (checker {}))
-  ([{:keys [max-configs-per-key model timeline? time-budget-ms]
+  ([{:keys [max-configs-per-key model timeline? time-budget-ms whole-gpu?]
      :or {max-configs-per-key 0 model :versioned-register timeline? true time-budget-ms 0}}]
    (reify checker/Checker
      (check [_ test history opts]
        (let [subs (subhistories history)]
          (if (empty? subs)
            {:valid? true :results {} :failures []}
-           (let [linear  (check-keys model max-configs-per-key time-budget-ms subs)
+           (let [linear  (check-keys model max-configs-per-key time-budget-ms
+                                     (if whole-gpu? LC_FLAG_WHOLE_GPU 0) subs)
                  results (into (array-map)
                                (for [[k r] linear]
                                  [k (composed test opts k (get subs k) r timeline?)]))]

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../../include/lincheck.h"
+#include "../../../include/lincheck_fx.h"
 #include "kernels.h"
 
 #ifndef LC_BUILD_ID
@@ -142,6 +143,7 @@ struct Dev {
 
 struct lc_ctx {
   std::vector<Dev> devs;
+  lc_fx *fx = nullptr;  // LC_FLAG_WHOLE_GPU: the frontier exchange, opened on first use
   std::string err;
   std::mutex err_mu;
   lc_stats stats{};
@@ -574,6 +576,7 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
 
 void lc_close(lc_ctx *c) {
   if (!c) return;
+  if (c->fx) lc_fx_close(c->fx);
   for (Dev &d : c->devs) {
     (void)hipSetDevice(d.id);
     if (d.stream) (void)hipStreamSynchronize(d.stream);
@@ -795,6 +798,37 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
     c->stats.hbm_kernel_ms += c->devs[di].hbm_ms;
     c->stats.n_hbm_keys += c->devs[di].n_hbm;
     c->stats.n_malformed += c->devs[di].malformed;
+  }
+  // LC_FLAG_WHOLE_GPU: a key the tiers left :unknown at the configuration
+  // budget (one workgroup's HBM sets were not enough) is searched again by
+  // the frontier exchange over the whole first GPU (include/lincheck_fx.h),
+  // whose budget bounds each return's configuration sets, as the oracle's
+  // does; its result replaces the tiers' (verdict, fail op, explored, frontier).
+  if (!rc && (flags & LC_FLAG_WHOLE_GPU)) {
+    for (int64_t k = 0; k < n_keys && !rc; k++) {
+      if (out[k].verdict != LC_UNKNOWN || out[k].reason != LC_REASON_CONFIG_BUDGET) continue;
+      if (!c->fx) {
+        lc_fx_params fp{};
+        fp.device = c->devs[0].id;
+        fp.virtual_ranks = 1;
+        fp.part_above = -1;
+        fp.repl_below = -1;
+        fp.table_log2 = 0;
+        if (int e = lc_fx_open(&fp, nullptr, &c->fx)) {
+          set_err(c, "lc_fx_open failed");
+          c->fx = nullptr;
+          rc = e;
+          break;
+        }
+      }
+      lc_key_result r;
+      if (int e = lc_fx_check(c->fx, ops + key_off[k], key_off[k + 1] - key_off[k], opts, &r)) {
+        set_err(c, std::string("lc_fx_check: ") + lc_fx_last_error(c->fx));
+        rc = e;
+        break;
+      }
+      out[k] = r;
+    }
   }
   c->stats.n_keys = n_keys;
   c->stats.n_ops = key_off[n_keys] - key_off[0];

@@ -147,6 +147,34 @@ def test_fx_budget_window_and_errors():
         assert empty["verdict"] == 1
 
 
+@pytest.mark.gpu
+def test_whole_gpu_flag_decides_budget_keys():
+    """LC_FLAG_WHOLE_GPU: keys the tiers leave :unknown at the configuration
+    budget (cumulative over one workgroup's search) are decided by the
+    frontier exchange, whose budget bounds each return's sets as the
+    oracle's does; keys the tiers decide are untouched."""
+    ops, off, _, _ = abi.synth(3, 1000, concurrency=28, p_info=0.002, seed=0xB16)
+    ops = ops.copy()
+    ops[:, 3] = -1
+    small, soff, _, _ = abi.synth(2, 200, concurrency=6, seed=0xB17)
+    small = small.copy()
+    small[:, 3] = -1
+    allops = np.concatenate([ops, small])
+    alloff = np.concatenate([off, soff[1:] + off[-1]])
+    budget = 100000
+    with abi.Context(1) as ctx:
+        _, plain = ctx.check(allops, alloff, abi.default_opts(max_configs_per_key=budget))
+        _, whole = ctx.check(allops, alloff, abi.default_opts(max_configs_per_key=budget,
+                                                              flags=abi.LC_FLAG_WHOLE_GPU))
+    assert (plain["reason"][:3] == abi.LC_REASON_CONFIG_BUDGET).all()
+    _, ref = oracle.check(allops, alloff, algo=oracle.JITC, max_configs=budget)
+    for k in range(len(alloff) - 1):
+        for f in FIELDS:
+            assert int(whole[f][k]) == int(ref[f][k]), (k, f)
+    assert (whole["verdict"][:3] == 1).all()
+    assert (whole[3:] == plain[3:]).all()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
