@@ -203,6 +203,50 @@ def _rank_main(rank, world, port, keys, q):
         dist.destroy_process_group()
 
 
+def _nccl_main(port, q):
+    import torch
+    import torch.distributed as dist
+    from jepsen.etcd_amd import fx as F
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0,
+                            world_size=1)
+    try:
+        tr = F.TorchTransport(dist.group.WORLD, device=0)
+        assert tr.on_device
+        import ctypes
+        send = (ctypes.c_int64 * 1)(7)
+        recv = (ctypes.c_int64 * 1)(0)
+        assert tr._counts(None, send, recv) == 0 and recv[0] == 7
+        src = torch.arange(48, dtype=torch.uint8, device="cuda")
+        dst = torch.zeros(48, dtype=torch.uint8, device="cuda")
+        sc = (ctypes.c_int64 * 1)(3)
+        rc = (ctypes.c_int64 * 1)(3)
+        assert tr._a2av(None, src.data_ptr(), sc, dst.data_ptr(), rc, 16) == 0, tr.error
+        vals = (ctypes.c_int64 * 2)(4, 9)
+        assert tr._allred(None, vals, 2, F.LC_FX_SUM) == 0 and list(vals) == [4, 9]
+        q.put(bool(torch.equal(src, dst)))
+    except Exception as e:
+        q.put(repr(e))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_torch_transport_rccl_device_buffers():
+    """TorchTransport under "nccl" (RCCL): the engine's device buffers reach
+    all_to_all_single through __cuda_array_interface__ with no copy.  One
+    rank (this pool has one GPU per box; RCCL refuses two ranks on one
+    device), so the collective is a self-exchange."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_main, args=(_free_port(), q))
+    p.start()
+    out = q.get(timeout=180)
+    p.join(timeout=60)
+    assert out is True, out
+
+
 @pytest.mark.gpu
 def test_fx_two_processes_over_torch_distributed():
     """Two ranks (processes) on one card, collectives over gloo through

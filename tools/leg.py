@@ -4,7 +4,9 @@ that must see only that leg's kernels).
 crash: C2 with 5 % crashed writes/CAS (gap_light_kernel / gap_tier_kernel)
 model: cas-register model, 1000 keys x 1000 ops, concurrency 20 (lds_tier,
        hbm_coop_kernel<4>)
-hot / hotx: C4 at 20 % crashed, valid / invalid (gap_tier_kernel)"""
+hot / hotx: C4 at 20 % crashed, valid / invalid (gap_tier_kernel)
+search: C2 with the version-order and gap tiers off (lds_tier_kernel)
+fx: bench.py's oversized key through the frontier exchange (fx_expand_kernel)"""
 import json
 import os
 import sys
@@ -23,16 +25,33 @@ elif leg == "model":
     ops, off, _, _ = abi.synth(1000, 1000, concurrency=20, seed=7)
     ops = ops.copy()
     ops[:, 3] = abi.LC_NIL
+elif leg == "search":  # C2 through the JIT search tier only (lds_tier_kernel)
+    ops, off, _, _ = abi.synth(10000, 1000, concurrency=20, seed=0x5EED0002)
+elif leg == "fx":  # bench.py's oversized key through the frontier exchange (fx_expand_kernel)
+    ops, off, _, _ = abi.synth(1, 2000, concurrency=50, seed=0x5EED0004)
+    ops = ops.copy()
+    ops[:, 3] = abi.LC_NIL
 elif leg in ("hot", "hotx"):
     ops, off, _, _ = abi.synth(1, 5000, concurrency=50, p_info=0.2, info_frac=0.2,
                                p_anomaly=1.0 if leg == "hotx" else 0.0,
                                seed=1007 if leg == "hotx" else 0x5EED0004)
 else:
     raise SystemExit("unknown leg " + leg)
+if leg == "fx":
+    from jepsen.etcd_amd.fx import FrontierExchange
+    with FrontierExchange(device=0) as fx:
+        for i in range(reps):
+            t = time.perf_counter()
+            r = fx.check(ops)
+            print(json.dumps({"leg": leg, "rep": i, "wall_ms": (time.perf_counter() - t) * 1e3,
+                              "configs": int(r["configs_explored"]), "verdict": int(r["verdict"]),
+                              "stats": fx.stats()}))
+    raise SystemExit(0)
+opts = abi.default_opts(flags=abi.LC_FLAG_NO_FAST_PATH) if leg == "search" else None
 with abi.Context(device_mask=1) as ctx:
     for i in range(reps):
         t = time.perf_counter()
-        _, r = ctx.check(ops, off)
+        _, r = ctx.check(ops, off, opts)
         s = ctx.stats()
         print(json.dumps({"leg": leg, "rep": i, "wall_ms": (time.perf_counter() - t) * 1e3,
                           "fast_ms": s["fast_kernel_ms"], "gap_ms": s["gap_kernel_ms"],
