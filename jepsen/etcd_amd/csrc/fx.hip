@@ -81,15 +81,16 @@ struct Win {
 };
 
 struct Ctr {
-  unsigned long long nR, nV;    // list sizes
-  unsigned long long lo, hi;    // current level of V
+  unsigned long long nR, nV;    // R list size; V entries of the levels expanded so far
+  unsigned long long cnt[3];    // V levels, triple-buffered: level k is list k % 3
+  unsigned long long kcur;      // fx_small_return_kernel: the first level it left unexpanded
   unsigned long long explored;  // successors generated (cumulative)
   unsigned long long levels;    // non-empty levels (cumulative)
   unsigned long long andmask;   // AND of R's masks
   unsigned long long overflow;  // a list ran out of room (the budget)
   unsigned long long nsel;      // filter output
   unsigned long long tfull;     // a table probe ran too long: redo the return with a larger table
-  unsigned long long pad[6];
+  unsigned long long pad[5];
   unsigned long long cand[64];  // partitioned: candidates per owner rank
 };
 
@@ -170,7 +171,11 @@ __device__ int tab_insert(unsigned long long *tags, Cfg *keys, uint64_t tmask, u
 struct Tabs {
   unsigned long long *tagR, *tagV;
   Cfg *keyR, *keyV;
-  Cfg *listR, *listV;
+  Cfg *listR;
+  // V levels: three lists of list_cap entries at vbase; a launch reads its
+  // level from vsrc and appends the next one to vdst, counted in *vcnt
+  Cfg *vbase, *vsrc, *vdst;
+  unsigned long long *vcnt;
   uint64_t tmask;
   unsigned long long list_cap;
   int compact;  // one-word keys (ctab_insert) instead of tag + 16-B key
@@ -251,7 +256,7 @@ __device__ inline void insert_rv(bool have, Cfg c, uint64_t xbit, const Tabs &t,
   if (have) r = any_insert(t, toR, epoch, c);
   if (have && r < 0) atomicOr(&ctr->tfull, 1ULL);
   wave_append(r == 1 && toR, c, t.listR, &ctr->nR, t.list_cap, &ctr->overflow);
-  wave_append(r == 1 && !toR, c, t.listV, &ctr->nV, t.list_cap, &ctr->overflow);
+  wave_append(r == 1 && !toR, c, t.vdst, t.vcnt, t.list_cap, &ctr->overflow);
 }
 
 __global__ __launch_bounds__(256) void fx_insert_kernel(const Cfg *__restrict__ in, int64_t n,
@@ -268,11 +273,6 @@ __global__ __launch_bounds__(256) void fx_insert_kernel(const Cfg *__restrict__ 
   }
 }
 
-__global__ void fx_mark_kernel(Ctr *ctr) {
-  ctr->lo = ctr->hi;
-  ctr->hi = ctr->nV;
-  if (ctr->hi > ctr->lo) ctr->levels++;
-}
 
 // One level of the expansion: every wave takes configurations of V[lo, hi)
 // one at a time, lane t tests window slot t (pending, not a read, its
@@ -313,7 +313,7 @@ __device__ inline void stage_put(bool isnew, bool toR, const Cfg &c, Stage *stg,
   nr += __popcll(mR);
   nv += __popcll(mV);
   if (nr > kStage - kW) stage_flush(stg->r, nr, t.listR, &ctr->nR, t.list_cap, &ctr->overflow);
-  if (nv > kStage - kW) stage_flush(stg->v, nv, t.listV, &ctr->nV, t.list_cap, &ctr->overflow);
+  if (nv > kStage - kW) stage_flush(stg->v, nv, t.vdst, t.vcnt, t.list_cap, &ctr->overflow);
 }
 
 // End of a level: the workgroup's waves reserve their staged entries with one
@@ -344,7 +344,7 @@ __device__ inline void wg_flush(WgFlush *wf, Stage *stg, int nr, int nv, unsigne
       te += wf->explored[k];
     }
     wf->base[0] = tr ? atomicAdd(&ctr->nR, tr) : 0;
-    wf->base[1] = tv ? atomicAdd(&ctr->nV, tv) : 0;
+    wf->base[1] = tv ? atomicAdd(t.vcnt, tv) : 0;
     if (te) atomicAdd(&t.exp[(blockIdx.x % kExpShards) * kExpStride], te);
   }
   __syncthreads();
@@ -358,7 +358,7 @@ __device__ inline void wg_flush(WgFlush *wf, Stage *stg, int nr, int nv, unsigne
     else atomicOr(&ctr->overflow, 1ULL);
   }
   for (int j = lane; j < nv; j += kW) {
-    if (bv + j < t.list_cap) t.listV[bv + j] = stg->v[j];
+    if (bv + j < t.list_cap) t.vdst[bv + j] = stg->v[j];
     else atomicOr(&ctr->overflow, 1ULL);
   }
 }
@@ -425,15 +425,15 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
   if (!cand_cap) {
     // the next pair's loads are issued before this pair's probes
     Cfg nA{}, nB{};
-    if (lo + wave < hi) nA = t.listV[lo + wave];
-    if (lo + wave + nwaves < hi) nB = t.listV[lo + wave + nwaves];
+    if (lo + wave < hi) nA = t.vsrc[lo + wave];
+    if (lo + wave + nwaves < hi) nB = t.vsrc[lo + wave + nwaves];
     for (int64_t i = lo + wave; i < hi; i += 2 * nwaves) {
       const int64_t j = i + nwaves;
       const bool hasB = j < hi;
       const Cfg cA = nA;
       const Cfg cB = hasB ? nB : cA;
-      if (i + 2 * nwaves < hi) nA = t.listV[i + 2 * nwaves];
-      if (j + 2 * nwaves < hi) nB = t.listV[j + 2 * nwaves];
+      if (i + 2 * nwaves < hi) nA = t.vsrc[i + 2 * nwaves];
+      if (j + 2 * nwaves < hi) nB = t.vsrc[j + 2 * nwaves];
       bool kA, kB;
       Cfg sA, sB;
       succ(cA, kA, sA);
@@ -456,7 +456,7 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
     }
   } else {
     for (int64_t i = lo + wave; i < hi; i += nwaves) {
-      const Cfg c = t.listV[i];
+      const Cfg c = t.vsrc[i];
       bool cand;
       Cfg s;
       succ(c, cand, s);
@@ -482,17 +482,28 @@ __device__ inline void load_win(Win &w, const Win *gwin) {
   for (int i = threadIdx.x; i < (int)(sizeof(Win) / 4); i += blockDim.x) dst[i] = src[i];
 }
 
-// A level over the grid: V[ctr->lo, ctr->hi) (lo_arg < 0) or [lo_arg, hi_arg).
-// Workgroups past the level's end leave before staging the window, so the
-// speculative launches of the replicated mode cost little when empty.
+// A level over the grid: level k whole (lo_arg < 0: replicated mode; its
+// size is ctr->cnt[k % 3], fixed while it runs, since this launch appends to
+// level k + 1 and only zeroes the count of level k + 2, whose list level k - 1
+// held) or [lo_arg, hi_arg) of it (partitioned mode: the host keeps the
+// books).  No level-marking launch sits between two levels.  Workgroups past
+// the level's end leave before staging the window, so the speculative
+// launches of the replicated mode cost little when empty.
 __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ gwin, Tabs t,
-                                                        uint32_t epoch, Ctr *ctr, int64_t lo_arg,
-                                                        int64_t hi_arg, Cfg *cbuf,
+                                                        uint32_t epoch, Ctr *ctr, int64_t k,
+                                                        int64_t lo_arg, int64_t hi_arg, Cfg *cbuf,
                                                         unsigned long long cand_cap) {
   int64_t lo, hi;
   if (lo_arg < 0) {
-    lo = (int64_t)ctr->lo;
-    hi = (int64_t)ctr->hi;
+    lo = 0;
+    hi = (int64_t)ctr->cnt[k % 3];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      ctr->cnt[(k + 2) % 3] = 0;
+      if (hi) {
+        ctr->levels++;
+        ctr->nV += (unsigned long long)hi;
+      }
+    }
   } else {
     lo = lo_arg;
     hi = hi_arg;
@@ -512,9 +523,9 @@ __device__ inline unsigned long long wave_and(unsigned long long v);
 
 // A whole return in one workgroup while the frontier is small (replicated
 // mode): split F, then levels separated by barriers, then the AND for
-// retirement — one launch instead of a launch pair per level.  A level
-// larger than `cutoff` is left to the grid (ctr->lo/hi stay at the last
-// level expanded, the protocol fx_mark_kernel continues from).
+// retirement — one launch instead of one per level.  A level larger than
+// `cutoff` is left to the grid: ctr->kcur names it, with the same books the
+// grid's launches keep.
 __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restrict__ F, int64_t nF,
                                                               const Win *__restrict__ gwin, Tabs t,
                                                               uint32_t epoch, Ctr *ctr,
@@ -522,8 +533,7 @@ __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restr
   __shared__ Win w;
   __shared__ Stage stg[4];
   __shared__ WgFlush wf;
-  __shared__ long long s_lo, s_hi;
-  __shared__ int s_go;
+  __shared__ long long s_n;
   load_win(w, gwin);
   __syncthreads();
   for (int64_t b = 0; b < nF; b += blockDim.x) {
@@ -535,26 +545,28 @@ __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restr
   }
   const int64_t wave = threadIdx.x / kW;
   const int64_t nwaves = blockDim.x / kW;
-  for (;;) {
+  for (int64_t k = 0;; k++) {
     __syncthreads();
     if (threadIdx.x == 0) {
-      const unsigned long long nV =
-          __hip_atomic_load(&ctr->nV, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long hi = ctr->hi;
-      int go = 0;
-      if (nV > hi && nV - hi <= cutoff) {
-        ctr->lo = hi;
-        ctr->hi = nV;
+      const unsigned long long n =
+          __hip_atomic_load(&ctr->cnt[k % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (n && n <= cutoff) {
+        ctr->cnt[(k + 2) % 3] = 0;
         ctr->levels++;
-        go = 1;
+        ctr->nV += n;
+        s_n = (long long)n;
+      } else {
+        ctr->kcur = (unsigned long long)k;
+        s_n = 0;
       }
-      s_lo = (long long)hi;
-      s_hi = (long long)nV;
-      s_go = go;
     }
     __syncthreads();
-    if (!s_go) break;
-    expand_range(w, t, epoch, ctr, s_lo, s_hi, wave, nwaves, nullptr, 0, &stg[threadIdx.x / kW], &wf);
+    if (!s_n) break;
+    Tabs tk = t;
+    tk.vsrc = t.vbase + (size_t)(k % 3) * t.list_cap;
+    tk.vdst = t.vbase + (size_t)((k + 1) % 3) * t.list_cap;
+    tk.vcnt = &ctr->cnt[(k + 1) % 3];
+    expand_range(w, tk, epoch, ctr, 0, s_n, wave, nwaves, nullptr, 0, &stg[threadIdx.x / kW], &wf);
   }
   // retirement AND over R (meaningful when the return finished here)
   const int64_t nR =
@@ -635,7 +647,8 @@ __global__ __launch_bounds__(256) void fx_filter_kernel(const Cfg *__restrict__ 
 // before the return.
 __global__ void fx_reset_kernel(Ctr *ctr, unsigned long long explored, unsigned long long *exp) {
   for (int i = 0; i < kExpShards; i++) exp[i * kExpStride] = i ? 0 : explored;
-  ctr->nR = ctr->nV = ctr->lo = ctr->hi = 0;
+  ctr->nR = ctr->nV = ctr->kcur = 0;
+  ctr->cnt[0] = ctr->cnt[1] = ctr->cnt[2] = 0;
   ctr->andmask = ~0ULL;
   ctr->nsel = 0;
   ctr->tfull = 0;
@@ -850,7 +863,7 @@ struct Rank {
       if (p) (void)hipFree(p);
     FX_TRY(hipMalloc(&F, need * sizeof(Cfg)));
     FX_TRY(hipMalloc(&Rl, need * sizeof(Cfg)));
-    FX_TRY(hipMalloc(&Vl, need * sizeof(Cfg)));
+    FX_TRY(hipMalloc(&Vl, 3 * need * sizeof(Cfg)));  // three V levels
     FX_TRY(hipMalloc(&tmp, need * sizeof(Cfg)));
     FX_TRY(hipMalloc(&tagR, tcap * 8));
     FX_TRY(hipMalloc(&tagV, tcap * 8));
@@ -878,7 +891,8 @@ struct Rank {
     return 0;
   }
 
-  Tabs tabs(int lg, int compact) const {
+  // k: the V level a launch reads (it appends level k + 1); k < 0: appends level 0
+  Tabs tabs(int lg, int compact, int64_t k) const {
     Tabs t;
     t.compact = compact;
     t.tagR = tagR;
@@ -886,7 +900,11 @@ struct Rank {
     t.keyR = keyR;
     t.keyV = keyV;
     t.listR = Rl;
-    t.listV = Vl;
+    t.vbase = Vl;
+    const int64_t src = k < 0 ? 2 : k % 3, dst = k < 0 ? 0 : (k + 1) % 3;
+    t.vsrc = Vl + (size_t)src * list_cap;
+    t.vdst = Vl + (size_t)dst * list_cap;
+    t.vcnt = &dCtr->cnt[dst];
     t.tmask = std::min<uint64_t>(tmask, (1ULL << lg) - 1);
     t.list_cap = list_cap;
     t.exp = dExp;
@@ -930,7 +948,7 @@ struct Rank {
     FX_TRY(hipMemsetAsync(dCtr->cand, 0, sizeof(unsigned long long) * P, st));
     if (b > a) {
       const int g = (int)std::max<int64_t>(1, std::min<int64_t>(kExpandWG, (b - a + 3) / 4));
-      fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tb, epoch, dCtr, a, b, cand, cand_cap);
+      fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tb, epoch, dCtr, 0, a, b, cand, cand_cap);
       FX_TRY(hipGetLastError());
     }
     if (int e = sync_ctr()) return e;
@@ -1195,7 +1213,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       while (tlog < tlog_full && (1LL << tlog) < guess) tlog++;
     }
     for (int attempt = 0;; attempt++) {
-      const Tabs tb = tabs(tlog, compact);
+      const Tabs tb = tabs(tlog, compact, -1);  // the split appends V level 0
       epoch++;
       if (compact) {
         // one-word tables start EMPTY; the prefix this attempt uses
@@ -1214,29 +1232,33 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         // replicated: a small return runs whole in one workgroup; otherwise
         // (or for what it leaves) speculative batches of levels over the
         // grid, one sync per batch
-        bool small = nF <= kSmallF && last_work <= kSmallWork;
+        const bool small = nF <= kSmallF && last_work <= kSmallWork;
+        int64_t k = 0;  // the next V level to expand
+        bool done = false;
         if (small) {
           fx_small_return_kernel<<<1, 256, 0, st>>>(F, nF, dWin, tb, epoch, dCtr, kSmallLevel);
           FX_TRY(hipGetLastError());
           if (int er = sync_ctr()) return er;
+          k = (int64_t)hCtr->kcur;
+          done = hCtr->tfull || hCtr->overflow || hCtr->cnt[k % 3] == 0;
         } else if (nF) {
           fx_insert_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, dWin, tb, epoch, dCtr);
           FX_TRY(hipGetLastError());
         }
         const int g = (int)std::max<int64_t>(16, std::min<int64_t>(kExpandWG, (std::max(nF, last_work) + 3) / 4));
-        for (int batch = 0; !(small && batch == 0 && hCtr->hi == hCtr->nV); batch++) {
-          if (small && batch == 0 && (hCtr->tfull || hCtr->overflow)) break;
+        while (!done) {
           FX_TRY(hipMemsetAsync(&dCtr->andmask, 0xFF, sizeof(unsigned long long), st));
-          for (int l = 0; l < spec_levels; l++) {
-            fx_mark_kernel<<<1, 1, 0, st>>>(dCtr);
-            fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tb, epoch, dCtr, -1, -1, nullptr, 0);
-          }
+          for (int l = 0; l < spec_levels; l++, k++)
+            fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tabs(tlog, compact, k), epoch, dCtr, k, -1, -1,
+                                                nullptr, 0);
           fx_and_kernel<<<grid_for((int64_t)std::max(nF, last_work)), 256, 0, st>>>(Rl, &dCtr->nR,
                                                                                      dCtr, dExp);
           FX_TRY(hipGetLastError());
           if (int er = sync_ctr()) return er;
-          if (hCtr->tfull || hCtr->overflow || (int64_t)(hCtr->nR + hCtr->nV) > budget) break;
-          if (hCtr->hi == hCtr->nV) break;  // the last level found nothing new
+          if (hCtr->tfull || hCtr->overflow ||
+              (int64_t)(hCtr->nR + hCtr->nV + hCtr->cnt[k % 3]) > budget)
+            break;
+          if (hCtr->cnt[k % 3] == 0) break;  // the last level found nothing new
           spec_levels = std::min(spec_levels * 2, 64);
         }
         if (hCtr->tfull && tlog < tlog_full) {
@@ -1244,7 +1266,9 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           stats.redos++;
           continue;
         }
-        if (hCtr->tfull || hCtr->overflow || (int64_t)(hCtr->nR + hCtr->nV) > budget) over = true;
+        if (hCtr->tfull || hCtr->overflow ||
+            (int64_t)(hCtr->nR + hCtr->nV + hCtr->cnt[k % 3]) > budget)
+          over = true;
         // next return: as many speculative levels as this one needed, plus one
         const int64_t used = (int64_t)hCtr->levels - levels_seen;
         levels_seen = (int64_t)hCtr->levels;
@@ -1270,17 +1294,21 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         FX_TRY(hipGetLastError());
       }
       if (int er = sync_ctr()) return er;
-      int64_t lvl_lo = 0, lvl_hi = (int64_t)hCtr->nV, pos = 0;
+      // level k: V list k % 3, n_k entries here; its successors become level
+      // k + 1, whose count the host zeroes before the level starts
+      int64_t k = 0, n_k = (int64_t)hCtr->cnt[0], v_done = 0, pos = 0;
       const int64_t chunk = (int64_t)(cand_cap / kW);
+      FX_TRY(hipMemsetAsync(&dCtr->cnt[1], 0, sizeof(unsigned long long), st));
       for (;;) {
-        const int64_t a = pos, b = std::min(lvl_hi, pos + chunk);
+        const int64_t a = pos, b = std::min(n_k, pos + chunk);
         pos = b;
-        if (int er = part_chunk(a, b, tb)) return er;
+        if (int er = part_chunk(a, b, tabs(tlog, compact, k))) return er;
         if (int er = sync_ctr()) return er;
         if (timed) timeout = std::chrono::duration<double, std::milli>(
                                  std::chrono::steady_clock::now() - t0).count() > (double)opts.time_budget_ms;
-        int64_t v[6] = {pos < lvl_hi ? 1 : 0, (int64_t)hCtr->nV - lvl_hi,
-                        (int64_t)(hCtr->nR + hCtr->nV), (int64_t)hCtr->overflow ? 1 : 0,
+        const int64_t n_next = (int64_t)hCtr->cnt[(k + 1) % 3];
+        int64_t v[6] = {pos < n_k ? 1 : 0, n_next,
+                        (int64_t)hCtr->nR + v_done + n_k + n_next, (int64_t)hCtr->overflow ? 1 : 0,
                         timeout ? 1 : 0, (int64_t)hCtr->tfull ? 1 : 0};
         FX_COLL(tr.allreduce(tr.user, v, 6, LC_FX_SUM));
         if (v[5]) {  // some rank's table is too small: every rank redoes the return
@@ -1297,12 +1325,14 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         }
         if (v[0]) continue;  // some rank has more of this level
         stats.part_levels++;
+        v_done += n_k;
         if (v[1] == 0) break;  // no rank found anything new
-        lvl_lo = lvl_hi;
-        lvl_hi = (int64_t)hCtr->nV;
-        pos = lvl_lo;
+        k++;
+        n_k = n_next;
+        pos = 0;
+        FX_TRY(hipMemsetAsync(&dCtr->cnt[(k + 1) % 3], 0, sizeof(unsigned long long), st));
       }
-      (void)lvl_lo;
+      const int64_t part_v = v_done;  // V entries of this return on this rank
       if (tfull) {
         if (hCtr->tfull && tlog < tlog_full) tlog = std::min(tlog + 2, tlog_full);
         int64_t v[1] = {hCtr->tfull && tlog >= tlog_full ? 1 : 0};  // full size and still full
@@ -1320,7 +1350,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       if (int er = sync_ctr()) return er;
       explored_part += (int64_t)(hCtr->explored - explored_seen);
       explored_seen = hCtr->explored;
-      last_work = (int64_t)(hCtr->nR + hCtr->nV);
+      last_work = (int64_t)hCtr->nR + part_v;
       // global |R| and the global AND (bit b set everywhere <=> no rank lacks it)
       int64_t v[1 + kW];
       v[0] = (int64_t)hCtr->nR;
