@@ -76,3 +76,52 @@ def test_merge_rule():
     assert merge_verdicts([1, -1]) == "unknown"
     assert merge_verdicts([-1, 0, 1]) is False
     assert merge_verdicts(np.array([], dtype=np.int32)) is True
+
+
+def _fx_transport_worker(rank, world, port, out):
+    import ctypes
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch.distributed as dist
+    from jepsen.etcd_amd import fx as F
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port,
+                            rank=rank, world_size=world)
+    try:
+        tr = F.TorchTransport(dist.group.WORLD, device=0)
+        send = (ctypes.c_int64 * world)(*[100 * rank + j for j in range(world)])
+        recv = (ctypes.c_int64 * world)()
+        rc1 = tr._counts(None, send, recv)
+        vals = (ctypes.c_int64 * 3)(rank + 1, 7, -rank)
+        rc2 = tr._allred(None, vals, 3, F.LC_FX_SUM)
+        mx = (ctypes.c_int64 * 1)(rank * 5)
+        rc3 = tr._allred(None, mx, 1, F.LC_FX_MAX)
+        out.put((rank, tr.on_device, rc1, list(recv), rc2, list(vals), rc3, mx[0],
+                 repr(tr.error)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fx_transport_collectives_two_ranks_gloo():
+    """The frontier exchange's collectives (jepsen/etcd_amd/fx.py
+    TorchTransport, the lc_fx_transport callbacks): the count exchange is an
+    all-to-all (recv[j] = what rank j sends here), the all-reduce sums or
+    maxes, host-staged under gloo.  The payload all-to-all-v needs device
+    buffers and runs in the GPU tests (tests/test_fx.py)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    world = 3
+    procs = [ctx.Process(target=_fx_transport_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, on_dev, rc1, recv, rc2, vals, rc3, mx, err in res:
+        assert not on_dev and rc1 == rc2 == rc3 == 0, err
+        assert recv == [100 * j + rank for j in range(world)]
+        assert vals == [1 + 2 + 3, 7 * world, -(0 + 1 + 2)]
+        assert mx == 5 * (world - 1)
