@@ -45,7 +45,13 @@ namespace {
 
 constexpr int kW = 64;
 constexpr int32_t kFieldMax = 0x7FFFFFFE;
-constexpr int kMaxProbe = 1 << 12;     // table probes per insert before giving up (overflow)
+// Table probes per insert before the return is redone with a 4x larger table
+// prefix.  Linear probing at the <= 25 % load the prefix is sized for keeps
+// chains short; a prefix that turns out too small (a return much larger than
+// the last) is caught after a bounded chain instead of probing a nearly full
+// table for thousands of steps per insert (measured: 43 such levels were 40 %
+// of the oversized key's expand time at 4,096).
+constexpr int kMaxProbe = 128;
 constexpr int kMaxSpin = 1 << 22;      // loop iterations per insert, busy waits included
 constexpr int kExpandWG = 2048;        // expand grid (most): 4 waves per workgroup
 constexpr int kFlatWG = 1024;          // thread-per-configuration kernels
@@ -509,6 +515,7 @@ __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ 
     hi = hi_arg;
   }
   if (lo + (int64_t)blockIdx.x * (blockDim.x / kW) >= hi) return;
+  if (ctr->tfull) return;  // this attempt will be redone with a larger table
   __shared__ Win w;
   __shared__ Stage stg[4];
   __shared__ WgFlush wf;
@@ -550,7 +557,9 @@ __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restr
     if (threadIdx.x == 0) {
       const unsigned long long n =
           __hip_atomic_load(&ctr->cnt[k % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (n && n <= cutoff) {
+      const bool full =
+          __hip_atomic_load(&ctr->tfull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      if (n && n <= cutoff && !full) {
         ctr->cnt[(k + 2) % 3] = 0;
         ctr->levels++;
         ctr->nV += n;
@@ -1106,7 +1115,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   int64_t explored_repl = 0, explored_part = 0;
   unsigned long long explored_seen = 0;
   int spec_levels = 4;
-  int64_t levels_seen = 0, last_work = 0;
+  int64_t levels_seen = 0, last_work = 0, work_hi = 0;
   bool tags_dirty = true;
   const int tlog_full = __builtin_ctzll(tmask + 1);
   int tlog = 12;
@@ -1208,7 +1217,9 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     // returns probe lines that stay in L2; a probe chain that runs too long
     // (tfull) redoes the return with a 4x larger prefix.
     {
-      const int64_t guess = std::max<int64_t>(nF, last_work) * 4;
+      // the prefix follows the recent peak (decaying), not only the last return
+    work_hi = std::max<int64_t>(last_work, work_hi - work_hi / 8);
+    const int64_t guess = std::max<int64_t>(std::max<int64_t>(nF, last_work), work_hi / 2) * 4;
       tlog = 12;
       while (tlog < tlog_full && (1LL << tlog) < guess) tlog++;
     }
