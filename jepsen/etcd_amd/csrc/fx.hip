@@ -654,7 +654,19 @@ __global__ __launch_bounds__(256) void fx_filter_kernel(const Cfg *__restrict__ 
 
 // Start (or redo) a return: empty R and V, explored back to its value
 // before the return.
-__global__ void fx_reset_kernel(Ctr *ctr, unsigned long long explored, unsigned long long *exp) {
+// ... and, with `words` > 0, fill the first `words` entries of both tables
+// with `fill` (the one-word tables' EMPTY): one launch where three were.
+__global__ __launch_bounds__(256) void fx_reset_kernel(Ctr *ctr, unsigned long long explored,
+                                                       unsigned long long *exp,
+                                                       unsigned long long *tagR,
+                                                       unsigned long long *tagV, int64_t words,
+                                                       unsigned long long fill) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
+    tagR[i] = fill;
+    tagV[i] = fill;
+  }
+  if (blockIdx.x || threadIdx.x) return;
   for (int i = 0; i < kExpShards; i++) exp[i * kExpStride] = i ? 0 : explored;
   ctr->nR = ctr->nV = ctr->kcur = 0;
   ctr->cnt[0] = ctr->cnt[1] = ctr->cnt[2] = 0;
@@ -1227,17 +1239,19 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       const Tabs tb = tabs(tlog, compact, -1);  // the split appends V level 0
       epoch++;
       if (compact) {
-        // one-word tables start EMPTY; the prefix this attempt uses
-        FX_TRY(hipMemsetAsync(tagR, 0xFF, (size_t)8 << tlog, st));
-        FX_TRY(hipMemsetAsync(tagV, 0xFF, (size_t)8 << tlog, st));
-        tags_dirty = true;
+        tags_dirty = true;  // one-word tables start EMPTY: the reset fills this attempt's prefix
       } else if (tags_dirty) {
         // back to epoch tags after compact returns: no stale word may look live
         FX_TRY(hipMemsetAsync(tagR, 0, (tmask + 1) * 8, st));
         FX_TRY(hipMemsetAsync(tagV, 0, (tmask + 1) * 8, st));
         tags_dirty = false;
       }
-      fx_reset_kernel<<<1, 1, 0, st>>>(dCtr, explored_seen, dExp);
+      {
+        const int64_t words = compact ? (int64_t)1 << tlog : 0;
+        fx_reset_kernel<<<grid_for(words), 256, 0, st>>>(dCtr, explored_seen, dExp, tagR, tagV,
+                                                          words, kEmpty);
+        FX_TRY(hipGetLastError());
+      }
       bool tfull = false;
       if (!part) {
         // replicated: a small return runs whole in one workgroup; otherwise
@@ -1257,8 +1271,9 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           FX_TRY(hipGetLastError());
         }
         const int g = (int)std::max<int64_t>(16, std::min<int64_t>(kExpandWG, (std::max(nF, last_work) + 3) / 4));
-        while (!done) {
-          FX_TRY(hipMemsetAsync(&dCtr->andmask, 0xFF, sizeof(unsigned long long), st));
+        for (int batch = 0; !done; batch++) {
+          if (small || batch)  // the reset set it for a first batch; a partial AND is stale
+            FX_TRY(hipMemsetAsync(&dCtr->andmask, 0xFF, sizeof(unsigned long long), st));
           for (int l = 0; l < spec_levels; l++, k++)
             fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tabs(tlog, compact, k), epoch, dCtr, k, -1, -1,
                                                 nullptr, 0);
