@@ -102,6 +102,34 @@ def test_fx_partition_switches_and_exchanges():
 
 
 @pytest.mark.gpu
+def test_fx_full_size_ranks_and_tiers_agree():
+    """Full-size keys the oracle takes seconds on: one rank, three in-process
+    ranks partitioned above a few thousand configurations, and (where they decide)
+    lc_check's tiers give the same verdict, configurations explored and
+    largest frontier — an order-independent count of a 10^7-configuration
+    search, so agreement pins the whole set semantics."""
+    from jepsen.etcd_amd.fx import FrontierExchange
+    for conc, info, n, pa in ((28, 0.002, 1000, 600), (40, 0.0, 2000, 4096)):
+        ops, off, _, _ = abi.synth(1, n, concurrency=conc, p_info=info, seed=0x5EED0004)
+        ops = ops.copy()
+        ops[:, 3] = -1
+        with FrontierExchange(device=0) as fx:
+            one = fx.check(ops)
+        with FrontierExchange(device=0, virtual_ranks=3, part_above=pa, repl_below=pa // 4) as fx:
+            three = fx.check(ops)
+            st = fx.stats()
+        assert st["part_returns"] > 0 and st["gathers"] > 0
+        for f in FIELDS:
+            assert int(one[f]) == int(three[f]), (conc, f)
+        assert one["verdict"] == 1
+        with abi.Context(1) as ctx:
+            _, t = ctx.check(ops, off)
+        if t["verdict"][0] == 1:
+            assert int(t["configs_explored"][0]) == int(one["configs_explored"])
+            assert int(t["max_frontier"][0]) == int(one["max_frontier"])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ranks", [1, 2])
 def test_fx_wide_tables(ranks):
     """Keys with more than 63 distinct values use the 16-byte-key tables

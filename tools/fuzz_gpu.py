@@ -1,7 +1,8 @@
 """Dev: broad differential fuzz, GPU vs the oracle, over random histories:
 tiny random keys (brute-force sized), synthetic register keys across crash and
 anomaly rates and concurrencies, version-stripped keys (cas-register), mutex
-and cas-register record generators.  Prints mismatches; exits 1 on any.
+and cas-register record generators, and the frontier exchange (one and three
+ranks) on version-less keys.  Prints mismatches; exits 1 on any.
     python tools/fuzz_gpu.py [rounds]"""
 import os
 import random
@@ -81,5 +82,30 @@ for rd in range(rounds):
     keys = [random_casreg(rng, rng.randrange(1, 24)) for _ in range(1500)]
     ops, off = pack_keys(keys)
     compare("casreg r%d" % rd, ops, off)
+    # the frontier exchange (one key at a time): every field against JITC,
+    # one rank and three in-process ranks with every level partitioned
+    from jepsen.etcd_amd.fx import FrontierExchange
+    keys = [random_casreg(rng, rng.randrange(1, 40), p_info=0.1) for _ in range(200)]
+    ops, off, _, _ = abi.synth(40, 150, concurrency=8, p_info=0.02, p_anomaly=0.5, seed=base + 7)
+    ops = ops.copy()
+    ops[:, 3] = -1
+    keys += [ops[off[k]:off[k + 1]].tolist() for k in range(40)]
+    kops, koff = pack_keys(keys)
+    _, o = oracle.check(kops, koff, algo=oracle.JITC, n_threads=16, max_configs=1 << 20)
+    fields = ("verdict", "fail_op", "configs_explored", "max_frontier")
+    for ranks, pa in ((1, -1), (3, 0)):
+        nbad = ndec = 0
+        with FrontierExchange(device=0, virtual_ranks=ranks, part_above=pa, table_log2=20) as fx:
+            for k in range(len(keys)):
+                r = fx.check(kops[koff[k]:koff[k + 1]])
+                if r["verdict"] == -1 or o["verdict"][k] == -1:
+                    continue
+                ndec += 1
+                if any(int(r[f]) != int(o[f][k]) for f in fields):
+                    nbad += 1
+                    print("   fx key", k, [int(r[f]) for f in fields], [int(o[f][k]) for f in fields])
+        print("%-34s keys %5d decided %5d mismatches %d" % ("fx ranks %d r%d" % (ranks, rd),
+                                                            len(keys), ndec, nbad), flush=True)
+        bad_total += nbad
 print("TOTAL mismatches", bad_total)
 sys.exit(1 if bad_total else 0)
