@@ -292,6 +292,7 @@ constexpr int kStage = 128;
 struct Stage {
   Cfg r[kStage];
   Cfg v[kStage];
+  Cfg s[64];  // successors gathered from several configurations, inserted together
 };
 
 __device__ inline void stage_flush(Cfg *buf, int &n, Cfg *list, unsigned long long *count,
@@ -369,21 +370,6 @@ __device__ inline void wg_flush(WgFlush *wf, Stage *stg, int nr, int nv, unsigne
   }
 }
 
-// Compact insert of two words with their first probes in flight together.
-__device__ inline void ctab_insert2(const Tabs &t, bool a, bool toRa, const Cfg &ca, int &ra,
-                                    bool b, bool toRb, const Cfg &cb, int &rb) {
-  unsigned long long *ta = toRa ? t.tagR : t.tagV, *tb = toRb ? t.tagR : t.tagV;
-  const unsigned long long wa = ca.mask | ((unsigned long long)ca.val << kCompactSlots);
-  const unsigned long long wb = cb.mask | ((unsigned long long)cb.val << kCompactSlots);
-  const uint64_t ia = mix64(wa) & t.tmask, ib = mix64(wb) & t.tmask;
-  unsigned long long oa = 0, ob = 0;
-  if (a) oa = atomicCAS(&ta[ia], kEmpty, wa);
-  if (b) ob = atomicCAS(&tb[ib], kEmpty, wb);
-  ra = rb = -2;  // -2: not inserted
-  if (a) ra = oa == kEmpty ? 1 : oa == wa ? 0 : ctab_insert(ta, t.tmask, ca, ia + 1);
-  if (b) rb = ob == kEmpty ? 1 : ob == wb ? 0 : ctab_insert(tb, t.tmask, cb, ib + 1);
-}
-
 // One level of the expansion: every wave takes configurations of V[lo, hi)
 // (two at a time in replicated mode, their table probes in flight
 // together), lane t tests window slot t (pending, not a read, its
@@ -429,37 +415,51 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
   };
   unsigned long long explored = 0;
   if (!cand_cap) {
-    // the next pair's loads are issued before this pair's probes
-    Cfg nA{}, nB{};
-    if (lo + wave < hi) nA = t.vsrc[lo + wave];
-    if (lo + wave + nwaves < hi) nB = t.vsrc[lo + wave + nwaves];
-    for (int64_t i = lo + wave; i < hi; i += 2 * nwaves) {
-      const int64_t j = i + nwaves;
-      const bool hasB = j < hi;
-      const Cfg cA = nA;
-      const Cfg cB = hasB ? nB : cA;
-      if (i + 2 * nwaves < hi) nA = t.vsrc[i + 2 * nwaves];
-      if (j + 2 * nwaves < hi) nB = t.vsrc[j + 2 * nwaves];
-      bool kA, kB;
-      Cfg sA, sB;
-      succ(cA, kA, sA);
-      succ(cB, kB, sB);
-      kB = kB && hasB;
-      explored += __popcll(__ballot(kA)) + __popcll(__ballot(kB));
-      const bool rA = kA && (sA.mask & w.xbit), rB = kB && (sB.mask & w.xbit);
-      if (rA) sA.mask &= ~w.xbit;
-      if (rB) sB.mask &= ~w.xbit;
-      int xA = -2, xB = -2;
-      if (t.compact) {
-        ctab_insert2(t, kA, rA, sA, xA, kB, rB, sB, xB);
-      } else {
-        if (kA) xA = any_insert(t, rA, epoch, sA);
-        if (kB) xB = any_insert(t, rB, epoch, sB);
+    // A wave takes a run of `chunk` configurations (one load per lane), lane t
+    // tests slot t of each in turn, and the successors are gathered in LDS
+    // until 64 are pending; then every lane inserts one, so a probe round trip
+    // serves up to 64 successors of several configurations.  The run length
+    // spreads the level over every wave first (chunk = 1 on small levels).
+    const uint64_t below = (1ULL << lane) - 1;
+    const int64_t n = hi - lo;
+    const int64_t chunk = std::min<int64_t>(kW, std::max<int64_t>(1, (n + nwaves - 1) / nwaves));
+    int ns = 0;
+    auto insert_stash = [&]() {
+      __builtin_amdgcn_wave_barrier();
+      const bool have = lane < ns;
+      Cfg sc{};
+      if (have) sc = stg->s[lane];
+      __builtin_amdgcn_wave_barrier();
+      const bool toR = have && (sc.mask & w.xbit);
+      if (toR) sc.mask &= ~w.xbit;
+      int x = -2;
+      if (have) x = any_insert(t, toR, epoch, sc);
+      if (x == -1) atomicOr(&ctr->tfull, 1ULL);
+      stage_put(x == 1, toR, sc, stg, nr, nv, t, ctr);
+      ns = 0;
+    };
+    for (int64_t base = lo + wave * chunk; base < hi; base += nwaves * chunk) {
+      const int cnt = (int)std::min<int64_t>(chunk, hi - base);
+      Cfg mine{};
+      if (lane < cnt) mine = t.vsrc[base + lane];
+      for (int j = 0; j < cnt; j++) {
+        Cfg c;
+        c.mask = ((uint64_t)__shfl((uint32_t)(mine.mask >> 32), j) << 32) |
+                 __shfl((uint32_t)mine.mask, j);
+        c.ver = __shfl(mine.ver, j);
+        c.val = __shfl(mine.val, j);
+        bool cand;
+        Cfg sc;
+        succ(c, cand, sc);
+        const uint64_t m = __ballot(cand);
+        const int k = __popcll(m);
+        explored += k;
+        if (ns + k > kW) insert_stash();
+        if (cand) stg->s[ns + __popcll(m & below)] = sc;
+        ns += k;
       }
-      if (xA == -1 || xB == -1) atomicOr(&ctr->tfull, 1ULL);
-      stage_put(xA == 1, rA, sA, stg, nr, nv, t, ctr);
-      stage_put(xB == 1, rB, sB, stg, nr, nv, t, ctr);
     }
+    if (ns) insert_stash();
   } else {
     for (int64_t i = lo + wave; i < hi; i += nwaves) {
       const Cfg c = t.vsrc[i];
