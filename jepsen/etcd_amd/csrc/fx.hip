@@ -81,10 +81,25 @@ struct Win {
   uint64_t reads;  // slots holding reads (never candidates: closed eagerly)
   uint64_t xbit;   // slot of the returning op
   uint64_t kzob;   // Zobrist words of every retired mutation, xor-ed
+  // One rank: the frontier's updates since the last return, applied to each
+  // configuration as the split reads it instead of by launches of their own:
+  // the ops retired then (clear), then the reads called since (closure).
+  uint64_t fclear, fclose;
   int32_t rank, n_ranks;
   int32_t pad[2];
   Slot s[kW];
 };
+
+__device__ inline bool legal(const Slot &s, uint32_t ver, uint32_t val);
+
+__device__ inline void fix_f(Cfg &c, const Win &w) {
+  c.mask &= ~w.fclear;
+  for (uint64_t pr = w.fclose; pr;) {
+    const int b = __builtin_ctzll(pr);
+    pr &= pr - 1;
+    if (legal(w.s[b], c.ver, c.val)) c.mask |= 1ULL << b;
+  }
+}
 
 struct Ctr {
   unsigned long long nR, nV;    // R list size; V entries of the levels expanded so far
@@ -269,12 +284,14 @@ __global__ __launch_bounds__(256) void fx_insert_kernel(const Cfg *__restrict__ 
                                                         const Win *__restrict__ win, Tabs t,
                                                         uint32_t epoch, Ctr *ctr) {
   const uint64_t xbit = win->xbit;
+  const bool fix = win->fclear | win->fclose;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x; b < n; b += stride) {
     const int64_t i = b + threadIdx.x;
     const bool have = i < n;
     Cfg c{};
     if (have) c = in[i];
+    if (have && fix) fix_f(c, *win);
     insert_rv(have, c, xbit, t, epoch, ctr);
   }
 }
@@ -548,6 +565,7 @@ __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restr
     const bool have = i < nF;
     Cfg c{};
     if (have) c = F[i];
+    if (have) fix_f(c, w);
     insert_rv(have, c, w.xbit, t, epoch, ctr);
   }
   const int64_t wave = threadIdx.x / kW;
@@ -660,8 +678,14 @@ __global__ __launch_bounds__(256) void fx_reset_kernel(Ctr *ctr, unsigned long l
                                                        unsigned long long *exp,
                                                        unsigned long long *tagR,
                                                        unsigned long long *tagV, int64_t words,
-                                                       unsigned long long fill) {
+                                                       unsigned long long fill, Win *dwin,
+                                                       const Win win, int put_win) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (put_win && blockIdx.x == 0) {  // the window travels as the argument: no copy of its own
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(&win);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(dwin);
+    for (int i = threadIdx.x; i < (int)(sizeof(Win) / 4); i += blockDim.x) dst[i] = src[i];
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
     tagR[i] = fill;
     tagV[i] = fill;
@@ -1092,6 +1116,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   int32_t slot_op[kW];
   uint64_t before[kW] = {0};
   uint64_t occ = 0, reads = 0, kzob = 0;
+  uint64_t fclear = 0, fclose = 0;  // one rank: F's pending retirement / read closures
   Win &w = *hWin;
   std::memset(&w, 0, sizeof(Win));
   w.rank = rank;
@@ -1177,8 +1202,11 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       if (ox.f == LC_F_READ) {
         reads |= sb;
         sl.zob = 0;
-        // closure: the new read is linearized wherever it is legal now
-        if (nF) {
+        // closure: the new read is linearized wherever it is legal now (one
+        // rank: by the next split, as it reads the frontier)
+        if (P == 1) {
+          fclose |= sb;
+        } else if (nF) {
           fx_close_read_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, sb, sl);
           FX_TRY(hipGetLastError());
         }
@@ -1203,7 +1231,10 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     w.xbit = xb;
     w.kzob = kzob;
     for (int u = 0; u < kW; u++) w.s[u].before = before[u];
-    FX_TRY(hipMemcpyAsync(dWin, &w, sizeof(Win), hipMemcpyHostToDevice, st));
+    w.fclear = fclear;
+    w.fclose = fclose;
+    fclear = fclose = 0;
+    if (P > 1) FX_TRY(hipMemcpyAsync(dWin, &w, sizeof(Win), hipMemcpyHostToDevice, st));
     // mode switches (several ranks only)
     if (P > 1 && !part && nFglobal > part_above) {
       FX_TRY(hipMemsetAsync(&dCtr->nsel, 0, sizeof(unsigned long long), st));
@@ -1249,7 +1280,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       {
         const int64_t words = compact ? (int64_t)1 << tlog : 0;
         fx_reset_kernel<<<grid_for(words), 256, 0, st>>>(dCtr, explored_seen, dExp, tagR, tagV,
-                                                          words, kEmpty);
+                                                          words, kEmpty, dWin, w, P == 1);
         FX_TRY(hipGetLastError());
       }
       bool tfull = false;
@@ -1424,7 +1455,9 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
               rank, x, sx, (int)part, (long long)nF, (long long)nFglobal, hCtr->nV, hCtr->explored,
               hCtr->andmask, (unsigned long long)occ);
     if (all) {
-      if (nF) {
+      if (P == 1) {
+        fclear |= all;  // applied by the next split
+      } else if (nF) {
         fx_clear_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, all);
         FX_TRY(hipGetLastError());
       }

@@ -173,6 +173,14 @@ def test_fx_budget_window_and_errors():
         assert fx.check(unk)["reason"] == abi.LC_REASON_UNKNOWN_F
         empty = fx.check(np.zeros((0, 6), dtype=np.int64))
         assert empty["verdict"] == 1
+    # the time budget: every rank agrees the key is :unknown (reason 7)
+    big, _, _, _ = abi.synth(1, 2000, concurrency=40, seed=0x5EED0004)
+    big = big.copy()
+    big[:, 3] = -1
+    for ranks in (1, 2):
+        with FrontierExchange(device=0, virtual_ranks=ranks, part_above=0 if ranks > 1 else -1) as fx:
+            r = fx.check(big, abi.default_opts(time_budget_ms=5))
+            assert r["verdict"] == -1 and r["reason"] == 7, (ranks, r)
 
 
 @pytest.mark.gpu
