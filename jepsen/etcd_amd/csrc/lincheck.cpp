@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -52,6 +53,7 @@ constexpr int64_t kDefaultBudget = 1 << 24;   // configurations per key
 #endif
 constexpr unsigned kEventFlags = LC_EVENT_FLAGS;
 constexpr int kHbmTiers = 3;
+constexpr size_t kFxEngines = 4;  // LC_FLAG_WHOLE_GPU: oversized keys searched at once
 constexpr int64_t kHbmCap[kHbmTiers] = {1 << 14, 1 << 18, 1 << 21};
 constexpr int kHbmWaves[kHbmTiers] = {2048, 128, 16};
 // HBM tier lists up to these sizes get a workgroup of 16 (4) wavefronts per
@@ -143,7 +145,7 @@ struct Dev {
 
 struct lc_ctx {
   std::vector<Dev> devs;
-  lc_fx *fx = nullptr;  // LC_FLAG_WHOLE_GPU: the frontier exchange, opened on first use
+  std::vector<lc_fx *> fxs;  // LC_FLAG_WHOLE_GPU: frontier-exchange engines, opened on first use
   std::string err;
   std::mutex err_mu;
   lc_stats stats{};
@@ -576,7 +578,7 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
 
 void lc_close(lc_ctx *c) {
   if (!c) return;
-  if (c->fx) lc_fx_close(c->fx);
+  for (lc_fx *f : c->fxs) lc_fx_close(f);
   for (Dev &d : c->devs) {
     (void)hipSetDevice(d.id);
     if (d.stream) (void)hipStreamSynchronize(d.stream);
@@ -804,30 +806,50 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
   // the frontier exchange over the whole first GPU (include/lincheck_fx.h),
   // whose budget bounds each return's configuration sets, as the oracle's
   // does; its result replaces the tiers' (verdict, fail op, explored, frontier).
+  // Several such keys are searched at once, each by its own engine (own
+  // stream and tables): one key's levels are latency-bound, so concurrent
+  // searches fill the GPU the way one cannot.
   if (!rc && (flags & LC_FLAG_WHOLE_GPU)) {
-    for (int64_t k = 0; k < n_keys && !rc; k++) {
-      if (out[k].verdict != LC_UNKNOWN || out[k].reason != LC_REASON_CONFIG_BUDGET) continue;
-      if (!c->fx) {
-        lc_fx_params fp{};
-        fp.device = c->devs[0].id;
-        fp.virtual_ranks = 1;
-        fp.part_above = -1;
-        fp.repl_below = -1;
-        fp.table_log2 = 0;
-        if (int e = lc_fx_open(&fp, nullptr, &c->fx)) {
-          set_err(c, "lc_fx_open failed");
-          c->fx = nullptr;
-          rc = e;
-          break;
-        }
-      }
-      lc_key_result r;
-      if (int e = lc_fx_check(c->fx, ops + key_off[k], key_off[k + 1] - key_off[k], opts, &r)) {
-        set_err(c, std::string("lc_fx_check: ") + lc_fx_last_error(c->fx));
+    std::vector<int64_t> todo;
+    for (int64_t k = 0; k < n_keys; k++)
+      if (out[k].verdict == LC_UNKNOWN && out[k].reason == LC_REASON_CONFIG_BUDGET) todo.push_back(k);
+    const int ne = (int)std::min<size_t>(kFxEngines, todo.size());
+    while (!rc && (int)c->fxs.size() < ne) {
+      lc_fx_params fp{};
+      fp.device = c->devs[0].id;
+      fp.virtual_ranks = 1;
+      fp.part_above = -1;
+      fp.repl_below = -1;
+      fp.table_log2 = 0;
+      lc_fx *f = nullptr;
+      if (int e = lc_fx_open(&fp, nullptr, &f)) {
+        set_err(c, "lc_fx_open failed");
         rc = e;
         break;
       }
-      out[k] = r;
+      c->fxs.push_back(f);
+    }
+    if (!rc && ne > 0) {
+      std::atomic<size_t> next{0};
+      std::vector<int> erc(ne, 0);
+      auto run = [&](int e) {
+        for (;;) {
+          const size_t i = next.fetch_add(1);
+          if (i >= todo.size()) break;
+          const int64_t k = todo[i];
+          lc_key_result r;
+          if (int x = lc_fx_check(c->fxs[e], ops + key_off[k], key_off[k + 1] - key_off[k], opts, &r)) {
+            set_err(c, std::string("lc_fx_check: ") + lc_fx_last_error(c->fxs[e]));
+            erc[e] = x;
+            break;
+          }
+          out[k] = r;
+        }
+      };
+      std::vector<std::thread> th;
+      for (int e = 0; e < ne; e++) th.emplace_back(run, e);
+      for (auto &t : th) t.join();
+      for (int e = 0; e < ne && !rc; e++) rc = erc[e];
     }
   }
   c->stats.n_keys = n_keys;
