@@ -76,7 +76,12 @@ typedef struct lc_fx_params {
   int64_t part_above;     /* partition while the frontier exceeds this (< 0: default 65536) */
   int64_t repl_below;     /* replicate again below this (< 0: default part_above / 4) */
   int64_t table_log2;     /* log2 of each dedup table's entries (0: from the budget) */
+  int64_t flags;          /* LC_FX_FLAG_* */
 } lc_fx_params;
+
+/* Always use the 16-byte-key tables (epoch tags, fenced publication) instead
+ * of one-word entries: for tests of that path. */
+#define LC_FX_FLAG_WIDE_TABLES 1
 
 typedef struct lc_fx_stats {
   double  total_ms;         /* host wall time of the last lc_fx_check */
@@ -88,7 +93,8 @@ typedef struct lc_fx_stats {
   int64_t gathers;          /* partitioned -> replicated switches */
   int64_t max_local_frontier; /* largest frontier share held by this rank */
   int64_t redos;            /* returns redone with a larger dedup table */
-  int64_t wide_returns;     /* returns on 16-byte-key tables (a slot >= 58 open, or > 63 values) */
+  int64_t wide_returns;     /* returns on 16-byte-key tables (an open slot at or above 64 minus the
+                               key's value-id bits, over 2^20 - 1 values, or LC_FX_FLAG_WIDE_TABLES) */
 } lc_fx_stats;
 
 typedef struct lc_fx lc_fx;

@@ -200,6 +200,7 @@ struct Tabs {
   uint64_t tmask;
   unsigned long long list_cap;
   int compact;  // one-word keys (ctab_insert) instead of tag + 16-B key
+  int cshift;   // compact: the value id's bit offset in the word (64 - value bits)
   unsigned long long *exp;  // explored, sharded over kExpShards lines (summed by fx_and_kernel)
 };
 
@@ -223,18 +224,18 @@ __device__ inline unsigned long long wave_sum_shards(unsigned long long *exp) {
 // retired mutations plus those its mask names, so its version is
 // V0 + (retired mutations) + popcount(mask & mutation slots): a function of
 // the mask.  The state reduces to the value, which the host interns per key
-// to a dense id.  With every occupied slot below kCompactSlots and at most
-// 63 value ids, (mask, value id) packs into one 64-bit word, and a table
-// entry is that word: insertion is one device-scope atomicCAS per probe
-// (EMPTY -> word; the value returned says new, present, or occupied by
+// to a dense id.  With v bits for the value ids (6 to 20, as the key needs:
+// the all-ones id is never used) and every occupied slot below 64 - v,
+// (mask, value id) packs into one 64-bit word (Tabs::cshift = 64 - v), and
+// a table entry is that word: insertion is one device-scope atomicCAS per
+// probe (EMPTY -> word; the value returned says new, present, or occupied by
 // another word), with no key payload, tag or fence.  Tables are reset to
-// EMPTY (all ones: value id 63 is never used) before each return.
-constexpr int kCompactSlots = 58;
+// EMPTY (all ones) before each return.
 constexpr unsigned long long kEmpty = ~0ULL;
 
-__device__ inline int ctab_insert(unsigned long long *tab, uint64_t tmask, const Cfg &c,
+__device__ inline int ctab_insert(unsigned long long *tab, uint64_t tmask, const Cfg &c, int cshift,
                                   uint64_t start = ~0ULL) {
-  const unsigned long long word = c.mask | ((unsigned long long)c.val << kCompactSlots);
+  const unsigned long long word = c.mask | ((unsigned long long)c.val << cshift);
   uint64_t i = (start == ~0ULL ? mix64(word) : start) & tmask;
   for (int probes = 0; probes < kMaxProbe; probes++) {
     const unsigned long long old = atomicCAS(&tab[i], kEmpty, word);
@@ -246,7 +247,7 @@ __device__ inline int ctab_insert(unsigned long long *tab, uint64_t tmask, const
 }
 
 __device__ inline int any_insert(const Tabs &t, bool toR, uint32_t epoch, const Cfg &c) {
-  if (t.compact) return ctab_insert(toR ? t.tagR : t.tagV, t.tmask, c);
+  if (t.compact) return ctab_insert(toR ? t.tagR : t.tagV, t.tmask, c, t.cshift);
   return tab_insert(toR ? t.tagR : t.tagV, toR ? t.keyR : t.keyV, t.tmask, epoch, c);
 }
 
@@ -840,6 +841,8 @@ struct Rank {
   lc_fx_transport tr{};
   int64_t part_above = 65536, repl_below = 16384;
   int table_log2 = 0;
+  bool force_wide = false;  // LC_FX_FLAG_WIDE_TABLES (tests)
+  int cur_cshift = 58;      // this key's compact-word split (tabs())
   hipStream_t st = nullptr;
   std::string err;
   lc_fx_stats stats{};
@@ -940,6 +943,7 @@ struct Rank {
   Tabs tabs(int lg, int compact, int64_t k) const {
     Tabs t;
     t.compact = compact;
+    t.cshift = cur_cshift;
     t.tagR = tagR;
     t.tagV = tagV;
     t.keyR = keyR;
@@ -1140,6 +1144,10 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     if (o[i].f == LC_F_CAS) vid(o[i].expected);
   }
   const int64_t n_vals = (int64_t)vids.size();
+  int vbits = 6;  // value-id bits of the compact word: ids 0 .. n_vals - 1, all-ones unused
+  while ((1LL << vbits) - 1 < n_vals) vbits++;
+  const int cshift = 64 - vbits;  // < 44 (over 2^20 - 1 values): 16-byte keys
+  cur_cshift = cshift;
 
   // F = {(init state, nothing linearized)}
   Cfg init{0, (uint32_t)opts.init_version, (uint32_t)vid(opts.init_value)};
@@ -1251,7 +1259,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       part = false;
     }
     stats.returns++;
-    const int compact = (occ >> kCompactSlots) == 0 && n_vals <= 63;
+    const int compact = !force_wide && (occ >> cshift) == 0 && cshift >= 44;
     if (!compact) stats.wide_returns++;
     int64_t nRg = 0;   // global size of R after this return
     bool over = false, timeout = false;
@@ -1548,6 +1556,7 @@ int lc_fx_open(const lc_fx_params *params, const lc_fx_transport *transport, lc_
     if (params->part_above >= 0) r->part_above = params->part_above;
     r->repl_below = params->repl_below >= 0 ? params->repl_below : r->part_above / 4;
     r->table_log2 = (int)params->table_log2;
+    r->force_wide = (params->flags & LC_FX_FLAG_WIDE_TABLES) != 0;
     fx->ranks.push_back(r);
     if (int e = r->open()) {
       fx->err = r->err;

@@ -43,7 +43,10 @@ class LcFxTransport(ctypes.Structure):
 class LcFxParams(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("virtual_ranks", ctypes.c_int32),
                 ("part_above", ctypes.c_int64), ("repl_below", ctypes.c_int64),
-                ("table_log2", ctypes.c_int64)]
+                ("table_log2", ctypes.c_int64), ("flags", ctypes.c_int64)]
+
+
+LC_FX_FLAG_WIDE_TABLES = 1
 
 
 class LcFxStats(ctypes.Structure):
@@ -167,13 +170,14 @@ class FrontierExchange:
     process is one rank of it); else `virtual_ranks` ranks run as threads on
     `device`.  part_above / repl_below: the frontier size above which it is
     partitioned by owner, and below which it is replicated again (-1: the
-    library's defaults).  table_log2: dedup table size (0: from the budget)."""
+    library's defaults).  table_log2: dedup table size (0: from the budget).
+    flags: LC_FX_FLAG_* (LC_FX_FLAG_WIDE_TABLES: 16-byte-key tables only)."""
 
     def __init__(self, device=0, virtual_ranks=1, group=None, part_above=-1, repl_below=-1,
-                 table_log2=0):
+                 table_log2=0, flags=0):
         L = _lib()
         self._h = ctypes.c_void_p()
-        prm = LcFxParams(device, virtual_ranks, part_above, repl_below, table_log2)
+        prm = LcFxParams(device, virtual_ranks, part_above, repl_below, table_log2, flags)
         self.transport = None
         tr = None
         if group is not None:

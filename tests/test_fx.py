@@ -132,10 +132,11 @@ def test_fx_full_size_ranks_and_tiers_agree():
 @pytest.mark.gpu
 @pytest.mark.parametrize("ranks", [1, 2])
 def test_fx_wide_tables(ranks):
-    """Keys with more than 63 distinct values use the 16-byte-key tables
-    (epoch tags, fenced publication) instead of one-word entries; results
-    are the same as the oracle's, and a compact key after them is too."""
-    from jepsen.etcd_amd.fx import FrontierExchange
+    """Keys with many distinct values still pack (mask, value id) into one
+    word (fewer mask bits, more value bits); the 16-byte-key tables (epoch
+    tags, fenced publication) serve what does not fit and, forced, every key:
+    both give the oracle's results."""
+    from jepsen.etcd_amd.fx import LC_FX_FLAG_WIDE_TABLES, FrontierExchange
     ops, off, _, _ = abi.synth(3, 300, concurrency=10, n_values=400, p_info=0.01,
                                p_anomaly=0.5, seed=0x71DE + ranks)
     ops = ops.copy()
@@ -143,15 +144,14 @@ def test_fx_wide_tables(ranks):
     keys = [ops[off[k]:off[k + 1]] for k in range(3)]
     small = abi.synth(1, 200, concurrency=8, seed=0x71DF)[0].copy()
     small[:, 3] = -1
-    with FrontierExchange(device=0, virtual_ranks=ranks, part_above=0 if ranks > 1 else -1,
-                          table_log2=18) as fx:
-        for k in keys + [small, keys[0]]:
-            got = fx.check(k)
-            _compare(got, _oracle(k.tolist(), -1), ("wide", ranks))
-            if k is not small:
-                assert fx.stats()["wide_returns"] > 0
-            else:
-                assert fx.stats()["wide_returns"] == 0
+    for flags in (0, LC_FX_FLAG_WIDE_TABLES):
+        with FrontierExchange(device=0, virtual_ranks=ranks, part_above=0 if ranks > 1 else -1,
+                              table_log2=18, flags=flags) as fx:
+            for k in keys + [small, keys[0]]:
+                got = fx.check(k)
+                _compare(got, _oracle(k.tolist(), -1), ("wide", ranks, flags))
+                wide = fx.stats()["wide_returns"]
+                assert (wide > 0) if flags else (wide == 0), (flags, wide)
 
 
 @pytest.mark.gpu

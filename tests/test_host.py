@@ -41,7 +41,7 @@ def test_struct_sizes():
     assert ctypes.sizeof(abi.LcStats) == 104
     assert ctypes.sizeof(abi.LcAux) == 16
     from jepsen.etcd_amd import fx
-    assert ctypes.sizeof(fx.LcFxParams) == 32
+    assert ctypes.sizeof(fx.LcFxParams) == 40
     assert ctypes.sizeof(fx.LcFxTransport) == 40
     assert ctypes.sizeof(fx.LcFxStats) == 80
 
