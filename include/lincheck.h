@@ -84,7 +84,7 @@ typedef struct lc_opts {
 #define LC_FLAG_NO_FAST_PATH 2  /* skip the version-order and gap tiers: JIT search for every key */
 #define LC_FLAG_NO_GAP_TIER  4  /* skip the gap-matching tier: keys the version-order tier
                                    hands over go straight to the JIT search */
-#define LC_FLAG_WHOLE_GPU    8  /* lc_check / lc_check_ex: a key the tiers leave :unknown at the
+#define LC_FLAG_WHOLE_GPU    8  /* every entry point: a key the tiers leave :unknown at the
                                    configuration budget is searched again over the whole first
                                    GPU (the frontier exchange, include/lincheck_fx.h), whose
                                    budget bounds each return's configuration sets */

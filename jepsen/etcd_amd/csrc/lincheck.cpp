@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -512,6 +513,65 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   return 0;
 }
 
+
+// LC_FLAG_WHOLE_GPU: keys the tiers left :unknown at the configuration
+// budget (one workgroup's HBM sets were not enough) are searched again by the
+// frontier exchange over the whole first GPU (include/lincheck_fx.h), whose
+// budget bounds each return's configuration sets, as the oracle's does; its
+// result replaces the tiers' (verdict, fail op, explored, frontier).  Several
+// such keys are searched at once, each by its own engine (own stream and
+// tables): one key's levels are latency-bound, so concurrent searches fill the
+// GPU the way one cannot.  fetch(k, records) and store(k, result) move a key
+// between the caller's memory (host or device) and the engine.
+int whole_gpu(lc_ctx *c, const std::vector<int64_t> &todo, const lc_opts *opts,
+              const std::function<int(int64_t, std::vector<lc_op> &)> &fetch,
+              const std::function<int(int64_t, const lc_key_result &)> &store) {
+  const int ne = (int)std::min<size_t>(kFxEngines, todo.size());
+  while ((int)c->fxs.size() < ne) {
+    lc_fx_params fp{};
+    fp.device = c->devs[0].id;
+    fp.virtual_ranks = 1;
+    fp.part_above = -1;
+    fp.repl_below = -1;
+    lc_fx *f = nullptr;
+    if (int e = lc_fx_open(&fp, nullptr, &f)) {
+      set_err(c, "lc_fx_open failed");
+      return e;
+    }
+    c->fxs.push_back(f);
+  }
+  if (ne == 0) return 0;
+  std::atomic<size_t> next{0};
+  std::vector<int> erc(ne, 0);
+  auto run = [&](int e) {
+    (void)hipSetDevice(c->devs[0].id);
+    std::vector<lc_op> recs;
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= todo.size()) break;
+      const int64_t k = todo[i];
+      lc_key_result r;
+      int x = fetch(k, recs);
+      if (!x) x = lc_fx_check(c->fxs[e], recs.data(), (int64_t)recs.size(), opts, &r);
+      if (x) {
+        set_err(c, std::string("lc_fx_check: ") + lc_fx_last_error(c->fxs[e]));
+        erc[e] = x;
+        break;
+      }
+      if ((x = store(k, r))) {
+        erc[e] = x;
+        break;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int e = 0; e < ne; e++) th.emplace_back(run, e);
+  for (auto &t : th) t.join();
+  for (int e = 0; e < ne; e++)
+    if (erc[e]) return erc[e];
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -801,56 +861,20 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
     c->stats.n_hbm_keys += c->devs[di].n_hbm;
     c->stats.n_malformed += c->devs[di].malformed;
   }
-  // LC_FLAG_WHOLE_GPU: a key the tiers left :unknown at the configuration
-  // budget (one workgroup's HBM sets were not enough) is searched again by
-  // the frontier exchange over the whole first GPU (include/lincheck_fx.h),
-  // whose budget bounds each return's configuration sets, as the oracle's
-  // does; its result replaces the tiers' (verdict, fail op, explored, frontier).
-  // Several such keys are searched at once, each by its own engine (own
-  // stream and tables): one key's levels are latency-bound, so concurrent
-  // searches fill the GPU the way one cannot.
   if (!rc && (flags & LC_FLAG_WHOLE_GPU)) {
     std::vector<int64_t> todo;
     for (int64_t k = 0; k < n_keys; k++)
       if (out[k].verdict == LC_UNKNOWN && out[k].reason == LC_REASON_CONFIG_BUDGET) todo.push_back(k);
-    const int ne = (int)std::min<size_t>(kFxEngines, todo.size());
-    while (!rc && (int)c->fxs.size() < ne) {
-      lc_fx_params fp{};
-      fp.device = c->devs[0].id;
-      fp.virtual_ranks = 1;
-      fp.part_above = -1;
-      fp.repl_below = -1;
-      fp.table_log2 = 0;
-      lc_fx *f = nullptr;
-      if (int e = lc_fx_open(&fp, nullptr, &f)) {
-        set_err(c, "lc_fx_open failed");
-        rc = e;
-        break;
-      }
-      c->fxs.push_back(f);
-    }
-    if (!rc && ne > 0) {
-      std::atomic<size_t> next{0};
-      std::vector<int> erc(ne, 0);
-      auto run = [&](int e) {
-        for (;;) {
-          const size_t i = next.fetch_add(1);
-          if (i >= todo.size()) break;
-          const int64_t k = todo[i];
-          lc_key_result r;
-          if (int x = lc_fx_check(c->fxs[e], ops + key_off[k], key_off[k + 1] - key_off[k], opts, &r)) {
-            set_err(c, std::string("lc_fx_check: ") + lc_fx_last_error(c->fxs[e]));
-            erc[e] = x;
-            break;
-          }
+    rc = whole_gpu(
+        c, todo, opts,
+        [&](int64_t k, std::vector<lc_op> &v) {
+          v.assign(ops + key_off[k], ops + key_off[k + 1]);
+          return 0;
+        },
+        [&](int64_t k, const lc_key_result &r) {
           out[k] = r;
-        }
-      };
-      std::vector<std::thread> th;
-      for (int e = 0; e < ne; e++) th.emplace_back(run, e);
-      for (auto &t : th) t.join();
-      for (int e = 0; e < ne && !rc; e++) rc = erc[e];
-    }
+          return 0;
+        });
   }
   c->stats.n_keys = n_keys;
   c->stats.n_ops = key_off[n_keys] - key_off[0];
@@ -901,6 +925,33 @@ int lc_check_device_ex(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
   // base themselves, so a key_off slice of a larger array may be passed.
   rc = run_device(c, d, d_ops, d_key_off, n_keys, p, d_out, st,
                   opts ? opts->flags : 0, wo);
+  if (!rc && opts && (opts->flags & LC_FLAG_WHOLE_GPU) && n_keys > 0) {
+    // the results and the keys' records are in device memory: read back the
+    // verdicts, and each key the frontier exchange takes
+    std::vector<lc_key_result> res((size_t)n_keys);
+    int64_t base = 0;
+    HIP_TRY(c, hipMemcpyAsync(res.data(), d_out, sizeof(lc_key_result) * (size_t)n_keys,
+                              hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipMemcpyAsync(&base, d_key_off, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    std::vector<int64_t> todo;
+    for (int64_t k = 0; k < n_keys; k++)
+      if (res[k].verdict == LC_UNKNOWN && res[k].reason == LC_REASON_CONFIG_BUDGET) todo.push_back(k);
+    rc = whole_gpu(
+        c, todo, opts,
+        [&](int64_t k, std::vector<lc_op> &v) {
+          int64_t se[2];
+          if (hipMemcpy(se, d_key_off + k, sizeof se, hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
+          v.resize((size_t)(se[1] - se[0]));
+          if (!v.empty() && hipMemcpy(v.data(), d_ops + (se[0] - base), sizeof(lc_op) * v.size(),
+                                      hipMemcpyDeviceToHost) != hipSuccess)
+            return -EIO;
+          return 0;
+        },
+        [&](int64_t k, const lc_key_result &r) {
+          return hipMemcpy(d_out + k, &r, sizeof r, hipMemcpyHostToDevice) == hipSuccess ? 0 : -EIO;
+        });
+  }
   c->stats.kernel_ms = d.kernel_ms;
   c->stats.fast_kernel_ms = d.fast_ms;
   c->stats.jit_kernel_ms = d.jit_ms;

@@ -209,6 +209,22 @@ def test_whole_gpu_flag_decides_budget_keys():
             assert int(whole[f][k]) == int(ref[f][k]), (k, f)
     assert (whole["verdict"][:3] == 1).all()
     assert (whole[3:] == plain[3:]).all()
+    # the device entry point: records, offsets and results in device memory
+    # (a slice of the batch: d_ops starts at the record key_off[1] names)
+    import torch
+    dev = torch.device("cuda:0")
+    d_ops = torch.from_numpy(allops[alloff[1]:]).to(dev)
+    d_off = torch.from_numpy(alloff[1:].copy()).to(dev)
+    n = len(alloff) - 2
+    d_out = torch.zeros(n * abi.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    with abi.Context(1) as ctx:
+        ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), n, d_out.data_ptr(),
+                         opts=abi.default_opts(max_configs_per_key=budget,
+                                               flags=abi.LC_FLAG_WHOLE_GPU))
+    torch.cuda.synchronize()
+    got = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)
+    for f in FIELDS:
+        assert (got[f] == whole[f][1:]).all(), f
 
 
 def _free_port():
