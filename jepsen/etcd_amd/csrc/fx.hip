@@ -15,13 +15,17 @@
 //     legal(ver, val) <=> (((ver ^ nv) & nvm) | ((val ^ nl) & nlm)) == 0.
 //
 // Device layout (per rank):
-//   F, R, V lists   16-B configurations (mask over the 64 window slots,
+//   F, R lists      16-B configurations (mask over the 64 window slots,
 //                   int32 version, int32 value id); F is the frontier, R the
-//                   configurations that linearized x, V the worklist whose
-//                   levels are ranges [lo, hi) of the list
-//   R and V tables  open-addressed dedup sets: 16-B keys plus an 8-B tag
-//                   (epoch << 32 | fingerprint; fingerprint 0 = being
-//                   written), epoch bumped per return so nothing is cleared
+//                   configurations that linearized x (the next frontier)
+//   V levels        three lists of the same entries: level k of the
+//                   expansion is list k % 3 (one launch reads level k and
+//                   appends level k + 1)
+//   R and V tables  open-addressed dedup sets.  Compact (the usual case): one
+//                   64-bit word per entry, (mask, value id), claimed by one
+//                   atomicCAS and reset to EMPTY per return.  Wide: a 16-B key
+//                   plus an 8-B tag (epoch << 32 | fingerprint; fingerprint 0
+//                   = being written), epoch bumped per return
 //   candidate regions (partitioned mode) one per owner rank
 #include <hip/hip_runtime.h>
 
