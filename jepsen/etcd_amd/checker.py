@@ -90,7 +90,7 @@ class RegisterChecker:
     result is then one key's map (no :results)."""
 
     def __init__(self, model=None, device_mask=0, max_configs_per_key=0, independent=True,
-                 timeline_dir=None, time_budget_ms=0, whole_gpu=False):
+                 timeline_dir=None, time_budget_ms=0, whole_gpu=True):
         self.model = model or VersionedRegister(0, None)
         self.device_mask = device_mask
         self.max_configs_per_key = max_configs_per_key
@@ -98,7 +98,9 @@ class RegisterChecker:
         self.timeline_dir = timeline_dir
         self.time_budget_ms = time_budget_ms
         # a key one workgroup's search leaves :unknown at the configuration
-        # budget is searched again over the whole GPU (LC_FLAG_WHOLE_GPU)
+        # budget is searched again over the whole GPU (LC_FLAG_WHOLE_GPU):
+        # knossos keeps searching until it runs out of memory or time, so the
+        # drop-in does too by default (time_budget_ms bounds it)
         self.whole_gpu = whole_gpu
         self._ctx = None
 

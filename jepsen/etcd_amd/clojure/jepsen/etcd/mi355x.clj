@@ -311,7 +311,7 @@
   :cas-register, :register, :mutex.  The lock workload's checker
   (lock.clj:243-244) becomes (linearizable {:model :mutex})."
   [{:keys [model max-configs-per-key time-budget-ms whole-gpu?]
-    :or {model :versioned-register max-configs-per-key 0 time-budget-ms 0}}]
+    :or {model :versioned-register max-configs-per-key 0 time-budget-ms 0 whole-gpu? true}}]
   (reify checker/Checker
     (check [_ test history _opts]
       (let [ops (filterv client-op? history)]
@@ -354,12 +354,14 @@
   :model (default :versioned-register, register.clj:111), :timeline?
   (default true: keep register.clj:112's timeline/html per key),
   :time-budget-ms (0 = none: a key whose frontier search runs longer is
-  :unknown, as knossos's aborts are), :whole-gpu? (a key one workgroup's
-  search leaves :unknown at the configuration budget is searched again over
-  the whole GPU: LC_FLAG_WHOLE_GPU, include/lincheck_fx.h)."
+  :unknown, as knossos's aborts are), :whole-gpu? (default true: a key one
+  workgroup's search leaves :unknown at the configuration budget is searched
+  again over the whole GPU, LC_FLAG_WHOLE_GPU, include/lincheck_fx.h, as
+  knossos keeps searching until it runs out of memory or time)."
   ([] (checker {}))
   ([{:keys [max-configs-per-key model timeline? time-budget-ms whole-gpu?]
-     :or {max-configs-per-key 0 model :versioned-register timeline? true time-budget-ms 0}}]
+     :or {max-configs-per-key 0 model :versioned-register timeline? true time-budget-ms 0
+          whole-gpu? true}}]
    (reify checker/Checker
      (check [_ test history opts]
        (let [subs (subhistories history)]

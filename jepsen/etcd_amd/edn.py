@@ -130,8 +130,12 @@ def check(src, device_mask=0, independent=True, ctx=None, opts=None, model="vers
     (result map, EdnHistory); the map has independent/checker's shape with
     EDN key texts as keys."""
     h = src if isinstance(src, EdnHistory) else read(src, independent, model=model)
-    if opts is None and model == "mutex":
-        opts = abi.default_opts(init_value=0)  # the lock starts free
+    if opts is None:
+        # the lock starts free; a key one workgroup's search cannot finish
+        # within its budget gets the whole GPU (LC_FLAG_WHOLE_GPU), as knossos
+        # would keep searching until it ran out of memory
+        opts = abi.default_opts(init_value=0 if model == "mutex" else abi.LC_NIL,
+                                flags=abi.LC_FLAG_WHOLE_GPU)
     own = ctx is None
     ctx = ctx or abi.Context(device_mask)
     try:
