@@ -152,6 +152,9 @@ def main():
              [[0, ka, kb, n_ops, own * 1e3 / args.steps, float(np.mean(kms))]])
     elapsed, (total_ops, n_valid, n_invalid, n_unknown) = reduce_run(
         elapsed, n_ops, res, distributed, dev)
+    # every rank together, outside the timed region: the one collective path
+    fx_ranks = (oversized_key_ranks(abi, world, local)
+                if distributed and world > 1 and not args.bare else None)
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = total_ops * args.steps / elapsed
@@ -226,6 +229,8 @@ def main():
         "cpu_baseline": None,
         "hot_key": None,
     }
+    if fx_ranks is not None:
+        line["oversized_key_ranks"] = fx_ranks
     if rank == 0 and not args.bare:
         line["c1_leg"] = c1_leg(ctx, abi)
         line["host_leg"] = host_leg(ctx, abi, ops, key_off, n_inv)
@@ -446,6 +451,39 @@ def oversized_key_ops(abi):
     ops = ops.copy()
     ops[:, 3] = abi.LC_NIL
     return ops, off
+
+
+def oversized_key_ranks(abi, world, local):
+    """SURVEY §8(e)'s exchange on real ranks: the oversized key searched by
+    every rank together (include/lincheck_fx.h), its frontier partitioned by
+    hash owner while above 16,384 configurations, successors exchanged by an
+    all-to-all-v per level.  Collectives over a gloo group (host-staged; its
+    timeout turns a stuck collective into an error, never a hang of the
+    bench), or the RCCL group with LC_BENCH_FX_BACKEND=nccl.  Not part of
+    `value`; every rank returns the same result."""
+    import datetime
+    import torch.distributed as dist
+    from jepsen.etcd_amd.fx import FrontierExchange
+    backend = os.environ.get("LC_BENCH_FX_BACKEND", "gloo")
+    try:
+        group = (dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
+                 if backend == "gloo" else dist.group.WORLD)
+        ops, _ = oversized_key_ops(abi)
+        with FrontierExchange(device=local, group=group, part_above=16384) as fx:
+            fx.check(ops)  # warm-up (allocations)
+            dist.barrier(group=group)
+            t0 = time.perf_counter()
+            r = fx.check(ops)
+            ms = (time.perf_counter() - t0) * 1e3
+            st = fx.stats()
+        return {"ranks": world, "backend": backend, "ms": ms, "verdict": int(r["verdict"]),
+                "configs_explored": int(r["configs_explored"]),
+                "max_frontier": int(r["max_frontier"]),
+                "part_returns": st["part_returns"], "part_levels": st["part_levels"],
+                "gathers": st["gathers"], "sent_configs_rank0": st["sent_configs"],
+                "max_local_frontier_rank0": st["max_local_frontier"]}
+    except Exception as e:  # reported, never fatal to the bench line
+        return {"ranks": world, "backend": backend, "error": repr(e)}
 
 
 def oversized_key(ctx, abi):
