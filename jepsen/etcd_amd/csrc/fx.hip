@@ -1178,6 +1178,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   const bool timed = opts.time_budget_ms > 0;
   bool decided = false;
   const bool debug = getenv("LC_FX_DEBUG") != nullptr;
+  const int64_t tmul = getenv("LC_FX_TABLE_MUL") ? std::max(1, atoi(getenv("LC_FX_TABLE_MUL"))) : 4;
 
   auto slot_pre = [&](const lc_op &a, Slot &s) {
     const int32_t ver = clamp_ver(a.version);
@@ -1281,7 +1282,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     {
       // the prefix follows the recent peak (decaying), not only the last return
     work_hi = std::max<int64_t>(last_work, work_hi - work_hi / 8);
-    const int64_t guess = std::max<int64_t>(std::max<int64_t>(nF, last_work), work_hi / 2) * 4;
+    const int64_t guess = std::max<int64_t>(std::max<int64_t>(nF, last_work), work_hi / 2) * tmul;
       tlog = 12;
       while (tlog < tlog_full && (1LL << tlog) < guess) tlog++;
     }
