@@ -1179,6 +1179,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   bool decided = false;
   const bool debug = getenv("LC_FX_DEBUG") != nullptr;
   const int64_t tmul = getenv("LC_FX_TABLE_MUL") ? std::max(1, atoi(getenv("LC_FX_TABLE_MUL"))) : 4;
+  const int64_t spad = getenv("LC_FX_SPEC_PAD") ? atoi(getenv("LC_FX_SPEC_PAD")) : 1;
 
   auto slot_pre = [&](const lc_op &a, Slot &s) {
     const int32_t ver = clamp_ver(a.version);
@@ -1349,7 +1350,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         // next return: as many speculative levels as this one needed, plus one
         const int64_t used = (int64_t)hCtr->levels - levels_seen;
         levels_seen = (int64_t)hCtr->levels;
-        spec_levels = (int)std::max<int64_t>(2, std::min<int64_t>(64, used + 1));
+        spec_levels = (int)std::max<int64_t>(spad > 0 ? 2 : 1, std::min<int64_t>(64, used + spad));
         const unsigned long long ex = hCtr->explored;
         explored_repl += (int64_t)(ex - explored_seen);
         explored_seen = ex;
