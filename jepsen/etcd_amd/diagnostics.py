@@ -60,7 +60,9 @@ def step(state, op):
 
 
 def _s(x):
-    return "nil" if x is None else str(x)
+    """Clojure `str`, which the model's messages use (register.clj:78,93):
+    nil prints as the empty string."""
+    return "" if x is None else str(x)
 
 
 def _model(state):

@@ -15,8 +15,11 @@ def test_step_messages_follow_register_clj():
     assert D.step((2, 5), w) == ((3, 7), None)
     c = {"f": "cas", "value": [None, [4, 9]]}
     assert D.step((2, 5), c) == (None, "can't CAS 5 from 4 to 9")
+    # Clojure `str` prints nil as "" (register.clj:78), so does the model's message
     assert D.step((0, None), {"f": "cas", "value": [1, [0, 1]]}) == \
-        (None, "can't CAS nil from 0 to 1")
+        (None, "can't CAS  from 0 to 1")
+    assert D.step((1, None), {"f": "read", "value": [1, 3]}) == \
+        (None, "can't read 3 from register ")
     r = {"f": "read", "value": [2, 1]}
     assert D.step((3, 1), r) == (None, "can't read version 2 from version 3")
     assert D.step((2, 4), r) == (None, "can't read 1 from register 4")
