@@ -457,25 +457,39 @@ def oversized_key_ranks(abi, world, local):
     """SURVEY §8(e)'s exchange on real ranks: the oversized key searched by
     every rank together (include/lincheck_fx.h), its frontier partitioned by
     hash owner while above 16,384 configurations, successors exchanged by an
-    all-to-all-v per level.  Collectives over a gloo group (host-staged; its
-    timeout turns a stuck collective into an error, never a hang of the
-    bench), or the RCCL group with LC_BENCH_FX_BACKEND=nccl.  Not part of
-    `value`; every rank returns the same result."""
+    all-to-all-v per level.  Collectives by the library's own RCCL transport
+    (lc_fx_open_rccl: ncclCommInitRank, counts by ncclAllToAll on the device,
+    payload by grouped ncclSend / ncclRecv on the engine's stream; the unique
+    id travels over the bench's process group), with a watchdog that aborts
+    the communicators (lc_fx_abort) rather than let a stuck collective hang
+    the bench.  LC_BENCH_FX_BACKEND=gloo|nccl drives the same engine through
+    torch.distributed callbacks instead.  Not part of `value`; every rank
+    returns the same result."""
     import datetime
+    import threading
     import torch.distributed as dist
     from jepsen.etcd_amd.fx import FrontierExchange
-    backend = os.environ.get("LC_BENCH_FX_BACKEND", "gloo")
+    backend = os.environ.get("LC_BENCH_FX_BACKEND", "rccl")
+    fx = None
+    timer = None
     try:
-        group = (dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
-                 if backend == "gloo" else dist.group.WORLD)
         ops, _ = oversized_key_ops(abi)
-        with FrontierExchange(device=local, group=group, part_above=16384) as fx:
-            fx.check(ops)  # warm-up (allocations)
-            dist.barrier(group=group)
-            t0 = time.perf_counter()
-            r = fx.check(ops)
-            ms = (time.perf_counter() - t0) * 1e3
-            st = fx.stats()
+        if backend == "rccl":
+            group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
+            fx = FrontierExchange(device=local, rccl_group=group, part_above=16384)
+        else:
+            group = (dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
+                     if backend == "gloo" else dist.group.WORLD)
+            fx = FrontierExchange(device=local, group=group, part_above=16384)
+        timer = threading.Timer(120.0, fx.abort)
+        timer.daemon = True
+        timer.start()
+        fx.check(ops)  # warm-up (allocations)
+        dist.barrier(group=group)
+        t0 = time.perf_counter()
+        r = fx.check(ops)
+        ms = (time.perf_counter() - t0) * 1e3
+        st = fx.stats()
         return {"ranks": world, "backend": backend, "ms": ms, "verdict": int(r["verdict"]),
                 "configs_explored": int(r["configs_explored"]),
                 "max_frontier": int(r["max_frontier"]),
@@ -484,6 +498,11 @@ def oversized_key_ranks(abi, world, local):
                 "max_local_frontier_rank0": st["max_local_frontier"]}
     except Exception as e:  # reported, never fatal to the bench line
         return {"ranks": world, "backend": backend, "error": repr(e)}
+    finally:
+        if timer is not None:
+            timer.cancel()
+        if fx is not None:
+            fx.close()
 
 
 def oversized_key(ctx, abi):

@@ -85,9 +85,14 @@ typedef struct lc_opts {
 #define LC_FLAG_NO_GAP_TIER  4  /* skip the gap-matching tier: keys the version-order tier
                                    hands over go straight to the JIT search */
 #define LC_FLAG_WHOLE_GPU    8  /* every entry point: a key the tiers leave :unknown at the
-                                   configuration budget is searched again over the whole first
-                                   GPU (the frontier exchange, include/lincheck_fx.h), whose
-                                   budget bounds each return's configuration sets */
+                                   configuration budget is searched again by the frontier
+                                   exchange (include/lincheck_fx.h), whose budget bounds each
+                                   return's configuration sets: with fewer such keys than the
+                                   context has GPUs, each over ALL of them (one rank per GPU,
+                                   RCCL all-to-all of the hash-partitioned frontier); else
+                                   several keys at once, each over a whole GPU.  A failed
+                                   re-search leaves that key :unknown (text in lc_last_error);
+                                   the call still returns 0 */
 
 /* Verdicts: Knossos :valid? true / false / :unknown. */
 #define LC_VALID    1

@@ -27,12 +27,21 @@
  * gathered back and every rank holds (and expands) all of it, with no
  * traffic.
  *
- * The collectives are the caller's: `lc_fx_transport` is three callbacks
- * (jepsen/etcd_amd/fx.py implements them with torch.distributed — RCCL
- * over xGMI with device buffers under "nccl", host-staged under "gloo").
- * With transport == NULL and virtual_ranks = k the library runs k ranks as
- * threads on one device with an in-process transport (device copies), so the
- * partitioned path is testable on one GPU.
+ * Collectives, three ways:
+ *  - native RCCL (librccl, loaded at run time): lc_fx_open_devices runs one
+ *    rank per listed GPU of this process, each on a host thread of its own,
+ *    over communicators from ncclCommInitAll; lc_fx_open_rccl makes this
+ *    process one rank of a multi-process search (ncclCommInitRank, the id
+ *    from lc_fx_rccl_unique_id passed around by the caller).  Counts are
+ *    exchanged on the device (ncclAllToAll), configurations by grouped
+ *    ncclSend / ncclRecv straight from the per-owner regions on the engine's
+ *    stream, reductions by ncclAllReduce.  lincheck.h's LC_FLAG_WHOLE_GPU uses
+ *    lc_fx_open_devices over every GPU of the lc_ctx;
+ *  - the caller's callbacks (`lc_fx_transport`; jepsen/etcd_amd/fx.py's
+ *    TorchTransport implements them with torch.distributed);
+ *  - transport == NULL and virtual_ranks = k: k ranks as threads on one
+ *    device with an in-process transport (device copies), so the partitioned
+ *    path is testable on one GPU.
  *
  * Plain C types only.
  */
@@ -82,6 +91,12 @@ typedef struct lc_fx_params {
 /* Always use the 16-byte-key tables (epoch tags, fenced publication) instead
  * of one-word entries: for tests of that path. */
 #define LC_FX_FLAG_WIDE_TABLES 1
+/* Run the multi-rank protocol even with one rank, and send each rank's own
+ * configurations through the exchange like every other owner's: with one
+ * rank on a one-device RCCL communicator every configuration then moves
+ * through ncclSend / ncclRecv to itself (tests of the transport on a one-GPU
+ * machine; RCCL refuses two ranks on one device). */
+#define LC_FX_FLAG_EXCHANGE_SELF 2
 
 typedef struct lc_fx_stats {
   double  total_ms;         /* host wall time of the last lc_fx_check */
@@ -89,7 +104,8 @@ typedef struct lc_fx_stats {
   int64_t levels;           /* BFS levels run (replicated + partitioned) */
   int64_t part_returns;     /* returns expanded with the frontier partitioned */
   int64_t part_levels;      /* levels run partitioned (one exchange each) */
-  int64_t sent_configs;     /* configurations this rank sent to other ranks */
+  int64_t sent_configs;     /* configurations this rank sent to other ranks (and to itself,
+                               with LC_FX_FLAG_EXCHANGE_SELF) */
   int64_t gathers;          /* partitioned -> replicated switches */
   int64_t max_local_frontier; /* largest frontier share held by this rank */
   int64_t redos;            /* returns redone with a larger dedup table */
@@ -103,6 +119,20 @@ typedef struct lc_fx lc_fx;
  * Returns 0, -EINVAL, -ENODEV, -ENOMEM or -EIO (text in lc_fx_last_error). */
 int lc_fx_open(const lc_fx_params *params, const lc_fx_transport *transport, lc_fx **out);
 
+/* One engine over the GPUs devices[0 .. n_devices) of this process: rank i
+ * on devices[i] (distinct devices; RCCL refuses two ranks on one), one host
+ * thread per rank inside lc_fx_check.  -ENOSYS without a loadable librccl,
+ * -EINVAL for a list RCCL rejects (duplicates). */
+int lc_fx_open_devices(const lc_fx_params *params, const int32_t *devices, int32_t n_devices,
+                       lc_fx **out);
+
+/* Multi-process RCCL: rank 0 makes an id, every rank opens with it (params->
+ * device = this process's GPU).  ncclGetUniqueId / ncclCommInitRank. */
+#define LC_FX_RCCL_ID_BYTES 128
+int lc_fx_rccl_unique_id(uint8_t *id /* LC_FX_RCCL_ID_BYTES */);
+int lc_fx_open_rccl(const lc_fx_params *params, const uint8_t *id, int32_t rank, int32_t n_ranks,
+                    lc_fx **out);
+
 /* Decide one key: ops[0..n) are its records (lincheck.h layout, host memory,
  * sorted by call).  Every rank calls it with the same key.  `out` gets the
  * same result lc_check gives (verdict, reason, fail_op, fail_prefix_end,
@@ -110,6 +140,12 @@ int lc_fx_open(const lc_fx_params *params, const lc_fx_transport *transport, lc_
  * than LC_MAX_WINDOW open ops are :unknown (LC_REASON_WINDOW_OVERFLOW). */
 int lc_fx_check(lc_fx *fx, const lc_op *ops, int64_t n, const lc_opts *opts,
                 lc_key_result *out);
+
+/* From another thread: stop a search in progress.  Every RCCL communicator
+ * of the engine is aborted (ncclCommAbort), so ranks waiting in a collective
+ * return and lc_fx_check fails; an RCCL engine is unusable afterwards.  For
+ * in-process ranks the hub is aborted.  A watchdog's way out of a hang. */
+void lc_fx_abort(lc_fx *fx);
 
 int lc_fx_last_stats(lc_fx *fx, lc_fx_stats *out);   /* rank 0's (or this rank's) */
 const char *lc_fx_last_error(lc_fx *fx);

@@ -27,9 +27,11 @@
 //                   plus an 8-B tag (epoch << 32 | fingerprint; fingerprint 0
 //                   = being written), epoch bumped per return
 //   candidate regions (partitioned mode) one per owner rank
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <chrono>
 #include <condition_variable>
@@ -44,6 +46,46 @@
 #include <vector>
 
 #include "../../../include/lincheck_fx.h"
+#include "rccl_dl.h"
+
+// RCCL, loaded on first use.  librccl is part of ROCm; a host without it
+// keeps every single-GPU path (only lc_fx_open_devices / lc_fx_open_rccl
+// need it).
+const RcclApi &rccl_api() {
+  static RcclApi api;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void *h = nullptr;
+    for (const char *name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL))) break;
+    if (!h) {
+      api.err = std::string("cannot load librccl: ") + dlerror();
+      return;
+    }
+    bool all = true;
+    auto get = [&](auto &fp, const char *sym) {
+      fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, sym));
+      if (!fp) {
+        all = false;
+        api.err += std::string(api.err.empty() ? "librccl lacks " : ", ") + sym;
+      }
+    };
+    get(api.GetUniqueId, "ncclGetUniqueId");
+    get(api.CommInitAll, "ncclCommInitAll");
+    get(api.CommInitRank, "ncclCommInitRank");
+    get(api.CommDestroy, "ncclCommDestroy");
+    get(api.CommAbort, "ncclCommAbort");
+    get(api.GroupStart, "ncclGroupStart");
+    get(api.GroupEnd, "ncclGroupEnd");
+    get(api.Send, "ncclSend");
+    get(api.Recv, "ncclRecv");
+    get(api.AllReduce, "ncclAllReduce");
+    get(api.AllToAll, "ncclAllToAll");
+    get(api.GetErrorString, "ncclGetErrorString");
+    api.ok = all;
+  });
+  return api;
+}
 
 namespace {
 
@@ -846,10 +888,36 @@ int hub_allreduce(void *u, int64_t *vals, int32_t n, int32_t op) {
     }                                                                         \
   } while (0)
 
+#define NC_TRY(expr)                                                          \
+  do {                                                                        \
+    ncclResult_t r_ = (expr);                                                 \
+    if (r_ != ncclSuccess) {                                                  \
+      err = std::string(#expr) + ": " + nc->api->GetErrorString(r_);          \
+      return -EIO;                                                            \
+    }                                                                         \
+  } while (0)
+
+// A rank's RCCL communicator (lc_fx_open_devices / lc_fx_open_rccl), with a
+// small device + pinned host scratch for the count exchange and the
+// reductions.
+struct Nccl {
+  const RcclApi *api = nullptr;
+  ncclComm_t comm = nullptr;
+  int64_t *d = nullptr;  // kScr int64: [0, 64) send counts / values, [64, 128) received
+  int64_t *h = nullptr;
+  bool aborted = false;  // ncclCommAbort freed the communicator
+  static constexpr int kScr = 192;
+};
+
 struct Rank {
   int dev = 0;
   int rank = 0, P = 1;
   lc_fx_transport tr{};
+  Nccl *nc = nullptr;       // collectives over RCCL instead of tr
+  bool xself = false;       // LC_FX_FLAG_EXCHANGE_SELF: own candidates go through the exchange too
+  // the search runs the multi-rank protocol (ownership, exchange, reductions):
+  // several ranks, or one rank exchanging with itself
+  bool multi() const { return P > 1 || xself; }
   int64_t part_above = 65536, repl_below = 16384;
   int table_log2 = 0;
   bool force_wide = false;  // LC_FX_FLAG_WIDE_TABLES (tests)
@@ -890,8 +958,85 @@ struct Rank {
     hWin = nullptr;
     hCtr = nullptr;
     list_cap = 0;
+    if (nc) {
+      if (nc->d) (void)hipFree(nc->d);
+      if (nc->h) (void)hipHostFree(nc->h);
+      if (nc->comm && !nc->aborted) (void)nc->api->CommDestroy(nc->comm);
+      delete nc;
+      nc = nullptr;
+    }
     if (st) (void)hipStreamDestroy(st);
     st = nullptr;
+  }
+
+  // ---- collectives: the caller's callbacks / the in-process hub (tr), or
+  // RCCL on this rank's stream (nc).  Every rank calls them in one order.
+  int coll_counts(const int64_t *send, int64_t *recv) {
+    if (!nc) return tr.exchange_counts(tr.user, send, recv);
+    FX_TRY(hipMemcpyAsync(nc->d, send, sizeof(int64_t) * P, hipMemcpyHostToDevice, st));
+    NC_TRY(nc->api->AllToAll(nc->d, nc->d + 64, 1, ncclInt64, nc->comm, st));
+    FX_TRY(hipMemcpyAsync(nc->h, nc->d + 64, sizeof(int64_t) * P, hipMemcpyDeviceToHost, st));
+    FX_TRY(hipStreamSynchronize(st));
+    std::memcpy(recv, nc->h, sizeof(int64_t) * P);
+    return 0;
+  }
+
+  // Grouped point-to-point sends and receives on the engine's stream: no host
+  // synchronisation (the inserts that read d_recv follow on the same stream).
+  int nc_a2av(const char *const *src, const int64_t *sc, char *d_recv, const int64_t *rc,
+              int64_t bytes) {
+    NC_TRY(nc->api->GroupStart());
+    int64_t roff = 0;
+    for (int j = 0; j < P; j++) {
+      if (sc[j]) {
+        const ncclResult_t r = nc->api->Send(src[j], (size_t)(sc[j] * bytes / 8), ncclUint64, j,
+                                             nc->comm, st);
+        if (r != ncclSuccess) {
+          (void)nc->api->GroupEnd();
+          err = std::string("ncclSend: ") + nc->api->GetErrorString(r);
+          return -EIO;
+        }
+      }
+      if (rc[j]) {
+        const ncclResult_t r = nc->api->Recv(d_recv + roff * bytes, (size_t)(rc[j] * bytes / 8),
+                                             ncclUint64, j, nc->comm, st);
+        if (r != ncclSuccess) {
+          (void)nc->api->GroupEnd();
+          err = std::string("ncclRecv: ") + nc->api->GetErrorString(r);
+          return -EIO;
+        }
+      }
+      roff += rc[j];
+    }
+    NC_TRY(nc->api->GroupEnd());
+    return 0;
+  }
+
+  int coll_a2av(const void *d_send, const int64_t *sc, void *d_recv, const int64_t *rc,
+                int64_t bytes) {
+    if (!nc) return tr.alltoallv(tr.user, d_send, sc, d_recv, rc, bytes);
+    std::vector<const char *> src(P);
+    int64_t off = 0;
+    for (int j = 0; j < P; j++) {
+      src[j] = static_cast<const char *>(d_send) + off * bytes;
+      off += sc[j];
+    }
+    return nc_a2av(src.data(), sc, static_cast<char *>(d_recv), rc, bytes);
+  }
+
+  int coll_allreduce(int64_t *vals, int n, int op) {
+    if (!nc) return tr.allreduce(tr.user, vals, n, op);
+    if (n > Nccl::kScr) {
+      err = "allreduce: too many values";
+      return -EINVAL;
+    }
+    FX_TRY(hipMemcpyAsync(nc->d, vals, sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
+    NC_TRY(nc->api->AllReduce(nc->d, nc->d, (size_t)n, ncclInt64, op == LC_FX_MAX ? ncclMax : ncclSum,
+                              nc->comm, st));
+    FX_TRY(hipMemcpyAsync(nc->h, nc->d, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+    FX_TRY(hipStreamSynchronize(st));
+    std::memcpy(vals, nc->h, sizeof(int64_t) * n);
+    return 0;
   }
 
   int open() {
@@ -904,11 +1049,19 @@ struct Rank {
     FX_TRY(hipHostMalloc(&hWin, sizeof(Win), hipHostMallocDefault));
     FX_TRY(hipHostMalloc(&hCtr, sizeof(Ctr), hipHostMallocDefault));
     std::memset(hWin, 0, sizeof(Win));
+    if (nc) {
+      FX_TRY(hipMalloc(&nc->d, sizeof(int64_t) * Nccl::kScr));
+      FX_TRY(hipHostMalloc(&nc->h, sizeof(int64_t) * Nccl::kScr, hipHostMallocDefault));
+    }
     return 0;
   }
 
   // Lists and tables for a budget of `budget` configurations.
   int reserve(int64_t budget) {
+    if (const char *f = getenv("LC_FX_FAIL_RESERVE"); f && f[0] == '1') {
+      err = "list allocation failed (injected: LC_FX_FAIL_RESERVE)";  // test hook
+      return -ENOMEM;
+    }
     unsigned long long need = (unsigned long long)budget + 1;
     int lg = table_log2;
     if (lg <= 0) {
@@ -933,7 +1086,7 @@ struct Rank {
     list_cap = need;
     tmask = tcap - 1;
     epoch = 0;
-    if (P > 1 && !cand) {
+    if (multi() && !cand) {
       cand_cap = 1ULL << 21;  // per owner: a chunk of cand_cap / 64 configurations
       FX_TRY(hipMalloc(&cand, (size_t)P * cand_cap * sizeof(Cfg)));
     }
@@ -990,20 +1143,25 @@ struct Rank {
       if (nF)
         FX_TRY(hipMemcpyAsync(sendb + (size_t)j * nF, F, nF * sizeof(Cfg), hipMemcpyDeviceToDevice, st));
     FX_TRY(hipStreamSynchronize(st));
-    FX_COLL(tr.exchange_counts(tr.user, sc.data(), rc.data()));
+    FX_COLL(coll_counts(sc.data(), rc.data()));
     int64_t tot = 0;
     for (int j = 0; j < P; j++) tot += rc[j];
     if ((unsigned long long)tot > list_cap) {
       err = "gathered frontier exceeds the list capacity";
       return -ENOMEM;
     }
-    FX_COLL(tr.alltoallv(tr.user, sendb, sc.data(), F, rc.data(), sizeof(Cfg)));
+    FX_COLL(coll_a2av(sendb, sc.data(), F, rc.data(), sizeof(Cfg)));
     *nOut = tot;
     stats.gathers++;
     return 0;
   }
 
   // One partitioned level chunk: candidates of V[a, b) to their owners.
+  // Over RCCL the per-owner counts the expand kernel left in dCtr->cand are
+  // exchanged on the device (one all-to-all of P words, read back with the
+  // counters in one copy), and each owner's region is sent straight from
+  // where the kernel wrote it (grouped ncclSend / ncclRecv, no packing, no
+  // host synchronisation before the inserts that follow on the stream).
   int part_chunk(int64_t a, int64_t b, const Tabs &tb) {
     FX_TRY(hipMemsetAsync(dCtr->cand, 0, sizeof(unsigned long long) * P, st));
     if (b > a) {
@@ -1011,35 +1169,54 @@ struct Rank {
       fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tb, epoch, dCtr, 0, a, b, cand, cand_cap);
       FX_TRY(hipGetLastError());
     }
-    if (int e = sync_ctr()) return e;
     std::vector<int64_t> sc(P), rc(P);
-    int64_t tot_send = 0;
-    for (int j = 0; j < P; j++) {
-      const unsigned long long c = std::min<unsigned long long>(hCtr->cand[j], cand_cap);
-      sc[j] = j == rank ? 0 : (int64_t)c;
-      tot_send += sc[j];
+    if (nc) {
+      static_assert(sizeof(unsigned long long) == sizeof(int64_t), "count words");
+      NC_TRY(nc->api->AllToAll(dCtr->cand, nc->d + 64, 1, ncclInt64, nc->comm, st));
+      FX_TRY(hipMemcpyAsync(nc->h + 64, nc->d + 64, sizeof(int64_t) * P, hipMemcpyDeviceToHost, st));
     }
-    // own candidates are inserted directly
-    const int64_t self = (int64_t)std::min<unsigned long long>(hCtr->cand[rank], cand_cap);
+    if (int e = sync_ctr()) return e;
+    int64_t tot_send = 0, tot = 0;
+    for (int j = 0; j < P; j++) {
+      const bool peer = j != rank || xself;  // own candidates are inserted directly
+      sc[j] = peer ? (int64_t)std::min<unsigned long long>(hCtr->cand[j], cand_cap) : 0;
+      // (a sender clamps an overflowing region to cand_cap and raises the
+      // overflow flag, which makes the level :unknown on every rank)
+      if (nc) rc[j] = peer ? std::min<int64_t>(nc->h[64 + j], (int64_t)cand_cap) : 0;
+      tot_send += sc[j];  // (its own only with LC_FX_FLAG_EXCHANGE_SELF)
+    }
+    const int64_t self =
+        xself ? 0 : (int64_t)std::min<unsigned long long>(hCtr->cand[rank], cand_cap);
     if (self) {
       fx_insert_kernel<<<grid_for(self), 256, 0, st>>>(cand + (size_t)rank * cand_cap, self, dWin,
                                                       tb, epoch, dCtr);
       FX_TRY(hipGetLastError());
     }
-    if (int e = ensure_buf(&sendb, &send_cap, (size_t)std::max<int64_t>(tot_send, 1))) return e;
-    int64_t off = 0;
-    for (int j = 0; j < P; j++) {
-      if (sc[j])
-        FX_TRY(hipMemcpyAsync(sendb + off, cand + (size_t)j * cand_cap, sc[j] * sizeof(Cfg),
-                              hipMemcpyDeviceToDevice, st));
-      off += sc[j];
+    if (nc) {
+      for (int j = 0; j < P; j++) tot += rc[j];
+      if (int e = ensure_buf(&recvb, &recv_cap, (size_t)std::max<int64_t>(tot, 1))) return e;
+      std::vector<const char *> src(P);
+      for (int j = 0; j < P; j++)
+        src[j] = reinterpret_cast<const char *>(cand + (size_t)j * cand_cap);
+      FX_COLL(nc_a2av(src.data(), sc.data(), reinterpret_cast<char *>(recvb), rc.data(),
+                      sizeof(Cfg)));
+    } else {
+      int64_t n_send = 0;
+      for (int j = 0; j < P; j++) n_send += sc[j];
+      if (int e = ensure_buf(&sendb, &send_cap, (size_t)std::max<int64_t>(n_send, 1))) return e;
+      int64_t off = 0;
+      for (int j = 0; j < P; j++) {
+        if (sc[j])
+          FX_TRY(hipMemcpyAsync(sendb + off, cand + (size_t)j * cand_cap, sc[j] * sizeof(Cfg),
+                                hipMemcpyDeviceToDevice, st));
+        off += sc[j];
+      }
+      FX_TRY(hipStreamSynchronize(st));
+      FX_COLL(coll_counts(sc.data(), rc.data()));
+      for (int j = 0; j < P; j++) tot += rc[j];
+      if (int e = ensure_buf(&recvb, &recv_cap, (size_t)std::max<int64_t>(tot, 1))) return e;
+      FX_COLL(coll_a2av(sendb, sc.data(), recvb, rc.data(), sizeof(Cfg)));
     }
-    FX_TRY(hipStreamSynchronize(st));
-    FX_COLL(tr.exchange_counts(tr.user, sc.data(), rc.data()));
-    int64_t tot = 0;
-    for (int j = 0; j < P; j++) tot += rc[j];
-    if (int e = ensure_buf(&recvb, &recv_cap, (size_t)std::max<int64_t>(tot, 1))) return e;
-    FX_COLL(tr.alltoallv(tr.user, sendb, sc.data(), recvb, rc.data(), sizeof(Cfg)));
     stats.sent_configs += tot_send;
     if (tot) {
       fx_insert_kernel<<<grid_for(tot), 256, 0, st>>>(recvb, tot, dWin, tb, epoch, dCtr);
@@ -1225,7 +1402,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         sl.zob = 0;
         // closure: the new read is linearized wherever it is legal now (one
         // rank: by the next split, as it reads the frontier)
-        if (P == 1) {
+        if (!multi()) {
           fclose |= sb;
         } else if (nF) {
           fx_close_read_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, sb, sl);
@@ -1255,9 +1432,9 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     w.fclear = fclear;
     w.fclose = fclose;
     fclear = fclose = 0;
-    if (P > 1) FX_TRY(hipMemcpyAsync(dWin, &w, sizeof(Win), hipMemcpyHostToDevice, st));
+    if (multi()) FX_TRY(hipMemcpyAsync(dWin, &w, sizeof(Win), hipMemcpyHostToDevice, st));
     // mode switches (several ranks only)
-    if (P > 1 && !part && nFglobal > part_above) {
+    if (multi() && !part && nFglobal > part_above) {
       FX_TRY(hipMemsetAsync(&dCtr->nsel, 0, sizeof(unsigned long long), st));
       fx_filter_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, dWin, tmp, list_cap, dCtr);
       FX_TRY(hipGetLastError());
@@ -1265,7 +1442,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       std::swap(F, tmp);
       nF = (int64_t)hCtr->nsel;
       part = true;
-    } else if (P > 1 && part && nFglobal < repl_below) {
+    } else if (multi() && part && nFglobal < repl_below) {
       int64_t tot = 0;
       if (int er = gather_all(nF, &tot)) return er;
       nF = tot;
@@ -1301,7 +1478,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       {
         const int64_t words = compact ? (int64_t)1 << tlog : 0;
         fx_reset_kernel<<<grid_for(words), 256, 0, st>>>(dCtr, explored_seen, dExp, tagR, tagV,
-                                                          words, kEmpty, dWin, w, P == 1);
+                                                          words, kEmpty, dWin, w, !multi());
         FX_TRY(hipGetLastError());
       }
       bool tfull = false;
@@ -1339,14 +1516,31 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           if (hCtr->cnt[k % 3] == 0) break;  // the last level found nothing new
           spec_levels = std::min(spec_levels * 2, 64);
         }
-        if (hCtr->tfull && tlog < tlog_full) {
-          tlog = std::min(tlog + 2, tlog_full);
-          stats.redos++;
-          continue;
+        const bool my_tfull = hCtr->tfull != 0;
+        const bool my_redo = my_tfull && tlog < tlog_full;
+        const bool my_over = my_tfull || hCtr->overflow ||
+                             (int64_t)(hCtr->nR + hCtr->nV + hCtr->cnt[k % 3]) > budget;
+        if (multi()) {
+          // A probe chain's length depends on the order of the atomic inserts,
+          // so ranks expanding the same replicated frontier may disagree on
+          // tfull: agree, so that every rank takes the same branch (and makes
+          // the same collectives) next.  Full at full size anywhere: :unknown.
+          int64_t v[3] = {my_redo ? 1 : 0, my_tfull && !my_redo ? 1 : 0, my_over ? 1 : 0};
+          FX_COLL(coll_allreduce(v, 3, LC_FX_SUM));
+          if (!v[1] && v[0]) {
+            if (my_redo) tlog = std::min(tlog + 2, tlog_full);
+            stats.redos++;
+            continue;
+          }
+          over = v[1] || v[2];
+        } else {
+          if (my_redo) {
+            tlog = std::min(tlog + 2, tlog_full);
+            stats.redos++;
+            continue;
+          }
+          over = my_over;
         }
-        if (hCtr->tfull || hCtr->overflow ||
-            (int64_t)(hCtr->nR + hCtr->nV + hCtr->cnt[k % 3]) > budget)
-          over = true;
         // next return: as many speculative levels as this one needed, plus one
         const int64_t used = (int64_t)hCtr->levels - levels_seen;
         levels_seen = (int64_t)hCtr->levels;
@@ -1358,9 +1552,9 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         last_work = (int64_t)(hCtr->nR + hCtr->nV);
         if (timed) timeout = std::chrono::duration<double, std::milli>(
                                  std::chrono::steady_clock::now() - t0).count() > (double)opts.time_budget_ms;
-        if (P > 1 && timed) {
+        if (multi() && timed) {
           int64_t v[1] = {timeout ? 1 : 0};
-          FX_COLL(tr.allreduce(tr.user, v, 1, LC_FX_SUM));
+          FX_COLL(coll_allreduce(v, 1, LC_FX_SUM));
           timeout = v[0] > 0;
         }
         break;
@@ -1388,7 +1582,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         int64_t v[6] = {pos < n_k ? 1 : 0, n_next,
                         (int64_t)hCtr->nR + v_done + n_k + n_next, (int64_t)hCtr->overflow ? 1 : 0,
                         timeout ? 1 : 0, (int64_t)hCtr->tfull ? 1 : 0};
-        FX_COLL(tr.allreduce(tr.user, v, 6, LC_FX_SUM));
+        FX_COLL(coll_allreduce(v, 6, LC_FX_SUM));
         if (v[5]) {  // some rank's table is too small: every rank redoes the return
           tfull = true;
           break;
@@ -1412,9 +1606,12 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       }
       const int64_t part_v = v_done;  // V entries of this return on this rank
       if (tfull) {
-        if (hCtr->tfull && tlog < tlog_full) tlog = std::min(tlog + 2, tlog_full);
-        int64_t v[1] = {hCtr->tfull && tlog >= tlog_full ? 1 : 0};  // full size and still full
-        FX_COLL(tr.allreduce(tr.user, v, 1, LC_FX_SUM));
+        // "full at full size" must be judged on the table this attempt used,
+        // before it grows: a table grown to full size here has not been tried
+        const bool at_full = tlog >= tlog_full;
+        if (hCtr->tfull && !at_full) tlog = std::min(tlog + 2, tlog_full);
+        int64_t v[1] = {hCtr->tfull && at_full ? 1 : 0};  // full size and still full
+        FX_COLL(coll_allreduce(v, 1, LC_FX_SUM));
         if (!v[0]) {
           stats.redos++;
           continue;
@@ -1433,7 +1630,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       int64_t v[1 + kW];
       v[0] = (int64_t)hCtr->nR;
       for (int b = 0; b < kW; b++) v[1 + b] = ((hCtr->andmask >> b) & 1) ? 0 : 1;
-      FX_COLL(tr.allreduce(tr.user, v, 1 + kW, LC_FX_SUM));
+      FX_COLL(coll_allreduce(v, 1 + kW, LC_FX_SUM));
       nRg = v[0];
       unsigned long long gand = 0;
       for (int b = 0; b < kW; b++)
@@ -1476,7 +1673,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
               rank, x, sx, (int)part, (long long)nF, (long long)nFglobal, hCtr->nV, hCtr->explored,
               hCtr->andmask, (unsigned long long)occ);
     if (all) {
-      if (P == 1) {
+      if (!multi()) {
         fclear |= all;  // applied by the next split
       } else if (nF) {
         fx_clear_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, all);
@@ -1494,9 +1691,9 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   }
   // every rank reports the same totals
   int64_t tot_part = explored_part;
-  if (P > 1) {
+  if (multi()) {
     int64_t v[1] = {explored_part};
-    FX_COLL(tr.allreduce(tr.user, v, 1, LC_FX_SUM));
+    FX_COLL(coll_allreduce(v, 1, LC_FX_SUM));
     tot_part = v[0];
   }
   res->configs_explored = 1 + explored_repl + tot_part;
@@ -1511,13 +1708,48 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
 
 struct lc_fx {
   lc_fx_params params{};
-  bool virt = false;
-  std::vector<Rank *> ranks;    // virtual: P of them; real: one
-  std::unique_ptr<Hub> hub;
+  bool threads = false;         // several ranks of this process, one host thread each
+  std::atomic<bool> broken{false};  // its RCCL communicators were aborted (failure, lc_fx_abort)
+  std::mutex abort_mu;
+  std::vector<Rank *> ranks;    // threads: all of them; else this process's one rank
+  std::unique_ptr<Hub> hub;     // in-process transport (virtual ranks)
   std::vector<HubRank> hub_ranks;
   std::string err;
   lc_fx_stats stats{};
 };
+
+namespace {
+
+void configure(Rank *r, const lc_fx_params *params) {
+  if (params->part_above >= 0) r->part_above = params->part_above;
+  r->repl_below = params->repl_below >= 0 ? params->repl_below : r->part_above / 4;
+  r->table_log2 = (int)params->table_log2;
+  r->force_wide = (params->flags & LC_FX_FLAG_WIDE_TABLES) != 0;
+  r->xself = (params->flags & LC_FX_FLAG_EXCHANGE_SELF) != 0;
+}
+
+// Abort every RCCL communicator of the engine (once): collectives waiting on
+// a rank that failed or hangs return, and the engine is unusable after.
+void abort_comms(lc_fx *fx) {
+  std::lock_guard<std::mutex> g(fx->abort_mu);
+  for (Rank *r : fx->ranks)
+    if (r->nc && r->nc->comm && !r->nc->aborted) {
+      (void)r->nc->api->CommAbort(r->nc->comm);
+      r->nc->aborted = true;
+    }
+  fx->broken = true;
+}
+
+int open_ranks(lc_fx *fx) {
+  for (Rank *r : fx->ranks)
+    if (int e = r->open()) {
+      fx->err = r->err;
+      return e;
+    }
+  return 0;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -1527,24 +1759,21 @@ int lc_fx_open(const lc_fx_params *params, const lc_fx_transport *transport, lc_
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -ENODEV;
   if (params->device < 0 || params->device >= ndev) return -ENODEV;
-  lc_fx *fx = new lc_fx();
-  fx->params = *params;
   int P = 1;
   if (transport) {
     if (transport->n_ranks < 1 || transport->n_ranks > 64 || transport->rank < 0 ||
         transport->rank >= transport->n_ranks || !transport->exchange_counts ||
-        !transport->alltoallv || !transport->allreduce) {
-      delete fx;
+        !transport->alltoallv || !transport->allreduce)
       return -EINVAL;
-    }
     P = transport->n_ranks;
   } else {
     P = std::max(1, params->virtual_ranks);
-    if (P > 64) {
-      delete fx;
-      return -EINVAL;
-    }
-    fx->virt = true;
+    if (P > 64) return -EINVAL;
+  }
+  lc_fx *fx = new lc_fx();
+  fx->params = *params;
+  if (!transport) {
+    fx->threads = P > 1;
     fx->hub.reset(new Hub(P));
     fx->hub_ranks.resize(P);
   }
@@ -1566,16 +1795,93 @@ int lc_fx_open(const lc_fx_params *params, const lc_fx_transport *transport, lc_
       r->tr.alltoallv = hub_alltoallv;
       r->tr.allreduce = hub_allreduce;
     }
-    if (params->part_above >= 0) r->part_above = params->part_above;
-    r->repl_below = params->repl_below >= 0 ? params->repl_below : r->part_above / 4;
-    r->table_log2 = (int)params->table_log2;
-    r->force_wide = (params->flags & LC_FX_FLAG_WIDE_TABLES) != 0;
+    configure(r, params);
     fx->ranks.push_back(r);
-    if (int e = r->open()) {
-      fx->err = r->err;
-      lc_fx_close(fx);
-      return e;
-    }
+  }
+  if (int e = open_ranks(fx)) {
+    lc_fx_close(fx);
+    return e;
+  }
+  *out = fx;
+  return 0;
+}
+
+int lc_fx_open_devices(const lc_fx_params *params, const int32_t *devices, int32_t n_devices,
+                       lc_fx **out) {
+  if (!params || !out || !devices || n_devices < 1 || n_devices > 64) return -EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -ENODEV;
+  for (int i = 0; i < n_devices; i++)
+    if (devices[i] < 0 || devices[i] >= ndev) return -ENODEV;
+  const RcclApi &api = rccl_api();
+  if (!api.ok) return -ENOSYS;
+  std::vector<ncclComm_t> comms((size_t)n_devices, nullptr);
+  std::vector<int> devlist(devices, devices + n_devices);
+  const ncclResult_t nr = api.CommInitAll(comms.data(), n_devices, devlist.data());
+  if (nr != ncclSuccess) return nr == ncclInvalidUsage || nr == ncclInvalidArgument ? -EINVAL : -EIO;
+  lc_fx *fx = new lc_fx();
+  fx->params = *params;
+  fx->threads = n_devices > 1;
+  for (int i = 0; i < n_devices; i++) {
+    Rank *r = new Rank();
+    r->dev = devices[i];
+    r->P = n_devices;
+    r->rank = i;
+    r->nc = new Nccl();
+    r->nc->api = &api;
+    r->nc->comm = comms[(size_t)i];
+    configure(r, params);
+    fx->ranks.push_back(r);
+  }
+  if (int e = open_ranks(fx)) {
+    lc_fx_close(fx);
+    return e;
+  }
+  *out = fx;
+  return 0;
+}
+
+int lc_fx_rccl_unique_id(uint8_t *id) {
+  if (!id) return -EINVAL;
+  const RcclApi &api = rccl_api();
+  if (!api.ok) return -ENOSYS;
+  ncclUniqueId u;
+  if (api.GetUniqueId(&u) != ncclSuccess) return -EIO;
+  static_assert(sizeof(u) == LC_FX_RCCL_ID_BYTES, "ncclUniqueId size");
+  std::memcpy(id, &u, sizeof u);
+  return 0;
+}
+
+int lc_fx_open_rccl(const lc_fx_params *params, const uint8_t *id, int32_t rank, int32_t n_ranks,
+                    lc_fx **out) {
+  if (!params || !out || !id || n_ranks < 1 || n_ranks > 64 || rank < 0 || rank >= n_ranks)
+    return -EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -ENODEV;
+  if (params->device < 0 || params->device >= ndev) return -ENODEV;
+  const RcclApi &api = rccl_api();
+  if (!api.ok) return -ENOSYS;
+  if (hipSetDevice(params->device) != hipSuccess) return -EIO;
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  ncclComm_t comm = nullptr;
+  if (api.CommInitRank(&comm, n_ranks, u, rank) != ncclSuccess) return -EIO;
+  lc_fx *fx = new lc_fx();
+  fx->params = *params;
+  Rank *r = new Rank();
+  r->dev = params->device;
+  r->P = n_ranks;
+  r->rank = rank;
+  r->nc = new Nccl();
+  r->nc->api = &api;
+  r->nc->comm = comm;
+  configure(r, params);
+  fx->ranks.push_back(r);
+  if (int e = open_ranks(fx)) {
+    lc_fx_close(fx);
+    return e;
   }
   *out = fx;
   return 0;
@@ -1583,7 +1889,11 @@ int lc_fx_open(const lc_fx_params *params, const lc_fx_transport *transport, lc_
 
 int lc_fx_check(lc_fx *fx, const lc_op *ops, int64_t n, const lc_opts *opts, lc_key_result *out) {
   if (!fx || !out || n < 0 || (n > 0 && !ops)) return -EINVAL;
-  if (!fx->virt) {
+  if (fx->broken) {
+    fx->err = "the engine's RCCL communicators were aborted after an earlier failure";
+    return -EIO;
+  }
+  if (!fx->threads) {
     Rank *r = fx->ranks[0];
     (void)hipSetDevice(r->dev);
     const int e = r->check(ops, n, opts, out);
@@ -1592,8 +1902,11 @@ int lc_fx_check(lc_fx *fx, const lc_op *ops, int64_t n, const lc_opts *opts, lc_
     return e;
   }
   const int P = (int)fx->ranks.size();
-  fx->hub.reset(new Hub(P));
-  for (int i = 0; i < P; i++) fx->hub_ranks[i].hub = fx->hub.get();
+  if (fx->hub) {
+    std::lock_guard<std::mutex> g(fx->abort_mu);
+    fx->hub.reset(new Hub(P));
+    for (int i = 0; i < P; i++) fx->hub_ranks[i].hub = fx->hub.get();
+  }
   std::vector<lc_key_result> res(P);
   std::vector<int> rc(P, 0);
   std::vector<std::thread> th;
@@ -1601,7 +1914,15 @@ int lc_fx_check(lc_fx *fx, const lc_op *ops, int64_t n, const lc_opts *opts, lc_
     th.emplace_back([&, i] {
       (void)hipSetDevice(fx->ranks[i]->dev);
       rc[i] = fx->ranks[i]->check(ops, n, opts, &res[i]);
-      if (rc[i]) fx->hub->abort();
+      if (!rc[i]) return;
+      if (fx->hub) {
+        std::lock_guard<std::mutex> g(fx->abort_mu);
+        fx->hub->abort();
+      } else {
+        // the other ranks may be waiting in a collective that will never
+        // complete: abort every communicator (RCCL's kernels then exit)
+        abort_comms(fx);
+      }
     });
   for (auto &t : th) t.join();
   for (int i = 0; i < P; i++)
@@ -1622,6 +1943,17 @@ int lc_fx_check(lc_fx *fx, const lc_op *ops, int64_t n, const lc_opts *opts, lc_
   *out = res[0];
   fx->stats = fx->ranks[0]->stats;
   return 0;
+}
+
+void lc_fx_abort(lc_fx *fx) {
+  if (!fx) return;
+  {
+    std::lock_guard<std::mutex> g(fx->abort_mu);
+    if (fx->hub) fx->hub->abort();
+  }
+  bool rccl = false;
+  for (Rank *r : fx->ranks) rccl |= r->nc != nullptr;
+  if (rccl) abort_comms(fx);
 }
 
 int lc_fx_last_stats(lc_fx *fx, lc_fx_stats *out) {

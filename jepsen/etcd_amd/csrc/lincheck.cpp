@@ -146,7 +146,11 @@ struct Dev {
 
 struct lc_ctx {
   std::vector<Dev> devs;
-  std::vector<lc_fx *> fxs;  // LC_FLAG_WHOLE_GPU: frontier-exchange engines, opened on first use
+  // LC_FLAG_WHOLE_GPU: frontier-exchange engines, opened on first use —
+  // single-GPU ones (engine, device) and one over every GPU of the context
+  std::vector<std::pair<lc_fx *, int>> fxs;
+  lc_fx *fx_all = nullptr;
+  bool fx_all_failed = false;
   std::string err;
   std::mutex err_mu;
   lc_stats stats{};
@@ -516,56 +520,128 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
 
 // LC_FLAG_WHOLE_GPU: keys the tiers left :unknown at the configuration
 // budget (one workgroup's HBM sets were not enough) are searched again by the
-// frontier exchange over the whole first GPU (include/lincheck_fx.h), whose
-// budget bounds each return's configuration sets, as the oracle's does; its
-// result replaces the tiers' (verdict, fail op, explored, frontier).  Several
-// such keys are searched at once, each by its own engine (own stream and
-// tables): one key's levels are latency-bound, so concurrent searches fill the
-// GPU the way one cannot.  fetch(k, records) and store(k, result) move a key
-// between the caller's memory (host or device) and the engine.
+// frontier exchange (include/lincheck_fx.h), whose budget bounds each
+// return's configuration sets, as the oracle's does; its result replaces the
+// tiers' (verdict, fail op, explored, frontier).  fetch(k, records) and
+// store(k, result) move a key between the caller's memory (host or device)
+// and the engine.
+//
+// * Fewer such keys than the context has GPUs: each key's search spans every
+//   GPU of the context — one rank per GPU over RCCL (lc_fx_open_devices),
+//   the frontier partitioned by hash owner while it is large.
+//   Device contexts that share one GPU (LC_VIRTUAL_DEVICES) run their ranks
+//   in process instead (RCCL refuses two ranks on one device).
+// * Otherwise keys are independent (register.clj:108): up to kFxEngines
+//   single-GPU engines per GPU search different keys at once (one key's
+//   levels are latency-bound, so concurrent searches fill a GPU the way one
+//   cannot), as many as the GPU's free memory holds.
+//
+// A failure of the re-search (an allocation, say) is this key's alone: it
+// keeps the tiers' :unknown, the error text goes to lc_last_error, and the
+// call still succeeds — as jepsen.independent loses only the key whose check
+// throws.
 int whole_gpu(lc_ctx *c, const std::vector<int64_t> &todo, const lc_opts *opts,
               const std::function<int(int64_t, std::vector<lc_op> &)> &fetch,
               const std::function<int(int64_t, const lc_key_result &)> &store) {
-  const int ne = (int)std::min<size_t>(kFxEngines, todo.size());
-  while ((int)c->fxs.size() < ne) {
-    lc_fx_params fp{};
-    fp.device = c->devs[0].id;
-    fp.virtual_ranks = 1;
-    fp.part_above = -1;
-    fp.repl_below = -1;
-    lc_fx *f = nullptr;
-    if (int e = lc_fx_open(&fp, nullptr, &f)) {
-      set_err(c, "lc_fx_open failed");
-      return e;
+  if (todo.empty()) return 0;
+  std::vector<int> ids;  // the context's distinct GPUs
+  for (const Dev &d : c->devs)
+    if (std::find(ids.begin(), ids.end(), d.id) == ids.end()) ids.push_back(d.id);
+  const int nranks = (int)c->devs.size();
+  std::atomic<int> failed{0};
+  auto note = [&](int64_t k, const std::string &what) {
+    failed++;
+    set_err(c, "LC_FLAG_WHOLE_GPU: key " + std::to_string(k) + " kept :unknown: " + what);
+  };
+  if (nranks > 1 && todo.size() < (size_t)nranks) {
+    if (!c->fx_all && !c->fx_all_failed) {
+      lc_fx_params fp{};
+      fp.part_above = -1;
+      fp.repl_below = -1;
+      int e;
+      if ((int)ids.size() == nranks) {
+        e = lc_fx_open_devices(&fp, ids.data(), (int32_t)ids.size(), &c->fx_all);
+      } else {
+        fp.device = ids[0];
+        fp.virtual_ranks = nranks;
+        e = lc_fx_open(&fp, nullptr, &c->fx_all);
+      }
+      if (e) {
+        c->fx_all = nullptr;
+        c->fx_all_failed = true;  // (e.g. no librccl) the single-GPU engines below take over
+        set_err(c, "LC_FLAG_WHOLE_GPU: multi-GPU frontier exchange unavailable (" +
+                       std::to_string(e) + "); searching keys one GPU each");
+      }
     }
-    c->fxs.push_back(f);
+    if (c->fx_all) {
+      std::vector<lc_op> recs;
+      for (int64_t k : todo) {
+        if (int x = fetch(k, recs)) return x;
+        lc_key_result r;
+        if (int x = lc_fx_check(c->fx_all, recs.data(), (int64_t)recs.size(), opts, &r)) {
+          note(k, std::string("lc_fx_check: ") + lc_fx_last_error(c->fx_all) + " (" +
+                      std::to_string(x) + ")");
+          continue;
+        }
+        if (int x = store(k, r)) return x;
+      }
+      return 0;
+    }
   }
-  if (ne == 0) return 0;
+  // key-parallel: engines per GPU, bounded by its free memory (lists and
+  // tables take up to ~288 B per configuration of the budget)
+  const int64_t budget = opts && opts->max_configs_per_key > 0 ? opts->max_configs_per_key
+                                                                : kDefaultBudget;
+  const double per_engine = 288.0 * (double)(budget + 1) + (64 << 20);
+  for (int id : ids) {
+    int have = 0;
+    for (const auto &e : c->fxs) have += e.second == id;
+    size_t fr = 0, tot = 0;
+    (void)hipSetDevice(id);
+    int want = (int)kFxEngines;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+      want = (int)std::max<double>(1.0, std::min<double>(want, 0.8 * (double)fr / per_engine + have));
+    const int per_dev = (int)std::min<size_t>((size_t)want, (todo.size() + ids.size() - 1) / ids.size());
+    for (; have < per_dev; have++) {
+      lc_fx_params fp{};
+      fp.device = id;
+      fp.virtual_ranks = 1;
+      fp.part_above = -1;
+      fp.repl_below = -1;
+      lc_fx *f = nullptr;
+      if (int e = lc_fx_open(&fp, nullptr, &f)) {
+        set_err(c, "LC_FLAG_WHOLE_GPU: lc_fx_open failed (" + std::to_string(e) + ")");
+        break;
+      }
+      c->fxs.emplace_back(f, id);
+    }
+  }
+  const int ne = (int)c->fxs.size();
+  if (ne == 0) {
+    for (int64_t k : todo) note(k, "no frontier-exchange engine could be opened");
+    return 0;
+  }
   std::atomic<size_t> next{0};
   std::vector<int> erc(ne, 0);
   auto run = [&](int e) {
-    (void)hipSetDevice(c->devs[0].id);
+    (void)hipSetDevice(c->fxs[e].second);
     std::vector<lc_op> recs;
     for (;;) {
       const size_t i = next.fetch_add(1);
       if (i >= todo.size()) break;
       const int64_t k = todo[i];
       lc_key_result r;
-      int x = fetch(k, recs);
-      if (!x) x = lc_fx_check(c->fxs[e], recs.data(), (int64_t)recs.size(), opts, &r);
-      if (x) {
-        set_err(c, std::string("lc_fx_check: ") + lc_fx_last_error(c->fxs[e]));
-        erc[e] = x;
-        break;
+      if ((erc[e] = fetch(k, recs))) break;
+      if (int x = lc_fx_check(c->fxs[e].first, recs.data(), (int64_t)recs.size(), opts, &r)) {
+        note(k, std::string("lc_fx_check: ") + lc_fx_last_error(c->fxs[e].first) + " (" +
+                    std::to_string(x) + ")");
+        continue;
       }
-      if ((x = store(k, r))) {
-        erc[e] = x;
-        break;
-      }
+      if ((erc[e] = store(k, r))) break;
     }
   };
   std::vector<std::thread> th;
-  for (int e = 0; e < ne; e++) th.emplace_back(run, e);
+  for (int e = 0; e < std::min<int>(ne, (int)todo.size()); e++) th.emplace_back(run, e);
   for (auto &t : th) t.join();
   for (int e = 0; e < ne; e++)
     if (erc[e]) return erc[e];
@@ -638,7 +714,8 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
 
 void lc_close(lc_ctx *c) {
   if (!c) return;
-  for (lc_fx *f : c->fxs) lc_fx_close(f);
+  for (auto &f : c->fxs) lc_fx_close(f.first);
+  if (c->fx_all) lc_fx_close(c->fx_all);
   for (Dev &d : c->devs) {
     (void)hipSetDevice(d.id);
     if (d.stream) (void)hipStreamSynchronize(d.stream);

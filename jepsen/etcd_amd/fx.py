@@ -47,6 +47,8 @@ class LcFxParams(ctypes.Structure):
 
 
 LC_FX_FLAG_WIDE_TABLES = 1
+LC_FX_FLAG_EXCHANGE_SELF = 2
+LC_FX_RCCL_ID_BYTES = 128
 
 
 class LcFxStats(ctypes.Structure):
@@ -68,6 +70,14 @@ def _lib():
         L.lc_fx_open.argtypes = [ctypes.POINTER(LcFxParams), ctypes.POINTER(LcFxTransport),
                                  ctypes.POINTER(vp)]
         L.lc_fx_open.restype = ctypes.c_int
+        L.lc_fx_open_devices.argtypes = [ctypes.POINTER(LcFxParams), ctypes.POINTER(ctypes.c_int32),
+                                         ctypes.c_int32, ctypes.POINTER(vp)]
+        L.lc_fx_open_devices.restype = ctypes.c_int
+        L.lc_fx_rccl_unique_id.argtypes = [ctypes.c_char_p]
+        L.lc_fx_rccl_unique_id.restype = ctypes.c_int
+        L.lc_fx_open_rccl.argtypes = [ctypes.POINTER(LcFxParams), ctypes.c_char_p, ctypes.c_int32,
+                                      ctypes.c_int32, ctypes.POINTER(vp)]
+        L.lc_fx_open_rccl.restype = ctypes.c_int
         L.lc_fx_check.argtypes = [vp, p, ctypes.c_int64, ctypes.POINTER(abi.LcOpts), p]
         L.lc_fx_check.restype = ctypes.c_int
         L.lc_fx_last_stats.argtypes = [vp, ctypes.POINTER(LcFxStats)]
@@ -76,6 +86,8 @@ def _lib():
         L.lc_fx_last_error.restype = ctypes.c_char_p
         L.lc_fx_close.argtypes = [vp]
         L.lc_fx_close.restype = None
+        L.lc_fx_abort.argtypes = [vp]
+        L.lc_fx_abort.restype = None
         _bound = True
     return L
 
@@ -166,26 +178,57 @@ class TorchTransport:
 
 
 class FrontierExchange:
-    """One engine (lc_fx_open).  group: a torch.distributed group (this
-    process is one rank of it); else `virtual_ranks` ranks run as threads on
-    `device`.  part_above / repl_below: the frontier size above which it is
-    partitioned by owner, and below which it is replicated again (-1: the
-    library's defaults).  table_log2: dedup table size (0: from the budget).
-    flags: LC_FX_FLAG_* (LC_FX_FLAG_WIDE_TABLES: 16-byte-key tables only)."""
+    """One engine.  Collectives, by argument:
+
+    * rccl_devices=[d0, d1, ...]: one rank per listed GPU of this process,
+      native RCCL inside the library (lc_fx_open_devices);
+    * rccl_group=<torch.distributed group>: this process is one rank, native
+      RCCL inside the library (lc_fx_open_rccl; the unique id travels over
+      the group, then torch is out of the data path);
+    * group=<torch.distributed group>: this process is one rank, collectives
+      called back into torch.distributed (TorchTransport);
+    * none of them: `virtual_ranks` ranks as threads on `device`.
+
+    part_above / repl_below: the frontier size above which it is partitioned
+    by owner, and below which it is replicated again (-1: the library's
+    defaults).  table_log2: dedup table size (0: from the budget).  flags:
+    LC_FX_FLAG_* (LC_FX_FLAG_WIDE_TABLES: 16-byte-key tables only;
+    LC_FX_FLAG_EXCHANGE_SELF: own configurations through the exchange too)."""
 
     def __init__(self, device=0, virtual_ranks=1, group=None, part_above=-1, repl_below=-1,
-                 table_log2=0, flags=0):
+                 table_log2=0, flags=0, rccl_devices=None, rccl_group=None):
         L = _lib()
         self._h = ctypes.c_void_p()
         prm = LcFxParams(device, virtual_ranks, part_above, repl_below, table_log2, flags)
         self.transport = None
-        tr = None
-        if group is not None:
-            self.transport = TorchTransport(group, device)
-            tr = ctypes.byref(self.transport._c)
-        rc = L.lc_fx_open(ctypes.byref(prm), tr, ctypes.byref(self._h))
+        if rccl_devices is not None:
+            devs = (ctypes.c_int32 * len(rccl_devices))(*rccl_devices)
+            rc = L.lc_fx_open_devices(ctypes.byref(prm), devs, len(rccl_devices),
+                                      ctypes.byref(self._h))
+            what = "lc_fx_open_devices"
+        elif rccl_group is not None:
+            import torch.distributed as dist
+            buf = ctypes.create_string_buffer(LC_FX_RCCL_ID_BYTES)
+            rank = dist.get_rank(rccl_group)
+            if rank == 0:
+                rc = L.lc_fx_rccl_unique_id(buf)
+                if rc != 0:
+                    raise abi.LcError(rc, "lc_fx_rccl_unique_id")
+            obj = [buf.raw if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=dist.get_global_rank(rccl_group, 0),
+                                       group=rccl_group)
+            rc = L.lc_fx_open_rccl(ctypes.byref(prm), obj[0], rank,
+                                   dist.get_world_size(rccl_group), ctypes.byref(self._h))
+            what = "lc_fx_open_rccl"
+        else:
+            tr = None
+            if group is not None:
+                self.transport = TorchTransport(group, device)
+                tr = ctypes.byref(self.transport._c)
+            rc = L.lc_fx_open(ctypes.byref(prm), tr, ctypes.byref(self._h))
+            what = "lc_fx_open"
         if rc != 0:
-            raise abi.LcError(rc, "lc_fx_open")
+            raise abi.LcError(rc, what)
 
     def check(self, ops, opts=None):
         """Decide one key (records (n, 6) int64): a RESULT_DTYPE record."""
@@ -205,6 +248,13 @@ class FrontierExchange:
         s = LcFxStats()
         _lib().lc_fx_last_stats(self._h, ctypes.byref(s))
         return {k: getattr(s, k) for k, _ in LcFxStats._fields_}
+
+    def abort(self):
+        """From another thread (a watchdog): stop the search in progress —
+        RCCL communicators are aborted, so a rank stuck in a collective
+        returns and check() raises; an RCCL engine is unusable afterwards."""
+        if self._h:
+            _lib().lc_fx_abort(self._h)
 
     def close(self):
         if self._h:

@@ -80,6 +80,48 @@ def test_fx_matches_oracle_jitc(ranks, part_above):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["rccl", "hub"])
+def test_fx_self_exchange_matches_oracle(transport):
+    """The multi-rank protocol with one rank exchanging with itself
+    (LC_FX_FLAG_EXCHANGE_SELF, every level partitioned): under "rccl" every
+    configuration moves through the library's own RCCL transport — a
+    one-device communicator from ncclCommInitAll, counts by ncclAllToAll on
+    the device, payload by grouped ncclSend / ncclRecv — which is the path
+    LC_FLAG_WHOLE_GPU takes over several GPUs (this pool has one GPU per box
+    and RCCL refuses two ranks on one device).  Every field equals JITC's."""
+    from jepsen.etcd_amd.fx import LC_FX_FLAG_EXCHANGE_SELF, FrontierExchange
+    keys = _keys(0xF0E, n_each=25)
+    kw = dict(rccl_devices=[0]) if transport == "rccl" else dict(virtual_ranks=1)
+    sent = 0
+    with FrontierExchange(device=0, part_above=0, table_log2=18,
+                          flags=LC_FX_FLAG_EXCHANGE_SELF, **kw) as fx:
+        for i, (recs, init) in enumerate(keys):
+            got = fx.check(np.array(recs, dtype=np.int64).reshape(-1, 6),
+                           abi.default_opts(init_value=init))
+            if got["reason"] == abi.LC_REASON_WINDOW_OVERFLOW:
+                continue
+            _compare(got, _oracle(recs, init), (transport, i))
+            st = fx.stats()
+            sent += st["sent_configs"]
+            if len(recs) > 20 and got["verdict"] != -1:
+                assert st["part_returns"] > 0, (i, st)
+    assert sent > 1000
+
+
+@pytest.mark.gpu
+def test_fx_rccl_one_rank_plain():
+    """A one-device RCCL engine without self-exchange: the single-rank path
+    (no collective runs), same results as the in-process engine."""
+    from jepsen.etcd_amd.fx import FrontierExchange
+    ops, off, _, _ = abi.synth(1, 600, concurrency=14, p_info=0.005, seed=0xFACE)
+    ops = ops.copy()
+    ops[:, 3] = -1
+    with FrontierExchange(device=0, rccl_devices=[0]) as fx:
+        got = fx.check(ops)
+    _compare(got, _oracle(ops.tolist(), -1), "rccl one rank")
+
+
+@pytest.mark.gpu
 def test_fx_partition_switches_and_exchanges():
     """A key whose frontier crosses the thresholds both ways: replicated ->
     partitioned (filter by owner) -> replicated (gather), same result as one
@@ -155,6 +197,38 @@ def test_fx_wide_tables(ranks):
 
 
 @pytest.mark.gpu
+def test_fx_small_tables_redo_and_decide(monkeypatch):
+    """Table prefixes sized to the expected work itself (LC_FX_TABLE_MUL=1,
+    a dev knob; the default is 4x) and full tables only 4x the largest
+    frontier: returns outgrow their prefix, are redone with a 4x larger one
+    up to the full table, and the key is still decided — partitioned over
+    two in-process ranks and replicated over two (where the ranks must agree
+    on a redo, since probe-chain lengths follow the order of atomic inserts)
+    — with the results of a default run."""
+    from jepsen.etcd_amd.fx import FrontierExchange
+    ops, off, _, _ = abi.synth(1, 2000, concurrency=40, seed=0x5EED0004)
+    ops = ops.copy()
+    ops[:, 3] = -1
+    with FrontierExchange(device=0) as fx:
+        want = fx.check(ops)
+    assert want["verdict"] == 1
+    full = 1
+    while (1 << full) < 4 * int(want["max_frontier"]):
+        full += 1
+    monkeypatch.setenv("LC_FX_TABLE_MUL", "1")
+    redos = 0
+    for ranks, pa in ((2, 0), (2, 1 << 30), (1, -1)):
+        for lg in (full, full + 1):
+            with FrontierExchange(device=0, virtual_ranks=ranks, part_above=pa,
+                                  table_log2=lg) as fx:
+                got = fx.check(ops)
+                redos += fx.stats()["redos"]
+            for f in FIELDS:
+                assert int(got[f]) == int(want[f]), (ranks, pa, lg, f)
+    assert redos > 0
+
+
+@pytest.mark.gpu
 def test_fx_budget_window_and_errors():
     from jepsen.etcd_amd.fx import FrontierExchange
     ops, off, _, _ = abi.synth(1, 400, concurrency=16, p_info=0.02, seed=0xB0B)
@@ -227,6 +301,60 @@ def test_whole_gpu_flag_decides_budget_keys():
         assert (got[f] == whole[f][1:]).all(), f
 
 
+@pytest.mark.gpu
+def test_whole_gpu_key_spans_every_device_of_the_context(monkeypatch):
+    """LC_FLAG_WHOLE_GPU with fewer budget keys than the context has GPUs:
+    each key's search spans all of them (one rank per GPU, the frontier
+    partitioned by owner above part_above).  Two device contexts on this
+    box's one GPU (LC_VIRTUAL_DEVICES) run their ranks in process; results
+    equal the oracle's in every field, and keys the tiers decide keep
+    their results."""
+    monkeypatch.setenv("LC_VIRTUAL_DEVICES", "2")
+    ops, off, _, _ = abi.synth(1, 1000, concurrency=28, p_info=0.002, seed=0xB16)
+    ops = ops.copy()
+    ops[:, 3] = -1
+    small, soff, _, _ = abi.synth(3, 200, concurrency=6, seed=0xB17)
+    small = small.copy()
+    small[:, 3] = -1
+    allops = np.concatenate([ops, small])
+    alloff = np.concatenate([off, soff[1:] + off[-1]])
+    budget = 100000
+    with abi.Context(1) as ctx:
+        _, plain = ctx.check(allops, alloff, abi.default_opts(max_configs_per_key=budget))
+        _, whole = ctx.check(allops, alloff, abi.default_opts(max_configs_per_key=budget,
+                                                              flags=abi.LC_FLAG_WHOLE_GPU))
+        assert ctx.stats()["n_devices"] == 2
+    assert plain["reason"][0] == abi.LC_REASON_CONFIG_BUDGET
+    _, ref = oracle.check(allops, alloff, algo=oracle.JITC, max_configs=budget)
+    for k in range(len(alloff) - 1):
+        for f in FIELDS:
+            assert int(whole[f][k]) == int(ref[f][k]), (k, f)
+    assert whole["verdict"][0] == 1
+    assert (whole[1:] == plain[1:]).all()
+
+
+@pytest.mark.gpu
+def test_whole_gpu_failed_research_keeps_key_unknown(monkeypatch):
+    """A re-search that cannot run costs only its key: it stays :unknown at
+    the budget, every other key is decided, the call returns 0 and
+    lc_last_error says why.  LC_FX_FAIL_RESERVE=1 (a test hook) makes the
+    engine's list allocation fail, as an over-large budget would."""
+    monkeypatch.setenv("LC_FX_FAIL_RESERVE", "1")
+    ops, off, _, _ = abi.synth(1, 1000, concurrency=28, p_info=0.002, seed=0xB16)
+    ops = ops.copy()
+    ops[:, 3] = -1
+    small, soff, _, _ = abi.synth(2, 200, concurrency=6, seed=0xB17)
+    allops = np.concatenate([ops, small])
+    alloff = np.concatenate([off, soff[1:] + off[-1]])
+    opts = abi.default_opts(max_configs_per_key=100000, flags=abi.LC_FLAG_WHOLE_GPU)
+    with abi.Context(1) as ctx:
+        _, r = ctx.check(allops, alloff, opts)
+        err = ctx.last_error()
+    assert r["verdict"][0] == -1 and r["reason"][0] == abi.LC_REASON_CONFIG_BUDGET
+    assert (r["verdict"][1:] == 1).all()
+    assert "kept :unknown" in err and "injected" in err, err
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -281,6 +409,50 @@ def _nccl_main(port, q):
         q.put(repr(e))
     finally:
         dist.destroy_process_group()
+
+
+def _rccl_rank_main(port, keys, q):
+    import torch.distributed as dist
+    from jepsen.etcd_amd.fx import LC_FX_FLAG_EXCHANGE_SELF, FrontierExchange
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=0,
+                            world_size=1)
+    try:
+        fx = FrontierExchange(device=0, rccl_group=dist.group.WORLD, part_above=0,
+                              flags=LC_FX_FLAG_EXCHANGE_SELF)
+        out = []
+        for recs in keys:
+            r = fx.check(np.array(recs, dtype=np.int64).reshape(-1, 6))
+            out.append([int(r[f]) for f in FIELDS])
+        st = fx.stats()
+        fx.close()
+        q.put((out, st))
+    except Exception as e:
+        q.put((repr(e), None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_fx_rccl_multiprocess_entry_point():
+    """lc_fx_open_rccl, the one-process-per-GPU form (torchrun): rank 0's
+    ncclUniqueId travels over a torch.distributed group, then the library's
+    own communicator carries the search (one rank here, exchanging with
+    itself; RCCL refuses two ranks on one device)."""
+    import torch.multiprocessing as mp
+    rng = random.Random(0xD17)
+    keys = [random_casreg(rng, rng.randrange(5, 50), p_info=0.1) for _ in range(8)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_rank_main, args=(_free_port(), keys, q))
+    p.start()
+    out, st = q.get(timeout=180)
+    p.join(timeout=60)
+    assert st is not None, out
+    assert st["part_returns"] > 0
+    for recs, got in zip(keys, out):
+        if got[1] == abi.LC_REASON_WINDOW_OVERFLOW:
+            continue
+        _compare(dict(zip(FIELDS, got)), _oracle(recs, -1), "rccl process")
 
 
 @pytest.mark.gpu

@@ -28,7 +28,8 @@ def test_library_exports_every_declared_symbol():
         "lc_synth_register", "lc_synth_key", "lc_edn_parse", "lc_edn_n_keys", "lc_edn_n_ops",
         "lc_edn_n_events", "lc_edn_ops", "lc_edn_key_off", "lc_edn_key", "lc_edn_op_text",
         "lc_edn_value", "lc_edn_free", "lc_fx_open", "lc_fx_check", "lc_fx_last_stats",
-        "lc_fx_last_error", "lc_fx_close"}
+        "lc_fx_last_error", "lc_fx_close", "lc_fx_open_devices", "lc_fx_rccl_unique_id",
+        "lc_fx_open_rccl", "lc_fx_abort"}
     for n in names:
         assert hasattr(lib, n), n
     assert abi.lib().lc_abi_version() == 2
