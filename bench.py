@@ -239,6 +239,8 @@ def main():
         line["mixed_leg"] = mixed_leg(ctx, abi, dev, stream)
         line["model_leg"] = model_leg(ctx, abi)
         line["crash_leg"] = crash_leg(ctx, abi, dev, stream)
+        if world == 1:
+            line["c3_shards"] = c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream)
         line["oversized_key"] = oversized_key(ctx, abi)
 
     if rank == 0 and world == 1 and not (args.no_cpu_baseline or args.bare):
@@ -249,6 +251,51 @@ def main():
     ctx.close()
     if distributed:
         dist.destroy_process_group()
+
+
+def c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream, steps=30, warmup=5):
+    """A one-GPU predictor of BASELINE configs[2] (C3): the same C2 batch cut
+    by lc_plan_partition into 1, 2, 4 and 8 shards, and each shard timed as
+    one lc_check_device step on this GPU.  A step at N GPUs takes as long as
+    its slowest shard (the ranks share nothing but the timing barrier), so
+    max over shards is the implied N-GPU step and records / that the implied
+    throughput.  A per-shard cost, not a scaling curve: the driver's 8-GPU
+    run measures the curve.  Not part of `value`."""
+    import torch
+    out = []
+    n_rec = int(key_off[-1] - key_off[0])
+    for n in (1, 2, 4, 8):
+        bounds = abi.plan_partition(key_off, n, ops=ops)
+        shard_ms = []
+        for p in range(n):
+            a, b = int(bounds[p]), int(bounds[p + 1])
+            outb = torch.zeros(max(b - a, 1) * abi.RESULT_DTYPE.itemsize, dtype=torch.uint8,
+                               device=dev)
+            step = ctx.bind_check_device(d_ops.data_ptr() + int(key_off[a] - key_off[0]) * 48,
+                                         d_off.data_ptr() + a * 8, b - a, outb.data_ptr(),
+                                         stream=stream.cuda_stream, opts=abi.default_opts(),
+                                         stats=abi.LcStats())
+            for _ in range(warmup):
+                step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            kms = []
+            for _ in range(steps):
+                kms.append(step().kernel_ms)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3 / steps
+            res = np.frombuffer(outb.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)[:b - a]
+            shard_ms.append({"keys": [a, b], "ms_per_step": ms, "kernel_ms": float(np.mean(kms)),
+                             "valid": int((res["verdict"] == 1).sum())})
+        worst = max(x["ms_per_step"] for x in shard_ms)
+        out.append({"n_gpus": n, "implied_ms_per_step": worst,
+                    "implied_ops_per_s": n_rec / (worst * 1e-3),
+                    "shard_ms_min_max": [min(x["ms_per_step"] for x in shard_ms), worst],
+                    "shards": shard_ms})
+    base = out[0]["implied_ms_per_step"]
+    for o in out:
+        o["implied_speedup"] = base / o["implied_ms_per_step"]
+    return out
 
 
 def c1_leg(ctx, abi):

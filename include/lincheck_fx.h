@@ -141,6 +141,29 @@ int lc_fx_open_rccl(const lc_fx_params *params, const uint8_t *id, int32_t rank,
 int lc_fx_check(lc_fx *fx, const lc_op *ops, int64_t n, const lc_opts *opts,
                 lc_key_result *out);
 
+/* One configuration of a key's search frontier — knossos's `:configs` entry
+ * (`{:model (->VersionedRegister version value), :pending [...]}`,
+ * register.clj:55, checker/linearizable's result at register.clj:110-111):
+ * the model state and the ops (record indices of the key) that have been
+ * called but are not linearized in it.  Ops linearized in every
+ * configuration are retired and never pending; reads that can never
+ * constrain (crashed, [nil nil]) take no part in the search. */
+typedef struct lc_fx_config {
+  int64_t version;
+  int64_t value;        /* the caller's value id; LC_NIL for nil */
+  int64_t n_pending;
+  int64_t pending[64];  /* sorted */
+} lc_fx_config;
+
+/* Run the key's search up to the :ok return of record stop_op and copy up
+ * to `max` configurations of the frontier that return expands — for an
+ * invalid key with fail_op = stop_op, the configurations just before the
+ * failure, which knossos reports as :configs.  One-rank engines only.
+ * *n_out = configurations copied (0 when stop_op's return is a no-op: the op
+ * was retired). */
+int lc_fx_frontier(lc_fx *fx, const lc_op *ops, int64_t n, const lc_opts *opts, int64_t stop_op,
+                   lc_fx_config *out, int32_t max, int32_t *n_out);
+
 /* From another thread: stop a search in progress.  Every RCCL communicator
  * of the engine is aborted (ncclCommAbort), so ranks waiting in a collective
  * return and lc_fx_check fails; an RCCL engine is unusable afterwards.  For

@@ -22,8 +22,11 @@ shape, {"valid?", "linear": <the GPU verdict>, "timeline": ...}; with
 timeline_dir set, the timeline half renders <dir>/independent/<k>/
 timeline.html on the host (timeline.py), as jepsen's timeline/html would.
 An invalid key's map also carries knossos's diagnostics (diagnostics.py):
-"previous-ok", and — from the witness of the prefix before the failing
-return (lc_aux) — "configs", "last-op" and "final-paths".
+"previous-ok", "configs" and "final-paths" — from the search's own frontier
+just before the failing return (lc_fx_frontier, up to 10 configurations) for
+keys the frontier search decided, from the witness of the prefix before the
+failing return (lc_aux, with "last-op") for keys the version-order and gap
+tiers decided.
 
 Errors: a key with malformed records is "unknown" alone (cause
 "malformed"), as jepsen.independent would lose only that key; unusable
@@ -103,16 +106,27 @@ class RegisterChecker:
         # drop-in does too by default (time_budget_ms bounds it)
         self.whole_gpu = whole_gpu
         self._ctx = None
+        self._fx = None
 
     def _context(self):
         if self._ctx is None:
             self._ctx = abi.Context(self.device_mask)
         return self._ctx
 
+    def _frontier(self):
+        if self._fx is None:
+            from .fx import FrontierExchange
+            dev = 0
+            while self.device_mask and not (self.device_mask >> dev) & 1:
+                dev += 1
+            self._fx = FrontierExchange(device=dev)
+        return self._fx
+
     def check(self, test, history, opts=None):
         m = self.model
+        values = []
         keys, ops, key_off, done = H.pack(history, model=m.name, independent=self.independent,
-                                          init_value=m.value)
+                                          init_value=m.value, values_out=values)
         if not keys:
             return {"valid?": True, "results": {}, "failures": []}
         # the initial value is interned first in every key (id 0); the mutex
@@ -133,12 +147,19 @@ class RegisterChecker:
                 d = done[i][int(r["fail_op"])]
                 out["op"] = d["completion"] or d["invoke"]
                 out["fail-prefix-end"] = int(r["fail_prefix_end"])
-                w = None
                 if m.name == "versioned-register" and kind[i] == abi.LC_WITNESS_PREFIX:
                     w = wit[key_off[i]:key_off[i + 1]]
-                out.update(D.invalid_analysis(done[i], int(r["fail_op"]),
-                                              int(r["fail_prefix_end"]), w,
-                                              init=(m.version, m.value)))
+                    out.update(D.invalid_analysis(done[i], int(r["fail_op"]),
+                                                  int(r["fail_prefix_end"]), w,
+                                                  init=(m.version, m.value)))
+                else:
+                    # decided by the frontier search: its configurations just
+                    # before the failing return (knossos's :configs)
+                    cfgs = self._frontier().frontier(ops[key_off[i]:key_off[i + 1]],
+                                                     int(r["fail_op"]), D.MAX_ENTRIES, o)
+                    out.update(D.frontier_analysis(
+                        done[i], int(r["fail_op"]), int(r["fail_prefix_end"]), cfgs, values[i],
+                        versioned=m.name == "versioned-register"))
             elif v == UNKNOWN:
                 out["cause"] = abi.REASONS.get(int(r["reason"]), "?")
             results[k] = out
@@ -171,6 +192,9 @@ class RegisterChecker:
         if self._ctx is not None:
             self._ctx.close()
             self._ctx = None
+        if self._fx is not None:
+            self._fx.close()
+            self._fx = None
 
 
 def register_checker(**kw):

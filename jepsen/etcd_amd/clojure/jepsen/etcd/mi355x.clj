@@ -27,10 +27,16 @@
     :checker (jepsen.etcd.mi355x/checker)
 
   An invalid key's :linear map carries knossos's diagnostics: :op,
-  :previous-ok and, from the witness of the prefix before the failing
-  return (lc_check_ex, lc_aux), one :configs entry, :last-op and
-  :final-paths (jepsen/etcd_amd/diagnostics.py restates the same).  A key
-  with malformed records is :unknown alone.
+  :previous-ok, :configs and :final-paths — for keys the frontier search
+  decided, up to 10 configurations of that search's frontier just before
+  the failing return (lc_fx_frontier, include/lincheck_fx.h); for keys the
+  version-order and gap tiers decided, the one configuration the witness of
+  the prefix before the failing return names (lc_check_ex, lc_aux), with its
+  :last-op.  :final-paths step the reference's own model
+  (jepsen.etcd.register/->VersionedRegister, register.clj:55-96) through
+  knossos.model/step, so the messages are the model's own
+  (jepsen/etcd_amd/diagnostics.py restates the same).  A key with malformed
+  records is :unknown alone.
 
   Untested in the build container (no JVM there); the same contract is
   exercised from Python by tests/test_gpu.py::test_register_checker_end_to_end."
@@ -110,13 +116,18 @@
           (recur (rest ops) pending out)))
       (vec (remove :fail? out)))))
 
-(defn- interner []
+(defn- interner
+  "A value -> dense id fn (nil -> LC_NIL); (intern) with no argument returns
+  the id -> value map."
+  []
   (let [ids (volatile! {})]
-    (fn [v]
-      (if (nil? v)
-        LC_NIL
-        (or (@ids v)
-            (let [i (count @ids)] (vswap! ids assoc v i) i))))))
+    (fn
+      ([] (into {} (map (fn [[v i]] [i v])) @ids))
+      ([v]
+       (if (nil? v)
+         LC_NIL
+         (or (@ids v)
+             (let [i (count @ids)] (vswap! ids assoc v i) i)))))))
 
 (defn- record
   "[f value expected version call ret] for one completed op under model
@@ -155,14 +166,16 @@
 
 (defn- pack
   "Packs all keys: returns [keys completed-per-key ^Memory ops ^Memory key-off
-  n-records].  Records are filled into one long[] and written to the
-  off-heap buffer in a single bulk copy."
+  n-records values-per-key] (values: each key's id -> value map).  Records
+  are filled into one long[] and written to the off-heap buffer in a single
+  bulk copy."
   [model subs]
   (let [keys  (vec (keys subs))
         done  (mapv (fn [k] (complete (get subs k))) keys)
         n     (long (reduce + (map count done)))
         arr   (long-array (* 6 n))
-        offs  (long-array (inc (count keys)))]
+        offs  (long-array (inc (count keys)))
+        vals  (transient [])]
     (loop [ki 0, i 0]
       (aset offs ki i)
       (when (< ki (count keys))
@@ -175,84 +188,120 @@
                                  (aset arr (+ b 4) (long call)) (aset arr (+ b 5) (long ret))
                                  (inc i)))
                              i (nth done ki))]
+          (conj! vals (intern))
           (recur (inc ki) i'))))
     (let [ops (Memory. (max 1 (* op-bytes n)))
           off (Memory. (* 8 (inc (count keys))))]
       (.write ops 0 arr 0 (alength arr))
       (.write off 0 offs 0 (alength offs))
-      [keys done ops off n])))
+      [keys done ops off n (persistent! vals)])))
 
 ;; ---- knossos's invalid-analysis keys (diagnostics.py restates the same)
 
-(defn- vr-step
-  "VersionedRegister.step (register.clj:60-96) over [version value] state
-  and a completed op: the next state, or (model/inconsistent msg)."
-  [[version value :as state] op]
-  (let [[op-version op-value] (:value op)
-        version' (inc version)]
-    (case (:f op)
-      :write (if (and (some? op-version) (not= version' op-version))
-               (model/inconsistent (str "can't go from version " version " to " op-version))
-               [version' op-value])
-      :cas   (let [[v v'] op-value]
-               (cond (and (some? op-version) (not= version' op-version))
-                     (model/inconsistent (str "can't go from version " version " to " op-version))
-                     (not= value v)
-                     (model/inconsistent (str "can't CAS " value " from " v " to " v'))
-                     :else [version' v']))
-      :read  (cond (and (some? op-version) (not= version op-version))
-                   (model/inconsistent (str "can't read version " op-version " from version " version))
-                   (and (some? op-value) (not= value op-value))
-                   (model/inconsistent (str "can't read " op-value " from register " value))
-                   :else state)
-      (model/inconsistent (str "no step for " (:f op))))))
+(defn- ref-model
+  "The reference's own model, register.clj:55 (->VersionedRegister version
+  value), resolved at run time from the test's classpath: :final-paths step
+  it through knossos.model/step, so every message is the model's own."
+  [version value]
+  ((requiring-resolve 'jepsen.etcd.register/->VersionedRegister) version value))
 
-(defn- model-map [s] (if (model/inconsistent? s) s {:version (first s) :value (second s)}))
+(defn- model-map [m] (if (model/inconsistent? m) m {:version (:version m) :value (:value m)}))
 
 (defn- op-map [r] (if (not= LC_INF (:ret r)) (:completion r) (:op r)))
 
-(defn- invalid-analysis
-  ":previous-ok, and from the prefix witness (positions per record, or nil)
-  :configs [one configuration], :last-op and :final-paths."
-  [done fail-op fail-ret witness init]
-  (let [oks  (filter #(and (= :ok (:type (:completion %))) (< (:ret %) fail-ret)) done)
-        prev (when (seq oks) (:completion (apply max-key :ret oks)))
-        out  {:previous-ok prev}]
-    (if-not witness
-      out
-      (let [cut   (dec fail-ret)
-            muts  (->> (map-indexed vector witness) (filter #(>= (second %) 0))
-                       (sort-by second) (map first))
-            state (reduce (fn [s i] (if (model/inconsistent? s) s (vr-step s (:op (nth done i)))))
-                          init muts)]
-        (if (model/inconsistent? state)
-          out
-          (let [lin      (set muts)
-                freads   (->> (map-indexed vector done)
-                              (filter (fn [[_ r]] (and (= :read (:f (:op r))) (<= (:ret r) cut)
-                                                       (= (first (:value (:op r))) (first state)))))
-                              (map first))
-                last-i   (if (seq freads) (apply max-key #(:ret (nth done %)) freads) (last muts))
-                last-op  (when last-i (op-map (nth done last-i)))
-                pending  (->> (range (count done))
-                              (filter #(let [r (nth done %)]
-                                         (and (<= (:call r) cut) (not (lin %)) (> (:ret r) cut)))))
-                head     {:op last-op :model (model-map state)}
-                try-op   (fn [s i] (let [s' (vr-step s (:op (nth done i)))]
-                                     [s' {:op (op-map (nth done i)) :model (model-map s')}]))
-                direct   [head (second (try-op state fail-op))]
-                via      (for [i pending :when (not= i fail-op)
-                               :let [[s' mid] (try-op state i)]
-                               :when (or (model/inconsistent? s')
-                                         (model/inconsistent? (first (try-op s' fail-op))))]
-                           (if (model/inconsistent? s')
-                             [head mid]
-                             [head mid (second (try-op s' fail-op))]))]
-            (assoc out
-                   :configs     [{:model (model-map state) :last-op last-op
-                                  :pending (mapv #(:op (nth done %)) pending)}]
-                   :last-op     last-op
-                   :final-paths (vec (take 10 (cons direct via))))))))))
+(defn- final-paths
+  "From each [model last-index pending-indices] configuration, the paths that
+  try to linearize the failing op — directly, or after one pending op — and
+  end inconsistent; at most 10, as knossos keeps."
+  [done fail-op configs]
+  (let [try-op (fn [m i] (let [m' (model/step m (:op (nth done i)))]
+                           [m' {:op (op-map (nth done i)) :model (model-map m')}]))]
+    (->> (for [[m last-i pending] configs
+               :let [head   {:op (when last-i (op-map (nth done last-i))) :model (model-map m)}
+                     [d end] (try-op m fail-op)]
+               path (cons (when (model/inconsistent? d) [head end])
+                          (for [i pending :when (not= i fail-op)
+                                :let [[m' mid] (try-op m i)]
+                                :when (or (model/inconsistent? m')
+                                          (model/inconsistent? (first (try-op m' fail-op))))]
+                            (if (model/inconsistent? m')
+                              [head mid]
+                              [head mid (second (try-op m' fail-op))])))
+               :when path]
+           path)
+         (take 10)
+         vec)))
+
+(defn- previous-ok [done fail-ret]
+  (let [oks (filter #(and (= :ok (:type (:completion %))) (< (:ret %) fail-ret)) done)]
+    (when (seq oks) (:completion (apply max-key :ret oks)))))
+
+(defn- witness-analysis
+  ":configs [the one configuration the prefix witness names], :last-op and
+  :final-paths, for keys the version-order / gap tiers decided."
+  [done fail-op fail-ret witness [v0 x0]]
+  (let [cut   (dec fail-ret)
+        muts  (->> (map-indexed vector witness) (filter #(>= (second %) 0))
+                   (sort-by second) (map first))
+        state (reduce (fn [m i] (if (model/inconsistent? m) m (model/step m (:op (nth done i)))))
+                      (ref-model v0 x0) muts)]
+    (when-not (model/inconsistent? state)
+      (let [lin      (set muts)
+            freads   (->> (map-indexed vector done)
+                          (filter (fn [[_ r]] (and (= :read (:f (:op r))) (<= (:ret r) cut)
+                                                   (= (first (:value (:op r))) (:version state)))))
+                          (map first))
+            last-i   (if (seq freads) (apply max-key #(:ret (nth done %)) freads) (last muts))
+            last-op  (when last-i (op-map (nth done last-i)))
+            pending  (->> (range (count done))
+                          (filter #(let [r (nth done %)]
+                                     (and (<= (:call r) cut) (not (lin %)) (> (:ret r) cut)))))]
+        {:configs     [{:model (model-map state) :last-op last-op
+                        :pending (mapv #(:op (nth done %)) pending)}]
+         :last-op     last-op
+         :final-paths (final-paths done fail-op [[state last-i pending]])}))))
+
+(def ^:const fx-config-bytes 536)  ; lc_fx_config: version, value, n_pending, pending[64]
+
+(defonce ^:private fx-engine
+  (delay
+    (let [prm (doto (Memory. 40) (.clear)
+                (.setInt 0 0) (.setInt 4 1)            ; device 0, one rank
+                (.setLong 8 -1) (.setLong 16 -1))      ; default thresholds
+          out (PointerByReference.)
+          rc  (.invokeInt (fun "lc_fx_open") (object-array [prm nil out]))]
+      (when-not (zero? rc) (throw (ex-info "lc_fx_open failed" {:rc rc})))
+      (.getValue out))))
+
+(defn- frontier-analysis
+  ":configs — up to 10 configurations of the frontier search's own frontier
+  just before the failing return (lc_fx_frontier) — and :final-paths, for
+  keys the frontier search decided."
+  [model done ops k0 fail-op vals opts]
+  (let [n   (count done)
+        buf (Memory. (* 10 fx-config-bytes))
+        cnt (Memory. 4)
+        rc  (locking fx-engine
+              (.invokeInt (fun "lc_fx_frontier")
+                          (object-array [@fx-engine (.share ^Memory ops (* op-bytes k0))
+                                         (long n) opts (long fail-op) buf (int 10) cnt])))]
+    (when (zero? rc)
+      (let [configs (for [i (range (.getInt cnt 0))
+                          :let [b   (* i fx-config-bytes)
+                                ver (.getLong buf b)
+                                vid (.getLong buf (+ b 8))
+                                np  (.getLong buf (+ b 16))
+                                x   (when (not= vid LC_NIL) (get vals vid vid))]]
+                      [ver x (vec (for [j (range np)] (.getLong buf (+ b 24 (* 8 j)))))])]
+        (cond-> {:configs (vec (for [[ver x pending] configs]
+                                 {:model (if (= model :versioned-register)
+                                           {:version ver :value x}
+                                           {:value x})
+                                  :pending (mapv #(:op (nth done %)) pending)}))}
+          (= model :versioned-register)
+          (assoc :final-paths
+                 (final-paths done fail-op
+                              (for [[ver x pending] configs] [(ref-model ver x) nil pending]))))))))
 
 (defn- merge-valid [vs]
   (cond (some false? vs)          false
@@ -267,7 +316,7 @@
   come back :unknown one by one; lc_check_ex fails (and this throws, for
   check-safe) only on unusable arguments or a GPU error."
   [model max-configs-per-key time-budget-ms flags subs]
-  (let [[keys done ops off n] (pack model subs)
+  (let [[keys done ops off n vals] (pack model subs)
         nk   (count keys)
         out  (Memory. (* result-bytes nk))
         wit  (Memory. (max 4 (* 4 n)))
@@ -301,8 +350,12 @@
                (cond-> {:valid?   v
                         :analyzer :mi355x
                         :configs-explored (.getLong out (+ b 24))}
-                 (false? v)     (merge {:op (op-map (nth d fail-op))}
-                                       (invalid-analysis d fail-op fail-at witness [0 nil]))
+                 (false? v)     (merge {:op (op-map (nth d fail-op))
+                                        :previous-ok (previous-ok d fail-at)}
+                                       (if witness
+                                         (witness-analysis d fail-op fail-at witness [0 nil])
+                                         (frontier-analysis model d ops k0 fail-op
+                                                            (nth vals ki) o)))
                  (= v :unknown) (assoc :error [:lincheck-reason (reasons reason reason)]))])))))
 
 (defn linearizable

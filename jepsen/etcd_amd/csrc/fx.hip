@@ -755,6 +755,428 @@ __global__ __launch_bounds__(256) void fx_reset_kernel(Ctr *ctr, unsigned long l
   for (int i = 0; i < 64; i++) ctr->cand[i] = 0;
 }
 
+// ------------------------------------------------------------ the queue path
+//
+// One rank, one-word tables (the usual case): a return is ONE launch, with
+// no level structure.  The order in which configurations are expanded does
+// not change what a return computes — R (the configurations that linearized
+// x), the configurations explored (every V configuration is expanded exactly
+// once, by whoever wins its table insert) and the AND over R are functions of
+// the frontier and the window alone — so instead of level-synchronous BFS
+// (one launch or one grid barrier per level, ~4.6 per return on the oversized
+// key, each waiting for the level's slowest wave), the V configurations go
+// through one device-wide work queue:
+//
+//   * every wave first splits its share of F (insert into R / V), then
+//     claims runs of queue entries (one atomicAdd on qhead), expands each
+//     (lane = window slot), inserts the successors 64 per probe round, and
+//     appends the new V ones to the queue (one atomicAdd on qtail per flush);
+//   * a queue entry is the configuration's one-word table key, written and
+//     read by atomic exchange, which is performed where every CU's atomics
+//     are (so no cache of any XCD can hold a stale copy, and no fence is
+//     needed); the reader exchanges in EMPTY, so a consumed queue is empty
+//     again for the next launch;
+//   * termination: total = |F| + qtail counts an item before it exists (at
+//     its reservation) and `done` after it is finished (after its successors
+//     are reserved), so done <= total always; done read before qtail and
+//     equal to |F| + qtail means nothing is left anywhere;
+//   * each configuration's version is a function of its mask (vbase +
+//     popcount(mask & mutation slots)), so the word is all a queue entry
+//     needs;
+//   * two table sets and two counter blocks alternate between launches: a
+//     launch clears the other set's dirty prefix and zeroes the other
+//     counters for the next launch, so a return needs no reset launch;
+//   * each workgroup reports (explored, AND of the R entries it appended,
+//     the R and V entries it reserved, table-full / overflow flags) to
+//     host-mapped memory; the host sums them after one stream sync.  (R
+//     entries are flushed after the wave's last item, so no counter read in
+//     the kernel can be final for R.)
+struct QCtr {
+  unsigned long long qtail;  // V entries reserved (the queue's length)
+  unsigned long long p0[15];
+  unsigned long long qhead;  // V entries claimed
+  unsigned long long p1[15];
+  unsigned long long done;   // items finished: F entries split + V entries expanded
+  unsigned long long p2[15];
+  unsigned long long nR;     // R entries reserved
+  unsigned long long p3[15];
+};
+static_assert(sizeof(QCtr) == 512, "one 128-B line per counter");
+
+struct QRep {
+  unsigned long long explored;
+  unsigned long long andmask;
+  unsigned long long flags;  // kQTfull | kQOverflow
+  unsigned long long nR, nV; // R and V entries this workgroup reserved (the lists' lengths are the sums)
+  unsigned long long pad[3];
+};
+constexpr unsigned long long kQTfull = 1, kQOverflow = 2;
+constexpr int kQMaxWG = 512;
+
+struct QArgs {
+  const Cfg *F;
+  long long nF;
+  unsigned long long *Q;  // V queue: one-word keys, EMPTY when free
+  Cfg *listR;
+  unsigned long long cap;  // capacity of Q and of listR
+  unsigned long long *tabR, *tabV;
+  uint64_t tmask;
+  int cshift;
+  uint32_t vbase;  // version of a configuration: vbase + popcount(mask & mutation slots)
+  QCtr *ctr;       // this launch's counters (zero on entry)
+  QCtr *ctr_next;  // zeroed here for the next launch
+  unsigned long long *clrR, *clrV;  // the other table set, whose first clr_words entries ...
+  long long clr_words;              // ... are cleared here for the next launch
+  QRep *rep;                        // host-mapped, one per workgroup
+  int min_claim;                    // smallest run of queue entries a wave claims
+  int local;                        // V entries a wave keeps on its own stack (<= kLoc - 64)
+  int qatomic;                      // queue entries by atomic exchange (A/B)
+  int max_g;
+};
+
+// Read a counter where its atomics are performed.  Not an atomic load: the
+// compiler turns an idempotent read-modify-write (fetch_add 0) into
+// `global_load ... sc1`, which an XCD's L2 may serve from a stale line — a
+// stale qtail makes the termination test fire early (configurations lost).
+// A returning atomic add of 0, in asm, is a real read-modify-write.
+__device__ inline unsigned long long q_read(unsigned long long *p) {
+  unsigned long long v;
+  asm volatile("global_atomic_add_x2 %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)"
+               : "=v"(v)
+               : "v"(p), "v"(0ULL)
+               : "memory");
+  return v;
+}
+
+// A cheap look at a counter: an agent-scope atomic load (`global_load ...
+// sc1`), served by the XCD's L2 and possibly behind — never above — the
+// counter (the counters only grow).  Idle waves poll with it, so that they
+// do not queue their reads behind the busy waves' claims and reservations
+// at the one place the counter's atomics are performed; anything a decision
+// rests on is then confirmed with q_read.
+__device__ inline unsigned long long q_peek(unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Finished when every item that exists is done: done read before qtail, and
+// done <= |F| + qtail always.  Looked at cheaply first; confirmed by real
+// reads (or every `every`-th look, so stale peeks cannot hold it off).
+__device__ inline bool q_finished(QCtr *ctr, unsigned long long nF, int look, int every) {
+  const unsigned long long d = q_peek(&ctr->done);
+  const unsigned long long t = q_peek(&ctr->qtail);
+  if (d != nF + t && (look % every) != every - 1) return false;
+  const unsigned long long d2 = q_read(&ctr->done);
+  const unsigned long long t2 = q_read(&ctr->qtail);
+  return d2 == nF + t2;
+}
+
+// Queue entries.  A producer writes its entry with one 8-byte write-through
+// (sc1) store; the consumer polls it with sc1 loads until it is not EMPTY,
+// then stores EMPTY back (the queue is empty again for the next launch).
+// Every 8th poll of an entry that has not arrived is a read-modify-write
+// (compare EMPTY -> EMPTY: changes nothing, returns the entry where the
+// atomics are performed), so a stale cached line cannot hold a consumer off.
+// qatomic (LC_FXQ_ATOMIC=1, A/B): atomic exchange both ways instead.
+__device__ inline void q_put(unsigned long long *e, unsigned long long w, int qatomic) {
+  if (qatomic) (void)atomicExch(e, w);
+  else __hip_atomic_store(e, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline unsigned long long q_take(unsigned long long *e, bool rmw) {
+  unsigned long long w;
+  if (rmw) w = atomicCAS(e, kEmpty, kEmpty);
+  else w = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (w != kEmpty) __hip_atomic_store(e, kEmpty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return w;
+}
+
+__device__ inline void q_sleep(int n) {
+  for (int i = 0; i < n; i++) __builtin_amdgcn_s_sleep(8);
+}
+
+constexpr int kLoc = 256;
+struct QStage {
+  Cfg s[64];                     // successors gathered, inserted together
+  Cfg r[kStage];                 // new R entries
+  unsigned long long v[kStage];  // new V entries to spill to the queue (one-word keys)
+  unsigned long long loc[kLoc];  // the wave's own stack of V entries to expand
+};
+
+__global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win warg) {
+  __shared__ Win w;
+  __shared__ QStage stg_all[4];
+  __shared__ unsigned long long red_e[4], red_a[4], red_f[4], red_r[4], red_v[4];
+  // the other table set and counters, for the next launch (plain stores: the
+  // launch boundary publishes them)
+  {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < a.clr_words; i += stride) {
+      a.clrR[i] = kEmpty;
+      a.clrV[i] = kEmpty;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 4) {
+      unsigned long long *z = &a.ctr_next->qtail + 16 * threadIdx.x;
+      *z = 0;
+    }
+  }
+  load_win(w, &warg);
+  __syncthreads();
+  const int lane = __lane_id(), wid = threadIdx.x / kW;
+  QStage *stg = &stg_all[wid];
+  const long long wave = (long long)blockIdx.x * (blockDim.x / kW) + wid;
+  const long long nwaves = (long long)gridDim.x * (blockDim.x / kW);
+  const uint64_t below = (1ULL << lane) - 1;
+  const Slot me = w.s[lane];
+  const uint64_t bit = 1ULL << lane;
+  const uint64_t muts = w.occ & ~w.reads;
+  const uint64_t reads = w.occ & w.reads;
+  const bool is_mut = (muts & bit) != 0;
+  const uint64_t lowmask = (1ULL << a.cshift) - 1;
+  uint64_t rv_me = 0, vreads = 0;
+  for (uint64_t pr = reads; pr;) {
+    const int b = __builtin_ctzll(pr);
+    pr &= pr - 1;
+    const Slot &r = w.s[b];
+    if (r.nvm) vreads |= 1ULL << b;
+    else if (!r.nlm || r.nl == me.value) rv_me |= 1ULL << b;
+  }
+  int ns = 0, nr = 0, nv = 0, nl = 0;  // stash / R stage / V spill stage / local stack (wave-uniform)
+  unsigned long long explored = 0, andm = ~0ULL, flags = 0;
+  unsigned long long cnt_r = 0, cnt_v = 0;  // entries this wave reserved (wave-uniform)
+
+  auto flush_r = [&]() {
+    if (!nr) return;
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&a.ctr->nR, (unsigned long long)nr);
+    base = __shfl(base, 0);
+    cnt_r += nr;
+    for (int j = lane; j < nr; j += kW) {
+      if (base + j < a.cap) a.listR[base + j] = stg->r[j];
+      else flags |= kQOverflow;
+    }
+    __builtin_amdgcn_wave_barrier();
+    nr = 0;
+  };
+  auto flush_v = [&]() {
+    if (!nv) return;
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&a.ctr->qtail, (unsigned long long)nv);
+    base = __shfl(base, 0);
+    cnt_v += nv;
+    for (int j = lane; j < nv; j += kW) {
+      if (base + j < a.cap) q_put(&a.Q[base + j], stg->v[j], a.qatomic);
+      else flags |= kQOverflow;
+    }
+    __builtin_amdgcn_wave_barrier();
+    nv = 0;
+  };
+  // insert one configuration per lane (have): R when it linearized x (x's
+  // bit cleared), else V; the new ones are staged
+  auto insert_put = [&](bool have, Cfg c) {
+    const bool toR = have && (c.mask & w.xbit);
+    if (toR) c.mask &= ~w.xbit;
+    int r = -2;
+    if (have) r = ctab_insert(toR ? a.tabR : a.tabV, a.tmask, c, a.cshift);
+    if (r == -1) flags |= kQTfull;
+    const bool nR = r == 1 && toR, nV = r == 1 && !toR;
+    const uint64_t mR = __ballot(nR), mV = __ballot(nV);
+    if (nR) {
+      stg->r[nr + __popcll(mR & below)] = c;
+      andm &= c.mask;
+    }
+    // new V: the wave's own stack first, up to a.local entries; the excess
+    // spills to the queue
+    const int kv = __popcll(mV), room = max(0, a.local - nl), rk = __popcll(mV & below);
+    const unsigned long long word = c.mask | ((unsigned long long)c.val << a.cshift);
+    if (nV && rk < room) stg->loc[nl + rk] = word;
+    else if (nV) stg->v[nv + rk - room] = word;
+    const int kl = min(kv, room);
+    nl += kl;
+    nr += __popcll(mR);
+    nv += kv - kl;
+    if (nr > kStage - kW) flush_r();
+    if (nv > kStage - kW) flush_v();
+  };
+  auto insert_stash = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    const bool have = lane < ns;
+    Cfg sc{};
+    if (have) sc = stg->s[lane];
+    __builtin_amdgcn_wave_barrier();
+    insert_put(have, sc);
+    ns = 0;
+  };
+  // expand one configuration (wave-uniform c): lane t tests slot t
+  auto expand = [&](const Cfg &c) {
+    const bool cand = is_mut && !(c.mask & bit) && !(me.before & ~c.mask) && legal(me, c.ver, c.val);
+    Cfg s = c;
+    if (cand) {
+      s.mask |= bit | rv_me;
+      s.ver = c.ver + 1;
+      s.val = (uint32_t)me.value;
+      uint64_t pr = vreads & ~s.mask;
+      while (pr) {
+        const int b = __builtin_ctzll(pr);
+        pr &= pr - 1;
+        if (legal(w.s[b], s.ver, s.val)) s.mask |= 1ULL << b;
+      }
+    }
+    const uint64_t m = __ballot(cand);
+    const int k = __popcll(m);
+    explored += k;
+    if (ns + k > kW) insert_stash();
+    if (cand) stg->s[ns + __popcll(m & below)] = s;
+    ns += k;
+  };
+
+  // Work-first: a wave finishes what it finds.  New V configurations go to
+  // the wave's own LDS stack (up to a.local of them) and are expanded by the
+  // wave itself; only the excess spills to the device-wide queue, where idle
+  // waves claim it.  So the hot queue counters are touched per spilled batch
+  // and per claim, not per configuration.  Termination accounting is per
+  // GLOBAL item (an F entry, or a queue entry): it counts as done once its
+  // local subtree is finished and the wave's spills are reserved.
+  unsigned long long g = 0;  // global items taken whose local subtrees are not finished
+  auto drain_local = [&]() {
+    for (;;) {
+      if (nl == 0) {
+        if (ns) {  // pending successors may still push local work
+          insert_stash();
+          continue;
+        }
+        break;
+      }
+      const int k = min(nl, kW);
+      unsigned long long word = 0;
+      if (lane < k) word = stg->loc[nl - k + lane];
+      __builtin_amdgcn_wave_barrier();
+      nl -= k;
+      for (int j = 0; j < k; j++) {
+        const unsigned long long wj =
+            ((unsigned long long)__shfl((uint32_t)(word >> 32), j) << 32) | __shfl((uint32_t)word, j);
+        Cfg c;
+        c.mask = wj & lowmask;
+        c.val = (uint32_t)(wj >> a.cshift);
+        c.ver = a.vbase + (uint32_t)__popcll(c.mask & muts);
+        expand(c);
+      }
+    }
+    flush_v();  // spills reserved before the items are counted done
+    if (g && lane == 0) atomicAdd(&a.ctr->done, g);
+    g = 0;
+  };
+
+  // 1. F: a wave takes 64 entries at a time, splits them, and finishes
+  // their local subtrees
+  for (long long b = wave * kW; b < a.nF; b += nwaves * kW) {
+    const int cnt = (int)min((long long)kW, a.nF - b);
+    Cfg c{};
+    if (lane < cnt) {
+      c = a.F[b + lane];
+      fix_f(c, w);
+    }
+    insert_put(lane < cnt, c);
+    g += (unsigned long long)cnt;
+    drain_local();
+  }
+
+  // 2. the queue: claim runs of spilled entries, finish each one's subtree
+  uint64_t pending = 0;  // lanes holding a claimed entry not yet read
+  unsigned long long my_idx = 0, t_seen = 0;
+  int idle = 0, waits = 0;
+  const unsigned long long nF = (unsigned long long)a.nF;
+  for (;;) {
+    if (!pending) {
+      unsigned long long h = 0, t = 0;
+      if (lane == 0) {
+        t = q_peek(&a.ctr->qtail);
+        h = q_peek(&a.ctr->qhead);
+      }
+      h = __shfl(h, 0);
+      t = __shfl(t, 0);
+      t_seen = max(t_seen, t);
+      if (h < t) {
+        const unsigned long long c = min(
+            64ULL, max((unsigned long long)a.min_claim,
+                       (t - h + (unsigned long long)nwaves - 1) / (unsigned long long)nwaves));
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(&a.ctr->qhead, c);
+        base = __shfl(base, 0);
+        pending = c == 64 ? ~0ULL : ((1ULL << c) - 1);
+        my_idx = base + lane;
+        idle = 0;
+      } else {
+        // nothing to claim: finished when every item that exists is done
+        // (done read before qtail; done <= |F| + qtail always)
+        int fin = 0;
+        if (lane == 0) fin = q_finished(a.ctr, nF, idle, 16);
+        if (__shfl(fin, 0)) break;
+        q_sleep(idle < 6 ? 1 << idle : 64);
+        idle++;
+        continue;
+      }
+    }
+    // read the claimed entries that have arrived (an entry reserved beyond
+    // the capacity is never written: it is done as soon as it exists)
+    const bool mine = (pending >> lane) & 1;
+    const bool beyond = my_idx >= a.cap;
+    const bool dead = mine && beyond && my_idx < t_seen;
+    unsigned long long word = kEmpty;
+    if (mine && !beyond) word = q_take(&a.Q[my_idx], a.qatomic || (waits & 7) == 7);
+    const bool got = mine && !beyond && word != kEmpty;
+    const uint64_t mgot = __ballot(got), mdead = __ballot(dead);
+    pending &= ~(mgot | mdead);
+    g += (unsigned long long)__popcll(mgot | mdead);
+    if (got) stg->loc[__popcll(mgot & below)] = word;  // the local stack is empty here
+    nl = __popcll(mgot);
+    if (g) drain_local();
+    if (pending && !mgot) {
+      // claimed entries not written yet (their producer is mid-flush), or
+      // beyond the queue's final length: wait, or finish with everyone
+      int end = 0;
+      unsigned long long t2 = 0;
+      if (lane == 0) {
+        end = q_finished(a.ctr, nF, waits, 16);
+        t2 = q_peek(&a.ctr->qtail);
+      }
+      if (__shfl(end, 0)) break;
+      t_seen = max(t_seen, __shfl(t2, 0));
+      waits++;
+      q_sleep(1);
+    }
+  }
+  flush_r();
+  // 3. report: this workgroup's explored, R AND, flags
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)andm, off), hi = __shfl_xor((uint32_t)(andm >> 32), off);
+    andm &= ((unsigned long long)hi << 32) | lo;
+    flags |= ((unsigned long long)__shfl_xor((uint32_t)(flags >> 32), off) << 32) |
+             __shfl_xor((uint32_t)flags, off);
+  }
+  if (lane == 0) {
+    red_e[wid] = explored;
+    red_a[wid] = andm;
+    red_f[wid] = flags;
+    red_r[wid] = cnt_r;
+    red_v[wid] = cnt_v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    QRep r{};
+    r.andmask = ~0ULL;
+    for (int k = 0; k < (int)(blockDim.x / kW); k++) {
+      r.explored += red_e[k];
+      r.andmask &= red_a[k];
+      r.flags |= red_f[k];
+      r.nR += red_r[k];
+      r.nV += red_v[k];
+    }
+    a.rep[blockIdx.x] = r;
+  }
+}
+
 // ------------------------------------------------------------ host side
 
 uint64_t splitmix(uint64_t x) {
@@ -940,6 +1362,22 @@ struct Rank {
   Cfg *sendb = nullptr, *recvb = nullptr;
   size_t send_cap = 0, recv_cap = 0;
   uint32_t epoch = 0;
+  // queue path (fx_return_kernel): queue, two table sets, two counter blocks,
+  // host-mapped per-workgroup reports
+  bool qpath = true;  // LC_FX_QUEUE=0: the level-synchronous launches (A/B)
+  int qdbg_g = 0, qmax_g = kQMaxWG, qmin_claim = 1;
+  bool qdbg_time = false;  // LC_FXQ_TIME: host-side launch / sync split on stderr
+  double qt_launch = 0, qt_sync = 0;
+  int64_t qt_n = 0;
+  int64_t qper_wg = 256;
+  int qlocal = 64, qatomic = 0;
+  bool qdbg_hostclear = false;
+  unsigned long long *qQ = nullptr;
+  unsigned long long *qtab[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  QCtr *qctr = nullptr;
+  QRep *qrep = nullptr, *qrep_dev = nullptr;
+  int qpar = 0;
+  long long qdirty[2] = {0, 0};
 
   ~Rank() { release(); }
 
@@ -953,6 +1391,14 @@ struct Rank {
     dWin = nullptr;
     dCtr = nullptr;
     dExp = nullptr;
+    for (void *p : {(void *)qQ, (void *)qtab[0][0], (void *)qtab[0][1], (void *)qtab[1][0],
+                    (void *)qtab[1][1], (void *)qctr})
+      if (p) (void)hipFree(p);
+    qQ = nullptr;
+    qtab[0][0] = qtab[0][1] = qtab[1][0] = qtab[1][1] = nullptr;
+    qctr = nullptr;
+    if (qrep) (void)hipHostFree(qrep);
+    qrep = qrep_dev = nullptr;
     if (hWin) (void)hipHostFree(hWin);
     if (hCtr) (void)hipHostFree(hCtr);
     hWin = nullptr;
@@ -1049,6 +1495,19 @@ struct Rank {
     FX_TRY(hipHostMalloc(&hWin, sizeof(Win), hipHostMallocDefault));
     FX_TRY(hipHostMalloc(&hCtr, sizeof(Ctr), hipHostMallocDefault));
     std::memset(hWin, 0, sizeof(Win));
+    if (const char *q = getenv("LC_FX_QUEUE")) qpath = q[0] != '0';
+    if (const char *q = getenv("LC_FXQ_G")) qdbg_g = atoi(q);
+    qdbg_time = getenv("LC_FXQ_TIME") != nullptr;
+    if (const char *q = getenv("LC_FXQ_MAXG")) qmax_g = std::max(1, std::min(kQMaxWG, atoi(q)));
+    if (const char *q = getenv("LC_FXQ_MINCLAIM")) qmin_claim = std::max(1, std::min(64, atoi(q)));
+    if (const char *q = getenv("LC_FXQ_PERWG")) qper_wg = std::max(1, atoi(q));
+    if (const char *q = getenv("LC_FXQ_LOCAL")) qlocal = std::max(0, std::min(kLoc - 64, atoi(q)));
+    if (const char *q = getenv("LC_FXQ_ATOMIC")) qatomic = q[0] == '1';
+    if (const char *q = getenv("LC_FXQ_HOSTCLEAR")) qdbg_hostclear = q[0] == '1';
+    FX_TRY(hipMalloc(&qctr, 2 * sizeof(QCtr)));
+    FX_TRY(hipMemset(qctr, 0, 2 * sizeof(QCtr)));
+    FX_TRY(hipHostMalloc(&qrep, kQMaxWG * sizeof(QRep), hipHostMallocMapped | hipHostMallocCoherent));
+    FX_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&qrep_dev), qrep, 0));
     if (nc) {
       FX_TRY(hipMalloc(&nc->d, sizeof(int64_t) * Nccl::kScr));
       FX_TRY(hipHostMalloc(&nc->h, sizeof(int64_t) * Nccl::kScr, hipHostMallocDefault));
@@ -1083,6 +1542,21 @@ struct Rank {
     FX_TRY(hipMalloc(&keyV, tcap * sizeof(Cfg)));
     FX_TRY(hipMemsetAsync(tagR, 0, tcap * 8, st));
     FX_TRY(hipMemsetAsync(tagV, 0, tcap * 8, st));
+    for (void *p : {(void *)qQ, (void *)qtab[0][0], (void *)qtab[0][1], (void *)qtab[1][0],
+                    (void *)qtab[1][1]})
+      if (p) (void)hipFree(p);
+    qQ = nullptr;
+    qtab[0][0] = qtab[0][1] = qtab[1][0] = qtab[1][1] = nullptr;
+    if (qpath) {
+      FX_TRY(hipMalloc(&qQ, need * 8));
+      FX_TRY(hipMemsetAsync(qQ, 0xFF, need * 8, st));
+      for (int sI = 0; sI < 2; sI++)
+        for (int t = 0; t < 2; t++) {
+          FX_TRY(hipMalloc(&qtab[sI][t], tcap * 8));
+          FX_TRY(hipMemsetAsync(qtab[sI][t], 0xFF, tcap * 8, st));
+        }
+      qdirty[0] = qdirty[1] = 0;
+    }
     list_cap = need;
     tmask = tcap - 1;
     epoch = 0;
@@ -1226,6 +1700,12 @@ struct Rank {
   }
 
   int check(const lc_op *o, int64_t n, const lc_opts *opts, lc_key_result *res);
+
+  // lc_fx_frontier: stop at the return of record stop_op and copy out up to
+  // dump_max configurations of the frontier that return would expand
+  int64_t stop_op = -1;
+  lc_fx_config *dump = nullptr;
+  int32_t dump_max = 0, dump_n = 0;
 };
 
 bool same_class(const lc_op &a, const lc_op &b) {
@@ -1357,6 +1837,10 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   const bool debug = getenv("LC_FX_DEBUG") != nullptr;
   const int64_t tmul = getenv("LC_FX_TABLE_MUL") ? std::max(1, atoi(getenv("LC_FX_TABLE_MUL"))) : 4;
   const int64_t spad = getenv("LC_FX_SPEC_PAD") ? atoi(getenv("LC_FX_SPEC_PAD")) : 1;
+  // queue path: the version every configuration of a return has before the
+  // mutation slots its mask names (the initial one plus every mutation that
+  // left the window linearized: returned, or retired)
+  uint32_t vbase = (uint32_t)opts.init_version;
 
   auto slot_pre = [&](const lc_op &a, Slot &s) {
     const int32_t ver = clamp_ver(a.version);
@@ -1421,6 +1905,41 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       continue;
     }
     if (slot_of[x] < 0) continue;  // trivial read, or retired
+    if (x == stop_op) {
+      // lc_fx_frontier: the frontier this return would expand, with the
+      // updates the next split would apply (retirements, reads called since)
+      const int64_t k = std::min<int64_t>(nF, dump_max);
+      std::vector<Cfg> hc((size_t)k);
+      if (k) FX_TRY(hipMemcpy(hc.data(), F, sizeof(Cfg) * (size_t)k, hipMemcpyDeviceToHost));
+      std::vector<int64_t> val_of(vids.size());
+      for (const auto &kv : vids) val_of[(size_t)kv.second] = kv.first;
+      for (int64_t i = 0; i < k; i++) {
+        Cfg c = hc[(size_t)i];
+        c.mask &= ~fclear;
+        for (uint64_t pr = fclose; pr;) {
+          const int b = __builtin_ctzll(pr);
+          pr &= pr - 1;
+          const Slot &r = w.s[b];
+          if (((((int32_t)c.ver ^ r.nv) & r.nvm) | (((int32_t)c.val ^ r.nl) & r.nlm)) == 0)
+            c.mask |= 1ULL << b;
+        }
+        lc_fx_config &d = dump[i];
+        d.version = (int64_t)c.ver;
+        d.value = val_of[c.val];
+        d.n_pending = 0;
+        for (uint64_t pend = occ & ~c.mask; pend;) {
+          const int b = __builtin_ctzll(pend);
+          pend &= pend - 1;
+          d.pending[d.n_pending++] = slot_op[b];
+        }
+        std::sort(d.pending, d.pending + d.n_pending);
+      }
+      dump_n = (int32_t)k;
+      res->verdict = LC_UNKNOWN;
+      res->reason = LC_REASON_NONE;
+      decided = true;
+      break;
+    }
     const int sx = slot_of[x];
     const uint64_t xb = 1ULL << sx;
     // the window as the device sees it during this return
@@ -1482,6 +2001,77 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         FX_TRY(hipGetLastError());
       }
       bool tfull = false;
+      if (qpath && !multi() && compact) {
+        // one launch per attempt (fx_return_kernel): split, queue, report
+        int G = (int)std::min<int64_t>(
+            qmax_g, std::max<int64_t>(1, (std::max(nF, last_work) + qper_wg - 1) / qper_wg));
+        if (qdbg_g > 0) G = qdbg_g;  // LC_FXQ_G (debug)
+        QArgs qa;
+        qa.F = F;
+        qa.nF = nF;
+        qa.Q = qQ;
+        qa.listR = Rl;
+        qa.cap = list_cap;
+        qa.tabR = qtab[qpar][0];
+        qa.tabV = qtab[qpar][1];
+        qa.tmask = std::min<uint64_t>(tmask, (1ULL << tlog) - 1);
+        qa.cshift = cshift;
+        qa.vbase = vbase;
+        qa.ctr = qctr + qpar;
+        qa.ctr_next = qctr + (qpar ^ 1);
+        qa.clrR = qtab[qpar ^ 1][0];
+        qa.clrV = qtab[qpar ^ 1][1];
+        qa.clr_words = qdirty[qpar ^ 1];
+        qa.rep = qrep_dev;
+        qa.min_claim = qmin_claim;
+        qa.local = qlocal;
+        qa.qatomic = qatomic;
+        qa.max_g = 0;
+        if (qdbg_hostclear) {  // LC_FXQ_HOSTCLEAR (debug): tables cleared by the host instead
+          FX_TRY(hipMemsetAsync(qa.tabR, 0xFF, (qa.tmask + 1) * 8, st));
+          FX_TRY(hipMemsetAsync(qa.tabV, 0xFF, (qa.tmask + 1) * 8, st));
+          qa.clr_words = 0;
+        }
+        const auto tq0 = std::chrono::steady_clock::now();
+        fx_return_kernel<<<G, 256, 0, st>>>(qa, w);
+        FX_TRY(hipGetLastError());
+        qdirty[qpar ^ 1] = 0;
+        qdirty[qpar] = (long long)qa.tmask + 1;
+        qpar ^= 1;
+        const auto tq1 = std::chrono::steady_clock::now();
+        FX_TRY(hipStreamSynchronize(st));
+        if (qdbg_time) {
+          const auto tq2 = std::chrono::steady_clock::now();
+          qt_launch += std::chrono::duration<double, std::micro>(tq1 - tq0).count();
+          qt_sync += std::chrono::duration<double, std::micro>(tq2 - tq1).count();
+          qt_n++;
+        }
+        unsigned long long q_expl = 0, q_and = ~0ULL, q_flags = 0;
+        int64_t q_nR = 0, q_nV = 0;
+        for (int g = 0; g < G; g++) {
+          q_expl += qrep[g].explored;
+          q_and &= qrep[g].andmask;
+          q_flags |= qrep[g].flags;
+          q_nR += (int64_t)qrep[g].nR;
+          q_nV += (int64_t)qrep[g].nV;
+        }
+        const bool q_tfull = (q_flags & kQTfull) != 0;
+        if (q_tfull && tlog < tlog_full) {
+          tlog = std::min(tlog + 2, tlog_full);
+          stats.redos++;
+          continue;
+        }
+        over = q_tfull || (q_flags & kQOverflow) || q_nR + q_nV > budget;
+        explored_repl += (int64_t)q_expl;
+        explored_seen += q_expl;  // the level path's counters start from it
+        hCtr->nR = (unsigned long long)q_nR;
+        hCtr->andmask = q_and;
+        nRg = q_nR;
+        last_work = q_nR + q_nV;
+        if (timed) timeout = std::chrono::duration<double, std::milli>(
+                                 std::chrono::steady_clock::now() - t0).count() > (double)opts.time_budget_ms;
+        break;
+      }
       if (!part) {
         // replicated: a small return runs whole in one workgroup; otherwise
         // (or for what it leaves) speculative batches of levels over the
@@ -1653,6 +2243,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     nF = (int64_t)hCtr->nR;
     nFglobal = nRg;
     stats.max_local_frontier = std::max<int64_t>(stats.max_local_frontier, nF);
+    if (!((reads >> sx) & 1)) vbase++;  // x, linearized in every configuration now
     occ &= ~xb;
     reads &= ~xb;
     kzob ^= w.s[sx].zob;
@@ -1683,6 +2274,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         if (!((all >> u) & 1)) continue;
         slot_of[slot_op[u]] = -1;  // its return (if any) is now a no-op
         kzob ^= w.s[u].zob;
+        if (!((reads >> u) & 1)) vbase++;
       }
       occ &= ~all;
       reads &= ~all;
@@ -1701,6 +2293,13 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   FX_TRY(hipStreamSynchronize(st));
   stats.levels = (int64_t)hCtr->levels + stats.part_levels;
   stats.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (qdbg_time) {
+    fprintf(stderr, "fxq: returns %lld redos %lld launches %lld launch us %.1f sync us %.1f total ms %.2f\n",
+            (long long)stats.returns, (long long)stats.redos, (long long)qt_n, qt_launch, qt_sync,
+            stats.total_ms);
+    qt_launch = qt_sync = 0;
+    qt_n = 0;
+  }
   return 0;
 }
 
@@ -1954,6 +2553,36 @@ void lc_fx_abort(lc_fx *fx) {
   bool rccl = false;
   for (Rank *r : fx->ranks) rccl |= r->nc != nullptr;
   if (rccl) abort_comms(fx);
+}
+
+int lc_fx_frontier(lc_fx *fx, const lc_op *ops, int64_t n, const lc_opts *opts, int64_t stop_op,
+                   lc_fx_config *out, int32_t max, int32_t *n_out) {
+  if (!fx || !n_out || n < 0 || (n > 0 && !ops) || max < 0 || (max > 0 && !out)) return -EINVAL;
+  *n_out = 0;
+  if (fx->threads || fx->ranks[0]->multi()) {
+    fx->err = "lc_fx_frontier: a one-rank engine only (the frontier is partitioned otherwise)";
+    return -EINVAL;
+  }
+  if (stop_op < 0 || stop_op >= n || ops[stop_op].ret == LC_INF) {
+    fx->err = "lc_fx_frontier: stop_op must be an op of the key that returns";
+    return -EINVAL;
+  }
+  Rank *r = fx->ranks[0];
+  (void)hipSetDevice(r->dev);
+  r->stop_op = stop_op;
+  r->dump = out;
+  r->dump_max = max;
+  r->dump_n = 0;
+  lc_key_result res;
+  const int e = r->check(ops, n, opts, &res);
+  r->stop_op = -1;
+  r->dump = nullptr;
+  if (e) {
+    fx->err = r->err;
+    return e;
+  }
+  *n_out = r->dump_n;
+  return 0;
 }
 
 int lc_fx_last_stats(lc_fx *fx, lc_fx_stats *out) {

@@ -14,15 +14,22 @@ unpinned]:
 * :final-paths  from a configuration, paths of [{:op, :model}] steps that
                 try to linearize :op and end in an inconsistent model.
 
-The GPU search does not return knossos's whole frontier.  What it returns is
-the witness of the history prefix just before :op's completion (lc_aux,
-LC_WITNESS_PREFIX: a linearization, certified independently by the tests).
-That linearization is one configuration of the frontier, so :configs holds
-that one configuration (knossos truncates to 10), and :final-paths are built
-from it by stepping the VersionedRegister model (register.clj:60-96) — with
-the model's own messages — through :op alone and through each pending op
-followed by :op.  Keys without a prefix witness (decided by the frontier
-search tiers) get :previous-ok and the failing :op only.
+Two sources, by the tier that decided the key:
+
+* keys the frontier search decided (no witness): the search's own frontier
+  just before :op's completion (include/lincheck_fx.h lc_fx_frontier — the
+  oracle's JITC frontier at that return, configuration for configuration, in
+  tests/test_fx.py), up to 10 configurations as knossos keeps;
+* keys the version-order / gap tiers decided: the witness of the history
+  prefix just before :op's completion (lc_aux, LC_WITNESS_PREFIX: a
+  linearization, certified independently by the tests), which is one
+  configuration of that frontier.
+
+:final-paths are built from those configurations by stepping the
+VersionedRegister model (register.clj:60-96) — with the model's own messages
+— through :op alone and through each pending op followed by :op.  The
+search does not record which op each configuration linearized last, so
+frontier configurations carry no :last-op.
 """
 from .abi import LC_INF
 
@@ -83,6 +90,58 @@ def previous_ok(done, fail_ret):
     return best["completion"] if best is not None else None
 
 
+def _final_paths(done, fail_op, states_pending, stepper=None):
+    """knossos's :final-paths: from each configuration (state, pending op
+    indices), the paths that try to linearize the failing op — directly, or
+    after one pending op — and end inconsistent; at most MAX_ENTRIES."""
+    stepper = stepper or step
+    paths = []
+
+    def try_op(st, i):
+        nxt, err = stepper(st, done[i])
+        return (nxt, {"op": _op_map(done[i]), "model": _model(nxt)}) if err is None else \
+            (None, {"op": _op_map(done[i]), "model": {"inconsistent": err}})
+
+    for state, last, pending in states_pending:
+        head = {"op": _op_map(done[last]) if last is not None else None, "model": _model(state)}
+        _, end = try_op(state, fail_op)
+        if "inconsistent" in end["model"] and len(paths) < MAX_ENTRIES:
+            paths.append([head, end])
+        for i in pending:
+            if i == fail_op or len(paths) >= MAX_ENTRIES:
+                continue
+            st2, mid = try_op(state, i)
+            path = [head, mid]
+            if st2 is not None:
+                _, end = try_op(st2, fail_op)
+                if "inconsistent" not in end["model"]:
+                    continue  # linearizes the op: not a final path
+                path.append(end)
+            paths.append(path)
+    return paths
+
+
+def frontier_analysis(done, fail_op, fail_ret, configs, values, versioned=True):
+    """knossos-shaped keys from the search's frontier before the failing
+    return.  configs: [(version, value id, pending record indices)] from
+    lc_fx_frontier; values: the key's value table (id -> value)."""
+    out = {"previous-ok": previous_ok(done, fail_ret)}
+
+    def val(i):
+        return None if i < 0 else values[i] if i < len(values) else i
+
+    cfgs, sp = [], []
+    for ver, vid, pending in configs[:MAX_ENTRIES]:
+        state = (ver, val(vid))
+        cfgs.append({"model": _model(state) if versioned else {"value": state[1]},
+                     "pending": [done[i]["invoke"] for i in pending]})
+        sp.append((state, None, list(pending)))
+    out["configs"] = cfgs
+    if versioned:
+        out["final-paths"] = _final_paths(done, fail_op, sp)
+    return out
+
+
 def invalid_analysis(done, fail_op, fail_ret, witness=None, init=(0, None)):
     """knossos-shaped keys for an invalid key.  done: the key's completed
     ops (history.complete order = record order); fail_op: index of the
@@ -112,26 +171,6 @@ def invalid_analysis(done, fail_op, fail_ret, witness=None, init=(0, None)):
     last_op = _op_map(done[last]) if last is not None else None
     cfg = {"model": _model(state), "last-op": last_op,
            "pending": [done[i]["invoke"] for i in pending]}
-    head = {"op": last_op, "model": _model(state)}
-    paths = []
-
-    def try_op(st, i):
-        nxt, err = step(st, done[i])
-        return (nxt, {"op": _op_map(done[i]), "model": _model(nxt)}) if err is None else \
-            (None, {"op": _op_map(done[i]), "model": {"inconsistent": err}})
-
-    _, end = try_op(state, fail_op)
-    paths.append([head, end])
-    for i in pending:
-        if i == fail_op or len(paths) >= MAX_ENTRIES:
-            continue
-        st2, mid = try_op(state, i)
-        path = [head, mid]
-        if st2 is not None:
-            _, end = try_op(st2, fail_op)
-            if "inconsistent" not in end["model"]:
-                continue  # linearizes the op: not a final path
-            path.append(end)
-        paths.append(path)
+    paths = _final_paths(done, fail_op, [(state, last, pending)])
     out.update({"configs": [cfg], "last-op": last_op, "final-paths": paths})
     return out

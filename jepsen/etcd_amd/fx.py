@@ -51,6 +51,11 @@ LC_FX_FLAG_EXCHANGE_SELF = 2
 LC_FX_RCCL_ID_BYTES = 128
 
 
+class LcFxConfig(ctypes.Structure):
+    _fields_ = [("version", ctypes.c_int64), ("value", ctypes.c_int64),
+                ("n_pending", ctypes.c_int64), ("pending", ctypes.c_int64 * 64)]
+
+
 class LcFxStats(ctypes.Structure):
     _fields_ = [("total_ms", ctypes.c_double), ("returns", ctypes.c_int64),
                 ("levels", ctypes.c_int64), ("part_returns", ctypes.c_int64),
@@ -88,6 +93,10 @@ def _lib():
         L.lc_fx_close.restype = None
         L.lc_fx_abort.argtypes = [vp]
         L.lc_fx_abort.restype = None
+        L.lc_fx_frontier.argtypes = [vp, p, ctypes.c_int64, ctypes.POINTER(abi.LcOpts),
+                                     ctypes.c_int64, p, ctypes.c_int32,
+                                     ctypes.POINTER(ctypes.c_int32)]
+        L.lc_fx_frontier.restype = ctypes.c_int
         _bound = True
     return L
 
@@ -243,6 +252,22 @@ class FrontierExchange:
                 err += " (transport: %r)" % (self.transport.error,)
             raise abi.LcError(rc, "lc_fx_check: " + err)
         return out[0]
+
+    def frontier(self, ops, stop_op, max_configs=10, opts=None):
+        """knossos's :configs: up to max_configs configurations of the
+        frontier just before the :ok return of record stop_op (for an invalid
+        key, its fail_op), as (version, value id, pending record indices)."""
+        L = _lib()
+        ops = abi.as_ops(ops)
+        buf = (LcFxConfig * max(1, max_configs))()
+        n = ctypes.c_int32(0)
+        o = opts if opts is not None else abi.default_opts()
+        rc = L.lc_fx_frontier(self._h, abi._ptr(ops), len(ops), ctypes.byref(o), int(stop_op),
+                              ctypes.cast(buf, ctypes.c_void_p), max_configs, ctypes.byref(n))
+        if rc != 0:
+            raise abi.LcError(rc, "lc_fx_frontier: " + L.lc_fx_last_error(self._h).decode())
+        return [(int(c.version), int(c.value), tuple(int(c.pending[j]) for j in range(c.n_pending)))
+                for c in buf[:n.value]]
 
     def stats(self):
         s = LcFxStats()

@@ -213,13 +213,15 @@ def pack_key(subhistory, intern=None, model="versioned-register"):
     return recs, done
 
 
-def pack(history, model="versioned-register", independent=True, init_value=None):
+def pack(history, model="versioned-register", independent=True, init_value=None,
+         values_out=None):
     """Whole history -> (keys, ops (n,6), key_off, per-key completed ops).
 
     independent=False checks the history as one key (checker/linearizable
     without jepsen.independent, as lock.clj:243-244 does); its key is None.
     A non-nil init_value is interned first in every key, so it is id 0 there
-    (pass 0 as lc_opts.init_value)."""
+    (pass 0 as lc_opts.init_value).  values_out (a list), if given, receives
+    each key's value table (id -> value)."""
     hist = index_history(history)
     if independent:
         subs = split_by_key(hist)
@@ -232,6 +234,8 @@ def pack(history, model="versioned-register", independent=True, init_value=None)
         if init_value is not None and model != "mutex":
             it(init_value)
         recs, d = pack_key(subs[k], it, model)
+        if values_out is not None:
+            values_out.append(it.values)
         parts.append(recs)
         done.append(d)
     key_off = np.zeros(len(keys) + 1, dtype=np.int64)

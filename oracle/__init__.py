@@ -56,6 +56,9 @@ def lib():
         L.oracle_check_witness.argtypes = [vp, vp, ctypes.c_int64, ctypes.POINTER(_Opts), vp, vp,
                                            vp, vp, vp, ctypes.c_int]
         L.oracle_check_witness.restype = ctypes.c_int
+        L.oracle_frontier.argtypes = [vp, ctypes.c_int64, ctypes.POINTER(_Opts), ctypes.c_int,
+                                      ctypes.c_int64, vp, ctypes.c_int64, vp]
+        L.oracle_frontier.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -73,6 +76,25 @@ def check(ops, key_off, algo=JIT, n_threads=1, max_configs=0, init_version=0,
                             ctypes.byref(o), out.ctypes.data_as(ctypes.c_void_p),
                             algo, n_threads)
     return rc, out
+
+
+CFG_WORDS = 67
+
+
+def frontier(ops, stop_op, algo=JITC, max_configs=100000, init_value=-1, init_version=0):
+    """The JIT search's frontier just before the :ok return of record
+    stop_op: a set of (version, value, pending ops tuple)."""
+    ops = np.ascontiguousarray(ops, dtype=np.int64).reshape(-1, 6)
+    out = np.zeros((max_configs, CFG_WORDS), dtype=np.int64)
+    n = ctypes.c_int64(0)
+    o = _Opts(init_version, init_value, 0, 0, 0)
+    rc = lib().oracle_frontier(ops.ctypes.data_as(ctypes.c_void_p), len(ops), ctypes.byref(o),
+                               algo, int(stop_op), out.ctypes.data_as(ctypes.c_void_p),
+                               max_configs, ctypes.byref(n))
+    if rc != 0:
+        raise ValueError("oracle_frontier: %d" % rc)
+    k = min(n.value, max_configs)
+    return {(int(r[0]), int(r[1]), tuple(int(v) for v in r[3:3 + r[2]])) for r in out[:k]}, n.value
 
 
 WIT_OK, WIT_NONE = 1, 0

@@ -291,8 +291,27 @@ static void close_reads(const lc_op *o, const int32_t *slot_op, const uint64_t *
 
 #define BIT(a, s) (((a)[(s) >> 6] >> ((s) & 63)) & 1)
 
+/* oracle_frontier: stop at the return of stop_op and dump the frontier that
+ * return expands (every configuration: state + sorted pending ops). */
+typedef struct frontier_req {
+  int64_t stop_op;
+  int64_t *out;  /* max entries of ORACLE_CFG_WORDS int64 */
+  int64_t max;
+  int64_t n;     /* configurations in the frontier (may exceed max) */
+} frontier_req;
+
+static void check_key_jit_fr(const lc_op *o, int64_t n, const lc_opts *opts,
+                             int64_t budget, int reduce, lc_key_result *res,
+                             frontier_req *fr);
+
 static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
                           int64_t budget, int reduce, lc_key_result *res) {
+  check_key_jit_fr(o, n, opts, budget, reduce, res, NULL);
+}
+
+static void check_key_jit_fr(const lc_op *o, int64_t n, const lc_opts *opts,
+                             int64_t budget, int reduce, lc_key_result *res,
+                             frontier_req *fr) {
   const int closure = (reduce & ORACLE_FLAG_READ_CLOSURE) != 0;
   const int symmetry = (reduce & ORACLE_FLAG_CRASH_SYMMETRY) != 0;
   const int retire = (reduce & ORACLE_FLAG_RETIRE) != 0;
@@ -398,6 +417,27 @@ static void check_key_jit(const lc_op *o, int64_t n, const lc_opts *opts,
       continue;
     }
     if (slot_of[x] < 0) continue; /* trivial read: nothing to do */
+    if (fr && x == fr->stop_op) {
+      fr->n = (int64_t)F.n;
+      for (size_t i = 0; i < F.n && (int64_t)i < fr->max; i++) {
+        const uint64_t *c = cset_get(&F, i);
+        int64_t *d = fr->out + i * ORACLE_CFG_WORDS;
+        d[0] = (int64_t)c[bw];
+        d[1] = (int64_t)c[bw + 1];
+        int64_t np = 0;
+        for (int u = 0; u < bw * 64 && np < 64; u++)
+          if (BIT(occ, u) && !BIT(c, u)) d[3 + np++] = slot_op[u];
+        d[2] = np;
+        /* sorted by op index */
+        for (int64_t a = 1; a < np; a++)
+          for (int64_t b = a; b > 0 && d[3 + b - 1] > d[3 + b]; b--) {
+            const int64_t t = d[3 + b];
+            d[3 + b] = d[3 + b - 1];
+            d[3 + b - 1] = t;
+          }
+      }
+      goto done;
+    }
     const int sx = slot_of[x];
     const int wx = sx >> 6;
     const uint64_t bx = 1ULL << (sx & 63);
@@ -719,6 +759,21 @@ static void *worker(void *arg) {
       check_key_jit(o, n, j->opts, j->budget, j->reduce, r);
   }
   return NULL;
+}
+
+int oracle_frontier(const lc_op *ops, int64_t n, const lc_opts *opts, int algo,
+                    int64_t stop_op, int64_t *out, int64_t max, int64_t *n_out) {
+  if (!ops || n < 0 || !n_out || stop_op < 0 || stop_op >= n || (max > 0 && !out)) return -EINVAL;
+  if ((algo & 0xff) != ORACLE_JIT || key_malformed(ops, n)) return -EINVAL;
+  lc_opts dflt = {0, LC_NIL, 0, 0, 0};
+  if (!opts) opts = &dflt;
+  frontier_req fr = {stop_op, out, max, 0};
+  lc_key_result r;
+  check_key_jit_fr(ops, n, opts,
+                   opts->max_configs_per_key > 0 ? opts->max_configs_per_key : (int64_t)4000000,
+                   algo & ~0xff, &r, &fr);
+  *n_out = fr.n;
+  return 0;
 }
 
 int oracle_check(const lc_op *ops, const int64_t *key_off, int64_t n_keys,

@@ -40,6 +40,15 @@ int oracle_check(const lc_op *ops, const int64_t *key_off, int64_t n_keys,
                  const lc_opts *opts, lc_key_result *out, int algo,
                  int n_threads);
 
+/* The JIT search (algo = ORACLE_JIT | reductions) of one key, stopped at the
+ * :ok return of record stop_op: the frontier that return expands, up to max
+ * configurations of ORACLE_CFG_WORDS int64 each — version, value, number of
+ * pending ops, then the pending ops (record indices, sorted; at most 64).
+ * *n_out = the frontier's size (0 when stop_op's return is a no-op). */
+#define ORACLE_CFG_WORDS 67
+int oracle_frontier(const lc_op *ops, int64_t n, const lc_opts *opts, int algo,
+                    int64_t stop_op, int64_t *out, int64_t max, int64_t *n_out);
+
 /* The VersionedRegister step (register.clj:60-96) on int64 fields.
  * Returns 1 and writes the next state if legal, 0 if inconsistent,
  * -1 for an unknown f (the reference's condp has no default, :63). */

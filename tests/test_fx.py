@@ -122,6 +122,40 @@ def test_fx_rccl_one_rank_plain():
 
 
 @pytest.mark.gpu
+def test_fx_frontier_is_the_oracles_frontier():
+    """knossos's :configs for keys only the frontier search decides: the
+    frontier just before the failing return (lc_fx_frontier) is exactly the
+    oracle's JITC frontier at that return — each configuration's state and
+    pending ops, built there by replaying oracle_step — and a truncated copy
+    (knossos keeps 10) is a subset of it."""
+    from jepsen.etcd_amd.fx import FrontierExchange
+    rng = random.Random(0xC0F)
+    keys = [(random_casreg(rng, rng.randrange(4, 40), p_info=0.1), -1) for _ in range(150)]
+    keys += [(random_mutex(rng, rng.randrange(4, 40), p_info=0.1), FREE) for _ in range(100)]
+    ops, off, _, _ = abi.synth(12, 150, concurrency=8, p_info=0.01, p_anomaly=1.0, seed=0xC10)
+    ops = ops.copy()
+    ops[:, 3] = -1
+    keys += [(ops[off[k]:off[k + 1]].tolist(), -1) for k in range(12)]
+    n_inv = n_cfg = 0
+    with FrontierExchange(device=0) as fx:
+        for i, (recs, init) in enumerate(keys):
+            a = np.array(recs, dtype=np.int64).reshape(-1, 6)
+            o = abi.default_opts(init_value=init)
+            r = fx.check(a, o)
+            if r["verdict"] != 0:
+                continue
+            fo = int(r["fail_op"])
+            want, n_want = oracle.frontier(a, fo, init_value=init)
+            got = fx.frontier(a, fo, max_configs=1 << 16, opts=o)
+            assert set(got) == want and len(got) == n_want, (i, len(got), n_want)
+            top = fx.frontier(a, fo, max_configs=10, opts=o)
+            assert len(top) == min(10, n_want) and set(top) <= want, i
+            n_inv += 1
+            n_cfg += len(got)
+    assert n_inv >= 20 and n_cfg > n_inv
+
+
+@pytest.mark.gpu
 def test_fx_partition_switches_and_exchanges():
     """A key whose frontier crosses the thresholds both ways: replicated ->
     partitioned (filter by owner) -> replicated (gather), same result as one

@@ -461,6 +461,47 @@ def test_check_device_path_with_torch(ctx):
     assert (r2 == r).all()
 
 
+def test_register_checker_frontier_configs():
+    """knossos's :configs for keys the frontier search decides: a history
+    whose :ok completions carry no versions ([nil v], which the
+    VersionedRegister checks only by value, register.clj:64,71,84) sends every
+    key to the search tiers; each invalid key's "configs" (at most 10) are
+    configurations of the oracle's JITC frontier just before the failing
+    return — state and pending ops — and its final paths end inconsistent."""
+    from jepsen.etcd_amd import checker as C, history as H, synth
+    hist, _ = synth.jepsen_history(40, 80, concurrency=8, p_info=0.02,
+                                        p_anomaly=0.5, seed=11)
+    for op in hist:
+        v = op.get("value")
+        if op.get("type") == "ok" and isinstance(v, H.Tuple) and isinstance(v.value, (list, tuple)):
+            op["value"] = H.Tuple(v.key, [None, v.value[1]])
+    chk = C.register_checker(device_mask=1)
+    res = chk.check({"name": "etcd register"}, hist, {})
+    chk.close()
+    vals = []
+    keys, ops, off, done = H.pack(hist, values_out=vals)
+    n_checked = 0
+    for i, k in enumerate(keys):
+        lin = res["results"][k]["linear"]
+        if lin["valid?"] is not False:
+            continue
+        kops = ops[off[i]:off[i + 1]]
+        fo = next(j for j, d in enumerate(done[i])
+                  if (d["completion"] or d["invoke"])["index"] == lin["op"]["index"])
+        want, n_want = oracle.frontier(kops, fo)
+        assert 1 <= len(lin["configs"]) <= min(10, n_want)
+        for cfg in lin["configs"]:
+            val = cfg["model"]["value"]
+            vid = -1 if val is None else vals[i].index(val)
+            pend = tuple(sorted(next(j for j, d in enumerate(done[i])
+                                     if d["invoke"]["index"] == inv["index"])
+                                for inv in cfg["pending"]))
+            assert (cfg["model"]["version"], vid, pend) in want, (k, cfg)
+        assert all("inconsistent" in p[-1]["model"] for p in lin["final-paths"])
+        n_checked += 1
+    assert n_checked >= 5
+
+
 def test_register_checker_end_to_end(tmp_path):
     from jepsen.etcd_amd import checker as C, synth
     hist, labels = synth.jepsen_history(60, 120, concurrency=10, p_info=0.03,

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
         "lc_edn_n_events", "lc_edn_ops", "lc_edn_key_off", "lc_edn_key", "lc_edn_op_text",
         "lc_edn_value", "lc_edn_free", "lc_fx_open", "lc_fx_check", "lc_fx_last_stats",
         "lc_fx_last_error", "lc_fx_close", "lc_fx_open_devices", "lc_fx_rccl_unique_id",
-        "lc_fx_open_rccl", "lc_fx_abort"}
+        "lc_fx_open_rccl", "lc_fx_abort", "lc_fx_frontier"}
     for n in names:
         assert hasattr(lib, n), n
     assert abi.lib().lc_abi_version() == 2
