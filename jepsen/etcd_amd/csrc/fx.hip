@@ -1364,7 +1364,7 @@ struct Rank {
   uint32_t epoch = 0;
   // queue path (fx_return_kernel): queue, two table sets, two counter blocks,
   // host-mapped per-workgroup reports
-  bool qpath = true;  // LC_FX_QUEUE=0: the level-synchronous launches (A/B)
+  bool qpath = false;  // LC_FX_QUEUE=1: the one-launch-per-return queue path (dev A/B)
   int qdbg_g = 0, qmax_g = kQMaxWG, qmin_claim = 1;
   bool qdbg_time = false;  // LC_FXQ_TIME: host-side launch / sync split on stderr
   double qt_launch = 0, qt_sync = 0;
@@ -1495,7 +1495,7 @@ struct Rank {
     FX_TRY(hipHostMalloc(&hWin, sizeof(Win), hipHostMallocDefault));
     FX_TRY(hipHostMalloc(&hCtr, sizeof(Ctr), hipHostMallocDefault));
     std::memset(hWin, 0, sizeof(Win));
-    if (const char *q = getenv("LC_FX_QUEUE")) qpath = q[0] != '0';
+    if (const char *q = getenv("LC_FX_QUEUE")) qpath = q[0] == '1';
     if (const char *q = getenv("LC_FXQ_G")) qdbg_g = atoi(q);
     qdbg_time = getenv("LC_FXQ_TIME") != nullptr;
     if (const char *q = getenv("LC_FXQ_MAXG")) qmax_g = std::max(1, std::min(kQMaxWG, atoi(q)));
