@@ -1614,11 +1614,17 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, con
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const int64_t base_idx = kops[0].call;
   const int V0 = p.init_ver, init = p.init_val;
-  // unheld positions start with no value requirement
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int k = 4 * tid + j;
-    if (k < n && s.Own[k] == 0xFFFF) s.Val[k] = kAny;
+  // unheld positions start with no value requirement.  Thread t owns
+  // positions 4t..4t+3: one 8-byte / 16-byte LDS access per array instead of
+  // four lane-strided ones (4-way bank conflicts)
+  if (4 * tid < n) {
+    const uint2 own2 = reinterpret_cast<const uint2 *>(s.Own)[tid];
+    int4 v4 = reinterpret_cast<const int4 *>(s.Val)[tid];
+    if ((own2.x & 0xFFFF) == 0xFFFF) v4.x = kAny;
+    if ((own2.x >> 16) == 0xFFFF && 4 * tid + 1 < n) v4.y = kAny;
+    if ((own2.y & 0xFFFF) == 0xFFFF && 4 * tid + 2 < n) v4.z = kAny;
+    if ((own2.y >> 16) == 0xFFFF && 4 * tid + 3 < n) v4.w = kAny;
+    reinterpret_cast<int4 *>(s.Val)[tid] = v4;
   }
   __syncthreads();
   // pass G1: duplicates, value claims, the extent M, optional ops per chunk
@@ -1693,11 +1699,17 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, con
   // deadlines: Uh[k] = min(B[k..M-1]) for this thread's positions 4t..4t+3
   uint32_t bmin = kNever;
   int gapc = 0;
+  {
+    const uint4 b4 = reinterpret_cast<const uint4 *>(s.B)[tid];
+    const uint2 own2 = reinterpret_cast<const uint2 *>(s.Own)[tid];
+    const uint32_t bb[4] = {b4.x, b4.y, b4.z, b4.w};
+    const uint32_t oo[4] = {own2.x & 0xFFFF, own2.x >> 16, own2.y & 0xFFFF, own2.y >> 16};
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int k = 4 * tid + j;
-    bmin = umin(bmin, k < M ? s.B[k] : kNever);
-    gapc += (k < M) && s.Own[k] == 0xFFFF;
+    for (int j = 0; j < 4; j++) {
+      const int k = 4 * tid + j;
+      bmin = umin(bmin, k < M ? bb[j] : kNever);
+      gapc += (k < M) && oo[j] == 0xFFFF;
+    }
   }
   const int gpre = fg_prefix_wave(gapc, s);
   const uint32_t after = fg_suffix_min_excl(bmin, s);
@@ -1721,17 +1733,24 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, con
   c.moff = 0;
   int *opt_rec = reinterpret_cast<int *>(lds_dyn) + kFgMatchBytes / 4;
   int *brPos = opt_rec + kFgMaxOps, *brVal = brPos + kFgMaxGaps;
-  {
+  if (gapc) {
     // this thread's positions high to low: the suffix minimum runs down
     uint32_t uh = after;
     int gi = gbase + gapc;
+    const uint4 b4 = reinterpret_cast<const uint4 *>(s.B)[tid];
+    const uint2 own2 = reinterpret_cast<const uint2 *>(s.Own)[tid];
+    const int4 v4 = reinterpret_cast<const int4 *>(s.Val)[tid];
+    const int vprev = tid == 0 ? init : s.Val[4 * tid - 1];
+    const uint32_t bb[4] = {b4.x, b4.y, b4.z, b4.w};
+    const uint32_t oo[4] = {own2.x & 0xFFFF, own2.x >> 16, own2.y & 0xFFFF, own2.y >> 16};
+    const int vv[5] = {vprev, v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
     for (int j = 3; j >= 0; j--) {
       const int k = 4 * tid + j;
-      uh = umin(uh, k < M ? s.B[k] : kNever);
-      if ((k < M) && s.Own[k] == 0xFFFF) {
+      uh = umin(uh, k < M ? bb[j] : kNever);
+      if ((k < M) && oo[j] == 0xFFFF) {
         gi--;
-        c.gaps()[gi] = make_int4((int)uh, s.Val[k], k == 0 ? init : s.Val[k - 1], k);
+        c.gaps()[gi] = make_int4((int)uh, vv[j + 1], vv[j], k);
         c.at(aMG, gi) = -1;
       }
     }
@@ -1805,19 +1824,31 @@ struct FastSinks {
   int32_t *kind;
 };
 
-template <bool LIGHT>
+// Who runs fast_key: the version-order tier over every key; the crash-light
+// pass over the keys that tier handed to the gap tier; or both in one pass
+// (FUSED: the version order, and for a key whose only obstacle is crashed
+// writes/CAS the crash-light decision, over every key — for batches where
+// most keys carry crashed ops, which would otherwise be read twice).
+enum { kModeFast = 0, kModeLight = 1, kModeFused = 2 };
+
+template <int MODE>
 __device__ __forceinline__ void fast_pass_on(int64_t key, const FastSinks &o, bool jit_only = false) {
-  if constexpr (LIGHT)
+  if constexpr (MODE == kModeLight) {
     o.pass[atomicAdd(&o.status->n_gap2, 1)] = (int32_t)key;  // few: invalid / large keys
-  else
+  } else {
+    // fused: status->n_light counts the keys the gap procedure takes, here
+    // or in the crash-light decision (fast_key)
+    if constexpr (MODE == kModeFused)
+      if (!jit_only) atomicAdd(&o.status->n_light, 1);
     fast_tier_handoff(key, o.flags, o.status, o.h_handoff, jit_only);
+  }
 }
 
 
 // Decide one key (records in b when 0 < n64 <= kFastMax) or hand it over.
 // Three barriers: after the LDS init, after pass 1, before thread 0 reads
 // the per-wave verdicts.
-template <bool LIGHT>
+template <int MODE>
 __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *__restrict__ kops,
                                          const FastRecs &b, const KParams &p, FastLds &s,
                                          lc_key_result *__restrict__ out, const FastSinks &o,
@@ -1828,7 +1859,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
       if (n64 == 0)
         out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 0};
       else
-        fast_pass_on<LIGHT>(key, o);
+        fast_pass_on<MODE>(key, o);
     }
     return;
   }
@@ -1917,13 +1948,16 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
   const int M = (int)((ws.x & 0xFFFF) + (ws.y & 0xFFFF) + (ws.z & 0xFFFF) + (ws.w & 0xFFFF));
   if (wor >> 16) {  // ineligible or a version out of range: hand over
     // crash-light pass: crashed writes/CAS are the only obstacle
-    if constexpr (LIGHT)
-      if ((wor >> 16) == 1 && fast_gap(key, n, kops, b, p, s, out, wit, o.kind)) return;
-    if (tid == 0) fast_pass_on<LIGHT>(key, o, (wor >> 18) & 1);
+    if constexpr (MODE != kModeFast)
+      if ((wor >> 16) == 1 && fast_gap(key, n, kops, b, p, s, out, wit, o.kind)) {
+        if (MODE == kModeFused && tid == 0) atomicAdd(&o.status->n_light, 1);
+        return;
+      }
+    if (tid == 0) fast_pass_on<MODE>(key, o, (wor >> 18) & 1);
     return;
   }
-  if constexpr (LIGHT) {  // eligible here too: the version order found it invalid
-    if (tid == 0) fast_pass_on<LIGHT>(key, o);
+  if constexpr (MODE == kModeLight) {  // eligible here too: the version order found it invalid
+    if (tid == 0) fast_pass_on<MODE>(key, o);
     return;
   }
   // pass 2: positions, duplicates, CAS expectations and read claims against
@@ -1958,7 +1992,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     if (!(wb.x | wb.y | wb.z | wb.w))
       out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
     else
-      fast_pass_on<LIGHT>(key, o);
+      fast_pass_on<MODE>(key, o);
   }
 }
 
@@ -1978,7 +2012,7 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
   FastRecs r;
   if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
   const FastSinks o{flags, status, h_handoff, nullptr, nullptr, nullptr};
-  fast_key<false>(key, end - beg, kops, r, p, s, out, o, nullptr);
+  fast_key<kModeFast>(key, end - beg, kops, r, p, s, out, o, nullptr);
 }
 
 // Crash-light pass over the keys the version-order tier handed to the gap
@@ -2000,16 +2034,38 @@ __global__ __launch_bounds__(kFastThreads) LC_LIGHT_ATTR void gap_light_kernel(
   __shared__ FastLds s;
   const int32_t n_list = __hip_atomic_load(&o.status->n_jit, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-  for (int t = blockIdx.x; t < n_list; t += gridDim.x) {
-    const int64_t key = keys[t];
-    const int64_t beg = key_off[key], end = key_off[key + 1];
-    const lc_op *kops = ops + (beg - key_off[0]);
-    FastRecs r;
-    if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
-    fast_key<true>(key, end - beg, kops, r, p, s, out, o,
-                   o.wit ? o.wit + (beg - key_off[0]) : nullptr);
-    __syncthreads();  // the next key reuses the shared memory
-  }
+  // one key per workgroup: the grid is sized for every key of the call, and
+  // workgroups past the list's length (on the device) leave at once.  (A
+  // grid-stride loop over the list kept the next iteration's state live: 128
+  // VGPRs with SGPR spills, 4 waves per SIMD; one key each, 72 and 7.)
+  const int t = blockIdx.x;
+  if (t >= n_list) return;
+  const int64_t key = keys[t];
+  const int64_t beg = key_off[key], end = key_off[key + 1];
+  const lc_op *kops = ops + (beg - key_off[0]);
+  FastRecs r;
+  if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
+  fast_key<kModeLight>(key, end - beg, kops, r, p, s, out, o,
+                       o.wit ? o.wit + (beg - key_off[0]) : nullptr);
+}
+
+// The version-order tier and the crash-light decision in one pass over every
+// key (kModeFused): one workgroup per key, as the version-order tier; keys it
+// does not decide are flagged for the same handoff compaction, and the gap
+// tier takes them without a crash-light pass.  The crash-light register
+// budget (4 waves per SIMD) — the host picks this kernel only for batches
+// where most keys carry crashed ops (lincheck.cpp).
+__global__ __launch_bounds__(kFastThreads) LC_LIGHT_ATTR void fused_tier_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off, const KParams p,
+    lc_key_result *__restrict__ out, const FastSinks o) {
+  __shared__ FastLds s;
+  const int64_t key = blockIdx.x;
+  const int64_t beg = key_off[key], end = key_off[key + 1];
+  const lc_op *kops = ops + (beg - key_off[0]);
+  FastRecs r;
+  if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
+  fast_key<kModeFused>(key, end - beg, kops, r, p, s, out, o,
+                       o.wit ? o.wit + (beg - key_off[0]) : nullptr);
 }
 
 // Workspace layout per wave: 3 regions of cap Cfg, 2 tables of 2*cap Cfg,
@@ -2278,15 +2334,26 @@ hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
   return hipGetLastError();
 }
 
+hipError_t launch_fused_tier(const lc_op *d_ops, const int64_t *d_key_off, int64_t n_keys,
+                             const KParams &p, lc_key_result *d_out, int32_t *d_flags,
+                             KStatus *d_status, int32_t *h_handoff, int32_t *d_witness,
+                             int32_t *d_witness_kind, hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  const FastSinks o{d_flags, d_status, h_handoff, nullptr, d_witness, d_witness_kind};
+  hipLaunchKernelGGL(fused_tier_kernel, dim3((unsigned)n_keys), dim3(kFastThreads),
+                     (unsigned)kFgLdsBytes, stream, d_ops, d_key_off, p, d_out, o);
+  return hipGetLastError();
+}
+
 hipError_t launch_gap_light(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
                             int64_t max_keys, const KParams &p, lc_key_result *d_out,
                             int32_t *d_pass, KStatus *d_status, int32_t *d_witness,
                             int32_t *d_witness_kind, hipStream_t stream) {
   if (max_keys <= 0) return hipSuccess;
   const FastSinks o{nullptr, d_status, nullptr, d_pass, d_witness, d_witness_kind};
-  // the matching region is dynamic LDS; 7 workgroups per CU x 256 CUs stay
-  // resident, so a larger grid only adds workgroups that find no key
-  const int64_t wgs = std::min<int64_t>(max_keys, 7 * 256);
+  // one workgroup per possible list entry (the list's length is on the
+  // device); the ones past its end return at once
+  const int64_t wgs = max_keys;
   hipLaunchKernelGGL(gap_light_kernel, dim3((unsigned)wgs), dim3(kFastThreads),
                      (unsigned)kFgLdsBytes, stream, d_ops, d_key_off, d_keys, p, d_out, o);
   return hipGetLastError();

@@ -808,6 +808,7 @@ struct QRep {
   unsigned long long andmask;
   unsigned long long flags;  // kQTfull | kQOverflow
   unsigned long long nR, nV; // R and V entries this workgroup reserved (the lists' lengths are the sums)
+  unsigned long long tm[8];  // LC_FXQ_TIME: wave-cycles by phase (split, claim, take, drain, insert, flush, wait)
   unsigned long long pad[3];
 };
 constexpr unsigned long long kQTfull = 1, kQOverflow = 2;
@@ -905,7 +906,7 @@ struct QStage {
 __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win warg) {
   __shared__ Win w;
   __shared__ QStage stg_all[4];
-  __shared__ unsigned long long red_e[4], red_a[4], red_f[4], red_r[4], red_v[4];
+  __shared__ unsigned long long red_e[4], red_a[4], red_f[4], red_r[4], red_v[4], red_t[4][8];
   // the other table set and counters, for the next launch (plain stores: the
   // launch boundary publishes them)
   {
@@ -943,9 +944,13 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
   int ns = 0, nr = 0, nv = 0, nl = 0;  // stash / R stage / V spill stage / local stack (wave-uniform)
   unsigned long long explored = 0, andm = ~0ULL, flags = 0;
   unsigned long long cnt_r = 0, cnt_v = 0;  // entries this wave reserved (wave-uniform)
+  unsigned long long tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define QT0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define QT1(v, i) tm[i] += __builtin_amdgcn_s_memtime() - v
 
   auto flush_r = [&]() {
     if (!nr) return;
+    QT0(tf);
     __builtin_amdgcn_wave_barrier();
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(&a.ctr->nR, (unsigned long long)nr);
@@ -957,9 +962,11 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
     }
     __builtin_amdgcn_wave_barrier();
     nr = 0;
+    QT1(tf, 5);
   };
   auto flush_v = [&]() {
     if (!nv) return;
+    QT0(tf);
     __builtin_amdgcn_wave_barrier();
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(&a.ctr->qtail, (unsigned long long)nv);
@@ -971,15 +978,18 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
     }
     __builtin_amdgcn_wave_barrier();
     nv = 0;
+    QT1(tf, 5);
   };
   // insert one configuration per lane (have): R when it linearized x (x's
   // bit cleared), else V; the new ones are staged
   auto insert_put = [&](bool have, Cfg c) {
+    QT0(ti);
     const bool toR = have && (c.mask & w.xbit);
     if (toR) c.mask &= ~w.xbit;
     int r = -2;
     if (have) r = ctab_insert(toR ? a.tabR : a.tabV, a.tmask, c, a.cshift);
     if (r == -1) flags |= kQTfull;
+    QT1(ti, 4);
     const bool nR = r == 1 && toR, nV = r == 1 && !toR;
     const uint64_t mR = __ballot(nR), mV = __ballot(nV);
     if (nR) {
@@ -1070,6 +1080,7 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
 
   // 1. F: a wave takes 64 entries at a time, splits them, and finishes
   // their local subtrees
+  QT0(tsplit);
   for (long long b = wave * kW; b < a.nF; b += nwaves * kW) {
     const int cnt = (int)min((long long)kW, a.nF - b);
     Cfg c{};
@@ -1082,6 +1093,7 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
     drain_local();
   }
 
+  QT1(tsplit, 0);
   // 2. the queue: claim runs of spilled entries, finish each one's subtree
   uint64_t pending = 0;  // lanes holding a claimed entry not yet read
   unsigned long long my_idx = 0, t_seen = 0;
@@ -1089,6 +1101,7 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
   const unsigned long long nF = (unsigned long long)a.nF;
   for (;;) {
     if (!pending) {
+      QT0(tc);
       unsigned long long h = 0, t = 0;
       if (lane == 0) {
         t = q_peek(&a.ctr->qtail);
@@ -1107,14 +1120,19 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
         pending = c == 64 ? ~0ULL : ((1ULL << c) - 1);
         my_idx = base + lane;
         idle = 0;
+        QT1(tc, 1);
       } else {
         // nothing to claim: finished when every item that exists is done
         // (done read before qtail; done <= |F| + qtail always)
         int fin = 0;
         if (lane == 0) fin = q_finished(a.ctr, nF, idle, 16);
-        if (__shfl(fin, 0)) break;
+        if (__shfl(fin, 0)) {
+          QT1(tc, 1);
+          break;
+        }
         q_sleep(idle < 6 ? 1 << idle : 64);
         idle++;
+        QT1(tc, 1);
         continue;
       }
     }
@@ -1124,6 +1142,7 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
     const bool beyond = my_idx >= a.cap;
     const bool dead = mine && beyond && my_idx < t_seen;
     unsigned long long word = kEmpty;
+    QT0(tt);
     if (mine && !beyond) word = q_take(&a.Q[my_idx], a.qatomic || (waits & 7) == 7);
     const bool got = mine && !beyond && word != kEmpty;
     const uint64_t mgot = __ballot(got), mdead = __ballot(dead);
@@ -1131,8 +1150,14 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
     g += (unsigned long long)__popcll(mgot | mdead);
     if (got) stg->loc[__popcll(mgot & below)] = word;  // the local stack is empty here
     nl = __popcll(mgot);
-    if (g) drain_local();
+    QT1(tt, 2);
+    if (g) {
+      QT0(td);
+      drain_local();
+      QT1(td, 3);
+    }
     if (pending && !mgot) {
+      QT0(tw);
       // claimed entries not written yet (their producer is mid-flush), or
       // beyond the queue's final length: wait, or finish with everyone
       int end = 0;
@@ -1145,6 +1170,7 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
       t_seen = max(t_seen, __shfl(t2, 0));
       waits++;
       q_sleep(1);
+      QT1(tw, 6);
     }
   }
   flush_r();
@@ -1161,6 +1187,7 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
     red_f[wid] = flags;
     red_r[wid] = cnt_r;
     red_v[wid] = cnt_v;
+    for (int i = 0; i < 8; i++) red_t[wid][i] = tm[i];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1172,6 +1199,7 @@ __global__ __launch_bounds__(256) void fx_return_kernel(const QArgs a, const Win
       r.flags |= red_f[k];
       r.nR += red_r[k];
       r.nV += red_v[k];
+      for (int i = 0; i < 8; i++) r.tm[i] += red_t[k][i];
     }
     a.rep[blockIdx.x] = r;
   }
@@ -1367,7 +1395,7 @@ struct Rank {
   bool qpath = false;  // LC_FX_QUEUE=1: the one-launch-per-return queue path (dev A/B)
   int qdbg_g = 0, qmax_g = kQMaxWG, qmin_claim = 1;
   bool qdbg_time = false;  // LC_FXQ_TIME: host-side launch / sync split on stderr
-  double qt_launch = 0, qt_sync = 0;
+  double qt_launch = 0, qt_sync = 0, qt_ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int64_t qt_n = 0;
   int64_t qper_wg = 256;
   int qlocal = 64, qatomic = 0;
@@ -2049,6 +2077,8 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         unsigned long long q_expl = 0, q_and = ~0ULL, q_flags = 0;
         int64_t q_nR = 0, q_nV = 0;
         for (int g = 0; g < G; g++) {
+          if (qdbg_time)
+            for (int i = 0; i < 8; i++) qt_ph[i] += (double)qrep[g].tm[i];
           q_expl += qrep[g].explored;
           q_and &= qrep[g].andmask;
           q_flags |= qrep[g].flags;
@@ -2297,6 +2327,10 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     fprintf(stderr, "fxq: returns %lld redos %lld launches %lld launch us %.1f sync us %.1f total ms %.2f\n",
             (long long)stats.returns, (long long)stats.redos, (long long)qt_n, qt_launch, qt_sync,
             stats.total_ms);
+    fprintf(stderr, "fxq phases (G wave-cycles): split %.2f claim %.2f take %.2f drain %.2f [insert %.2f flush %.2f] wait %.2f\n",
+            qt_ph[0] * 1e-9, qt_ph[1] * 1e-9, qt_ph[2] * 1e-9, qt_ph[3] * 1e-9, qt_ph[4] * 1e-9,
+            qt_ph[5] * 1e-9, qt_ph[6] * 1e-9);
+    for (double &v : qt_ph) v = 0;
     qt_launch = qt_sync = 0;
     qt_n = 0;
   }

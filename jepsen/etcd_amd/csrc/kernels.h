@@ -31,6 +31,7 @@ struct KStatus {
   int32_t any_handoff;  // fast tier: some key was handed over (read before the host store)
   int32_t n_gap2;       // crash-light pass: keys it passes on to the gap tier
   int32_t hbm_next;     // HBM tiers: next list entry to claim (zeroed before each launch)
+  int32_t n_light;      // fused tier: keys that took the crash-light decision
 };
 
 constexpr int kWave = 64;
@@ -58,6 +59,15 @@ hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_flags,
                             KStatus *d_status, int32_t *h_handoff, hipStream_t stream);
+// The version-order tier and the crash-light decision in one pass over every
+// key, for batches where most keys carry crashed writes/CAS: undecided keys
+// are flagged for the handoff compaction (as launch_fast_tier), and go to the
+// gap tier without a crash-light pass.  status->n_light counts the keys that
+// took the crash-light decision.
+hipError_t launch_fused_tier(const lc_op *d_ops, const int64_t *d_key_off, int64_t n_keys,
+                             const KParams &p, lc_key_result *d_out, int32_t *d_flags,
+                             KStatus *d_status, int32_t *h_handoff, int32_t *d_witness,
+                             int32_t *d_witness_kind, hipStream_t stream);
 // Crash-light pass (check_kernel.hip, "Crash-light keys"): over the
 // compacted gap-tier list d_keys (status->n_jit keys, at most max_keys), a
 // key whose only obstacle is a few crashed writes/CAS is decided valid in

@@ -140,6 +140,7 @@ struct Dev {
   double kernel_ms = 0, hbm_ms = 0;
   int64_t n_hbm = 0;
   int malformed = 0;
+  bool use_fused = false;  // the next call takes the fused version-order + crash-light pass
 };
 
 }  // namespace
@@ -254,6 +255,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   d.status_dirty = true;
   float ms = 0;
   bool light = false;  // the crash-light pass ran (its time is in gap_ms)
+  bool fused = false;  // the version-order and crash-light decisions ran as one pass
   int64_t n_jit = n_keys;
   const int32_t *jit_list = nullptr;
   const bool want_wit = wo.wit && wo.kind;
@@ -265,21 +267,43 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     // tier 0: version-order decision for every key; the rest go to the JIT.
     // Only when some workgroup raised h_handoff is the count copied back.
     __atomic_store_n(d.h_handoff, 0, __ATOMIC_RELEASE);
-    HIP_TRY(c, lcdev::launch_fast_tier(d_ops, d_off, n_keys, p, d_out, d.d_flags,
-                                       d.d_status, d.h_handoff_dev, st));
+    // Crash-heavy batches (most keys carry crashed writes/CAS: every key goes
+    // on to the crash-light decision) take the fused pass, which reads each
+    // key's records once for both decisions; others the version-order tier,
+    // whose smaller register budget keeps 7 workgroups per CU.  Chosen from
+    // the previous call on this device (LC_FUSED=0/1 forces it).
+    const char *fenv = getenv("LC_FUSED");
+    fused = gap_on && (fenv ? fenv[0] == '1' : d.use_fused);
+    if (fused)
+      HIP_TRY(c, lcdev::launch_fused_tier(d_ops, d_off, n_keys, p, d_out, d.d_flags, d.d_status,
+                                          d.h_handoff_dev, want_wit ? wo.wit : nullptr,
+                                          want_wit ? wo.kind : nullptr, st));
+    else
+      HIP_TRY(c, lcdev::launch_fast_tier(d_ops, d_off, n_keys, p, d_out, d.d_flags,
+                                         d.d_status, d.h_handoff_dev, st));
     HIP_TRY(c, hipEventRecord(d.ef, st));
     HIP_TRY(c, hipEventSynchronize(d.ef));
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.ef));
     d.fast_ms = ms;
     n_jit = 0;
     jit_list = d.d_jit;
-    if (__atomic_load_n(d.h_handoff, __ATOMIC_ACQUIRE)) {
+    const bool handed = __atomic_load_n(d.h_handoff, __ATOMIC_ACQUIRE) != 0;
+    if (fused && !handed) {
+      // every key decided in the one pass: were most of them crash-light?
+      HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
+                                hipMemcpyDeviceToHost, st));
+      HIP_TRY(c, hipStreamSynchronize(st));
+      d.use_fused = 4 * (int64_t)d.h_status->n_light > n_keys;
+      d.n_gap = d.h_status->n_light;  // keys the crash-light decision took
+      d.status_dirty = true;
+    }
+    if (handed) {
       HIP_TRY(c, lcdev::launch_handoff_compact(d.d_flags, d_off, n_keys, gap_on ? 1 : 0, d.d_jit,
                                                d.d_jit2, d.d_status, want_wit ? wo.kind : nullptr,
                                                st));
       // the crash-light pass reads the list and its length from the device:
       // no host round trip between the compaction and it
-      if (gap_on) {
+      if (gap_on && !fused) {
         HIP_TRY(c, lcdev::launch_gap_light(d_ops, d_off, d.d_jit, n_keys, p, d_out, d.d_gap2,
                                            d.d_status, want_wit ? wo.wit : nullptr,
                                            want_wit ? wo.kind : nullptr, st));
@@ -289,7 +313,14 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                                 hipMemcpyDeviceToHost, st));
       HIP_TRY(c, hipStreamSynchronize(st));
       n_direct = d.h_status->n_jit2;
-      if (gap_on) {
+      if (fused) {
+        d.use_fused = 4 * (int64_t)d.h_status->n_light > n_keys;
+        d.gap_ms = 0;
+        d.n_gap = d.h_status->n_light;
+        n_jit = d.h_status->n_jit;  // undecided: straight to the gap tier
+      } else if (gap_on) {
+        // most keys handed to the gap tier: the next call fuses the passes
+        d.use_fused = 2 * (int64_t)d.h_status->n_jit > n_keys;
         light = true;
         HIP_TRY(c, hipEventElapsedTime(&ms, d.ef, d.el));
         d.gap_ms = ms;
@@ -421,7 +452,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     HIP_TRY(c, hipStreamSynchronize(st));
     HIP_TRY(c, hipEventElapsedTime(&ms, d.ef, d.eg));
     d.gap_ms = ms;
-    if (!light) d.n_gap = n_jit;
+    if (!light && !fused) d.n_gap = n_jit;
     n_jit = d.h_status->n_jit2;
     jit_list = d.d_jit2;
     before_jit = d.eg;

@@ -84,6 +84,34 @@ def test_crash_leg_every_key_certified(ctx):
     assert (st == oracle.WIT_OK).all()
 
 
+@pytest.mark.parametrize("case", ["crash_leg", "mixed", "clean"])
+def test_fused_pass_equals_two_passes(ctx, monkeypatch, case):
+    """Crash-heavy batches take one fused pass (version order + crash-light
+    decision over every key) instead of the version-order tier followed by
+    the crash-light pass over the keys it hands on (lincheck.cpp picks it
+    from the previous call; LC_FUSED forces either).  Results and witnesses
+    are identical, and the fused pass's decisions are certified."""
+    if case == "crash_leg":
+        ops, off, _, _ = abi.synth(2000, 1000, concurrency=20, p_info=0.05, seed=0x5EED0012)
+    elif case == "mixed":
+        ops, off, _, _ = abi.synth(2000, 120, concurrency=12, p_info=0.2, info_frac=0.15,
+                                   p_anomaly=0.35, seed=52)
+    else:
+        ops, off, _, _ = abi.synth(1000, 300, concurrency=10, p_anomaly=0.1, seed=53)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("LC_FUSED", mode)
+        _, r, wit, kind = ctx.check(ops, off, witness=True)
+        out[mode] = (r, wit, kind)
+    r0, w0, k0 = out["0"]
+    r1, w1, k1 = out["1"]
+    assert (r0 == r1).all() and (k0 == k1).all() and (w0 == w1).all()
+    st, _ = certify(ops, off, r1, w1, k1)
+    assert ((st == oracle.WIT_OK) | (k1 == abi.LC_WITNESS_NONE)).all()
+    if case == "crash_leg":
+        assert (r1["verdict"] == 1).all() and (k1 == abi.LC_WITNESS_FULL).all()
+
+
 def test_mixed_crash_batch_witnesses(ctx):
     """Many short crash-heavy keys, a third of them invalid: one-wave gap
     workgroups, in-place bisection, prefix witnesses."""
