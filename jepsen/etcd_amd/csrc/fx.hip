@@ -124,10 +124,29 @@ static_assert(sizeof(Cfg) == 16, "16-byte configuration");
 struct Slot {
   int32_t nv, nvm, nl, nlm;  // precondition
   int32_t value;             // effect of a write/CAS: the new value
-  int32_t pad;
+  int32_t cls;               // counted class lane: kClsLane | width << 8 | field shift; else 0
   uint64_t before;           // deadline order: same-class slots to linearize first
-  uint64_t zob;              // Zobrist word of the op (0 for reads)
+  uint64_t zob;              // Zobrist word of the op (0 for reads); class lane: members available
 };
+
+// Counted classes (one rank): crashed writes/CAS with equal (f, value,
+// expected, version) are interchangeable (their completion never arrived,
+// so their version stays nil — register.clj:64,71), and deadline order
+// linearizes them in call order, after every pending :ok member of the class.
+// So a configuration needs only how many of a class it has linearized, not
+// one window slot per crashed op: the class is a bit field of the mask (a
+// count, relative to the members every configuration has linearized, which
+// retire) and a lane of its own, the top lanes (kClsLane0 and up).  A key's
+// crashed ops then cost log2(count) bits per class instead of one slot each,
+// which lifts the 64-slot window for crash-heavy keys without versions.
+constexpr int32_t kClsLane = 1 << 30;
+constexpr int kMaxCls = 16;
+constexpr int kClsLane0 = 64 - kMaxCls;
+__host__ __device__ inline int cls_shift(int32_t c) { return c & 0xFF; }
+__host__ __device__ inline int cls_width(int32_t c) { return (c >> 8) & 0xFF; }
+__host__ __device__ inline uint64_t cls_get(uint64_t mask, int32_t c) {
+  return (mask >> cls_shift(c)) & ((1ULL << cls_width(c)) - 1);
+}
 
 struct Win {
   uint64_t occ;    // occupied slots
@@ -139,7 +158,7 @@ struct Win {
   // the ops retired then (clear), then the reads called since (closure).
   uint64_t fclear, fclose;
   int32_t rank, n_ranks;
-  int32_t pad[2];
+  uint64_t fsub;   // one rank: class members retired since the last return (fields to subtract)
   Slot s[kW];
 };
 
@@ -147,6 +166,7 @@ __device__ inline bool legal(const Slot &s, uint32_t ver, uint32_t val);
 
 __device__ inline void fix_f(Cfg &c, const Win &w) {
   c.mask &= ~w.fclear;
+  c.mask -= w.fsub;  // (every configuration holds at least the retired count in each field)
   for (uint64_t pr = w.fclose; pr;) {
     const int b = __builtin_ctzll(pr);
     pr &= pr - 1;
@@ -166,6 +186,7 @@ struct Ctr {
   unsigned long long tfull;     // a table probe ran too long: redo the return with a larger table
   unsigned long long pad[5];
   unsigned long long cand[64];  // partitioned: candidates per owner rank
+  unsigned long long cmin[kMaxCls];  // counted classes: the smallest field over R (retirement)
 };
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {
@@ -338,7 +359,7 @@ __global__ __launch_bounds__(256) void fx_insert_kernel(const Cfg *__restrict__ 
                                                         const Win *__restrict__ win, Tabs t,
                                                         uint32_t epoch, Ctr *ctr) {
   const uint64_t xbit = win->xbit;
-  const bool fix = win->fclear | win->fclose;
+  const bool fix = win->fclear | win->fclose | win->fsub;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x; b < n; b += stride) {
     const int64_t i = b + threadIdx.x;
@@ -469,11 +490,14 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
     if (r.nvm) vreads |= 1ULL << b;
     else if (!r.nlm || r.nl == me.value) rv_me |= 1ULL << b;
   }
+  const bool is_cls = me.cls != 0;
   auto succ = [&](const Cfg &c, bool &cand, Cfg &s) {
-    cand = is_mut && !(c.mask & bit) && !(me.before & ~c.mask) && legal(me, c.ver, c.val);
+    // a slot's op not yet linearized; or a class with a member left
+    const bool avail = is_cls ? cls_get(c.mask, me.cls) < me.zob : is_mut && !(c.mask & bit);
+    cand = avail && !(me.before & ~c.mask) && legal(me, c.ver, c.val);
     s = c;
     if (cand) {
-      s.mask |= bit | rv_me;
+      s.mask = (is_cls ? s.mask + (1ULL << cls_shift(me.cls)) : s.mask | bit) | rv_me;
       s.ver = c.ver + 1;
       s.val = (uint32_t)me.value;
       uint64_t pr = vreads & ~s.mask;
@@ -599,6 +623,31 @@ __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ 
 
 __device__ inline unsigned long long wave_and(unsigned long long v);
 
+// Counted classes: the smallest field of each class over list[lo, hi) (this
+// thread strided by `step`), into ctr->cmin (retirement of the members every
+// configuration has linearized).  Only when the window has class lanes.
+__device__ inline void cls_min_over(const Win &w, const Cfg *list, int64_t lo, int64_t hi,
+                                    int64_t step, Ctr *ctr) {
+  for (int k = 0; k < kMaxCls; k++) {
+    const int32_t cl = w.s[kClsLane0 + k].cls;
+    if (!cl) continue;
+    uint32_t m = 0xFFFFFFFFu;
+    for (int64_t i = lo; i < hi; i += step) m = min(m, (uint32_t)cls_get(list[i].mask, cl));
+    for (int off = 32; off > 0; off >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, off));
+    if (__lane_id() == 0 && m != 0xFFFFFFFFu) atomicMin(&ctr->cmin[k], (unsigned long long)m);
+  }
+}
+
+__global__ __launch_bounds__(256) void fx_cmin_kernel(const Cfg *__restrict__ list,
+                                                      const unsigned long long *n,
+                                                      const Win *__restrict__ gwin, Ctr *ctr) {
+  __shared__ Win w;
+  load_win(w, gwin);
+  __syncthreads();
+  cls_min_over(w, list, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)*n,
+               (int64_t)gridDim.x * blockDim.x, ctr);
+}
+
 // A whole return in one workgroup while the frontier is small (replicated
 // mode): split F, then levels separated by barriers, then the AND for
 // retirement — one launch instead of one per level.  A level larger than
@@ -656,6 +705,7 @@ __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restr
   for (int64_t i = threadIdx.x; i < nR; i += blockDim.x) a &= t.listR[i].mask;
   a = wave_and(a);
   if (__lane_id() == 0 && a != ~0ULL) atomicAnd(&ctr->andmask, a);
+  cls_min_over(w, t.listR, threadIdx.x, nR, blockDim.x, ctr);
   __syncthreads();
   if (threadIdx.x < kW) {
     const unsigned long long e = wave_sum_shards(t.exp);
@@ -753,6 +803,7 @@ __global__ __launch_bounds__(256) void fx_reset_kernel(Ctr *ctr, unsigned long l
   ctr->tfull = 0;
   ctr->explored = explored;
   for (int i = 0; i < 64; i++) ctr->cand[i] = 0;
+  for (int i = 0; i < kMaxCls; i++) ctr->cmin[i] = ~0ULL;
 }
 
 // ------------------------------------------------------------ the queue path
@@ -1888,6 +1939,61 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     }
   };
 
+  // Counted classes (one rank; see kClsLane): crashed writes/CAS grouped by
+  // (f, value, expected, version), each class a field wide enough for all of
+  // its members in the key, placed just below the value-id bits; the slots
+  // keep the bits below the fields.  LC_FX_CLASSES=0: one slot per crashed op.
+  std::vector<int32_t> cls_of((size_t)n, -1);
+  std::vector<std::vector<int32_t>> cls_members;  // call order
+  int64_t cls_called[kMaxCls] = {0}, cls_base[kMaxCls] = {0};
+  int slot_max = kW;  // slots are bits [0, slot_max)
+  uint64_t fsub = 0;  // one rank: class members retired since the last return
+  {
+    const char *ce = getenv("LC_FX_CLASSES");
+    const bool want = !multi() && !(ce && ce[0] == '0');
+    std::vector<int32_t> rep;
+    for (int64_t i = 0; want && i < n; i++) {
+      if (o[i].ret != LC_INF || o[i].f == LC_F_READ) continue;
+      int c = 0;
+      while (c < (int)rep.size() && !same_class(o[rep[c]], o[i])) c++;
+      if (c == (int)rep.size()) {
+        if (c == kMaxCls) break;  // too many classes: slots as before
+        rep.push_back((int32_t)i);
+        cls_members.emplace_back();
+      }
+      cls_members[c].push_back((int32_t)i);
+    }
+    int sumw = 0;
+    for (auto &m : cls_members) sumw += 64 - __builtin_clzll((unsigned long long)m.size());
+    const int top = cshift >= 44 ? cshift : kW;
+    const bool fits = !rep.empty() && (int)rep.size() <= kMaxCls &&
+                      (int64_t)rep.size() == (int64_t)cls_members.size() && sumw + 8 <= top;
+    bool complete = true;  // every crashed mutation found its class
+    for (int64_t i = 0; i < n && fits; i++)
+      if (o[i].ret == LC_INF && o[i].f != LC_F_READ) {
+        bool in = false;
+        for (auto &r : rep) in |= same_class(o[r], o[i]);
+        complete &= in;
+      }
+    if (fits && complete) {
+      int shift = top - sumw;
+      slot_max = std::min(shift, kClsLane0);
+      for (int c = 0; c < (int)rep.size(); c++) {
+        const int width = 64 - __builtin_clzll((unsigned long long)cls_members[c].size());
+        for (int32_t m : cls_members[c]) cls_of[m] = c;
+        Slot &cl = w.s[kClsLane0 + c];
+        std::memset(&cl, 0, sizeof(Slot));
+        slot_pre(o[rep[c]], cl);
+        cl.cls = kClsLane | (width << 8) | shift;
+        cl.zob = 0;  // members available (called, not retired)
+        shift += width;
+      }
+    } else {
+      cls_members.clear();
+    }
+  }
+  const int n_cls = (int)cls_members.size();
+
   for (size_t e = 0; e < ev.size() && !decided; e++) {
     const int32_t x = ev[e].op;
     const lc_op &ox = o[x];
@@ -1895,7 +2001,13 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       // trivial reads (crashed, or [nil nil]) never constrain: no slot
       if (ox.f == LC_F_READ && (ox.ret == LC_INF || (ox.version == LC_NIL && ox.value == LC_NIL)))
         continue;
-      if (occ == ~0ULL) {
+      if (cls_of[x] >= 0) {  // a crashed write/CAS: one more member of its class
+        const int c = cls_of[x];
+        cls_called[c]++;
+        w.s[kClsLane0 + c].zob = (uint64_t)(cls_called[c] - cls_base[c]);
+        continue;
+      }
+      if (occ == ~0ULL || __builtin_ctzll(~occ) >= slot_max) {
         result_unknown(res, LC_REASON_WINDOW_OVERFLOW);
         decided = true;
         break;
@@ -1929,6 +2041,9 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           if (o[slot_op[u]].ret <= ox.ret) before[s] |= 1ULL << u;
           else before[u] |= sb;
         }
+        // a counted class's crashed members wait for its pending :ok members
+        for (int c = 0; c < n_cls; c++)
+          if (same_class(o[cls_members[c][0]], ox)) before[kClsLane0 + c] |= sb;
       }
       continue;
     }
@@ -1960,6 +2075,12 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           pend &= pend - 1;
           d.pending[d.n_pending++] = slot_op[b];
         }
+        c.mask -= fsub;  // (class members retired since the last split)
+        for (int cc = 0; cc < n_cls; cc++) {  // a class's members past this configuration's count
+          const int64_t lin = cls_base[cc] + (int64_t)cls_get(c.mask, w.s[kClsLane0 + cc].cls);
+          for (int64_t j = lin; j < cls_called[cc] && d.n_pending < 64; j++)
+            d.pending[d.n_pending++] = cls_members[cc][(size_t)j];
+        }
         std::sort(d.pending, d.pending + d.n_pending);
       }
       dump_n = (int32_t)k;
@@ -1978,7 +2099,8 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     for (int u = 0; u < kW; u++) w.s[u].before = before[u];
     w.fclear = fclear;
     w.fclose = fclose;
-    fclear = fclose = 0;
+    w.fsub = fsub;
+    fclear = fclose = fsub = 0;
     if (multi()) FX_TRY(hipMemcpyAsync(dWin, &w, sizeof(Win), hipMemcpyHostToDevice, st));
     // mode switches (several ranks only)
     if (multi() && !part && nFglobal > part_above) {
@@ -2029,7 +2151,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         FX_TRY(hipGetLastError());
       }
       bool tfull = false;
-      if (qpath && !multi() && compact) {
+      if (qpath && !multi() && compact && !n_cls) {
         // one launch per attempt (fx_return_kernel): split, queue, report
         int G = (int)std::min<int64_t>(
             qmax_g, std::max<int64_t>(1, (std::max(nF, last_work) + qper_wg - 1) / qper_wg));
@@ -2121,13 +2243,18 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         }
         const int g = (int)std::max<int64_t>(16, std::min<int64_t>(kExpandWG, (std::max(nF, last_work) + 3) / 4));
         for (int batch = 0; !done; batch++) {
-          if (small || batch)  // the reset set it for a first batch; a partial AND is stale
+          if (small || batch) {  // the reset set it for a first batch; a partial AND is stale
             FX_TRY(hipMemsetAsync(&dCtr->andmask, 0xFF, sizeof(unsigned long long), st));
+            if (n_cls) FX_TRY(hipMemsetAsync(dCtr->cmin, 0xFF, sizeof(dCtr->cmin), st));
+          }
           for (int l = 0; l < spec_levels; l++, k++)
             fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tabs(tlog, compact, k), epoch, dCtr, k, -1, -1,
                                                 nullptr, 0);
           fx_and_kernel<<<grid_for((int64_t)std::max(nF, last_work)), 256, 0, st>>>(Rl, &dCtr->nR,
                                                                                      dCtr, dExp);
+          if (n_cls)
+            fx_cmin_kernel<<<grid_for((int64_t)std::max(nF, last_work)), 256, 0, st>>>(
+                Rl, &dCtr->nR, dWin, dCtr);
           FX_TRY(hipGetLastError());
           if (int er = sync_ctr()) return er;
           if (hCtr->tfull || hCtr->overflow ||
@@ -2309,6 +2436,17 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       occ &= ~all;
       reads &= ~all;
       for (int u = 0; u < kW; u++) before[u] &= ~all;
+    }
+    // counted classes: members every configuration has linearized retire
+    // (the fields shrink by as many, lazily, at the next split: fsub)
+    for (int c = 0; c < n_cls; c++) {
+      const unsigned long long m = hCtr->cmin[c];
+      if (m == 0 || m == ~0ULL) continue;
+      Slot &cl = w.s[kClsLane0 + c];
+      cls_base[c] += (int64_t)m;
+      cl.zob -= m;
+      fsub += (uint64_t)m << cls_shift(cl.cls);
+      vbase += (uint32_t)m;
     }
   }
   // every rank reports the same totals

@@ -567,13 +567,20 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
 //   levels are latency-bound, so concurrent searches fill a GPU the way one
 //   cannot), as many as the GPU's free memory holds.
 //
+// Keys left :unknown because more than LC_MAX_WINDOW ops were open at once
+// (crashed writes/CAS pile up in the tiers' windows) are searched again too,
+// by one-rank engines only (spread_ok false): there the crashed ops of a key
+// are counted per class instead of holding a window slot each (fx.hip,
+// "Counted classes").
+//
 // A failure of the re-search (an allocation, say) is this key's alone: it
 // keeps the tiers' :unknown, the error text goes to lc_last_error, and the
 // call still succeeds — as jepsen.independent loses only the key whose check
 // throws.
 int whole_gpu(lc_ctx *c, const std::vector<int64_t> &todo, const lc_opts *opts,
               const std::function<int(int64_t, std::vector<lc_op> &)> &fetch,
-              const std::function<int(int64_t, const lc_key_result &)> &store) {
+              const std::function<int(int64_t, const lc_key_result &)> &store,
+              bool spread_ok = true) {
   if (todo.empty()) return 0;
   std::vector<int> ids;  // the context's distinct GPUs
   for (const Dev &d : c->devs)
@@ -584,7 +591,7 @@ int whole_gpu(lc_ctx *c, const std::vector<int64_t> &todo, const lc_opts *opts,
     failed++;
     set_err(c, "LC_FLAG_WHOLE_GPU: key " + std::to_string(k) + " kept :unknown: " + what);
   };
-  if (nranks > 1 && todo.size() < (size_t)nranks) {
+  if (spread_ok && nranks > 1 && todo.size() < (size_t)nranks) {
     if (!c->fx_all && !c->fx_all_failed) {
       lc_fx_params fp{};
       fp.part_above = -1;
@@ -970,19 +977,21 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
     c->stats.n_malformed += c->devs[di].malformed;
   }
   if (!rc && (flags & LC_FLAG_WHOLE_GPU)) {
-    std::vector<int64_t> todo;
+    std::vector<int64_t> todo, todo_w;
     for (int64_t k = 0; k < n_keys; k++)
       if (out[k].verdict == LC_UNKNOWN && out[k].reason == LC_REASON_CONFIG_BUDGET) todo.push_back(k);
-    rc = whole_gpu(
-        c, todo, opts,
-        [&](int64_t k, std::vector<lc_op> &v) {
-          v.assign(ops + key_off[k], ops + key_off[k + 1]);
-          return 0;
-        },
-        [&](int64_t k, const lc_key_result &r) {
-          out[k] = r;
-          return 0;
-        });
+      else if (out[k].verdict == LC_UNKNOWN && out[k].reason == LC_REASON_WINDOW_OVERFLOW)
+        todo_w.push_back(k);
+    auto fetch = [&](int64_t k, std::vector<lc_op> &v) {
+      v.assign(ops + key_off[k], ops + key_off[k + 1]);
+      return 0;
+    };
+    auto store = [&](int64_t k, const lc_key_result &r) {
+      out[k] = r;
+      return 0;
+    };
+    rc = whole_gpu(c, todo, opts, fetch, store);
+    if (!rc) rc = whole_gpu(c, todo_w, opts, fetch, store, false);
   }
   c->stats.n_keys = n_keys;
   c->stats.n_ops = key_off[n_keys] - key_off[0];
@@ -1042,23 +1051,25 @@ int lc_check_device_ex(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
                               hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipMemcpyAsync(&base, d_key_off, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipStreamSynchronize(st));
-    std::vector<int64_t> todo;
+    std::vector<int64_t> todo, todo_w;
     for (int64_t k = 0; k < n_keys; k++)
       if (res[k].verdict == LC_UNKNOWN && res[k].reason == LC_REASON_CONFIG_BUDGET) todo.push_back(k);
-    rc = whole_gpu(
-        c, todo, opts,
-        [&](int64_t k, std::vector<lc_op> &v) {
-          int64_t se[2];
-          if (hipMemcpy(se, d_key_off + k, sizeof se, hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
-          v.resize((size_t)(se[1] - se[0]));
-          if (!v.empty() && hipMemcpy(v.data(), d_ops + (se[0] - base), sizeof(lc_op) * v.size(),
-                                      hipMemcpyDeviceToHost) != hipSuccess)
-            return -EIO;
-          return 0;
-        },
-        [&](int64_t k, const lc_key_result &r) {
-          return hipMemcpy(d_out + k, &r, sizeof r, hipMemcpyHostToDevice) == hipSuccess ? 0 : -EIO;
-        });
+      else if (res[k].verdict == LC_UNKNOWN && res[k].reason == LC_REASON_WINDOW_OVERFLOW)
+        todo_w.push_back(k);
+    auto fetch = [&](int64_t k, std::vector<lc_op> &v) {
+      int64_t se[2];
+      if (hipMemcpy(se, d_key_off + k, sizeof se, hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
+      v.resize((size_t)(se[1] - se[0]));
+      if (!v.empty() && hipMemcpy(v.data(), d_ops + (se[0] - base), sizeof(lc_op) * v.size(),
+                                  hipMemcpyDeviceToHost) != hipSuccess)
+        return -EIO;
+      return 0;
+    };
+    auto store = [&](int64_t k, const lc_key_result &r) {
+      return hipMemcpy(d_out + k, &r, sizeof r, hipMemcpyHostToDevice) == hipSuccess ? 0 : -EIO;
+    };
+    rc = whole_gpu(c, todo, opts, fetch, store);
+    if (!rc) rc = whole_gpu(c, todo_w, opts, fetch, store, false);
   }
   c->stats.kernel_ms = d.kernel_ms;
   c->stats.fast_kernel_ms = d.fast_ms;
