@@ -1797,7 +1797,7 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, con
   if (G > 0 && w == 0) {
     ClsSt cst;  // (generic matching: at most kFgMaxOps < kClsMinOps optional ops)
     cst.K = 0;
-    res = match_branch_m<true, false>(c, G, n_opt, brPos, brVal, &nodes, cst);
+    res = match_branch_m<true, false, false>(c, G, n_opt, brPos, brVal, brVal, &nodes, cst);
     if (lane == 0) s.wg[0] = res;
     if (res == GD_VALID && wit)
       for (int gi = lane; gi < G; gi += kWave) wit[opt_rec[c.at(aMG, gi)]] = c.gaps()[gi].w;

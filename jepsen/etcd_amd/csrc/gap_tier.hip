@@ -509,6 +509,7 @@ __device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int
   GapSh &sh = *g.sh;
 #ifdef GAP_PROFILE
   const uint64_t t0 = wall_clock64();
+  if (tid < 8) s_mprof[tid] = 0;
 #endif
   const int st = gap_setup<T, SL>(g, w, cut);
   if (st != GD_VALID) return st;
@@ -523,6 +524,8 @@ __device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int
   }
   if (G > n_opt) return GD_INVALID;
   const bool in_lds = 16 * w.moff + match_lds_bytes(G, n_opt) <= lds_bytes;
+  // room for the class-indexed matching's copies of matched gap records
+  const bool mgr_room = in_lds && 16 * w.moff + match_lds_bytes(G, n_opt) + match_mgr_bytes(n_opt) <= lds_bytes;
   // skeleton in LDS but no room left for this matching: the caller redoes the
   // decision with the skeleton in HBM (the whole LDS then holds the matching)
   if (SL && !in_lds) return GD_RETRY;
@@ -561,9 +564,9 @@ __device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int
   if (tid < kWave) {
     int r;
     if (SL || in_lds)
-      r = match_branch(cl, G, n_opt, w.Claim, w.Req, nodes);
+      r = match_branch(cl, G, n_opt, w.Claim, w.Req, w.PinExp, nodes, mgr_room);
     else
-      r = match_branch(cg, G, n_opt, w.Claim, w.Req, nodes);
+      r = match_branch(cg, G, n_opt, w.Claim, w.Req, w.PinExp, nodes, false);
     if (tid == 0) sh.res = r;
   }
   __syncthreads();
@@ -577,10 +580,9 @@ __device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int
   }
 #ifdef GAP_PROFILE
   if (tid == 0 && blockIdx.x < 2) {
-    printf("  matching wg %d: first-fits %llu augments %llu steps %llu failed %llu\n",
-           (int)blockIdx.x, g_mprof[blockIdx.x][0], g_mprof[blockIdx.x][1],
-           g_mprof[blockIdx.x][2], g_mprof[blockIdx.x][3]);
-    for (int i = 0; i < 8; i++) g_mprof[blockIdx.x][i] = 0;
+    printf("  matching wg %d: first-fits %llu augments %llu steps %llu failed %llu | cycles: first-fit %llu augment %llu fill %llu; cursor steps %llu\n",
+           (int)blockIdx.x, s_mprof[0], s_mprof[1], s_mprof[2], s_mprof[3], s_mprof[4],
+           s_mprof[5], s_mprof[7], s_mprof[6]);
   }
   if (tid == 0 && blockIdx.x < 2)
     printf("gap_decide wg %d cut %u n %d G %d n_opt %d lds %d nodes %ld: setup %lu [clr %lu p1 %lu (ld %lu c %lu %lu %lu %lu) pre %lu p2 %lu smin %lu chk %lu gcmp %lu] compact %lu match %lu (x10ns)\n",
@@ -858,6 +860,20 @@ hipError_t launch_gap_tier(const lc_op *d_ops, const int64_t *d_key_off, const i
                                         d_pass_keys, d_status, job, stream)
              : launch_gap_tier_t<kGapThreads>(d_ops, d_key_off, d_keys, p, d_out, d_ws, n_wg, cap,
                                               d_pass_keys, d_status, job, stream);
+}
+
+int gap_tier_resident(int lds_bytes) {
+  const void *fn = reinterpret_cast<const void *>(gap_tier_kernel<kGapThreads>);
+  if (lds_bytes > (64 << 10) &&
+      hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) != hipSuccess)
+    return 0;
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kGapThreads, (size_t)lds_bytes) !=
+          hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return per_cu * cus;
 }
 
 hipError_t launch_gap_narrow(const lc_op *d_ops, const int64_t *d_key_off, int32_t n_cex,

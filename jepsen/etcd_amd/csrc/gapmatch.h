@@ -18,6 +18,11 @@ constexpr int kAny = INT_MIN;      // no value required / not a CAS
 constexpr int kNodeBudget = 4096;  // matching passes per decision
 constexpr int kMaxCls = 64;        // class-indexed matching: at most one class per lane
 constexpr int kClsMinOps = 128;    // ... used from this many optional ops on
+#ifdef GAP_SINGLE_PUSH  // A/B: one violation branched on per matching
+constexpr bool kGapMultiPush = false;
+#else
+constexpr bool kGapMultiPush = true;
+#endif
 
 enum { GD_VALID = 1, GD_INVALID = 0, GD_NA = -1, GD_BUDGET = -2, GD_SKIP = -3, GD_RETRY = -4 };
 
@@ -88,7 +93,13 @@ struct Cmp {
     else
       return reinterpret_cast<int4 *>(ws + 30 * cap);
   }
+  // class-indexed matching in LDS, when there is room (ClsSt::mgr): per op
+  // a copy of the record of the gap it is matched to, after the class table
+  __device__ __forceinline__ int4 * mgr() const { return cls() + kMaxCls; }
 };
+
+// LDS for the per-op copies of matched gap records (Cmp::mgr)
+__host__ __device__ constexpr int match_mgr_bytes(int n_opt) { return 16 * n_opt; }
 
 // gap record: x = D, y = R, z = B, w = P;  op record: x = C, y = V, z = E, w = OP
 // (bitwise, no short-circuit: the wave's loops stay uniform, see below)
@@ -134,13 +145,21 @@ __device__ __forceinline__ bool scan_chunk(const Cmp<L> &c, const int4 gp, int b
 }
 
 #ifdef GAP_PROFILE
-// matching counters of workgroups 0..3: first-fits, augments, augment steps,
-// failed augments, nodes
-__device__ unsigned long long g_mprof[4][8];
+// matching counters of this workgroup: first-fits, augments, augment steps,
+// failed augments, cycles (first-fit, augment, cursor steps, fill); LDS adds
+// whose result is unused (no wait inside the timed sections)
+__shared__ unsigned long long s_mprof[8];
 #define MPROF(i, v) \
-  do { if (blockIdx.x < 4 && (threadIdx.x & 63) == 0) g_mprof[blockIdx.x][i] += (v); } while (0)
+  do { if ((threadIdx.x & 63) == 0) atomicAdd(&s_mprof[i], (unsigned long long)(v)); } while (0)
+// cycles of a section (s_memtime), and the wave-max of a per-lane loop count
+#define MCLK0(t) const uint64_t t = __builtin_amdgcn_s_memtime()
+#define MCLK1(t, i) MPROF(i, __builtin_amdgcn_s_memtime() - t)
+#define MITER(i, n) MPROF(i, (unsigned long long)(-wave_min_i32(-(n))))
 #else
 #define MPROF(i, v) do { } while (0)
+#define MCLK0(t) do { } while (0)
+#define MCLK1(t, i) do { } while (0)
+#define MITER(i, n) do { } while (0)
 #endif
 
 // First free op eligible for gap gi (or -1); *ff = first possibly-free op.
@@ -238,6 +257,11 @@ struct ClsSt {
   int f, p;              // lane k: free / visit cursor
   int fo, po;            // lane k: the op at each cursor (-1 past the end) ...
   uint32_t fc, pc;       // ... and its call (kNever past the end)
+  int mgr = 0;           // (uniform) Cmp::mgr holds each matched op's gap record
+  // lane k: matched ops of class k at or past its free cursor (every op
+  // before the cursor is matched; an augmenting path or a branch's unmatch
+  // leaves matched ops ahead of it).  While 0 the head is known free.
+  int ma = 0;
 };
 
 
@@ -377,19 +401,29 @@ __device__ __forceinline__ uint32_t cls_key(const ClsSt &st, const int4 gp, uint
   return st.E == kAny ? (head_call | 0x80000000u) : head_call;
 }
 
-// First free eligible op for gap gi in call order (class heads and the gap's
-// pinned list), or -1.  The caller matches it: its class's free cursor moves
-// on at once.
+// First free eligible op for gap gi (record gp) in call order (class heads
+// and the gap's pinned list), or -1.  The caller matches it: its class's
+// free cursor moves on at once.
 template <bool L>
-__device__ int first_fit_cls(const Cmp<L> &c, int gi, ClsSt &st) {
+__device__ int first_fit_cls(const Cmp<L> &c, int gi, const int4 gp, ClsSt &st) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int4 gp = uni4(c.gaps()[gi]);
   const auto ops = c.ops();
-  // a head matched since (the end of an augmenting path): move on
-  while (st.fo >= 0 && c.at(aMO, st.fo) != -1) {
+  // move each free cursor past matched heads (only lanes with matched ops
+  // ahead of the cursor look: no LDS round trip in the common case)
+#ifdef GAP_PROFILE
+  int adv = 0;
+#endif
+  while (st.ma > 0 && st.fo >= 0 && c.at(aMO, st.fo) != -1) {
     st.f++;
+    st.ma--;
     cls_head(c, st, st.f, &st.fo, &st.fc);
+#ifdef GAP_PROFILE
+    adv++;
+#endif
   }
+#ifdef GAP_PROFILE
+  MITER(6, adv);
+#endif
   uint32_t call = cls_key(st, gp, st.fc);
   int o = st.fo;
   if (st.any_pin) {
@@ -412,75 +446,87 @@ __device__ int first_fit_cls(const Cmp<L> &c, int gi, ClsSt &st) {
   return found;
 }
 
-// Augmenting path from the unmatched gap g0 over the class cursors.
+// Match gap SG[d] to op SO[d] for d = 0..depth (an augmenting path found).
 template <bool L>
-__device__ bool augment_cls(const Cmp<L> &c, int g0, int stamp, ClsSt &st) {
+__device__ __forceinline__ void flip_path(const Cmp<L> &c, int depth, int last, ClsSt &st) {
+  const int lane = threadIdx.x & (kWave - 1);
+  // the path's last op was free (so at or past its class's free cursor) and
+  // is matched now; every other op on it stays matched
+  if (lane == uni(c.at(aCls, last))) st.ma++;
+  match_fence<L>();
+  for (int d0 = 0; d0 <= depth; d0 += kWave) {
+    const int d = d0 + lane;
+    if (d <= depth) {
+      const int gg = c.at(aSG, d), oo = c.at(aSO, d);
+      c.at(aMG, gg) = oo;
+      c.at(aMO, oo) = gg;
+      if constexpr (L)
+        if (st.mgr) c.mgr()[oo] = c.gaps()[gg];
+    }
+  }
+  match_fence<L>();
+}
+
+// Augmenting path from the unmatched gap g0 (record gp0) over the class
+// cursors.  Called right after first_fit_cls failed on g0, so every free
+// cursor's head is free.  With st.mgr the op a step reaches
+// brings the record of its gap along (one LDS round trip per step).
+template <bool L>
+__device__ bool augment_cls(const Cmp<L> &c, int g0, const int4 gp0, int stamp, ClsSt &st) {
   const int lane = threadIdx.x & (kWave - 1);
   const auto ops = c.ops();
   st.p = 0;
   cls_head(c, st, 0, &st.po, &st.pc);
-  // free cursors past the ops matched since they last moved (nothing is
-  // matched or freed during the search itself)
-  while (st.fo >= 0 && c.at(aMO, st.fo) != -1) {
-    st.f++;
-    cls_head(c, st, st.f, &st.fo, &st.fc);
-  }
   int depth = 0, g = uni(g0);
+  int4 gp = gp0;
   for (;;) {
     MPROF(2, 1);
-    const int4 gp = uni4(c.gaps()[g]);
     const bool compat = cls_compat(st, gp);
     // lookahead: a free eligible op ends the path here (Kuhn's search would
     // reach it only after exhausting the matched ops called before it)
     uint32_t fcall = cls_key(st, gp, st.fc);
     int fop = st.fo;
-    if (st.any_pin) {
-      for (int q = uni(c.at(aPH, g)); q >= 0; q = uni(c.at(aPN, q))) {
-        const int4 op = uni4(ops[q]);
-        if (uni(c.at(aMO, q)) == -1 && elig(gp, op) && (uint32_t)op.x < fcall) {
-          fcall = (uint32_t)op.x;
-          fop = q;
-        }
-      }
-    }
-    const uint32_t fbest = wave_min_u32(fcall);
-    if (fbest != kNever) {
-      const int free_op = uni(__builtin_amdgcn_readlane(fop, first_lane(__ballot(fcall == fbest))));
-      c.at(aSG, depth) = g;
-      c.at(aSO, depth) = free_op;
-      match_fence<L>();
-      for (int d0 = 0; d0 <= depth; d0 += kWave) {
-        const int d = d0 + lane;
-        if (d <= depth) {
-          const int gg = c.at(aSG, d), oo = c.at(aSO, d);
-          c.at(aMG, gg) = oo;
-          c.at(aMO, oo) = gg;
-        }
-      }
-      match_fence<L>();
-      return true;
-    }
+    // else the first unvisited eligible op in call order
     uint32_t call = (compat & (st.pc < (uint32_t)gp.x)) ? st.pc : kNever;
     int o = st.po;
     if (st.any_pin) {
       for (int q = uni(c.at(aPH, g)); q >= 0; q = uni(c.at(aPN, q))) {
         const int4 op = uni4(ops[q]);
-        if (uni(c.at(aVis, q)) != stamp && elig(gp, op) && (uint32_t)op.x < call) {
+        const bool e = elig(gp, op);
+        if (uni(c.at(aMO, q)) == -1 && e && (uint32_t)op.x < fcall) {
+          fcall = (uint32_t)op.x;
+          fop = q;
+        }
+        if (uni(c.at(aVis, q)) != stamp && e && (uint32_t)op.x < call) {
           call = (uint32_t)op.x;
           o = q;
         }
       }
     }
+    const uint32_t fbest = wave_min_u32(fcall);
     const uint32_t best = wave_min_u32(call);
+    if (fbest != kNever) {
+      const int free_op = uni(__builtin_amdgcn_readlane(fop, first_lane(__ballot(fcall == fbest))));
+      c.at(aSG, depth) = g;
+      c.at(aSO, depth) = free_op;
+      flip_path(c, depth, free_op, st);
+      return true;
+    }
     if (best == kNever) {  // dead end: back to the previous gap
       if (depth == 0) return false;
       depth--;
       g = uni(c.at(aSG, depth));
+      gp = uni4(c.gaps()[g]);
       continue;
     }
     const int wl = first_lane(__ballot(call == best));
     const int found = uni(__builtin_amdgcn_readlane(o, wl));
     const int head = uni(__builtin_amdgcn_readlane(st.po, wl));
+    // the op's match (and, with mgr, its gap's record) in flight together
+    const int mo = c.at(aMO, found);
+    int4 gpn = make_int4(0, 0, 0, 0);
+    if constexpr (L)
+      if (st.mgr) gpn = c.mgr()[found];
     if (found != head) {
       c.at(aVis, found) = stamp;  // a pinned op
     } else if (lane == wl) {      // visited: the class's visit cursor moves past it
@@ -489,22 +535,17 @@ __device__ bool augment_cls(const Cmp<L> &c, int g0, int stamp, ClsSt &st) {
     }
     c.at(aSG, depth) = g;
     c.at(aSO, depth) = found;
-    const int m = uni(c.at(aMO, found));
+    const int m = uni(mo);
     if (m == -1) {  // flip the path
-      match_fence<L>();
-      for (int d0 = 0; d0 <= depth; d0 += kWave) {
-        const int d = d0 + lane;
-        if (d <= depth) {
-          const int gg = c.at(aSG, d), oo = c.at(aSO, d);
-          c.at(aMG, gg) = oo;
-          c.at(aMO, oo) = gg;
-        }
-      }
-      match_fence<L>();
+      flip_path(c, depth, found, st);
       return true;
     }
     depth++;
     g = m;
+    if (L && st.mgr)
+      gp = uni4(gpn);
+    else
+      gp = uni4(c.gaps()[g]);
   }
 }
 
@@ -517,28 +558,43 @@ __device__ bool fill(const Cmp<L> &c, int G, int n_opt, int *ff, int *stamp, Cls
   for (int g0 = 0; g0 < G; g0 = uni(g0 + kWave)) {
     const int gl = g0 + lane;
     uint64_t todo = __ballot((gl < G) & (c.at(aMG, min(gl, G - 1)) == -1));
+    // CM: the next gap's record is loaded while this one is filled
+    int4 gpv = make_int4(0, 0, 0, 0);
+    if (CM && todo) gpv = c.gaps()[uni(g0 + first_lane(todo))];
     while (todo) {
       const int gi = uni(g0 + first_lane(todo));
       todo &= todo - 1;
+      int4 gp = make_int4(0, 0, 0, 0);
+      if constexpr (CM) {
+        gp = uni4(gpv);
+        if (todo) gpv = c.gaps()[uni(g0 + first_lane(todo))];
+      }
       int o;
       MPROF(0, 1);
+      MCLK0(tf);
       if constexpr (CM)
-        o = first_fit_cls(c, gi, st);
+        o = first_fit_cls(c, gi, gp, st);
       else
         o = first_fit(c, gi, n_opt, ff);
+      MCLK1(tf, 4);
       if (o >= 0) {
         c.at(aMG, gi) = o;
         c.at(aMO, o) = gi;
+        if constexpr (CM && L)
+          if (st.mgr && lane == 0) c.mgr()[o] = gp;
         match_fence<L>();
         continue;
       }
       *stamp = uni(*stamp + 1);
       MPROF(1, 1);
       bool ok;
-      if constexpr (CM)
-        ok = augment_cls(c, gi, *stamp, st);
-      else
+      MCLK0(ta);
+      if constexpr (CM) {
+        ok = augment_cls(c, gi, gp, *stamp, st);
+      } else {
         ok = augment(c, gi, n_opt, *stamp);
+      }
+      MCLK1(ta, 5);
       if (!ok) {
         MPROF(3, 1);
         return false;
@@ -592,17 +648,23 @@ __device__ void set_req(const Cmp<L> &c, int gi, int v, int G, int *ff, ClsSt &s
     const int g = gi + k;
     const int o = uni(c.at(aMG, g));
     if (o < 0) continue;
-    if (!elig(uni4(gaps[g]), uni4(c.ops()[o]))) {
+    const int4 gr = uni4(gaps[g]);
+    if constexpr (CM && L)
+      if (st.mgr && lane == 0) c.mgr()[o] = gr;  // (stale if unmatched below: unread then)
+    if (!elig(gr, uni4(c.ops()[o]))) {
       c.at(aMG, g) = -1;
       c.at(aMO, o) = -1;
       if constexpr (CM) {
         const int k2 = uni(c.at(aCls, o));
         if (k2 >= 0 && lane == k2) {
           const int rk = c.at(aRank, o);
-          if (rk < st.f) {
+          if (rk < st.f) {  // the ops between it and the old cursor stay matched
+            st.ma += st.f - 1 - rk;
             st.f = rk;
             st.fo = o;
             st.fc = (uint32_t)c.ops()[o].x;
+          } else {
+            st.ma--;
           }
         }
       } else {
@@ -615,10 +677,19 @@ __device__ void set_req(const Cmp<L> &c, int gi, int v, int G, int *ff, ClsSt &s
 
 // Decide the gap filling by matching plus depth-first branching on the
 // values of free gaps that a matched CAS depends on.  Wave 0 only.  The
-// branch stack (gap, value) lives in the skeleton's Claim / Req arrays,
+// branch stack (gap, value, first value) lives in skeleton arrays that are
 // free once the compact arrays are built.
-template <bool L, bool CM, class P>
-__device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVal,
+//
+// A branch on free gap g (the CAS matched after it expects e, which the op
+// matched at g does not write) tries e first, when some op eligible for g
+// writes e: that one value repairs the violation, and the matching then
+// usually needs no further branch (C4: 65 -> see DESIGN §4).  Then the other
+// values in increasing order, e skipped.  Every value is tried once, so the
+// search is exactly as complete as the plain ascending order.  PREF false:
+// ascending order only (brFst unused; the crash-light pass, whose keys
+// rarely branch, keeps its register budget).
+template <bool L, bool CM, bool PREF, class P>
+__device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVal, P brFst,
                               int64_t *nodes, ClsSt &st) {
   const int lane = threadIdx.x & (kWave - 1);
   const auto gaps = c.gaps();
@@ -627,36 +698,62 @@ __device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVa
   for (int node = 0;; node++) {
     if (node >= kNodeBudget) return GD_BUDGET;
     (*nodes)++;
-    if (fill<L, CM>(c, G, n_opt, &ff, &stamp, st)) {
-      // the matching ignored CAS expectations after free gaps: check them
-      int viol = INT_MAX;
+    MCLK0(tn);
+    const bool filled = fill<L, CM>(c, G, n_opt, &ff, &stamp, st);
+    MCLK1(tn, 7);
+    if (filled) {
+      // the matching ignored CAS expectations after free gaps: check them.
+      // PREF: every violation whose expected value some eligible op writes
+      // is branched on at once, the expected value first (a run of levels
+      // of the same depth-first search, each level a gap of its own, pushed
+      // without a fill between: a failing fill prunes the deepest); else
+      // the first violation, ascending.
+      int pushed = 0, viol0 = INT_MAX;
       for (int g0 = 1; g0 < G; g0 = uni(g0 + kWave)) {
         const int gi = min(g0 + lane, G - 1);  // gaps gi-1, gi; gi-1 free if B = kAny
         const int e = ops[c.at(aMG, gi)].z, pv = ops[c.at(aMG, gi - 1)].y;
-        const uint64_t b =
-            __ballot((g0 + lane < G) & (gaps[gi].z == kAny) & (e != kAny) & (pv != e));
-        if (b) {
-          viol = uni(g0 + first_lane(b) - 1);
-          break;
+        uint64_t b = __ballot((g0 + lane < G) & (gaps[gi].z == kAny) & (e != kAny) & (pv != e));
+        if (b && viol0 == INT_MAX) viol0 = uni(g0 + first_lane(b) - 1);
+        if (!PREF) break;
+        for (; b; b &= b - 1) {
+          const int viol = uni(g0 + first_lane(b) - 1);
+          if (!kGapMultiPush && viol != viol0) break;
+          const int want = uni(__builtin_amdgcn_readlane(e, first_lane(b)));
+          if (uni(gaps[viol + 1].z) != kAny) continue;  // fixed by a push just made
+          if (next_value<L, CM>(c, viol, want - 1, n_opt, st) != want) continue;
+          if (lane == 0) {
+            brPos[depth] = viol;
+            brVal[depth] = want;
+            brFst[depth] = want;
+          }
+          depth++;
+          pushed++;
+          set_req<L, CM>(c, viol, want, G, &ff, st);
         }
+        if (viol0 != INT_MAX && !kGapMultiPush) break;
       }
-      if (viol == INT_MAX) return GD_VALID;
-      // branch on the value of free gap `viol`
-      const int v = next_value<L, CM>(c, viol, INT_MIN, n_opt, st);
-      if (lane == 0) {
-        brPos[depth] = viol;
-        brVal[depth] = v;
+      if (viol0 == INT_MAX) return GD_VALID;
+      if (!pushed) {  // branch on the first violation, ascending
+        const int v = next_value<L, CM>(c, viol0, INT_MIN, n_opt, st);
+        if (lane == 0) {
+          brPos[depth] = viol0;
+          brVal[depth] = v;
+          if (PREF) brFst[depth] = kAny;
+        }
+        depth++;
+        set_req<L, CM>(c, viol0, v, G, &ff, st);
       }
-      depth++;
-      set_req<L, CM>(c, viol, v, G, &ff, st);
       continue;
     }
     // no filling: next value of the deepest branch, else backtrack
     for (;;) {
       if (depth == 0) return GD_INVALID;
       const int gi = uni(brPos[depth - 1]), last = uni(brVal[depth - 1]);
+      const int fst = PREF ? uni(brFst[depth - 1]) : kAny;
       set_req<L, CM>(c, gi, kAny, G, &ff, st);
-      const int v = next_value<L, CM>(c, gi, last, n_opt, st);
+      // after the first value: ascending from the smallest, the first skipped
+      int v = next_value<L, CM>(c, gi, fst != kAny && last == fst ? INT_MIN : last, n_opt, st);
+      if (fst != kAny && v == fst) v = next_value<L, CM>(c, gi, v, n_opt, st);
       if (v != INT_MAX) {
         if (lane == 0) brVal[depth - 1] = v;
         set_req<L, CM>(c, gi, v, G, &ff, st);
@@ -670,13 +767,15 @@ __device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVa
 // Class-indexed when there are many optional ops of few classes (and, in
 // the HBM fallback, room for the class table); else the chunked scans.
 template <bool L, class P>
-__device__ int match_branch(const Cmp<L> &c, int G, int n_opt, P brPos, P brVal,
-                            int64_t *nodes) {
+__device__ int match_branch(const Cmp<L> &c, int G, int n_opt, P brPos, P brVal, P brFst,
+                            int64_t *nodes, bool mgr_room) {
   ClsSt st;
   st.K = 0;
-  if (n_opt >= kClsMinOps && (L || c.cap >= 4 * kMaxCls) && build_classes(c, G, n_opt, st) >= 0)
-    return match_branch_m<L, true>(c, G, n_opt, brPos, brVal, nodes, st);
-  return match_branch_m<L, false>(c, G, n_opt, brPos, brVal, nodes, st);
+  if (n_opt >= kClsMinOps && (L || c.cap >= 4 * kMaxCls) && build_classes(c, G, n_opt, st) >= 0) {
+    st.mgr = L && mgr_room;
+    return match_branch_m<L, true, true>(c, G, n_opt, brPos, brVal, brFst, nodes, st);
+  }
+  return match_branch_m<L, false, true>(c, G, n_opt, brPos, brVal, brFst, nodes, st);
 }
 
 }  // namespace

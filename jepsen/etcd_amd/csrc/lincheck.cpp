@@ -84,7 +84,8 @@ constexpr int kGapLdsFull = 48 << 10;
 constexpr int kGapLdsFew = 128 << 10;
 constexpr int64_t kGapFewKeys = 512;
 constexpr int64_t kGapSkelLdsMax = 78 << 10;  // two such workgroups per CU (160 KB)
-constexpr int kGapLdsProbe = 48 << 10;
+// (two 256-thread workgroups per CU either way: the kernel's 240 VGPRs)
+constexpr int kGapLdsProbe = 72 << 10;
 constexpr int kGapMaxRounds = 64;
 constexpr int kGapProbeMinLen = 1024;
 #ifndef LC_GAP_WAVE_MAX_LEN
@@ -411,9 +412,13 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       // the whole GPU
       job.mode = lcdev::kGapProbe;
       job.threads = 256;
-      job.P = wg_cap / n_cex;
-      job.n_tasks = n_cex * job.P;
       job.lds_bytes = no_lds ? 0 : kGapLdsProbe;
+      // as many probes as run at once: a round's time is its slowest batch
+      // of resident workgroups, and a second batch doubles it for a few
+      // more cuts (C4 invalid: 1,024 probes = two batches of 512 resident)
+      const int resident = lcdev::gap_tier_resident(job.lds_bytes);
+      job.P = (resident / n_cex >= 2 ? std::min(resident, wg_cap) : wg_cap) / n_cex;
+      job.n_tasks = n_cex * job.P;
       rc = ensure(c, reinterpret_cast<char **>(&d.d_gws), &d.gws_cap,
                   lcdev::gap_tier_ws_bytes(job.n_tasks, gap_cap));
       if (rc) return rc;
