@@ -16,6 +16,9 @@ namespace {
 
 constexpr int kAny = INT_MIN;      // no value required / not a CAS
 constexpr int kNodeBudget = 4096;  // matching passes per decision
+#ifndef GAP_PREF_BUDGET  // test builds: a tiny budget sends decisions to the plain-order rerun
+#define GAP_PREF_BUDGET kNodeBudget
+#endif
 constexpr int kMaxCls = 64;        // class-indexed matching: at most one class per lane
 constexpr int kClsMinOps = 128;    // ... used from this many optional ops on
 #ifdef GAP_SINGLE_PUSH  // A/B: one violation branched on per matching
@@ -262,6 +265,7 @@ struct ClsSt {
   // before the cursor is matched; an augmenting path or a branch's unmatch
   // leaves matched ops ahead of it).  While 0 the head is known free.
   int ma = 0;
+  int stamp = 0;         // (uniform) visit stamp of the last augmenting search: never reused
 };
 
 
@@ -694,9 +698,16 @@ __device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVa
   const int lane = threadIdx.x & (kWave - 1);
   const auto gaps = c.gaps();
   const auto ops = c.ops();
-  int ff = 0, stamp = 0, depth = 0;
+  int ff = 0, depth = 0;
+  int &stamp = st.stamp;  // (a rerun after the budget keeps counting: stale visits never match)
   for (int node = 0;; node++) {
-    if (node >= kNodeBudget) return GD_BUDGET;
+    if (node >= (PREF ? GAP_PREF_BUDGET : kNodeBudget)) {
+      // PREF: back to the gaps' own requirements (every branch gap was free),
+      // so the caller can rerun with the plain order
+      if (PREF)
+        for (; depth > 0; depth--) set_req<L, CM>(c, uni(brPos[depth - 1]), kAny, G, &ff, st);
+      return GD_BUDGET;
+    }
     (*nodes)++;
     MCLK0(tn);
     const bool filled = fill<L, CM>(c, G, n_opt, &ff, &stamp, st);
@@ -714,7 +725,10 @@ __device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVa
         const int e = ops[c.at(aMG, gi)].z, pv = ops[c.at(aMG, gi - 1)].y;
         uint64_t b = __ballot((g0 + lane < G) & (gaps[gi].z == kAny) & (e != kAny) & (pv != e));
         if (b && viol0 == INT_MAX) viol0 = uni(g0 + first_lane(b) - 1);
-        if (!PREF) break;
+        if (!PREF) {
+          if (viol0 != INT_MAX) break;  // the first violation only
+          continue;
+        }
         for (; b; b &= b - 1) {
           const int viol = uni(g0 + first_lane(b) - 1);
           if (!kGapMultiPush && viol != viol0) break;
@@ -754,6 +768,19 @@ __device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVa
       // after the first value: ascending from the smallest, the first skipped
       int v = next_value<L, CM>(c, gi, fst != kAny && last == fst ? INT_MIN : last, n_opt, st);
       if (fst != kAny && v == fst) v = next_value<L, CM>(c, gi, v, n_opt, st);
+      if (PREF && v != INT_MAX) {
+        // relaxation first: with gi free and only the levels above fixed, is
+        // there a filling at all?  If not, no value of gi (and nothing deeper)
+        // can give one: pop the level instead of trying each value.  (A run of
+        // levels pushed at once makes blind backtracking exponential.)
+        if (node + 1 >= GAP_PREF_BUDGET) break;  // (the loop's budget exit unwinds the stack)
+        node++;
+        (*nodes)++;
+        if (!fill<L, CM>(c, G, n_opt, &ff, &stamp, st)) {
+          depth--;
+          continue;
+        }
+      }
       if (v != INT_MAX) {
         if (lane == 0) brVal[depth - 1] = v;
         set_req<L, CM>(c, gi, v, G, &ff, st);
@@ -773,9 +800,16 @@ __device__ int match_branch(const Cmp<L> &c, int G, int n_opt, P brPos, P brVal,
   st.K = 0;
   if (n_opt >= kClsMinOps && (L || c.cap >= 4 * kMaxCls) && build_classes(c, G, n_opt, st) >= 0) {
     st.mgr = L && mgr_room;
-    return match_branch_m<L, true, true>(c, G, n_opt, brPos, brVal, brFst, nodes, st);
+    const int r = match_branch_m<L, true, true>(c, G, n_opt, brPos, brVal, brFst, nodes, st);
+    // the expected-value-first order ran out of nodes: the plain order (round 2's
+    // search) gets a budget of its own, so no key is left to the JIT tier that
+    // it decided
+    return r != GD_BUDGET ? r
+                          : match_branch_m<L, true, false>(c, G, n_opt, brPos, brVal, brFst, nodes, st);
   }
-  return match_branch_m<L, false, true>(c, G, n_opt, brPos, brVal, brFst, nodes, st);
+  const int r = match_branch_m<L, false, true>(c, G, n_opt, brPos, brVal, brFst, nodes, st);
+  return r != GD_BUDGET ? r
+                        : match_branch_m<L, false, false>(c, G, n_opt, brPos, brVal, brFst, nodes, st);
 }
 
 }  // namespace

@@ -13,6 +13,7 @@ from jepsen.etcd_amd import abi  # noqa: E402
 CFGS = {
     "C4": dict(n_keys=1, ops_per_key=5000, concurrency=50, p_info=0.2, info_frac=0.2, seed=0x5EED0004),
     "C4x": dict(n_keys=1, ops_per_key=5000, concurrency=50, p_info=0.2, info_frac=0.2, p_anomaly=1.0, seed=1007),
+    "C4x1004": dict(n_keys=1, ops_per_key=5000, concurrency=50, p_info=0.2, info_frac=0.2, p_anomaly=1.0, seed=1004),
     "C4r1": dict(n_keys=1, ops_per_key=5000, concurrency=50, p_info=0.2, seed=0x5EED0004),
     "C5": dict(n_keys=1000, ops_per_key=200, concurrency=10, p_anomaly=0.1, seed=0x5EED0005),
     "C5big": dict(n_keys=10000, ops_per_key=200, concurrency=10, p_info=0.1, p_anomaly=0.1, seed=77),
@@ -35,5 +36,6 @@ with abi.Context(device_mask=1) as ctx:
                               "gap_ms": round(s["gap_kernel_ms"], 4),
                               "jit_ms": round(s["jit_kernel_ms"], 4),
                               "nodes": int(r["configs_explored"].max()),
-                              "invalid": int(v[1]), "valid": int(v[2]), "unknown": int(v[0])}),
+                              "invalid": int(v[1]), "valid": int(v[2]), "unknown": int(v[0]),
+                              "reason": int(r["reason"].max())}),
                   flush=True)
