@@ -253,7 +253,7 @@ def main():
         dist.destroy_process_group()
 
 
-def c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream, steps=30, warmup=5):
+def c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream, steps=200, warmup=20):
     """A one-GPU predictor of BASELINE configs[2] (C3): the same C2 batch cut
     by lc_plan_partition into 1, 2, 4 and 8 shards, and each shard timed as
     one lc_check_device step on this GPU.  A step at N GPUs takes as long as
