@@ -34,6 +34,7 @@ with abi.Context(device_mask=1) as ctx:
             v = np.bincount(r["verdict"] + 1, minlength=3)
             print(json.dumps({"cfg": name, "rep": i, "wall_ms": round(wall, 3),
                               "gap_ms": round(s["gap_kernel_ms"], 4),
+                              "fast_ms": round(s["fast_kernel_ms"], 4),
                               "jit_ms": round(s["jit_kernel_ms"], 4),
                               "nodes": int(r["configs_explored"].max()),
                               "invalid": int(v[1]), "valid": int(v[2]), "unknown": int(v[0]),
