@@ -231,6 +231,7 @@ struct GapKey {
   int n;
   int64_t base;  // call index of the key's first record
   int V0, init;
+  int pref_budget;  // GapJob::pref_budget
   GapSh *sh;
 };
 
@@ -564,9 +565,9 @@ __device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int
   if (tid < kWave) {
     int r;
     if (SL || in_lds)
-      r = match_branch(cl, G, n_opt, w.Claim, w.Req, w.PinExp, nodes, mgr_room);
+      r = match_branch(cl, G, n_opt, w.Claim, w.Req, w.PinExp, nodes, mgr_room, g.pref_budget);
     else
-      r = match_branch(cg, G, n_opt, w.Claim, w.Req, w.PinExp, nodes, false);
+      r = match_branch(cg, G, n_opt, w.Claim, w.Req, w.PinExp, nodes, false, g.pref_budget);
     if (tid == 0) sh.res = r;
   }
   __syncthreads();
@@ -634,6 +635,7 @@ __global__ __launch_bounds__(T) void gap_tier_kernel(
   g.sh = &sh;
   g.V0 = p.init_ver;
   g.init = p.init_val;
+  g.pref_budget = job.pref_budget;
   for (int t = blockIdx.x; t < job.n_tasks; t += gridDim.x) {
     int ci = -1;  // counterexample index (probe / bisect)
     int64_t key;

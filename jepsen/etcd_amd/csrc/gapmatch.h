@@ -15,10 +15,7 @@ namespace lcdev {
 namespace {
 
 constexpr int kAny = INT_MIN;      // no value required / not a CAS
-constexpr int kNodeBudget = 4096;  // matching passes per decision
-#ifndef GAP_PREF_BUDGET  // test builds: a tiny budget sends decisions to the plain-order rerun
-#define GAP_PREF_BUDGET kNodeBudget
-#endif
+constexpr int kNodeBudget = kGapNodeBudget;  // matching passes per decision
 constexpr int kMaxCls = 64;        // class-indexed matching: at most one class per lane
 constexpr int kClsMinOps = 128;    // ... used from this many optional ops on
 #ifdef GAP_SINGLE_PUSH  // A/B: one violation branched on per matching
@@ -266,6 +263,9 @@ struct ClsSt {
   // leaves matched ops ahead of it).  While 0 the head is known free.
   int ma = 0;
   int stamp = 0;         // (uniform) visit stamp of the last augmenting search: never reused
+  // (uniform) node budget of the expected-value-first search before the plain
+  // rerun (GapJob::pref_budget: kNodeBudget; tests set a tiny one)
+  int pref_budget = kNodeBudget;
 };
 
 
@@ -701,7 +701,7 @@ __device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVa
   int ff = 0, depth = 0;
   int &stamp = st.stamp;  // (a rerun after the budget keeps counting: stale visits never match)
   for (int node = 0;; node++) {
-    if (node >= (PREF ? GAP_PREF_BUDGET : kNodeBudget)) {
+    if (node >= (PREF ? st.pref_budget : kNodeBudget)) {
       // PREF: back to the gaps' own requirements (every branch gap was free),
       // so the caller can rerun with the plain order
       if (PREF)
@@ -773,7 +773,7 @@ __device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVa
         // there a filling at all?  If not, no value of gi (and nothing deeper)
         // can give one: pop the level instead of trying each value.  (A run of
         // levels pushed at once makes blind backtracking exponential.)
-        if (node + 1 >= GAP_PREF_BUDGET) break;  // (the loop's budget exit unwinds the stack)
+        if (node + 1 >= st.pref_budget) break;  // (the loop's budget exit unwinds the stack)
         node++;
         (*nodes)++;
         if (!fill<L, CM>(c, G, n_opt, &ff, &stamp, st)) {
@@ -795,9 +795,10 @@ __device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVa
 // the HBM fallback, room for the class table); else the chunked scans.
 template <bool L, class P>
 __device__ int match_branch(const Cmp<L> &c, int G, int n_opt, P brPos, P brVal, P brFst,
-                            int64_t *nodes, bool mgr_room) {
+                            int64_t *nodes, bool mgr_room, int pref_budget) {
   ClsSt st;
   st.K = 0;
+  st.pref_budget = pref_budget;
   if (n_opt >= kClsMinOps && (L || c.cap >= 4 * kMaxCls) && build_classes(c, G, n_opt, st) >= 0) {
     st.mgr = L && mgr_room;
     const int r = match_branch_m<L, true, true>(c, G, n_opt, brPos, brVal, brFst, nodes, st);

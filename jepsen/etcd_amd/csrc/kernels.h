@@ -158,6 +158,7 @@ hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
 // LC_WITNESS_FULL; an invalid key bisected in place gets the witness of
 // the prefix before its failing return (LC_WITNESS_PREFIX).
 enum { kGapFull = 0, kGapProbe = 1, kGapWitness = 2 };
+constexpr int kGapNodeBudget = 4096;  // matching passes per decision (gapmatch.h)
 struct GapJob {
   int32_t mode;        // kGapFull / kGapProbe / kGapWitness
   int32_t bisect;      // kGapFull: bisect invalid keys in place
@@ -166,6 +167,8 @@ struct GapJob {
   int32_t threads;     // workgroup size: 256, or 64 for short keys (one wave per decision)
   int32_t n_tasks;     // keys (full), intervals x P (probe), intervals (witness)
   int32_t give_up;     // launch_gap_narrow: pass every open interval on to the JIT tier
+  int32_t pref_budget; // matching passes of the expected-value-first search before the
+                       //   plain-order rerun (gapmatch.h; LC_GAP_PREF_BUDGET tests it)
   int32_t *cex_key;    // per counterexample: the key
   uint32_t *cex_lo;    // key-relative event interval [lo, hi] holding the
   uint32_t *cex_hi;    //   first return whose prefix is not linearizable

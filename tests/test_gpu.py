@@ -255,6 +255,30 @@ def test_gap_tier_vs_oracle(ctx, opk, conc, seed):
             assert (g["fail_op"][k], g["fail_prefix_end"][k]) == gm.first_failure(recs)
 
 
+@pytest.mark.parametrize("budget", [1, 2, 3])
+def test_gap_plain_order_rerun(ctx, monkeypatch, budget):
+    """The gap tier's expected-value-first branching, cut off after `budget`
+    matching passes, unwinds and reruns the plain ascending search
+    (gapmatch.h): verdicts and counterexamples equal the full-budget run and
+    the restated procedure, on crash-heavy keys that branch (C4-shaped, valid
+    and invalid) and on a mixed batch."""
+    import gapmatch_ref as gm
+    cases = [abi.synth(1, 5000, concurrency=50, p_info=0.2, info_frac=0.2, p_anomaly=a, seed=s)[:2]
+             for s, a in ((0x5EED0004, 0.0), (1007, 1.0))]
+    cases.append(abi.synth(120, 200, concurrency=20, p_info=0.2, p_anomaly=0.3, seed=41)[:2])
+    fields = ("verdict", "fail_op", "fail_prefix_end")
+    for ops, off in cases:
+        monkeypatch.delenv("LC_GAP_PREF_BUDGET", raising=False)
+        _, full = ctx.check(ops, off)
+        monkeypatch.setenv("LC_GAP_PREF_BUDGET", str(budget))
+        _, cut = ctx.check(ops, off)
+        for f in fields:
+            assert (cut[f] == full[f]).all(), f
+        assert (cut["verdict"] != -1).all()
+        recs = _gm_recs(ops, off, 0)
+        assert cut["verdict"][0] == gm.decide(recs)
+
+
 @pytest.mark.parametrize("seed,anom", [(0x5EED0004, 0.0), (1007, 1.0), (1009, 1.0)])
 def test_c4_hot_key(ctx, seed, anom):
     """BASELINE configs[3] at full size: one key, 5k ops, concurrency 50,
