@@ -264,8 +264,8 @@ struct ClsSt {
   int ma = 0;
   int stamp = 0;         // (uniform) visit stamp of the last augmenting search: never reused
   // (uniform) node budget of the expected-value-first search before the plain
-  // rerun (GapJob::pref_budget: kNodeBudget; tests set a tiny one)
-  int pref_budget = kNodeBudget;
+  // rerun (GapJob::pref_budget: kGapPrefBudget; tests set a tiny one)
+  int pref_budget = kGapPrefBudget;
 };
 
 

@@ -159,6 +159,10 @@ hipError_t launch_hbm_tier(const lc_op *d_ops, const int64_t *d_key_off,
 // the prefix before its failing return (LC_WITNESS_PREFIX).
 enum { kGapFull = 0, kGapProbe = 1, kGapWitness = 2 };
 constexpr int kGapNodeBudget = 4096;  // matching passes per decision (gapmatch.h)
+// ... of which the expected-value-first search may spend this many before the
+// plain-order rerun takes over with the full budget (C4 decisions take 1-10;
+// a search that needs hundreds is better off in the plain order)
+constexpr int kGapPrefBudget = 512;
 struct GapJob {
   int32_t mode;        // kGapFull / kGapProbe / kGapWitness
   int32_t bisect;      // kGapFull: bisect invalid keys in place

@@ -372,7 +372,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     // LC_GAP_PREF_BUDGET (tests): a tiny budget sends every branching decision
     // through the plain-order rerun
     const char *pb_env = getenv("LC_GAP_PREF_BUDGET");
-    job.pref_budget = pb_env ? std::max(1, atoi(pb_env)) : lcdev::kGapNodeBudget;
+    job.pref_budget = pb_env ? std::max(1, atoi(pb_env)) : lcdev::kGapPrefBudget;
     job.cex_nodes = reinterpret_cast<int64_t *>(d.d_cex);
     job.cex_key = reinterpret_cast<int32_t *>(d.d_cex + 8 * nk);
     job.cex_lo = reinterpret_cast<uint32_t *>(job.cex_key + nk);
