@@ -65,6 +65,13 @@ def parse():
 
 def main():
     args = parse()
+    # stdout carries only the JSON line: everything else written to fd 1 —
+    # RCCL's version banner, gloo's "Rank r is connected to n peer ranks"
+    # whenever a gloo group forms, the library's RCCL communicators — goes to
+    # stderr; the line is written to a duplicate of the original stdout
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
     from jepsen.etcd_amd import abi
@@ -83,21 +90,11 @@ def main():
     # barrier and the max/sum reductions
     distributed = "TORCHELASTIC_RUN_ID" in os.environ or world > 1
     if distributed:
-        # RCCL prints a version banner on stdout at init; stdout carries
-        # only the JSON line, so send anything printed meanwhile to stderr
-        sys.stdout.flush()
-        saved = os.dup(1)
-        os.dup2(2, 1)
-        try:
-            if backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-            else:
-                dist.init_process_group(backend)
-            dist.barrier()
-        finally:
-            sys.stdout.flush()
-            os.dup2(saved, 1)
-            os.close(saved)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+        dist.barrier()
     dev = torch.device("cuda", local)
 
     # ---- workload: configs[1] = C2, seed 0x5EED0002, the same on every
@@ -247,7 +244,8 @@ def main():
         line["cpu_baseline"] = cpu_baseline(args, ops, key_off, res)
 
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        json_out.write(json.dumps(line) + "\n")
+        json_out.flush()
     ctx.close()
     if distributed:
         dist.destroy_process_group()
