@@ -687,7 +687,7 @@ __device__ void set_req(const Cmp<L> &c, int gi, int v, int G, int *ff, ClsSt &s
 // A branch on free gap g (the CAS matched after it expects e, which the op
 // matched at g does not write) tries e first, when some op eligible for g
 // writes e: that one value repairs the violation, and the matching then
-// usually needs no further branch (C4: 65 -> see DESIGN §4).  Then the other
+// usually needs no further branch (C4: 65 -> 4 matchings).  Then the other
 // values in increasing order, e skipped.  Every value is tried once, so the
 // search is exactly as complete as the plain ascending order.  PREF false:
 // ascending order only (brFst unused; the crash-light pass, whose keys
@@ -722,8 +722,12 @@ __device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVa
       int pushed = 0, viol0 = INT_MAX;
       for (int g0 = 1; g0 < G; g0 = uni(g0 + kWave)) {
         const int gi = min(g0 + lane, G - 1);  // gaps gi-1, gi; gi-1 free if B = kAny
-        const int e = ops[c.at(aMG, gi)].z, pv = ops[c.at(aMG, gi - 1)].y;
-        uint64_t b = __ballot((g0 + lane < G) & (gaps[gi].z == kAny) & (e != kAny) & (pv != e));
+        // (a push earlier in this scan may have unmatched a gap: such a pair
+        // is no violation of this matching)
+        const int mg = c.at(aMG, gi), mg1 = c.at(aMG, gi - 1);
+        const int e = ops[max(mg, 0)].z, pv = ops[max(mg1, 0)].y;
+        uint64_t b = __ballot((g0 + lane < G) & (mg >= 0) & (mg1 >= 0) & (gaps[gi].z == kAny) &
+                              (e != kAny) & (pv != e));
         if (b && viol0 == INT_MAX) viol0 = uni(g0 + first_lane(b) - 1);
         if (!PREF) {
           if (viol0 != INT_MAX) break;  // the first violation only
