@@ -174,6 +174,13 @@ __device__ inline void fix_f(Cfg &c, const Win &w) {
   }
 }
 
+// The explored counter is added to by every workgroup of every level: one
+// same-address atomic each serialised; 64 shards on lines of their own, in
+// Ctr so that the host's copy of Ctr after a batch carries them (sync_ctr
+// sums them).
+constexpr int kExpShards = 64;
+constexpr int kExpStride = 16;  // u64 per shard: 128 B
+
 struct Ctr {
   unsigned long long nR, nV;    // R list size; V entries of the levels expanded so far
   unsigned long long cnt[3];    // V levels, triple-buffered: level k is list k % 3
@@ -187,6 +194,7 @@ struct Ctr {
   unsigned long long pad[5];
   unsigned long long cand[64];  // partitioned: candidates per owner rank
   unsigned long long cmin[kMaxCls];  // counted classes: the smallest field over R (retirement)
+  alignas(128) unsigned long long exp[kExpShards * kExpStride];  // explored, sharded
 };
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {
@@ -275,14 +283,8 @@ struct Tabs {
   unsigned long long list_cap;
   int compact;  // one-word keys (ctab_insert) instead of tag + 16-B key
   int cshift;   // compact: the value id's bit offset in the word (64 - value bits)
-  unsigned long long *exp;  // explored, sharded over kExpShards lines (summed by fx_and_kernel)
+  unsigned long long *exp;  // Ctr::exp
 };
-
-// The explored counter is added to by every wave of every level: one
-// same-address atomic per wave serialised (~8k per level); 64 shards on
-// lines of their own, summed once per batch.
-constexpr int kExpShards = 64;
-constexpr int kExpStride = 16;  // u64 per shard: 128 B
 
 __device__ inline unsigned long long wave_sum_shards(unsigned long long *exp) {
   unsigned long long v =
@@ -325,6 +327,14 @@ __device__ inline int any_insert(const Tabs &t, bool toR, uint32_t epoch, const 
   return tab_insert(toR ? t.tagR : t.tagV, toR ? t.keyR : t.keyV, t.tmask, epoch, c);
 }
 
+__device__ inline unsigned long long wave_and(unsigned long long v) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, off), hi = __shfl_xor((uint32_t)(v >> 32), off);
+    v &= ((unsigned long long)hi << 32) | lo;
+  }
+  return v;
+}
+
 // Wave-aggregated append of the lanes in `take` (each with its own c).
 __device__ inline void wave_append(bool take, const Cfg &c, Cfg *list, unsigned long long *count,
                                    unsigned long long cap, unsigned long long *overflow) {
@@ -343,14 +353,16 @@ __device__ inline void wave_append(bool take, const Cfg &c, Cfg *list, unsigned 
 }
 
 // Insert successors (or split frontier configurations): those that
-// linearized x (xbit) go to R with x's bit cleared, the others to V.
+// linearized x (xbit) go to R with x's bit cleared, the others to V.  `rand`
+// (per lane) takes the AND of the masks this lane appended to R.
 __device__ inline void insert_rv(bool have, Cfg c, uint64_t xbit, const Tabs &t, uint32_t epoch,
-                                 Ctr *ctr) {
+                                 Ctr *ctr, uint64_t &rand) {
   bool toR = have && (c.mask & xbit);
   if (toR) c.mask &= ~xbit;
   int r = -1;
   if (have) r = any_insert(t, toR, epoch, c);
   if (have && r < 0) atomicOr(&ctr->tfull, 1ULL);
+  if (r == 1 && toR) rand &= c.mask;
   wave_append(r == 1 && toR, c, t.listR, &ctr->nR, t.list_cap, &ctr->overflow);
   wave_append(r == 1 && !toR, c, t.vdst, t.vcnt, t.list_cap, &ctr->overflow);
 }
@@ -361,13 +373,24 @@ __global__ __launch_bounds__(256) void fx_insert_kernel(const Cfg *__restrict__ 
   const uint64_t xbit = win->xbit;
   const bool fix = win->fclear | win->fclose | win->fsub;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  uint64_t rand = ~0ULL;
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x; b < n; b += stride) {
     const int64_t i = b + threadIdx.x;
     const bool have = i < n;
     Cfg c{};
     if (have) c = in[i];
     if (have && fix) fix_f(c, *win);
-    insert_rv(have, c, xbit, t, epoch, ctr);
+    insert_rv(have, c, xbit, t, epoch, ctr, rand);
+  }
+  // the R entries' AND, one atomic per workgroup (ctr->andmask holds the
+  // AND of R as it grows: the replicated levels add theirs in wg_flush)
+  __shared__ unsigned long long s_and[4];
+  rand = wave_and(rand);
+  if (__lane_id() == 0) s_and[threadIdx.x / kW] = rand;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long a = s_and[0] & s_and[1] & s_and[2] & s_and[3];
+    if (a != ~0ULL) atomicAnd(&ctr->andmask, a);
   }
 }
 
@@ -423,25 +446,30 @@ struct WgFlush {
   int n[4][2];
   unsigned long long base[2];
   unsigned long long explored[4];
+  unsigned long long andm[4];
 };
 
 __device__ inline void wg_flush(WgFlush *wf, Stage *stg, int nr, int nv, unsigned long long explored,
-                                const Tabs &t, Ctr *ctr) {
+                                uint64_t rand, const Tabs &t, Ctr *ctr) {
   const int w = threadIdx.x / kW, lane = __lane_id();
+  rand = wave_and(rand);
   if (lane == 0) {
     wf->n[w][0] = nr;
     wf->n[w][1] = nv;
     wf->explored[w] = explored;
+    wf->andm[w] = rand;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     const int nw = blockDim.x / kW;
-    unsigned long long tr = 0, tv = 0, te = 0;
+    unsigned long long tr = 0, tv = 0, te = 0, ta = ~0ULL;
     for (int k = 0; k < nw; k++) {
       tr += wf->n[k][0];
       tv += wf->n[k][1];
       te += wf->explored[k];
+      ta &= wf->andm[k];
     }
+    if (ta != ~0ULL) atomicAnd(&ctr->andmask, ta);
     wf->base[0] = tr ? atomicAdd(&ctr->nR, tr) : 0;
     wf->base[1] = tv ? atomicAdd(t.vcnt, tv) : 0;
     if (te) atomicAdd(&t.exp[(blockIdx.x % kExpShards) * kExpStride], te);
@@ -509,6 +537,7 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
     }
   };
   unsigned long long explored = 0;
+  uint64_t rand = ~0ULL;  // AND of the masks this lane put in R
   if (!cand_cap) {
     // A wave takes a run of `chunk` configurations (one load per lane), lane t
     // tests slot t of each in turn, and the successors are gathered in LDS
@@ -530,6 +559,7 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
       int x = -2;
       if (have) x = any_insert(t, toR, epoch, sc);
       if (x == -1) atomicOr(&ctr->tfull, 1ULL);
+      if (x == 1 && toR) rand &= sc.mask;
       stage_put(x == 1, toR, sc, stg, nr, nv, t, ctr);
       ns = 0;
     };
@@ -574,7 +604,7 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
       }
     }
   }
-  wg_flush(wf, stg, nr, nv, explored, t, ctr);
+  wg_flush(wf, stg, nr, nv, explored, rand, t, ctr);
 }
 
 __device__ inline void load_win(Win &w, const Win *gwin) {
@@ -621,7 +651,6 @@ __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ 
   expand_range(w, t, epoch, ctr, lo, hi, wave, nwaves, cbuf, cand_cap, &stg[threadIdx.x / kW], &wf);
 }
 
-__device__ inline unsigned long long wave_and(unsigned long long v);
 
 // Counted classes: the smallest field of each class over list[lo, hi) (this
 // thread strided by `step`), into ctr->cmin (retirement of the members every
@@ -668,8 +697,9 @@ __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restr
     const bool have = i < nF;
     Cfg c{};
     if (have) c = F[i];
+    uint64_t rand = ~0ULL;  // the full AND over R below covers these
     if (have) fix_f(c, w);
-    insert_rv(have, c, w.xbit, t, epoch, ctr);
+    insert_rv(have, c, w.xbit, t, epoch, ctr, rand);
   }
   const int64_t wave = threadIdx.x / kW;
   const int64_t nwaves = blockDim.x / kW;
@@ -713,13 +743,6 @@ __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restr
   }
 }
 
-__device__ inline unsigned long long wave_and(unsigned long long v) {
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint32_t lo = __shfl_xor((uint32_t)v, off), hi = __shfl_xor((uint32_t)(v >> 32), off);
-    v &= ((unsigned long long)hi << 32) | lo;
-  }
-  return v;
-}
 
 // AND of the masks of list[0 .. *n) into ctr->andmask (retirement).
 __global__ __launch_bounds__(256) void fx_and_kernel(const Cfg *__restrict__ list,
@@ -1462,7 +1485,7 @@ struct Rank {
 
   void release() {
     for (void *p : {(void *)F, (void *)Rl, (void *)Vl, (void *)tmp, (void *)tagR, (void *)tagV,
-                    (void *)keyR, (void *)keyV, (void *)dWin, (void *)dCtr, (void *)dExp, (void *)cand,
+                    (void *)keyR, (void *)keyV, (void *)dWin, (void *)dCtr, (void *)cand,
                     (void *)sendb, (void *)recvb})
       if (p) (void)hipFree(p);
     F = Rl = Vl = tmp = keyR = keyV = cand = sendb = recvb = nullptr;
@@ -1569,8 +1592,8 @@ struct Rank {
     FX_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     FX_TRY(hipMalloc(&dWin, sizeof(Win)));
     FX_TRY(hipMalloc(&dCtr, sizeof(Ctr)));
-    FX_TRY(hipMalloc(&dExp, sizeof(unsigned long long) * kExpShards * kExpStride));
-    FX_TRY(hipMemset(dExp, 0, sizeof(unsigned long long) * kExpShards * kExpStride));
+    FX_TRY(hipMemset(dCtr, 0, sizeof(Ctr)));
+    dExp = &dCtr->exp[0];  // device address, not dereferenced here
     FX_TRY(hipHostMalloc(&hWin, sizeof(Win), hipHostMallocDefault));
     FX_TRY(hipHostMalloc(&hCtr, sizeof(Ctr), hipHostMallocDefault));
     std::memset(hWin, 0, sizeof(Win));
@@ -1677,9 +1700,13 @@ struct Rank {
     return t;
   }
 
+  // Ctr to the host; its explored is the sum of the shards.
   int sync_ctr() {
     FX_TRY(hipMemcpyAsync(hCtr, dCtr, sizeof(Ctr), hipMemcpyDeviceToHost, st));
     FX_TRY(hipStreamSynchronize(st));
+    unsigned long long e = 0;
+    for (int i = 0; i < kExpShards; i++) e += hCtr->exp[i * kExpStride];
+    hCtr->explored = e;
     return 0;
   }
 
@@ -2243,18 +2270,21 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         }
         const int g = (int)std::max<int64_t>(16, std::min<int64_t>(kExpandWG, (std::max(nF, last_work) + 3) / 4));
         for (int batch = 0; !done; batch++) {
-          if (small || batch) {  // the reset set it for a first batch; a partial AND is stale
+          // ctr->andmask is the AND of R as it grows (the insert and every
+          // level add theirs): no pass over R unless counted classes need
+          // their minima, which that pass recomputes whole
+          if (n_cls && (small || batch)) {  // the reset set them for a first batch
             FX_TRY(hipMemsetAsync(&dCtr->andmask, 0xFF, sizeof(unsigned long long), st));
-            if (n_cls) FX_TRY(hipMemsetAsync(dCtr->cmin, 0xFF, sizeof(dCtr->cmin), st));
+            FX_TRY(hipMemsetAsync(dCtr->cmin, 0xFF, sizeof(dCtr->cmin), st));
           }
           for (int l = 0; l < spec_levels; l++, k++)
             fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tabs(tlog, compact, k), epoch, dCtr, k, -1, -1,
                                                 nullptr, 0);
-          fx_and_kernel<<<grid_for((int64_t)std::max(nF, last_work)), 256, 0, st>>>(Rl, &dCtr->nR,
-                                                                                     dCtr, dExp);
-          if (n_cls)
-            fx_cmin_kernel<<<grid_for((int64_t)std::max(nF, last_work)), 256, 0, st>>>(
-                Rl, &dCtr->nR, dWin, dCtr);
+          if (n_cls) {
+            const int ga = grid_for((int64_t)std::max(nF, last_work));
+            fx_and_kernel<<<ga, 256, 0, st>>>(Rl, &dCtr->nR, dCtr, dExp);
+            fx_cmin_kernel<<<ga, 256, 0, st>>>(Rl, &dCtr->nR, dWin, dCtr);
+          }
           FX_TRY(hipGetLastError());
           if (int er = sync_ctr()) return er;
           if (hCtr->tfull || hCtr->overflow ||
