@@ -138,10 +138,15 @@ def main():
         njit.append(s.n_jit_keys)
         cms.append(s.total_ms)
     torch.cuda.synchronize()
-    own = time.perf_counter() - t0  # this rank's own steps, before waiting for the others
+    # this rank's own K steps; the job time is the MAX of these over ranks
+    # (reduce_run).  The trailing barrier closes the timed region on every
+    # rank but is not counted: at N = 8 a step is ~27 us and one RCCL barrier
+    # would be a visible share of it.
+    own = time.perf_counter() - t0
     if distributed:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    after_barrier = time.perf_counter() - t0
+    elapsed = own
     res = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)[:my_keys]
     ranks = (D.gather_rows([rank, ka, kb, n_ops, own * 1e3 / args.steps,
                             float(np.mean(kms))])
@@ -149,9 +154,23 @@ def main():
              [[0, ka, kb, n_ops, own * 1e3 / args.steps, float(np.mean(kms))]])
     elapsed, (total_ops, n_valid, n_invalid, n_unknown) = reduce_run(
         elapsed, n_ops, res, distributed, dev)
+    after_barrier = reduce_run(after_barrier, 0, res, distributed, dev)[0]
     # every rank together, outside the timed region: the one collective path
     fx_ranks = (oversized_key_ranks(abi, world, local)
                 if distributed and world > 1 and not args.bare else None)
+    # rank 0 alone, the other ranks parked on a CPU (gloo) barrier so no
+    # spinning collective kernel shares their GPUs: the drop-in's own
+    # multi-GPU path — one lc_ctx over all N GPUs, lc_check from host memory
+    fanout = None
+    if not args.bare:
+        park = None
+        if distributed:
+            import datetime
+            park = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=600))
+        if rank == 0:
+            fanout = fanout_leg(abi, ops, key_off, world, local)
+        if park is not None:
+            dist.barrier(group=park)
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = total_ops * args.steps / elapsed
@@ -200,6 +219,10 @@ def main():
             "parallelism": "keys sharded by lc_plan_partition, 1 rank per GPU, "
                            "no data-path collective",
         },
+        "timing": "job time = max over ranks of each rank's own timed loop (barrier + "
+                  "synchronize before it, synchronize after it); ms_after_trailing_barrier "
+                  "also counts the closing barrier",
+        "ms_after_trailing_barrier": after_barrier * 1e3 / args.steps,
         "ranks": [{"rank": int(r[0]), "keys": [int(r[1]), int(r[2])], "records": int(r[3]),
                    "ms_per_step": r[4], "kernel_ms": r[5]} for r in ranks],
         "rank_ms_per_step_min_max": [min(r[4] for r in ranks), max(r[4] for r in ranks)],
@@ -228,6 +251,8 @@ def main():
     }
     if fx_ranks is not None:
         line["oversized_key_ranks"] = fx_ranks
+    if fanout is not None:
+        line["fanout_leg"] = fanout
     if rank == 0 and not args.bare:
         if world == 1:  # first, in the timed loop's own state (no leg has run on the context yet)
             line["c3_shards"] = c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream)
@@ -335,6 +360,75 @@ def host_leg(ctx, abi, ops, key_off, n_inv):
     return {"workload": "C2 batch from host memory (lc_check)", "call_ms": t * 1e3,
             "ops_per_s": int(key_off[-1]) / t, "h2d_gb_per_s": ops.nbytes / t / 1e9,
             "valid": int((r["verdict"] == 1).sum())}
+
+
+def fanout_leg(abi, ops, key_off, world, local, calls=3):
+    """BASELINE configs[2] (C3) as the drop-in runs it: ONE lc_ctx over all
+    N GPUs of this node (device_mask (1 << N) - 1) and lc_check on the whole
+    C2 batch from host memory — the JVM shim's call (lincheck.cpp: one host
+    thread and one HIP stream per GPU over its cost-balanced key range, no
+    collective; register.clj:108's independent keys).  Per device: key
+    range, H2D time (HIP events), kernel time, wall time; aggregate H2D rate.
+    A/B: the records as pageable memory, then page-locked by
+    lc_host_register (DMA straight from the caller's buffer; registration
+    time reported).  Median of `calls` after one warm-up; not `value` (the
+    PCIe-inclusive rate).  Rehearsal on one GPU (LC_BENCH_DEVICE): N device
+    contexts on that GPU (LC_VIRTUAL_DEVICES)."""
+    rehearsal = bool(os.environ.get("LC_BENCH_DEVICE"))
+    mask = (1 << local) if rehearsal else (1 << world) - 1
+    saved = os.environ.get("LC_VIRTUAL_DEVICES")
+    if rehearsal and world > 1:
+        os.environ["LC_VIRTUAL_DEVICES"] = str(world)
+    out = {"workload": "C2 batch (10000 keys x 1000 ops) from host buffers, one lc_ctx over "
+                       "all N GPUs (lc_check's in-process fan-out: the JVM drop-in's path)",
+           "rehearsal_virtual_devices": rehearsal and world > 1}
+    try:
+        ctx = abi.Context(device_mask=mask)
+    except Exception as e:  # reported, never fatal to the bench line
+        out["error"] = repr(e)
+        return out
+    finally:
+        if saved is None:
+            os.environ.pop("LC_VIRTUAL_DEVICES", None)
+        else:
+            os.environ["LC_VIRTUAL_DEVICES"] = saved
+    try:
+        for mode in ("pageable", "registered"):
+            if mode == "registered":
+                t0 = time.perf_counter()
+                ctx.host_register(ops)
+                out["register_ms"] = (time.perf_counter() - t0) * 1e3
+            try:
+                rows = []
+                for i in range(calls + 1):
+                    t0 = time.perf_counter()
+                    _, r = ctx.check(ops, key_off)
+                    ms = (time.perf_counter() - t0) * 1e3
+                    if i:
+                        rows.append((ms, ctx.device_stats()))
+                rows.sort(key=lambda x: x[0])
+                ms, devs = rows[len(rows) // 2]
+            finally:
+                if mode == "registered":
+                    ctx.host_unregister(ops)
+            h2d = sum(d["h2d_bytes"] for d in devs)
+            slow = max(d["h2d_ms"] for d in devs)
+            out[mode] = {
+                "call_ms": ms, "n_devices": len(devs),
+                "ops_per_s": int(key_off[-1] - key_off[0]) / (ms * 1e-3),
+                "h2d_gb_per_s_aggregate": h2d / (slow * 1e-3) / 1e9 if slow > 0 else None,
+                "valid": int((r["verdict"] == 1).sum()),
+                "devices": [{"device": d["device"], "keys": [d["key_begin"], d["key_end"]],
+                             "pinned": d["pinned"], "h2d_ms": d["h2d_ms"],
+                             "h2d_gb_per_s": d["h2d_bytes"] / (d["h2d_ms"] * 1e-3) / 1e9
+                             if d["h2d_ms"] > 0 else None,
+                             "kernel_ms": d["kernel_ms"], "total_ms": d["total_ms"]}
+                            for d in devs]}
+    except Exception as e:  # reported, never fatal to the bench line
+        out["error"] = repr(e)
+    finally:
+        ctx.close()
+    return out
 
 
 def hot_key(ctx, abi):
@@ -546,6 +640,7 @@ def oversized_key_ranks(abi, world, local):
     finally:
         if timer is not None:
             timer.cancel()
+            timer.join()  # a callback already running (fx.abort) ends before fx.close()
         if fx is not None:
             fx.close()
 

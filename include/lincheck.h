@@ -221,6 +221,35 @@ int lc_check_device_ex(lc_ctx *ctx, const lc_op *d_ops, const int64_t *d_key_off
                        void *stream, const lc_aux *aux);
 
 int lc_last_stats(lc_ctx *ctx, lc_stats *out);
+
+/* Per-device share of the most recent lc_check / lc_check_ex call (the
+ * multi-GPU fan-out: one host thread and one HIP stream per device, each over
+ * its contiguous cost-balanced key range, register.clj:108's independent
+ * keys).  Device i of lc_stats.n_devices; -EINVAL past the last. */
+typedef struct lc_device_stats {
+  int32_t device;      /* HIP device id */
+  int32_t pinned;      /* the records came from page-locked host memory (lc_host_register) */
+  int64_t key_begin;   /* [key_begin, key_end) of the call's keys */
+  int64_t key_end;
+  int64_t h2d_bytes;   /* records + key offsets copied to the device */
+  double  h2d_ms;      /* the host-to-device copies (HIP events on the device's stream) */
+  double  kernel_ms;   /* the tiers (as lc_stats.kernel_ms, this device's) */
+  double  total_ms;    /* host wall time of this device's thread, copies included */
+} lc_device_stats;
+
+int lc_last_device_stats(lc_ctx *ctx, int32_t i, lc_device_stats *out);
+
+/* Page-lock a caller buffer that will be handed to lc_check repeatedly (a
+ * JVM DirectByteBuffer / MemorySegment that outlives the call), so the
+ * host-to-device copies of every GPU of the context DMA straight from it
+ * instead of staging through the runtime's pageable-copy path (SURVEY.md
+ * §8(b): "the library copies to device, or pins with hipHostRegister").
+ * Registration costs about as much as one pageable copy of the buffer, so it
+ * pays from the second call on.  Unregister before freeing the buffer.
+ * Returns 0, -EINVAL, or -EIO (text in lc_last_error). */
+int lc_host_register(lc_ctx *ctx, const void *ptr, uint64_t bytes);
+int lc_host_unregister(lc_ctx *ctx, const void *ptr);
+
 const char *lc_last_error(lc_ctx *ctx);
 void lc_close(lc_ctx *ctx);
 

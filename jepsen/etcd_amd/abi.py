@@ -68,6 +68,13 @@ class LcStats(ctypes.Structure):
                 ("n_malformed", ctypes.c_int64)]
 
 
+class LcDeviceStats(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("pinned", ctypes.c_int32),
+                ("key_begin", ctypes.c_int64), ("key_end", ctypes.c_int64),
+                ("h2d_bytes", ctypes.c_int64), ("h2d_ms", ctypes.c_double),
+                ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+
+
 class LcAux(ctypes.Structure):
     _fields_ = [("witness", ctypes.c_void_p), ("witness_kind", ctypes.c_void_p)]
 
@@ -134,6 +141,12 @@ def lib():
         L.lc_key_cost.restype = ctypes.c_int
         L.lc_last_stats.argtypes = [vp, ctypes.POINTER(LcStats)]
         L.lc_last_stats.restype = ctypes.c_int
+        L.lc_last_device_stats.argtypes = [vp, i32, ctypes.POINTER(LcDeviceStats)]
+        L.lc_last_device_stats.restype = ctypes.c_int
+        L.lc_host_register.argtypes = [vp, vp, ctypes.c_uint64]
+        L.lc_host_register.restype = ctypes.c_int
+        L.lc_host_unregister.argtypes = [vp, vp]
+        L.lc_host_unregister.restype = ctypes.c_int
         L.lc_last_error.argtypes = [vp]
         L.lc_last_error.restype = ctypes.c_char_p
         L.lc_close.argtypes = [vp]
@@ -218,6 +231,29 @@ class Context:
         s = into if into is not None else LcStats()
         lib().lc_last_stats(self._h, ctypes.byref(s))
         return s
+
+    def device_stats(self):
+        """lc_last_device_stats for every device of the last lc_check: one
+        dict per device (its key range, copies, kernels, wall time)."""
+        out = []
+        for i in range(int(self.stats_raw().n_devices)):
+            d = LcDeviceStats()
+            if lib().lc_last_device_stats(self._h, i, ctypes.byref(d)) != 0:
+                break
+            out.append({f: getattr(d, f) for f, _ in LcDeviceStats._fields_})
+        return out
+
+    def host_register(self, arr):
+        """lc_host_register: page-lock a numpy array's buffer for repeated
+        lc_check calls (unregister with host_unregister before freeing it)."""
+        rc = lib().lc_host_register(self._h, ctypes.c_void_p(arr.ctypes.data), arr.nbytes)
+        if rc != 0:
+            raise LcError(rc, self.last_error())
+
+    def host_unregister(self, arr):
+        rc = lib().lc_host_unregister(self._h, ctypes.c_void_p(arr.ctypes.data))
+        if rc != 0:
+            raise LcError(rc, self.last_error())
 
     def check(self, ops, key_off, opts=None, raise_on_error=True, witness=False):
         """Host-buffer check. Returns (rc, results structured array), or with

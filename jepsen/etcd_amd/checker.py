@@ -38,6 +38,10 @@ import os
 from . import abi, diagnostics as D, history as H, linear_svg as LS, timeline as TL
 
 UNKNOWN = "unknown"
+# invalid keys the version-order / gap tiers decided get knossos's :configs
+# from a frontier re-search when they have at most this many crashed ops (the
+# frontier of a version-pinned key grows with its crashed ops only)
+FRONTIER_MAX_CRASHED = 16
 
 
 class VersionedRegister:
@@ -93,8 +97,12 @@ class RegisterChecker:
     result is then one key's map (no :results)."""
 
     def __init__(self, model=None, device_mask=0, max_configs_per_key=0, independent=True,
-                 timeline_dir=None, time_budget_ms=0, whole_gpu=True):
+                 timeline_dir=None, time_budget_ms=0, whole_gpu=True, frontier_max_keys=1000):
         self.model = model or VersionedRegister(0, None)
+        # cap on the frontier re-searches one check() runs for diagnostics of
+        # witnessed invalid keys (each is one key's search up to its failing
+        # return, bounded by max_configs_per_key / time_budget_ms); 0: none
+        self.frontier_max_keys = frontier_max_keys
         self.device_mask = device_mask
         self.max_configs_per_key = max_configs_per_key
         self.independent = independent
@@ -137,6 +145,7 @@ class RegisterChecker:
                              time_budget_ms=self.time_budget_ms)
         _, res, wit, kind = self._context().check(ops, key_off, o, witness=True)
         results = {}
+        n_frontier = 0  # frontier re-searches run for diagnostics in this call
         for i, k in enumerate(keys):
             r = res[i]
             v = {1: True, 0: False}.get(int(r["verdict"]), UNKNOWN)
@@ -147,19 +156,38 @@ class RegisterChecker:
                 d = done[i][int(r["fail_op"])]
                 out["op"] = d["completion"] or d["invoke"]
                 out["fail-prefix-end"] = int(r["fail_prefix_end"])
-                if m.name == "versioned-register" and kind[i] == abi.LC_WITNESS_PREFIX:
-                    w = wit[key_off[i]:key_off[i + 1]]
-                    out.update(D.invalid_analysis(done[i], int(r["fail_op"]),
-                                                  int(r["fail_prefix_end"]), w,
-                                                  init=(m.version, m.value)))
-                else:
-                    # decided by the frontier search: its configurations just
-                    # before the failing return (knossos's :configs)
-                    cfgs = self._frontier().frontier(ops[key_off[i]:key_off[i + 1]],
-                                                     int(r["fail_op"]), D.MAX_ENTRIES, o)
+                recs = ops[key_off[i]:key_off[i + 1]]
+                witnessed = m.name == "versioned-register" and kind[i] == abi.LC_WITNESS_PREFIX
+                # knossos's :configs are its search's frontier just before the
+                # failing return: re-run the frontier search up to there
+                # (lc_fx_frontier) for keys whose frontier stays small — any
+                # key the search decided, and witnessed keys with at most
+                # FRONTIER_MAX_CRASHED crashed ops — up to frontier_max_keys
+                # keys per call; beyond that, or if the re-search fails, the
+                # witness's one configuration (with "configs-error" saying why)
+                cfgs, err = None, None
+                if not witnessed or (n_frontier < self.frontier_max_keys and
+                                     int((recs[:, 5] == abi.LC_INF).sum()) <= FRONTIER_MAX_CRASHED):
+                    n_frontier += 1
+                    try:
+                        cfgs = self._frontier().frontier(recs, int(r["fail_op"]), D.MAX_ENTRIES, o)
+                    except Exception as e:  # noqa: BLE001 — diagnostics only; the verdict stands
+                        err = repr(e)
+                wa = D.invalid_analysis(done[i], int(r["fail_op"]), int(r["fail_prefix_end"]),
+                                        wit[key_off[i]:key_off[i + 1]],
+                                        init=(m.version, m.value)) if witnessed else None
+                if cfgs is not None:
                     out.update(D.frontier_analysis(
                         done[i], int(r["fail_op"]), int(r["fail_prefix_end"]), cfgs, values[i],
                         versioned=m.name == "versioned-register"))
+                    if wa is not None and "last-op" in wa:
+                        out["last-op"] = wa["last-op"]  # the witness's last linearized op
+                elif wa is not None:
+                    out.update(wa)
+                else:
+                    out["previous-ok"] = D.previous_ok(done[i], int(r["fail_prefix_end"]))
+                if err is not None:
+                    out["configs-error"] = err
             elif v == UNKNOWN:
                 out["cause"] = abi.REASONS.get(int(r["reason"]), "?")
             results[k] = out

@@ -281,11 +281,15 @@
   (let [n   (count done)
         buf (Memory. (* 10 fx-config-bytes))
         cnt (Memory. 4)
-        rc  (locking fx-engine
-              (.invokeInt (fun "lc_fx_frontier")
-                          (object-array [@fx-engine (.share ^Memory ops (* op-bytes k0))
-                                         (long n) opts (long fail-op) buf (int 10) cnt])))]
-    (when (zero? rc)
+        rc  (try
+              (locking fx-engine
+                (.invokeInt (fun "lc_fx_frontier")
+                            (object-array [@fx-engine (.share ^Memory ops (* op-bytes k0))
+                                           (long n) opts (long fail-op) buf (int 10) cnt])))
+              ;; diagnostics only: the verdict stands whatever happens here
+              (catch Exception e e))]
+    (if-not (and (number? rc) (zero? rc))
+      {:configs-error (if (number? rc) [:lc-fx-frontier rc] (str rc))}
       (let [configs (for [i (range (.getInt cnt 0))
                           :let [b   (* i fx-config-bytes)
                                 ver (.getLong buf b)
@@ -303,6 +307,12 @@
                  (final-paths done fail-op
                               (for [[ver x pending] configs] [(ref-model ver x) nil pending]))))))))
 
+;; invalid keys the version-order / gap tiers decided get :configs from a
+;; frontier re-search when they have at most this many crashed ops, up to
+;; frontier-max-keys such re-searches per check (checker.py: the same)
+(def ^:private frontier-max-crashed 16)
+(def ^:private frontier-max-keys 1000)
+
 (defn- merge-valid [vs]
   (cond (some false? vs)          false
         (some #{:unknown} vs)     :unknown
@@ -317,6 +327,7 @@
   check-safe) only on unusable arguments or a GPU error."
   [model max-configs-per-key time-budget-ms flags subs]
   (let [[keys done ops off n vals] (pack model subs)
+        n-frontier (atom 0)
         nk   (count keys)
         out  (Memory. (* result-bytes nk))
         wit  (Memory. (max 4 (* 4 n)))
@@ -352,10 +363,24 @@
                         :configs-explored (.getLong out (+ b 24))}
                  (false? v)     (merge {:op (op-map (nth d fail-op))
                                         :previous-ok (previous-ok d fail-at)}
-                                       (if witness
-                                         (witness-analysis d fail-op fail-at witness [0 nil])
-                                         (frontier-analysis model d ops k0 fail-op
-                                                            (nth vals ki) o)))
+                                       (let [wa (when witness
+                                                  (witness-analysis d fail-op fail-at witness
+                                                                    [0 nil]))
+                                             ;; knossos's :configs: the frontier search's
+                                             ;; own, re-run up to the failing return, for
+                                             ;; keys whose frontier stays small
+                                             fa (when (or (nil? witness)
+                                                          (and (< (swap! n-frontier inc)
+                                                                  frontier-max-keys)
+                                                               (<= (count (filter
+                                                                           #(= LC_INF (:ret %)) d))
+                                                                   frontier-max-crashed)))
+                                                  (frontier-analysis model d ops k0 fail-op
+                                                                     (nth vals ki) o))]
+                                         (cond (and fa (:configs fa))
+                                               (cond-> fa (:last-op wa) (assoc :last-op (:last-op wa)))
+                                               wa (merge wa (select-keys fa [:configs-error]))
+                                               :else fa)))
                  (= v :unknown) (assoc :error [:lincheck-reason (reasons reason reason)]))])))))
 
 (defn linearizable

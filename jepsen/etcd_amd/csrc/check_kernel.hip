@@ -1812,6 +1812,222 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, con
   return true;
 }
 
+// ---------------------------------------------------------------------------
+// First failure of an invalid version-pinned key, in O(n) (round 4).
+//
+// A key the version order decides invalid needs its canonical fail op: the
+// first :ok return r whose history prefix is not linearizable (knossos.linear
+// empties its frontier there).  The gap tier found it by bisection over
+// prefixes — nine dependent decisions for a 200-op key.  For a key with no
+// crashed ops the prefix's choices collapse, and r follows from one pass.
+//
+// The prefix at return r: ops called before r; those returned by r are
+// required, the others pending (optional, no return bound).  A pending read
+// is left out.  Position p (version V0+p+1) is *needed* once a required op
+// needs it — a mutation at p' >= p, or a read of version V0+k with k > p —
+// from N(p) = min{ret(o) : need(o) > p} on (need = pos+1 for a mutation, k
+// for a read; a suffix minimum over positions).  A needed position is held
+// by the required mutation on it if there is one, else by a pending one.
+// With one mutation per position the set S(r) of ops in the linearization is
+// forced: m_p enters at N(p) (its own return at the latest), a read at its
+// return; extra pending mutations only add constraints, so S(r) is minimal,
+// and it grows with r.  The version-order conditions on S(r) are a
+// conjunction whose terms, once present and false, stay false (L only grows,
+// U only falls as pending ops return), so r* = the earliest time any term is
+// present and false:
+//   * hole: p needed before its mutation is called (or p has none): N(p);
+//   * CAS at p against the value at p-1, once both are in: N(p) (N rises
+//     with p);
+//   * read [V0+k x] against the value at k-1: its return;
+//   * timing: an op a with call(a) > ret(b) for some b whose U bound sits at
+//     or after a's L bound (Uh = the suffix minimum of B, with final
+//     returns: b returned before a was called, so b is in): a's entry time
+//     (N(p) for m_p, the return for a read);
+//   * a version no state reaches (below V0, or more positions than records):
+//     the op's return.
+// Two mutations on one version (a lost CAS shapes exactly that): m*, the
+// one returning first, holds the position; the other enters only as the
+// second required op of it, a violation at its return.  The rule, using m*,
+// is then exact unless at r* the position is needed with m* still pending
+// and another of its mutations already called — a real choice: the key is
+// handed over (the gap tier bisects), which is rare (tests/test_oracle.py:
+// `test_first_failure_rule_matches_search` restates the rule in
+// tests/fastpath_ref.py and checks it against knossos.linear's fail op on
+// thousands of keys, dup-version keys included; it declines ~2 %).  Prefix
+// closure makes r* the first failure: every earlier prefix is linearizable
+// by S(r) itself (the witness written here, certified independently by
+// oracle/witness.c in the GPU tests).
+//
+// Runs where the version order's tables are already in LDS and the records
+// in registers (crash-light pass / fused pass), so it costs one more pass
+// over registers and five barriers.  LDS: A is reused for the earliest
+// return of each position's mutations, B becomes its suffix minimum Uh, the
+// dynamic region holds N, Own/Val are rewritten by m*.  Returns true when the
+// key was decided (result and, if wanted, its PREFIX witness written).
+__device__ __forceinline__ void suffix_min2_excl(uint32_t &a, uint32_t &b, FastLds &s) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  uint32_t ia = a, ib = b;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t ya = (uint32_t)__shfl_down((int)ia, o), yb = (uint32_t)__shfl_down((int)ib, o);
+    if (lane + o < kWave) ia = umin(ia, ya), ib = umin(ib, yb);
+  }
+  if (lane == 0) s.wg[8 + w] = (int)ia, s.wg[12 + w] = (int)ib;
+  uint32_t ea = (uint32_t)__shfl_down((int)ia, 1), eb = (uint32_t)__shfl_down((int)ib, 1);
+  if (lane == kWave - 1) ea = eb = kNever;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kFastWaves; j++)
+    if (j > w) ea = umin(ea, (uint32_t)s.wg[8 + j]), eb = umin(eb, (uint32_t)s.wg[12 + j]);
+  a = ea;
+  b = eb;
+}
+
+__device__ bool first_failure(int64_t key, int n, const lc_op *__restrict__ kops, const FastRecs &b,
+                              const KParams &p, FastLds &s, lc_key_result *__restrict__ out,
+                              int32_t *__restrict__ wit, int32_t *__restrict__ kind) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  const int64_t base_idx = kops[0].call;
+  const int V0 = p.init_ver, init = p.init_val;
+  uint32_t *MR = s.A;                                  // earliest return of each position's mutations
+  uint32_t *NR = reinterpret_cast<uint32_t *>(lds_dyn);  // ops' returns by need, then N(p)
+  if (4 * tid < n) reinterpret_cast<uint4 *>(MR)[tid] = make_uint4(kNever, kNever, kNever, kNever);
+  if (4 * tid <= n + 1) reinterpret_cast<uint4 *>(NR)[tid] = make_uint4(kNever, kNever, kNever, kNever);
+  __syncthreads();
+  uint32_t t = kNever;  // this thread's earliest violation
+  // step 1: each position's earliest-returning mutation; returns by need
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int r = tid + u * kFastThreads;
+    if (r >= n) continue;
+    const Rec d = decode(b.w[u], base_idx);
+    if (d.f != LC_F_READ) {
+      const int pos = d.ver - V0 - 1;
+      if (pos < 0 || pos >= n) {
+        t = umin(t, d.ret);  // no state reaches this version
+      } else {
+        atomicMin(&MR[pos], d.ret);
+        atomicMin(&NR[pos + 1], d.ret);
+      }
+    } else if (d.ret != kNever && d.ver != -1) {
+      const int k = d.ver - V0;
+      if (k < 0 || k > n) t = umin(t, d.ret);
+      else if (k > 0) atomicMin(&NR[k], d.ret);
+    }
+  }
+  __syncthreads();
+  // step 2: m* claims its position; suffix minima N(p) and Uh(p) in place
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int r = tid + u * kFastThreads;
+    if (r >= n) continue;
+    const Rec d = decode(b.w[u], base_idx);
+    const int pos = d.ver - V0 - 1;
+    if (d.f != LC_F_READ && pos >= 0 && pos < n) {
+      if (d.ret == MR[pos]) {
+        s.Own[pos] = (uint16_t)r;
+        s.Val[pos] = d.val;
+      } else {
+        t = umin(t, d.ret);  // a second mutation of the version becomes required
+      }
+    }
+  }
+  uint4 nr4 = make_uint4(kNever, kNever, kNever, kNever), b4 = nr4;
+  if (4 * tid <= n + 1) nr4 = reinterpret_cast<const uint4 *>(NR)[tid];
+  if (4 * tid <= n) b4 = reinterpret_cast<const uint4 *>(s.B)[tid];
+  uint32_t na = umin(umin(nr4.x, nr4.y), umin(nr4.z, nr4.w));
+  uint32_t ba = umin(umin(b4.x, b4.y), umin(b4.z, b4.w));
+  suffix_min2_excl(na, ba, s);  // (its barrier also orders step 2's stores)
+  if (4 * tid <= n + 1) {
+    // N(p) = min NR[p+1 ..]; Uh(p) = min B[p ..]
+    const uint32_t n3 = na, n2 = umin(n3, nr4.w), n1 = umin(n2, nr4.z), n0 = umin(n1, nr4.y);
+    reinterpret_cast<uint4 *>(NR)[tid] = make_uint4(n0, n1, n2, n3);
+  }
+  if (4 * tid <= n) {
+    const uint32_t u3 = umin(ba, b4.w), u2 = umin(u3, b4.z), u1 = umin(u2, b4.y), u0 = umin(u1, b4.x);
+    reinterpret_cast<uint4 *>(s.B)[tid] = make_uint4(u0, u1, u2, u3);
+  }
+  __syncthreads();
+  // step 3: every term's activation time
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int q = 4 * tid + j;
+    if (q < n && s.Own[q] == 0xFFFF) t = umin(t, NR[q]);  // needed, never held
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int r = tid + u * kFastThreads;
+    if (r >= n) continue;
+    const Rec d = decode(b.w[u], base_idx);
+    if (d.f != LC_F_READ) {
+      const int pos = d.ver - V0 - 1;
+      if (pos < 0 || pos >= n || s.Own[pos] != r) continue;
+      const uint32_t np = NR[pos];
+      bool v = d.call > np;  // needed before it was called
+      if (d.f == LC_F_CAS) {
+        if (pos == 0) v |= d.exp != init;
+        else if (s.Own[pos - 1] != 0xFFFF) v |= d.exp != s.Val[pos - 1];
+      }
+      v |= d.call >= s.B[pos];  // called after an op bounding it from above returned
+      if (v) t = umin(t, np);
+    } else if (d.ret != kNever && d.ver != -1) {
+      const int k = d.ver - V0;
+      if (k < 0 || k > n) continue;
+      bool v = false;
+      if (d.val != -1) {
+        if (k == 0) v = d.val != init;
+        else if (s.Own[k - 1] != 0xFFFF) v = d.val != s.Val[k - 1];
+      }
+      if (k < n) v |= d.call >= s.B[k];
+      if (v) t = umin(t, d.ret);
+    }
+  }
+  const uint32_t wt = wave_min_u32(t);
+  if (lane == 0) s.wg[w] = (int)wt;
+  __syncthreads();
+  const uint4 tw = *reinterpret_cast<const uint4 *>(s.wg);
+  const uint32_t T = umin(umin(tw.x, tw.y), umin(tw.z, tw.w));
+  if (T == kNever) return false;  // (cannot happen for an invalid key: hand it over)
+  // step 4: a real choice at T (declined), and the op returning at T
+  int amb = 0, fo = 0;
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int r = tid + u * kFastThreads;
+    if (r >= n) continue;
+    const Rec d = decode(b.w[u], base_idx);
+    if (d.ret == T) fo = r + 1;
+    const int pos = d.ver - V0 - 1;
+    if (d.f != LC_F_READ && pos >= 0 && pos < n && s.Own[pos] != r)
+      amb |= (d.call < T) & (NR[pos] <= T) & (T < MR[pos]);
+  }
+  const uint32_t wfo = wave_max_u32((uint32_t)fo);
+  const bool wamb = __ballot(amb) != 0;
+  if (lane == 0) s.wg[4 + w] = (int)(wfo | (wamb ? 0x80000000u : 0u));
+  __syncthreads();
+  const int4 fw = *reinterpret_cast<const int4 *>(&s.wg[4]);
+  if ((fw.x | fw.y | fw.z | fw.w) < 0) return false;  // ambiguous: the gap tier bisects
+  const int fail = max(max(fw.x, fw.y), max(fw.z, fw.w)) - 1;
+  if (fail < 0) return false;
+  if (wit) {
+    // the prefix just before T: m* of every position needed by then
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const int r = tid + u * kFastThreads;
+      if (r >= n) continue;
+      const Rec d = decode(b.w[u], base_idx);
+      const int pos = d.ver - V0 - 1;
+      const bool in = d.f != LC_F_READ && pos >= 0 && pos < n && s.Own[pos] == r && NR[pos] < T;
+      wit[r] = in ? pos : -1;
+    }
+  }
+  if (tid == 0) {
+    out[key] = lc_key_result{LC_INVALID, LC_REASON_NONLINEARIZABLE, fail,
+                             base_idx + (int64_t)T, 0, 1};
+    if (kind) kind[key] = LC_WITNESS_PREFIX;
+  }
+  return true;
+}
+
 // Where a key the workgroup does not decide goes: the version-order tier
 // flags it for the handoff compaction; the crash-light pass (LIGHT, over the
 // compacted list) appends it to the gap tier's list.  wit / kind: lc_aux.
@@ -1956,8 +2172,11 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     if (tid == 0) fast_pass_on<MODE>(key, o, (wor >> 18) & 1);
     return;
   }
-  if constexpr (MODE == kModeLight) {  // eligible here too: the version order found it invalid
-    if (tid == 0) fast_pass_on<MODE>(key, o);
+  if constexpr (MODE == kModeLight) {
+    // eligible here too: the version order found it invalid; name its first
+    // failure in place (declined: the gap tier bisects)
+    if (!first_failure(key, n, kops, b, p, s, out, wit, o.kind) && tid == 0)
+      fast_pass_on<MODE>(key, o);
     return;
   }
   // pass 2: positions, duplicates, CAS expectations and read claims against
@@ -1987,6 +2206,8 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
   const uint32_t wbad = __ballot(bad) ? 1u : 0u;
   if (lane == 0) s.wbad[w] = wbad;
   __syncthreads();
+  // (the fused pass hands invalid keys over: the first-failure rule there
+  // costs 5 VGPRs, 72 -> 77, and a wave per SIMD on crash-heavy batches)
   if (tid == 0) {
     const uint4 wb = *reinterpret_cast<const uint4 *>(s.wbad);
     if (!(wb.x | wb.y | wb.z | wb.w))

@@ -142,6 +142,8 @@ struct Dev {
   int64_t n_hbm = 0;
   int malformed = 0;
   bool use_fused = false;  // the next call takes the fused version-order + crash-light pass
+  hipEvent_t eh0 = nullptr, eh1 = nullptr;  // around lc_check's host-to-device copies
+  lc_device_stats last{};                   // this device's share of the last lc_check
 };
 
 }  // namespace
@@ -156,6 +158,9 @@ struct lc_ctx {
   std::string err;
   std::mutex err_mu;
   lc_stats stats{};
+  // lc_host_register: caller buffers page-locked for this context's devices
+  std::vector<std::pair<const char *, uint64_t>> pinned;
+  std::mutex pin_mu;
 };
 
 namespace {
@@ -212,6 +217,15 @@ int opts_to_params(lc_ctx *c, const lc_opts *o, lcdev::KParams *p) {
     p->time_ticks = (uint64_t)o->time_budget_ms * (uint64_t)khz;
   }
   return 0;
+}
+
+// Is [p, p + n) inside a buffer registered with lc_host_register?
+bool is_pinned(lc_ctx *c, const void *p, size_t n) {
+  std::lock_guard<std::mutex> g(c->pin_mu);
+  const char *q = static_cast<const char *>(p);
+  for (const auto &pr : c->pinned)
+    if (q >= pr.first && q + n <= pr.first + pr.second) return true;
+  return false;
 }
 
 // Device-side lc_aux outputs of one run_device call (null: not wanted).
@@ -738,6 +752,8 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
           hipEventCreateWithFlags(&d.ef, kEventFlags) != hipSuccess ||
           hipEventCreateWithFlags(&d.eg, kEventFlags) != hipSuccess ||
           hipEventCreateWithFlags(&d.el, kEventFlags) != hipSuccess ||
+          hipEventCreateWithFlags(&d.eh0, kEventFlags) != hipSuccess ||
+          hipEventCreateWithFlags(&d.eh1, kEventFlags) != hipSuccess ||
           hipMalloc(reinterpret_cast<void **>(&d.d_status), sizeof(lcdev::KStatus)) != hipSuccess ||
           hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess ||
           hipHostMalloc(reinterpret_cast<void **>(&d.h_handoff), sizeof(int32_t),
@@ -763,6 +779,7 @@ void lc_close(lc_ctx *c) {
   if (!c) return;
   for (auto &f : c->fxs) lc_fx_close(f.first);
   if (c->fx_all) lc_fx_close(c->fx_all);
+  for (auto &pr : c->pinned) (void)hipHostUnregister(const_cast<char *>(pr.first));
   for (Dev &d : c->devs) {
     (void)hipSetDevice(d.id);
     if (d.stream) (void)hipStreamSynchronize(d.stream);
@@ -787,6 +804,8 @@ void lc_close(lc_ctx *c) {
     if (d.d_wit) (void)hipFree(d.d_wit);
     if (d.d_kind) (void)hipFree(d.d_kind);
     if (d.eg) (void)hipEventDestroy(d.eg);
+    if (d.eh0) (void)hipEventDestroy(d.eh0);
+    if (d.eh1) (void)hipEventDestroy(d.eh1);
     if (d.el) (void)hipEventDestroy(d.el);
     if (d.d_gap2) (void)hipFree(d.d_gap2);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -800,6 +819,44 @@ int lc_last_stats(lc_ctx *c, lc_stats *out) {
   if (!c || !out) return -EINVAL;
   *out = c->stats;
   return 0;
+}
+
+int lc_last_device_stats(lc_ctx *c, int32_t i, lc_device_stats *out) {
+  if (!c || !out || i < 0 || i >= (int32_t)c->devs.size()) return -EINVAL;
+  *out = c->devs[(size_t)i].last;
+  return 0;
+}
+
+int lc_host_register(lc_ctx *c, const void *ptr, uint64_t bytes) {
+  if (!c || !ptr || !bytes) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->pin_mu);
+  // portable: page-locked for every device of the process (the fan-out's
+  // threads copy from it to each GPU of the context)
+  const hipError_t e = hipHostRegister(const_cast<void *>(ptr), (size_t)bytes,
+                                       hipHostRegisterPortable);
+  if (e != hipSuccess) {
+    set_err(c, std::string("hipHostRegister: ") + hipGetErrorString(e));
+    return -EIO;
+  }
+  c->pinned.emplace_back(static_cast<const char *>(ptr), bytes);
+  return 0;
+}
+
+int lc_host_unregister(lc_ctx *c, const void *ptr) {
+  if (!c || !ptr) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->pin_mu);
+  for (size_t i = 0; i < c->pinned.size(); i++)
+    if (c->pinned[i].first == ptr) {
+      const hipError_t e = hipHostUnregister(const_cast<void *>(ptr));
+      c->pinned.erase(c->pinned.begin() + (long)i);
+      if (e != hipSuccess) {
+        set_err(c, std::string("hipHostUnregister: ") + hipGetErrorString(e));
+        return -EIO;
+      }
+      return 0;
+    }
+  set_err(c, "lc_host_unregister: pointer not registered with this context");
+  return -EINVAL;
 }
 
 // Per-key device cost in record-scan units.  The tier a key
@@ -911,6 +968,12 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
     Dev &d = c->devs[di];
     const int64_t a = bounds[di], b = bounds[di + 1];
     const int64_t nk = b - a;
+    const auto tw = std::chrono::steady_clock::now();
+    d.last = lc_device_stats{};
+    d.last.device = d.id;
+    d.last.key_begin = a;
+    d.last.key_end = b;
+    d.kernel_ms = 0;
     if (nk <= 0) return;
     if (hipSetDevice(d.id) != hipSuccess) {
       rcs[di] = -EIO;
@@ -928,13 +991,16 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
       rcs[di] = r;
       return;
     }
-    hipError_t e = hipSuccess;
-    if (ops_bytes)
+    hipError_t e = hipEventRecord(d.eh0, d.stream);
+    if (e == hipSuccess && ops_bytes)
       e = hipMemcpyAsync(d.d_ops, ops + r0, ops_bytes, hipMemcpyHostToDevice,
                          d.stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(d.d_off, key_off + a, sizeof(int64_t) * (size_t)(nk + 1),
                          hipMemcpyHostToDevice, d.stream);
+    if (e == hipSuccess) e = hipEventRecord(d.eh1, d.stream);
+    d.last.h2d_bytes = (int64_t)(ops_bytes + sizeof(int64_t) * (size_t)(nk + 1));
+    d.last.pinned = is_pinned(c, ops + r0, ops_bytes);
     if (e != hipSuccess) {
       set_err(c, std::string("hipMemcpyAsync H2D: ") + hipGetErrorString(e));
       rcs[di] = -EIO;
@@ -964,7 +1030,13 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
     if (e != hipSuccess) {
       set_err(c, std::string("hipMemcpyAsync D2H: ") + hipGetErrorString(e));
       rcs[di] = -EIO;
+      return;
     }
+    float hms = 0;
+    if (hipEventElapsedTime(&hms, d.eh0, d.eh1) == hipSuccess) d.last.h2d_ms = hms;
+    d.last.kernel_ms = d.kernel_ms;
+    d.last.total_ms = std::chrono::duration<double, std::milli>(
+                          std::chrono::steady_clock::now() - tw).count();
   };
   if (nd == 1) {
     work(0);

@@ -163,3 +163,18 @@ def random_casreg(rng, n_ops, p_info=0.2, p_perturb=0.35, n_values=3):
     for r in out:
         r[3] = N
     return out
+
+
+def dup_versions(keys, seed, frac=0.5):
+    """Copies of keys with one :ok mutation's version given to another
+    mutation (two mutations claiming one version: the lost-CAS shape)."""
+    rng = random.Random(seed)
+    out = []
+    for recs in keys:
+        muts = [i for i, r in enumerate(recs) if r[0] != 0 and r[3] != -1 and r[5] != INF]
+        if len(muts) >= 2 and rng.random() < frac:
+            recs = [list(r) for r in recs]
+            a, b = rng.sample(muts, 2)
+            recs[b][3] = recs[a][3]
+        out.append(recs)
+    return out

@@ -109,6 +109,31 @@ def test_counterexamples_are_minimal_nonlinearizable_prefixes(ctx):
     assert (b["verdict"] == 1).all()
 
 
+@pytest.mark.parametrize("conc,seed,dup", [(10, 0x5EED0005, False), (6, 51, True),
+                                           (20, 52, True), (10, 53, False)])
+def test_first_failure_rule_vs_oracle(ctx, conc, seed, dup):
+    """Invalid version-pinned keys get their fail op from the first-failure
+    rule in the crash-light pass (check_kernel.hip, `first_failure`), not a
+    bisection: verdict, fail op and prefix end equal knossos.linear's on
+    every key, and every PREFIX witness the rule writes certifies
+    (oracle/witness.c).  Keys with two mutations on one version (lost CAS;
+    `dup`: one more such pair per key) are decided exactly or declined to the
+    gap tier, which bisects — the same answers either way."""
+    from helpers import dup_versions
+    ops, off, _, _ = abi.synth(600, 200, concurrency=conc, p_anomaly=0.6, seed=seed)
+    if dup:
+        ops, off = pack_keys(dup_versions([ops[off[k]:off[k + 1]].tolist()
+                                           for k in range(600)], seed, frac=0.7))
+    _, g, wit, kind = ctx.check(ops, off, witness=True)
+    _, j = oracle.check(ops, off, algo=oracle.JITC, n_threads=8)
+    assert (g["verdict"] == 0).sum() > 200
+    for f in ("verdict", "fail_op", "fail_prefix_end"):
+        assert (g[f] == j[f]).all(), f
+    st, _ = oracle.check_witness(ops, off, wit, kind, results=g)
+    assert (kind[g["verdict"] == 0] == abi.LC_WITNESS_PREFIX).all()
+    assert (st[kind != abi.LC_WITNESS_NONE] == oracle.WIT_OK).all()
+
+
 def test_c2_full_size_properties(ctx):
     """BASELINE configs[1] at full size: 10k keys x 1k ops, concurrency 20.
     Valid by construction; a 300-key sample matches the oracle."""
@@ -485,6 +510,24 @@ def test_check_device_path_with_torch(ctx):
     assert (r2 == r).all()
 
 
+def _assert_configs_in_frontier(lin, kops, done, vals, k):
+    """An invalid key's knossos :configs (at most 10) are configurations of
+    the oracle's JITC frontier just before the failing return — state and
+    pending ops — and its final paths end inconsistent."""
+    fo = next(j for j, d in enumerate(done)
+              if (d["completion"] or d["invoke"])["index"] == lin["op"]["index"])
+    want, n_want = oracle.frontier(kops, fo)
+    assert 1 <= len(lin["configs"]) <= min(10, n_want), k
+    for cfg in lin["configs"]:
+        val = cfg["model"]["value"]
+        vid = -1 if val is None else vals.index(val)
+        pend = tuple(sorted(next(j for j, d in enumerate(done)
+                                 if d["invoke"]["index"] == inv["index"])
+                            for inv in cfg["pending"]))
+        assert (cfg["model"]["version"], vid, pend) in want, (k, cfg)
+    assert all("inconsistent" in p[-1]["model"] for p in lin["final-paths"])
+
+
 def test_register_checker_frontier_configs():
     """knossos's :configs for keys the frontier search decides: a history
     whose :ok completions carry no versions ([nil v], which the
@@ -509,19 +552,7 @@ def test_register_checker_frontier_configs():
         lin = res["results"][k]["linear"]
         if lin["valid?"] is not False:
             continue
-        kops = ops[off[i]:off[i + 1]]
-        fo = next(j for j, d in enumerate(done[i])
-                  if (d["completion"] or d["invoke"])["index"] == lin["op"]["index"])
-        want, n_want = oracle.frontier(kops, fo)
-        assert 1 <= len(lin["configs"]) <= min(10, n_want)
-        for cfg in lin["configs"]:
-            val = cfg["model"]["value"]
-            vid = -1 if val is None else vals[i].index(val)
-            pend = tuple(sorted(next(j for j, d in enumerate(done[i])
-                                     if d["invoke"]["index"] == inv["index"])
-                                for inv in cfg["pending"]))
-            assert (cfg["model"]["version"], vid, pend) in want, (k, cfg)
-        assert all("inconsistent" in p[-1]["model"] for p in lin["final-paths"])
+        _assert_configs_in_frontier(lin, ops[off[i]:off[i + 1]], done[i], vals[i], k)
         n_checked += 1
     assert n_checked >= 5
 
@@ -534,7 +565,8 @@ def test_register_checker_end_to_end(tmp_path):
     res = chk.check({"name": "etcd register"}, hist, {})
     chk.close()
     from jepsen.etcd_amd import history as H
-    _, ops, off, _ = H.pack(hist)
+    vals = []
+    _, ops, off, done = H.pack(hist, values_out=vals)
     _, ref = oracle.check(ops, off, algo=oracle.JITC)
     bad = sorted(int(k) for k in np.nonzero(ref["verdict"] == 0)[0])
     assert set(k for k, l in enumerate(labels) if l == 1) <= set(bad)
@@ -543,11 +575,13 @@ def test_register_checker_end_to_end(tmp_path):
     for k in bad:
         r = res["results"][k]
         assert r["valid?"] is False and r["linear"]["op"]["type"] == "ok"
-        # knossos's diagnostics, from the prefix witness (diagnostics.py)
+        # knossos's diagnostics: :configs from the frontier re-search (keys
+        # with at most FRONTIER_MAX_CRASHED crashed ops: every key here),
+        # :last-op from the prefix witness (diagnostics.py)
         lin = r["linear"]
         assert lin["previous-ok"]["index"] < lin["fail-prefix-end"]
-        assert lin["configs"] and lin["last-op"] == lin["configs"][0]["last-op"]
-        assert all("inconsistent" in p[-1]["model"] for p in lin["final-paths"])
+        assert "configs-error" not in lin and "last-op" in lin
+        _assert_configs_in_frontier(lin, ops[off[k]:off[k + 1]], done[k], vals[k], k)
         page = open(r["timeline"]["file"]).read()  # independent/<k>/timeline.html
         assert 'cex"' in page and os.path.dirname(r["timeline"]["file"]).endswith("/%d" % k)
         svg = open(lin["linear-svg"]).read()  # independent/<k>/linear.svg

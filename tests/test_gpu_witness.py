@@ -169,6 +169,36 @@ def test_virtual_devices_fan_out_equals_one_device(ctx, monkeypatch):
     assert bounds[1] < 1000  # the clustered heavy keys are spread by cost
 
 
+def test_c2_fan_out_over_8_devices(ctx, monkeypatch):
+    """BASELINE configs[2] (C3) the way the drop-in runs it: one lc_ctx over
+    8 devices (here 8 device contexts on one GPU, LC_VIRTUAL_DEVICES), the
+    whole C2 batch (10k keys x 1k ops) from host buffers through lc_check's
+    in-process fan-out.  Every result field equals the one-device call; the
+    per-device stats cover the keys in 8 contiguous cost-balanced ranges;
+    with the caller's buffer page-locked (lc_host_register) the results are
+    the same and every device reports pinned copies."""
+    ops, off, _, _ = abi.synth(10000, 1000, concurrency=20, seed=0x5EED0002)
+    _, a = ctx.check(ops, off)
+    monkeypatch.setenv("LC_VIRTUAL_DEVICES", "8")
+    with abi.Context(device_mask=1) as c8:
+        _, b = c8.check(ops, off)
+        assert c8.stats()["n_devices"] == 8
+        ds = c8.device_stats()
+        c8.host_register(ops)
+        try:
+            _, c = c8.check(ops, off)
+            dp = c8.device_stats()
+        finally:
+            c8.host_unregister(ops)
+    assert (a == b).all() and (a == c).all() and (a["verdict"] == 1).all()
+    bounds = abi.plan_partition(off, 8, ops=ops)
+    assert [(d["key_begin"], d["key_end"]) for d in ds] == \
+        [(int(bounds[i]), int(bounds[i + 1])) for i in range(8)]
+    assert sum(d["h2d_bytes"] for d in ds) == ops.nbytes + 8 * 8 + 8 * 10000
+    assert all(d["pinned"] == 0 for d in ds) and all(d["pinned"] == 1 for d in dp)
+    assert all(d["h2d_ms"] > 0 and d["kernel_ms"] > 0 for d in ds + dp)
+
+
 def test_malformed_key_is_unknown_alone(ctx):
     """One malformed key no longer fails the call: it is :unknown with reason
     malformed (jepsen.independent would lose only that key), and the other

@@ -23,6 +23,7 @@ def test_library_exports_every_declared_symbol():
         names += re.findall(r"^\s*(?:const\s+)?\w+\s+\**(lc_\w+)\s*\(", src, re.M)
     assert set(names) == {
         "lc_open", "lc_check", "lc_check_device", "lc_last_stats", "lc_last_error",
+        "lc_last_device_stats", "lc_host_register", "lc_host_unregister",
         "lc_close", "lc_default_opts", "lc_plan_partition", "lc_abi_version",
         "lc_check_ex", "lc_check_device_ex", "lc_key_cost", "lc_build_id",
         "lc_synth_register", "lc_synth_key", "lc_edn_parse", "lc_edn_n_keys", "lc_edn_n_ops",
@@ -41,6 +42,7 @@ def test_struct_sizes():
     assert ctypes.sizeof(abi.LcSynthParams) == 56
     assert ctypes.sizeof(abi.LcStats) == 104
     assert ctypes.sizeof(abi.LcAux) == 16
+    assert ctypes.sizeof(abi.LcDeviceStats) == 56
     from jepsen.etcd_amd import fx
     assert ctypes.sizeof(fx.LcFxParams) == 40
     assert ctypes.sizeof(fx.LcFxTransport) == 40

@@ -8,7 +8,7 @@ import pytest
 
 import oracle
 from oracle import brute
-from helpers import load_kats, pack_keys, tiny_batch, INF
+from helpers import dup_versions, load_kats, pack_keys, tiny_batch, INF
 from jepsen.etcd_amd import abi
 
 KATS = load_kats()
@@ -153,6 +153,47 @@ def test_version_order_decision_matches_search():
     for k in KATS:
         d = fastpath_ref.decide([tuple(r) for r in k["ops"]])
         assert d is None or d == (1 if k["valid"] else 0), k["name"]
+
+
+def test_first_failure_rule_matches_search():
+    """The GPU's O(n) first-failure rule (restated in fastpath_ref.py) names
+    the same fail op as knossos.linear's frontier on every invalid key it
+    decides, and its prefix witness certifies; where two mutations claim one
+    version it either decides exactly or declines.  Random tiny keys,
+    synthetic keys with injected stale reads / lost CAS (C5's shapes) at
+    several concurrencies, and the same keys with versions duplicated."""
+    import fastpath_ref
+    sets = [tiny_batch(777, 3000, max_ops=8)]
+    for (nk, n, conc, pa, seed) in [(300, 120, 6, 1.0, 11), (300, 200, 10, 1.0, 12),
+                                    (200, 300, 20, 1.0, 13), (200, 200, 10, 0.3, 14)]:
+        ops, off, _, _ = abi.synth(nk, n, concurrency=conc, p_anomaly=pa, seed=seed)
+        sets.append([ops[off[k]:off[k + 1]].tolist() for k in range(nk)])
+    sets.append(dup_versions(sets[1], 21))
+    sets.append(dup_versions(sets[2] + sets[3], 22, frac=1.0))
+    decided = declined = 0
+    for ks in sets:
+        ops, off = pack_keys(ks)
+        _, j = oracle.check(ops, off, algo=oracle.JITC, n_threads=4)
+        wit = np.full(len(ops), -1, dtype=np.int32)
+        kind = np.zeros(len(ks), dtype=np.int32)
+        res = np.zeros(len(ks), dtype=oracle.RESULT_DTYPE)
+        res["fail_prefix_end"] = 0
+        for i, recs in enumerate(ks):
+            t = [tuple(r) for r in recs]
+            if fastpath_ref.decide(t) != 0:
+                continue
+            ff = fastpath_ref.first_failure(t)
+            if ff is None:
+                declined += 1
+                continue
+            decided += 1
+            assert j["verdict"][i] == 0 and ff[0] == j["fail_op"][i], (recs, ff, j["fail_op"][i])
+            wit[off[i]:off[i + 1]] = ff[1]
+            kind[i] = 2
+            res["fail_prefix_end"][i] = recs[ff[0]][5]
+        st, _ = oracle.check_witness(ops, off, wit, kind, results=res)
+        assert (st[kind == 2] == oracle.WIT_OK).all()
+    assert decided > 1500 and declined < decided // 10, (decided, declined)
 
 
 @pytest.mark.parametrize("conc,seed", [(6, 3), (10, 5), (14, 8)])
