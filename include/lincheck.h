@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 2
+#define LC_ABI_VERSION 3  /* 3: lc_aux certificates, lc_device_stats, lc_host_register */
 
 /* Op kinds: the three :f values of register.clj:98-100 (r / w / cas). */
 #define LC_F_READ  0
@@ -176,11 +176,56 @@ typedef struct lc_stats {
 typedef struct lc_aux {
   int32_t *witness;
   int32_t *witness_kind;
+  int32_t *certificate;      /* ABI 3: 4 int32 per key, or NULL (needs witness_kind) */
+  int32_t *certificate_set;  /* ABI 3: one int32 per record, indexed like ops, or NULL */
 } lc_aux;
 
 #define LC_WITNESS_NONE   0  /* no witness: decided by a search tier, or :unknown */
 #define LC_WITNESS_FULL   1  /* valid key: a linearization of the whole history */
 #define LC_WITNESS_PREFIX 2  /* invalid key: a linearization of the prefix just before the failing return */
+
+/*
+ * Infeasibility certificates (ABI 3).  The PREFIX witness shows that the
+ * prefix just before an invalid key's failing return is linearizable; the
+ * certificate shows that the prefix AT it is not, so together they certify
+ * fail_op as the first failure (linearizability is prefix-closed).  For every
+ * LC_INVALID key, certificate[4k .. 4k+3] = {kind, a, b, c}, a / b record
+ * indices within the key.  The prefix P: records called at or before
+ * fail_prefix_end; "required" = returned at or before it (the others pending,
+ * free to be left out).  Mutation = write or CAS; its position = version -
+ * init_version - 1.  Each kind names facts that no linearization of P can
+ * satisfy together (register.clj:60-96 steps the version by one per
+ * mutation, checks CAS expectations :77 and read claims :84-96):
+ *   LC_CERT_DUP      a, b: two required mutations with the same version.
+ *   LC_CERT_UNREACH  a: a required op whose version no linearization of P
+ *                    reaches (a mutation at a version <= init_version, or
+ *                    either kind beyond the number of mutations in P), or a
+ *                    read of init_version whose value is not the initial one.
+ *   LC_CERT_CLAIMS   a, b: two required reads of one version, different values.
+ *   LC_CERT_PAIR     c = q: b consumes the value at position q-1 (a CAS
+ *                    holding q: its expectation; a read of version init+q:
+ *                    its value) and a holds position q-1 (a = -1: q = 0, the
+ *                    initial value) with a different value; each of a, b is
+ *                    required (and pinned there), or the only op of P that
+ *                    can hold its (needed) position.
+ *   LC_CERT_ORDER    a, b required: b returned before a was called, yet the
+ *                    version order puts a's point before b's (a's lower-bound
+ *                    index <= b's upper-bound index).
+ *   LC_CERT_HALL     c positions, listed in certificate_set[key's first c
+ *                    records]: each needed by a required op and held by none,
+ *                    and fewer ops of P can hold any of them than c (Hall's
+ *                    condition fails for the gap matching).
+ * LC_CERT_NONE: no certificate (valid or :unknown keys, keys only a search
+ * decided where none of these applies).  oracle/witness.c checks them from
+ * the records alone (tests/).
+ */
+#define LC_CERT_NONE    0
+#define LC_CERT_DUP     1
+#define LC_CERT_UNREACH 2
+#define LC_CERT_CLAIMS  3
+#define LC_CERT_PAIR    4
+#define LC_CERT_ORDER   5
+#define LC_CERT_HALL    6
 
 typedef struct lc_ctx lc_ctx;
 

@@ -41,6 +41,8 @@ LC_FLAG_NO_FAST_PATH = 2
 LC_FLAG_NO_GAP_TIER = 4
 LC_FLAG_WHOLE_GPU = 8
 LC_WITNESS_NONE, LC_WITNESS_FULL, LC_WITNESS_PREFIX = 0, 1, 2
+LC_CERT_NONE, LC_CERT_DUP, LC_CERT_UNREACH, LC_CERT_CLAIMS, LC_CERT_PAIR, LC_CERT_ORDER, \
+    LC_CERT_HALL = range(7)
 
 # lc_op: 6 x int64 (f, value, expected, version, call, ret); arrays are (n, 6).
 OP_FIELDS = ("f", "value", "expected", "version", "call", "ret")
@@ -76,7 +78,8 @@ class LcDeviceStats(ctypes.Structure):
 
 
 class LcAux(ctypes.Structure):
-    _fields_ = [("witness", ctypes.c_void_p), ("witness_kind", ctypes.c_void_p)]
+    _fields_ = [("witness", ctypes.c_void_p), ("witness_kind", ctypes.c_void_p),
+                ("certificate", ctypes.c_void_p), ("certificate_set", ctypes.c_void_p)]
 
 
 class LcSynthParams(ctypes.Structure):
@@ -255,19 +258,28 @@ class Context:
         if rc != 0:
             raise LcError(rc, self.last_error())
 
-    def check(self, ops, key_off, opts=None, raise_on_error=True, witness=False):
+    def check(self, ops, key_off, opts=None, raise_on_error=True, witness=False,
+              certificate=False):
         """Host-buffer check. Returns (rc, results structured array), or with
         witness=True (rc, results, witness per record, witness kind per key)
-        from lc_check_ex (include/lincheck.h, lc_aux)."""
+        from lc_check_ex (include/lincheck.h, lc_aux); certificate=True adds
+        the infeasibility certificates (int32[n_keys, 4]) and their position
+        sets (int32 per record): (rc, results, witness, kind, cert, cert_set)."""
         ops = as_ops(ops)
         key_off = np.ascontiguousarray(key_off, dtype=np.int64)
         n_keys = len(key_off) - 1
         out = np.zeros(max(n_keys, 0), dtype=RESULT_DTYPE)
         o = opts if opts is not None else default_opts()
-        if witness:
+        if witness or certificate:
             wit = np.full(len(ops), -3, dtype=np.int32)
             kind = np.full(max(n_keys, 0), -3, dtype=np.int32)
-            aux = LcAux(wit.ctypes.data, kind.ctypes.data)
+            cert = cset = None
+            if certificate:
+                cert = np.full((max(n_keys, 0), 4), -3, dtype=np.int32)
+                cset = np.zeros(len(ops), dtype=np.int32)
+            aux = LcAux(wit.ctypes.data, kind.ctypes.data,
+                        cert.ctypes.data if certificate else None,
+                        cset.ctypes.data if certificate else None)
             rc = lib().lc_check_ex(self._h, _ptr(ops), _ptr(key_off), n_keys,
                                    ctypes.byref(o), _ptr(out), ctypes.byref(aux))
         else:
@@ -275,6 +287,8 @@ class Context:
                                 ctypes.byref(o), _ptr(out))
         if rc != 0 and raise_on_error:
             raise LcError(rc, self.last_error())
+        if certificate:
+            return rc, out, wit, kind, cert, cset
         return (rc, out, wit, kind) if witness else (rc, out)
 
     def check_device(self, d_ops, d_key_off, n_keys, d_out, stream=None, opts=None,
@@ -286,7 +300,7 @@ class Context:
                 ctypes.byref(o), ctypes.c_void_p(d_out),
                 ctypes.c_void_p(stream) if stream else None)
         if d_witness is not None:
-            aux = LcAux(d_witness, d_witness_kind)
+            aux = LcAux(d_witness, d_witness_kind, None, None)
             rc = lib().lc_check_device_ex(*args, ctypes.byref(aux))
         else:
             rc = lib().lc_check_device(*args)

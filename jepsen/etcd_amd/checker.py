@@ -42,6 +42,7 @@ UNKNOWN = "unknown"
 # from a frontier re-search when they have at most this many crashed ops (the
 # frontier of a version-pinned key grows with its crashed ops only)
 FRONTIER_MAX_CRASHED = 16
+CERT_KINDS = {0: "none", 1: "dup", 2: "unreach", 3: "claims", 4: "pair", 5: "order", 6: "hall"}
 
 
 class VersionedRegister:
@@ -143,7 +144,8 @@ class RegisterChecker:
         o = abi.default_opts(self.max_configs_per_key, m.version, init,
                              flags=abi.LC_FLAG_WHOLE_GPU if self.whole_gpu else 0,
                              time_budget_ms=self.time_budget_ms)
-        _, res, wit, kind = self._context().check(ops, key_off, o, witness=True)
+        _, res, wit, kind, cert, cset = self._context().check(ops, key_off, o, witness=True,
+                                                              certificate=True)
         results = {}
         n_frontier = 0  # frontier re-searches run for diagnostics in this call
         for i, k in enumerate(keys):
@@ -156,6 +158,16 @@ class RegisterChecker:
                 d = done[i][int(r["fail_op"])]
                 out["op"] = d["completion"] or d["invoke"]
                 out["fail-prefix-end"] = int(r["fail_prefix_end"])
+                # why the prefix at the failing return has no linearization
+                # (include/lincheck.h LC_CERT_*; checkable from the records)
+                ck = CERT_KINDS.get(int(cert[i][0]), "none")
+                out["certificate"] = {"kind": ck}
+                if ck in ("dup", "unreach", "claims", "pair", "order"):
+                    out["certificate"]["ops"] = [done[i][int(x)]["completion"] or done[i][int(x)]["invoke"]
+                                                 for x in cert[i][1:3] if x >= 0]
+                elif ck == "hall":
+                    out["certificate"]["positions"] = [
+                        int(x) for x in cset[key_off[i]:key_off[i] + int(cert[i][3])]]
                 recs = ops[key_off[i]:key_off[i + 1]]
                 witnessed = m.name == "versioned-register" and kind[i] == abi.LC_WITNESS_PREFIX
                 # knossos's :configs are its search's frontier just before the

@@ -307,6 +307,8 @@
                  (final-paths done fail-op
                               (for [[ver x pending] configs] [(ref-model ver x) nil pending]))))))))
 
+(def ^:private cert-kinds {0 :none 1 :dup 2 :unreach 3 :claims 4 :pair 5 :order 6 :hall})
+
 ;; invalid keys the version-order / gap tiers decided get :configs from a
 ;; frontier re-search when they have at most this many crashed ops, up to
 ;; frontier-max-keys such re-searches per check (checker.py: the same)
@@ -332,7 +334,10 @@
         out  (Memory. (* result-bytes nk))
         wit  (Memory. (max 4 (* 4 n)))
         kind (Memory. (max 4 (* 4 nk)))
-        aux  (doto (Memory. 16) (.setPointer 0 wit) (.setPointer 8 kind))
+        cert (Memory. (max 16 (* 16 nk)))       ; lc_aux certificates (ABI 3): 4 int32 per key
+        cset (Memory. (max 4 (* 4 n)))
+        aux  (doto (Memory. 32) (.setPointer 0 wit) (.setPointer 8 kind)
+               (.setPointer 16 cert) (.setPointer 24 cset))
         o    (doto (Memory. 40)
                (.setLong 0 0) (.setLong 8 (if (= model :mutex) 0 LC_NIL))
                (.setLong 16 max-configs-per-key)
@@ -362,7 +367,19 @@
                         :analyzer :mi355x
                         :configs-explored (.getLong out (+ b 24))}
                  (false? v)     (merge {:op (op-map (nth d fail-op))
-                                        :previous-ok (previous-ok d fail-at)}
+                                        :previous-ok (previous-ok d fail-at)
+                                        ;; why the prefix at the failing return has no
+                                        ;; linearization (include/lincheck.h LC_CERT_*)
+                                        :certificate
+                                        (let [c (.getIntArray cert (* 16 ki) 4)
+                                              kd (get cert-kinds (aget c 0) :none)
+                                              rec #(when (>= % 0) (op-map (nth d %)))]
+                                          (cond-> {:kind kd}
+                                            (#{:dup :unreach :claims :pair :order} kd)
+                                            (assoc :ops (vec (keep rec [(aget c 1) (aget c 2)])))
+                                            (= kd :hall)
+                                            (assoc :positions
+                                                   (vec (.getIntArray cset (* 4 k0) (aget c 3))))))}
                                        (let [wa (when witness
                                                   (witness-analysis d fail-op fail-at witness
                                                                     [0 nil]))

@@ -1,0 +1,349 @@
+// cert.hip — infeasibility certificates for invalid keys (lc_aux
+// certificate / certificate_set, include/lincheck.h, ABI 3).
+//
+// An invalid key's PREFIX witness shows that the history prefix just before
+// its failing return is linearizable; the certificate written here names
+// facts that rule out every linearization of the prefix AT the failing
+// return, so the pair certifies the fail op as the first failure (prefix
+// closure).  oracle/cert.c checks the facts from the records alone.
+//
+// The facts are those of the version order (register.clj:60-96): a mutation
+// claiming version v holds position v-V0-1 in every linearization, a read of
+// version v reads the value written at v-V0-1, a CAS expects the value
+// before it, and real time orders the points.  In the prefix P at the
+// failing return, in order of the search:
+//   UNREACH  a required op claims a version P cannot reach;
+//   DUP      two required mutations claim one version;
+//   CLAIMS   two required reads of one version read different values;
+//   PAIR     a required CAS / read against the required mutation before it;
+//   ORDER    the version order puts a's point before b's, yet b returned
+//            before a was called (L_j > Uh_j, the gap tier's fixed check);
+//   HALL     a needed position no required op holds that no op of P can
+//            hold (its candidates: mutations of P pinned to it or to none,
+//            called before its deadline, writing the value its successors
+//            need, expecting the value before it where P fixes that);
+//   PAIR     two needed positions whose only candidates disagree on the
+//            value between them (a CAS expecting another value);
+//   HALL     the needed open positions together outnumber their candidates.
+// The first five are the gap tier's fixed checks (gap_tier.hip,
+// gap_setup); the last three its matching's infeasibility at the root.  A
+// failure that only the matching's branching finds (a free value chosen
+// wrong) gets no certificate (LC_CERT_NONE) — none has been seen at a
+// failing prefix of the test batches, where the returning op itself
+// completes a fixed contradiction (tests/test_cert.py restates this search
+// in tests/cert_ref.py and checks it on the oracle's own failing prefixes).
+//
+// One 256-thread workgroup per key of the call (those not invalid leave at
+// once); its arrays live in a workspace of 6 int32 per (record + 2) of the
+// batch.  Only run when the caller asks for certificates: this is a
+// diagnostics pass, not on any timed path.
+#include <climits>
+
+#include "kernels.h"
+#include "records.h"
+#include "wave.h"
+
+namespace lcdev {
+namespace {
+
+constexpr int kCertThreads = 256;
+constexpr int kCertArrays = 6;
+constexpr int kFree = INT_MIN;  // no value fixed
+
+struct CertSh {
+  int n_mut, m_need, n_gap, n_cand;
+  unsigned long long best;  // a stage's lowest (a+1, b+1) pair found
+  int pos;                  // a stage's lowest position found
+  int ra, rb;               // ORDER: the two records
+  int wmin[kCertThreads / kWave];
+};
+
+__device__ __forceinline__ void cert_write(int32_t *c, int kind, int a, int b, int x) {
+  c[0] = kind;
+  c[1] = a;
+  c[2] = b;
+  c[3] = x;
+}
+
+__global__ __launch_bounds__(kCertThreads) void cert_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off, const KParams p,
+    const lc_key_result *__restrict__ res, int32_t *__restrict__ ws, int64_t ws_stride,
+    int32_t *__restrict__ cert, int32_t *__restrict__ cset) {
+  __shared__ CertSh sh;
+  const int64_t key = blockIdx.x;
+  const int tid = threadIdx.x;
+  int32_t *c = cert + 4 * key;
+  if (res[key].verdict != LC_INVALID) {
+    if (tid == 0) cert_write(c, LC_CERT_NONE, -1, -1, 0);
+    return;
+  }
+  const int64_t beg = key_off[key], end = key_off[key + 1];
+  const int64_t rb = beg - key_off[0];
+  const int n = (int)(end - beg);
+  const lc_op *kops = ops + rb;
+  int32_t *ks = cset + rb;
+  const int64_t base = n > 0 ? kops[0].call : 0;
+  const int64_t cut64 = res[key].fail_prefix_end - base;
+  const uint32_t cut = cut64 < 0 ? 0u : cut64 >= (int64_t)kNever ? kNever - 1 : (uint32_t)cut64;
+  const int V0 = p.init_ver, init = p.init_val;
+  // this key's arrays, positions 0..n+1 (ws_stride int32 per array)
+  const int64_t off = rb + 2 * key;
+  int *held_rec = ws + off;                  // lowest required mutation pinned at k
+  int *held_cnt = ws + ws_stride + off;      // how many; for an open position: its one candidate
+  int *claim_rec = ws + 2 * ws_stride + off; // lowest required read of version V0+k with a value
+  uint32_t *lo_call = reinterpret_cast<uint32_t *>(ws + 3 * ws_stride + off);  // max call + 1; then marks
+  uint32_t *uh = reinterpret_cast<uint32_t *>(ws + 4 * ws_stride + off);       // min ret; suffix minimum
+  int *cnt = ws + 5 * ws_stride + off;       // open positions: candidate count
+  for (int k = tid; k <= n + 1; k += kCertThreads) {
+    held_rec[k] = INT_MAX;
+    held_cnt[k] = 0;
+    claim_rec[k] = INT_MAX;
+    lo_call[k] = 0;
+    uh[k] = kNever;
+    cnt[k] = -1;
+  }
+  if (tid == 0) {
+    sh.n_mut = sh.m_need = sh.n_gap = sh.n_cand = 0;
+    sh.best = ~0ull;
+    sh.pos = sh.ra = sh.rb = INT_MAX;
+    cert_write(c, LC_CERT_NONE, -1, -1, 0);
+  }
+  __syncthreads();
+  auto rec = [&](int r) { return decode(load_raw(kops, r, n), base); };
+  auto in_p = [&](const Rec &d) { return d.call <= cut; };
+  auto req = [&](const Rec &d) { return d.call <= cut && d.ret <= cut; };
+  auto is_mut = [](const Rec &d) { return d.f == LC_F_WRITE || d.f == LC_F_CAS; };
+  auto found = [&](int a, int b) {
+    atomicMin(&sh.best, ((unsigned long long)(uint32_t)(a + 1) << 32) | (uint32_t)(b + 1));
+  };
+  // a stage's lowest find, written as `kind`; uniform across the workgroup
+  auto emit = [&](int kind) {
+    const unsigned long long bst = sh.best;
+    if (bst == ~0ull) return false;
+    if (tid == 0) cert_write(c, kind, (int)(bst >> 32) - 1, (int)(uint32_t)bst - 1, 0);
+    return true;
+  };
+  // mutations in P
+  int nm = 0;
+  for (int r = tid; r < n; r += kCertThreads) {
+    const Rec d = rec(r);
+    nm += in_p(d) && is_mut(d);
+  }
+  atomicAdd(&sh.n_mut, nm);
+  __syncthreads();
+  const int n_mut = sh.n_mut;
+  // UNREACH; and the positions held, the claims, the bounds of the required ops
+  int need = 0;
+  for (int r = tid; r < n; r += kCertThreads) {
+    const Rec d = rec(r);
+    if (!req(d) || d.ver == -1 || d.bad) continue;
+    if (is_mut(d)) {
+      const int pos = d.ver - V0 - 1;
+      if (pos < 0 || pos + 1 > n_mut) {
+        found(r, -1);
+        continue;
+      }
+      atomicAdd(&held_cnt[pos], 1);
+      atomicMin(&held_rec[pos], r);
+      atomicMax(&lo_call[pos], d.call + 1);
+      atomicMin(&uh[pos], d.ret);
+      need = max(need, pos + 1);
+    } else if (d.f == LC_F_READ) {
+      const int k = d.ver - V0;
+      if (k < 0 || k > n_mut || (k == 0 && d.val != -1 && d.val != init)) {
+        found(r, -1);
+        continue;
+      }
+      if (d.val != -1) atomicMin(&claim_rec[k], r);
+      atomicMax(&lo_call[k], d.call + 1);
+      if (k > 0) atomicMin(&uh[k - 1], d.ret);
+      need = max(need, k);
+    }
+  }
+  atomicMax(&sh.m_need, need);
+  __syncthreads();
+  if (emit(LC_CERT_UNREACH)) return;
+  const int M = sh.m_need;
+  // DUP
+  for (int r = tid; r < n; r += kCertThreads) {
+    const Rec d = rec(r);
+    if (!req(d) || !is_mut(d) || d.ver == -1 || d.bad) continue;
+    const int pos = d.ver - V0 - 1;
+    if (held_cnt[pos] > 1 && held_rec[pos] != r) found(held_rec[pos], r);
+  }
+  __syncthreads();
+  if (emit(LC_CERT_DUP)) return;
+  // CLAIMS
+  for (int r = tid; r < n; r += kCertThreads) {
+    const Rec d = rec(r);
+    if (!req(d) || d.f != LC_F_READ || d.ver == -1 || d.val == -1 || d.bad) continue;
+    const int o = claim_rec[d.ver - V0];
+    if (o != r && (int)kops[o].value != d.val) found(o, r);
+  }
+  __syncthreads();
+  if (emit(LC_CERT_CLAIMS)) return;
+  // PAIR against a required holder: the lowest consumer position q
+  for (int r = tid; r < n; r += kCertThreads) {
+    const Rec d = rec(r);
+    if (!req(d) || d.ver == -1 || d.bad) continue;
+    int q = -1, want = 0;
+    if (d.f == LC_F_CAS) q = d.ver - V0 - 1, want = d.exp;
+    else if (d.f == LC_F_READ && d.val != -1) q = d.ver - V0, want = d.val;
+    if ((q == 0 && d.f == LC_F_CAS && want != init) ||
+        (q >= 1 && held_rec[q - 1] != INT_MAX && (int)kops[held_rec[q - 1]].value != want))
+      atomicMin(&sh.pos, q);
+  }
+  __syncthreads();
+  if (sh.pos != INT_MAX) {
+    const int q = sh.pos;
+    for (int r = tid; r < n; r += kCertThreads) {  // its lowest consumer
+      const Rec d = rec(r);
+      if (!req(d) || d.ver == -1 || d.bad) continue;
+      int want;
+      if (d.f == LC_F_CAS && d.ver - V0 - 1 == q) want = d.exp;
+      else if (d.f == LC_F_READ && d.val != -1 && d.ver - V0 == q) want = d.val;
+      else continue;
+      const int have = q == 0 ? init : (int)kops[held_rec[q - 1]].value;
+      if (want != have) atomicMin(&sh.rb, r);
+    }
+    __syncthreads();
+    if (tid == 0) cert_write(c, LC_CERT_PAIR, q == 0 ? -1 : held_rec[q - 1], sh.rb, q);
+    return;
+  }
+  // ORDER: the suffix minimum of the upper bounds, then a lower bound above it
+  const int L = M + 1;  // indices 0..M (reads of the last version bound index M from below)
+  {
+    const int per = (L + kCertThreads - 1) / kCertThreads;
+    const int k0 = min(tid * per, L), k1 = min(k0 + per, L);
+    uint32_t loc = kNever;
+    for (int k = k0; k < k1; k++) loc = umin(loc, uh[k]);
+    const int lane = tid & (kWave - 1), wv = tid / kWave;
+    uint32_t incl = loc;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_down((int)incl, o);
+      if (lane + o < kWave) incl = umin(incl, y);
+    }
+    if (lane == 0) sh.wmin[wv] = (int)incl;
+    uint32_t run = (uint32_t)__shfl_down((int)incl, 1);
+    if (lane == kWave - 1) run = kNever;
+    __syncthreads();
+    for (int j = wv + 1; j < kCertThreads / kWave; j++) run = umin(run, (uint32_t)sh.wmin[j]);
+    for (int k = k1 - 1; k >= k0; k--) {
+      run = umin(run, uh[k]);
+      uh[k] = run;
+    }
+  }
+  __syncthreads();
+  for (int k = tid; k < L; k += kCertThreads)
+    if (lo_call[k] != 0 && lo_call[k] - 1 > uh[k]) atomicMin(&sh.pos, k);
+  __syncthreads();
+  if (sh.pos != INT_MAX) {
+    // a: the op whose call is the lower bound, b: the op whose return is the
+    // upper bound (calls and returns are distinct events)
+    const int j = sh.pos;
+    for (int r = tid; r < n; r += kCertThreads) {
+      const Rec d = rec(r);
+      if (!req(d)) continue;
+      if (d.call + 1 == lo_call[j]) atomicMin(&sh.ra, r);
+      if (d.ret == uh[j]) atomicMin(&sh.rb, r);
+    }
+    __syncthreads();
+    if (tid == 0) cert_write(c, LC_CERT_ORDER, sh.ra, sh.rb, 0);
+    return;
+  }
+  // the open positions (needed, held by no required op) and their candidates
+  uint32_t *mark = lo_call;
+  for (int k = tid; k <= n + 1; k += kCertThreads) mark[k] = 0;
+  __syncthreads();
+  int n_gap = 0;
+  for (int g = tid; g < M; g += kCertThreads) {
+    if (held_rec[g] != INT_MAX) continue;
+    n_gap++;
+    // what its holder must write; what a CAS holding it must expect
+    int want = kFree, before = kFree;
+    bool clash = false;
+    if (held_rec[g + 1] != INT_MAX && kops[held_rec[g + 1]].f == LC_F_CAS)
+      want = (int)kops[held_rec[g + 1]].expected;
+    if (claim_rec[g + 1] != INT_MAX) {
+      const int v = (int)kops[claim_rec[g + 1]].value;
+      clash = want != kFree && want != v;
+      want = v;
+    }
+    if (g == 0) before = init;
+    else if (held_rec[g - 1] != INT_MAX) before = (int)kops[held_rec[g - 1]].value;
+    else if (claim_rec[g] != INT_MAX) before = (int)kops[claim_rec[g]].value;
+    const uint32_t dl = uh[g];
+    int k = 0, one = -1;
+    if (!clash)
+      for (int x = 0; x < n; x++) {
+        const Rec d = rec(x);
+        if (!in_p(d) || !is_mut(d) || d.bad || (req(d) && d.ver != -1)) continue;
+        if (d.ver != -1 && d.ver - V0 - 1 != g) continue;
+        if (d.call >= dl) continue;
+        if (d.f == LC_F_CAS && before != kFree && d.exp != before) continue;
+        if (want != kFree && d.val != want) continue;
+        k++;
+        one = x;
+        mark[x] = 1;
+      }
+    cnt[g] = k;
+    held_cnt[g] = one;
+    if (k == 0) atomicMin(&sh.pos, g);
+  }
+  atomicAdd(&sh.n_gap, n_gap);
+  __syncthreads();
+  if (sh.pos != INT_MAX) {
+    if (tid == 0) {
+      ks[0] = sh.pos;
+      cert_write(c, LC_CERT_HALL, -1, -1, 1);
+    }
+    return;
+  }
+  // two open positions whose only candidates disagree on the value between
+  // them (or a required holder before an open one)
+  for (int q = 1 + tid; q < M; q += kCertThreads) {
+    if (cnt[q] != 1 || kops[held_cnt[q]].f != LC_F_CAS) continue;
+    const int a = held_rec[q - 1] != INT_MAX ? held_rec[q - 1] : cnt[q - 1] == 1 ? held_cnt[q - 1] : -1;
+    if (a >= 0 && kops[a].value != kops[held_cnt[q]].expected) atomicMin(&sh.pos, q);
+  }
+  __syncthreads();
+  if (sh.pos != INT_MAX) {
+    if (tid == 0) {
+      const int q = sh.pos;
+      cert_write(c, LC_CERT_PAIR,
+                 held_rec[q - 1] != INT_MAX ? held_rec[q - 1] : held_cnt[q - 1], held_cnt[q], q);
+    }
+    return;
+  }
+  // Hall's condition over every open position
+  int u = 0;
+  for (int x = tid; x < n; x += kCertThreads) u += mark[x] != 0;
+  atomicAdd(&sh.n_cand, u);
+  __syncthreads();
+  if (sh.n_gap > sh.n_cand && tid == 0) {
+    int i = 0;
+    for (int g = 0; g < M; g++)
+      if (held_rec[g] == INT_MAX) ks[i++] = g;
+    cert_write(c, LC_CERT_HALL, -1, -1, i);
+  }
+}
+
+}  // namespace
+
+size_t cert_ws_bytes(int64_t n_records, int64_t n_keys) {
+  return sizeof(int32_t) * (size_t)kCertArrays * (size_t)(n_records + 2 * n_keys + 2);
+}
+
+hipError_t launch_certificates(const lc_op *d_ops, const int64_t *d_key_off, int64_t n_keys,
+                               int64_t n_records, const KParams &p, const lc_key_result *d_out,
+                               int32_t *d_ws, int32_t *d_cert, int32_t *d_cset,
+                               hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  const int64_t stride = n_records + 2 * n_keys + 2;
+  hipLaunchKernelGGL(cert_kernel, dim3((unsigned)n_keys), dim3(kCertThreads), 0, stream, d_ops,
+                     d_key_off, p, d_out, d_ws, stride, d_cert, d_cset);
+  return hipGetLastError();
+}
+
+}  // namespace lcdev

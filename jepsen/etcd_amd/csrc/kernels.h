@@ -195,4 +195,15 @@ hipError_t launch_gap_narrow(const lc_op *d_ops, const int64_t *d_key_off, int32
                              lc_key_result *d_out, int32_t *d_pass_keys, KStatus *d_status,
                              const GapJob &job, hipStream_t stream);
 
+// Infeasibility certificates (cert.hip, lc_aux ABI 3): one 256-thread
+// workgroup per key; every LC_INVALID key of d_out gets {kind, a, b, c} in
+// d_cert (4 int32 per key) and, for LC_CERT_HALL, its positions at the start
+// of its records' slots of d_cset; other keys LC_CERT_NONE.  Workspace:
+// cert_ws_bytes(n_records, n_keys).
+size_t cert_ws_bytes(int64_t n_records, int64_t n_keys);
+hipError_t launch_certificates(const lc_op *d_ops, const int64_t *d_key_off, int64_t n_keys,
+                               int64_t n_records, const KParams &p, const lc_key_result *d_out,
+                               int32_t *d_ws, int32_t *d_cert, int32_t *d_cset,
+                               hipStream_t stream);
+
 }  // namespace lcdev

@@ -138,6 +138,12 @@ struct Dev {
   size_t wit_cap = 0;
   int32_t *d_kind = nullptr;
   size_t kind_cap = 0;
+  int32_t *d_cert = nullptr;           // lc_aux certificates (4 per key), their position sets
+  size_t cert_cap = 0;
+  int32_t *d_cset = nullptr;
+  size_t cset_cap = 0;
+  int32_t *d_cws = nullptr;            // certificate workspace
+  size_t cws_cap = 0;
   double kernel_ms = 0, hbm_ms = 0;
   int64_t n_hbm = 0;
   int malformed = 0;
@@ -232,8 +238,25 @@ bool is_pinned(lc_ctx *c, const void *p, size_t n) {
 struct WitOut {
   int32_t *wit = nullptr;   // per record, indexed like d_ops
   int32_t *kind = nullptr;  // per key
+  int32_t *cert = nullptr;  // per key, 4 int32 (infeasibility certificates)
+  int32_t *cset = nullptr;  // per record (HALL position sets)
   int64_t n_records = 0;
 };
+
+// Infeasibility certificates for the invalid keys of a run_device call
+// (cert.hip), after every tier has decided.
+int run_certificates(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off, int64_t n_keys,
+                     const lcdev::KParams &p, const lc_key_result *d_out, hipStream_t st,
+                     const WitOut &wo) {
+  if (!wo.cert || !wo.cset || n_keys <= 0) return 0;
+  if (int rc = ensure(c, reinterpret_cast<char **>(&d.d_cws), &d.cws_cap,
+                      lcdev::cert_ws_bytes(wo.n_records, n_keys)))
+    return rc;
+  HIP_TRY(c, lcdev::launch_certificates(d_ops, d_off, n_keys, wo.n_records, p, d_out, d.d_cws,
+                                        wo.cert, wo.cset, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  return 0;
+}
 
 // Run the tiers for n_keys keys whose device arrays are in place.
 int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
@@ -803,6 +826,9 @@ void lc_close(lc_ctx *c) {
     if (d.d_cex) (void)hipFree(d.d_cex);
     if (d.d_wit) (void)hipFree(d.d_wit);
     if (d.d_kind) (void)hipFree(d.d_kind);
+    if (d.d_cert) (void)hipFree(d.d_cert);
+    if (d.d_cset) (void)hipFree(d.d_cset);
+    if (d.d_cws) (void)hipFree(d.d_cws);
     if (d.eg) (void)hipEventDestroy(d.eg);
     if (d.eh0) (void)hipEventDestroy(d.eh0);
     if (d.eh1) (void)hipEventDestroy(d.eh1);
@@ -959,6 +985,7 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
   if (rc) return rc;
   const int64_t flags = opts ? opts->flags : 0;
   const bool want_wit = aux && aux->witness && aux->witness_kind;
+  const bool want_cert = aux && aux->certificate;
   const int nd = (int)c->devs.size();
   std::vector<int64_t> bounds(nd + 1);
   lc_plan_partition(nd > 1 ? ops : nullptr, key_off, n_keys, nd, bounds.data());
@@ -987,6 +1014,8 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
     if (!r) r = ensure(c, &d.d_out, &d.out_cap, sizeof(lc_key_result) * (size_t)nk);
     if (!r && want_wit) r = ensure(c, &d.d_wit, &d.wit_cap, sizeof(int32_t) * (size_t)nrec);
     if (!r && want_wit) r = ensure(c, &d.d_kind, &d.kind_cap, sizeof(int32_t) * (size_t)nk);
+    if (!r && want_cert) r = ensure(c, &d.d_cert, &d.cert_cap, 4 * sizeof(int32_t) * (size_t)nk);
+    if (!r && want_cert) r = ensure(c, &d.d_cset, &d.cset_cap, sizeof(int32_t) * (size_t)nrec);
     if (r) {
       rcs[di] = r;
       return;
@@ -1007,13 +1036,19 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
       return;
     }
     WitOut wo;
+    wo.n_records = nrec;
     if (want_wit) {
       wo.wit = d.d_wit;
       wo.kind = d.d_kind;
-      wo.n_records = nrec;
+    }
+    if (want_cert) {
+      wo.cert = d.d_cert;
+      wo.cset = d.d_cset;
     }
     r = run_device(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, nk, p,
                    d.d_out, d.stream, flags, wo);
+    if (!r) r = run_certificates(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, nk, p,
+                                 d.d_out, d.stream, wo);
     if (r) {
       rcs[di] = r;
       return;
@@ -1025,6 +1060,12 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
                          hipMemcpyDeviceToHost, d.stream);
     if (e == hipSuccess && want_wit)
       e = hipMemcpyAsync(aux->witness_kind + a, d.d_kind, sizeof(int32_t) * (size_t)nk,
+                         hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess && want_cert)
+      e = hipMemcpyAsync(aux->certificate + 4 * a, d.d_cert, 4 * sizeof(int32_t) * (size_t)nk,
+                         hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess && want_cert && aux->certificate_set && nrec)
+      e = hipMemcpyAsync(aux->certificate_set + r0, d.d_cset, sizeof(int32_t) * (size_t)nrec,
                          hipMemcpyDeviceToHost, d.stream);
     if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
     if (e != hipSuccess) {
@@ -1069,6 +1110,10 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
     };
     auto store = [&](int64_t k, const lc_key_result &r) {
       out[k] = r;
+      // re-decided by the frontier exchange: no certificate (cert.hip covers
+      // the tiers' decisions)
+      if (want_cert)
+        for (int j = 0; j < 4; j++) aux->certificate[4 * k + j] = j == 0 ? LC_CERT_NONE : j < 3 ? -1 : 0;
       return 0;
     };
     rc = whole_gpu(c, todo, opts, fetch, store);
@@ -1108,21 +1153,35 @@ int lc_check_device_ex(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
   HIP_TRY(c, hipSetDevice(d.id));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d.stream;
   WitOut wo;
-  if (aux && aux->witness && aux->witness_kind && n_keys > 0) {
+  const bool want_wit = aux && aux->witness && aux->witness_kind;
+  const bool want_cert = aux && aux->certificate;
+  if ((want_wit || want_cert) && n_keys > 0) {
     // the record count lives in device memory: key_off[n_keys] - key_off[0]
     int64_t ends[2] = {0, 0};
     HIP_TRY(c, hipMemcpyAsync(&ends[0], d_key_off, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipMemcpyAsync(&ends[1], d_key_off + n_keys, sizeof(int64_t), hipMemcpyDeviceToHost,
                               st));
     HIP_TRY(c, hipStreamSynchronize(st));
-    wo.wit = aux->witness;
-    wo.kind = aux->witness_kind;
     wo.n_records = ends[1] - ends[0];
+    if (want_wit) {
+      wo.wit = aux->witness;
+      wo.kind = aux->witness_kind;
+    }
+    if (want_cert) {
+      wo.cert = aux->certificate;
+      wo.cset = aux->certificate_set;
+      if (!wo.cset) {  // the position sets still need a home on the device
+        if (int e = ensure(c, &d.d_cset, &d.cset_cap, sizeof(int32_t) * (size_t)wo.n_records))
+          return e;
+        wo.cset = d.d_cset;
+      }
+    }
   }
   // d_ops points at the record of index d_key_off[0]; the kernels read that
   // base themselves, so a key_off slice of a larger array may be passed.
   rc = run_device(c, d, d_ops, d_key_off, n_keys, p, d_out, st,
                   opts ? opts->flags : 0, wo);
+  if (!rc) rc = run_certificates(c, d, d_ops, d_key_off, n_keys, p, d_out, st, wo);
   if (!rc && opts && (opts->flags & LC_FLAG_WHOLE_GPU) && n_keys > 0) {
     // the results and the keys' records are in device memory: read back the
     // verdicts, and each key the frontier exchange takes
@@ -1147,6 +1206,11 @@ int lc_check_device_ex(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
       return 0;
     };
     auto store = [&](int64_t k, const lc_key_result &r) {
+      if (want_cert) {
+        const int32_t none[4] = {LC_CERT_NONE, -1, -1, 0};
+        if (hipMemcpy(aux->certificate + 4 * k, none, sizeof none, hipMemcpyHostToDevice) != hipSuccess)
+          return -EIO;
+      }
       return hipMemcpy(d_out + k, &r, sizeof r, hipMemcpyHostToDevice) == hipSuccess ? 0 : -EIO;
     };
     rc = whole_gpu(c, todo, opts, fetch, store);

@@ -56,6 +56,9 @@ def lib():
         L.oracle_check_witness.argtypes = [vp, vp, ctypes.c_int64, ctypes.POINTER(_Opts), vp, vp,
                                            vp, vp, vp, ctypes.c_int]
         L.oracle_check_witness.restype = ctypes.c_int
+        L.oracle_check_certificate.argtypes = [vp, vp, ctypes.c_int64, ctypes.POINTER(_Opts),
+                                               vp, vp, vp, vp, ctypes.c_int]
+        L.oracle_check_certificate.restype = ctypes.c_int
         L.oracle_frontier.argtypes = [vp, ctypes.c_int64, ctypes.POINTER(_Opts), ctypes.c_int,
                                       ctypes.c_int64, vp, ctypes.c_int64, vp]
         L.oracle_frontier.restype = ctypes.c_int
@@ -125,3 +128,29 @@ def check_witness(ops, key_off, witness, kind, results=None, init_version=0, ini
     if rc != 0:
         raise RuntimeError("oracle_check_witness: %d" % rc)
     return st, ln
+
+
+CERT_OK, CERT_NONE, CERT_BAD = 1, 0, -1
+CERT_KINDS = {0: "none", 1: "dup", 2: "unreach", 3: "claims", 4: "pair", 5: "order", 6: "hall"}
+
+
+def check_certificate(ops, key_off, cert, cert_set, results, init_version=0, init_value=-1,
+                      n_threads=8):
+    """Check infeasibility certificates (lc_aux, include/lincheck.h) from the
+    records alone: per key CERT_OK, CERT_NONE or CERT_BAD.  `results` gives
+    each key's cut (fail_prefix_end); cert is int32[4 * n_keys], cert_set
+    int32 per record (or None)."""
+    ops = np.ascontiguousarray(ops, dtype=np.int64).reshape(-1, 6)
+    key_off = np.ascontiguousarray(key_off, dtype=np.int64)
+    n = len(key_off) - 1
+    cert = np.ascontiguousarray(cert, dtype=np.int32).reshape(-1)
+    cset = None if cert_set is None else np.ascontiguousarray(cert_set, dtype=np.int32)
+    cut = np.ascontiguousarray(results["fail_prefix_end"], dtype=np.int64)
+    st = np.zeros(max(n, 0), dtype=np.int32)
+    o = _Opts(init_version, init_value, 0, 0, 0)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+    rc = lib().oracle_check_certificate(p(ops), p(key_off), n, ctypes.byref(o), p(cert),
+                                        p(cset), p(cut), p(st), n_threads)
+    if rc != 0:
+        raise RuntimeError("oracle_check_certificate: %d" % rc)
+    return st

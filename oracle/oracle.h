@@ -75,6 +75,18 @@ int oracle_check_witness(const lc_op *ops, const int64_t *key_off, int64_t n_key
                          const int64_t *cut, int32_t *status, int64_t *order_len,
                          int n_threads);
 
+/* Infeasibility certificates (cert.c): check each key's certificate
+ * (lc_aux.certificate, 4 int32 per key; certificate_set, per record) against
+ * the prefix at cut[k] (fail_prefix_end) from the records alone.  Per key
+ * ORACLE_CERT_OK, ORACLE_CERT_NONE (kind LC_CERT_NONE) or ORACLE_CERT_BAD
+ * (the facts named do not rule out every linearization). */
+#define ORACLE_CERT_OK    1
+#define ORACLE_CERT_NONE  0
+#define ORACLE_CERT_BAD (-1)
+int oracle_check_certificate(const lc_op *ops, const int64_t *key_off, int64_t n_keys,
+                             const lc_opts *opts, const int32_t *cert, const int32_t *cert_set,
+                             const int64_t *cut, int32_t *status, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

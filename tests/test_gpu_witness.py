@@ -71,6 +71,67 @@ def test_c4_at_20pct_crashed_certified(ctx, seed, anom):
     assert st[0] == oracle.WIT_OK and ln[0] > (3000 if want else 0)
 
 
+def certify_invalid(ops, off, r, cert, cset, min_keys=1):
+    """Every invalid key with a PREFIX witness carries an infeasibility
+    certificate that oracle/cert.c accepts from the records alone (the
+    witness shows the prefix before the failing return linearizable, the
+    certificate the prefix at it not: the failing return is the first)."""
+    st = oracle.check_certificate(ops, off, cert.reshape(-1), cset, r, n_threads=16)
+    inv = np.nonzero(r["verdict"] == 0)[0]
+    assert len(inv) >= min_keys
+    assert not (st == oracle.CERT_BAD).any(), [(int(k), cert[k].tolist()) for k in
+                                              np.nonzero(st == oracle.CERT_BAD)[0][:5]]
+    return st
+
+
+@pytest.mark.parametrize("seed", [1004, 1007, 1009])
+def test_c4_invalid_certificates(ctx, seed):
+    """BASELINE configs[3]'s invalid keys (20 % crashed, an injected anomaly):
+    no oracle search finishes on them, so their counterexamples were certified
+    on one side only (the witness of the prefix before the failing return).
+    The certificate closes the other side: the prefix at the failing return
+    has no linearization, by facts oracle/cert.c checks from the records."""
+    ops, off, _, _ = abi.synth(1, 5000, concurrency=50, p_info=0.2, info_frac=0.2,
+                               p_anomaly=1.0, seed=seed)
+    _, r, wit, kind, cert, cset = ctx.check(ops, off, witness=True, certificate=True)
+    assert r["verdict"][0] == 0 and kind[0] == abi.LC_WITNESS_PREFIX
+    certify(ops, off, r, wit, kind)
+    st = certify_invalid(ops, off, r, cert, cset)
+    assert st[0] == oracle.CERT_OK, cert[0].tolist()
+
+
+@pytest.mark.parametrize("case", ["c5", "c2_crashes", "mixed_crash", "dup"])
+def test_invalid_keys_certified(ctx, case):
+    """Every invalid key the version-pinned tiers decide — by the first-failure
+    rule (C5 shapes, duplicated versions), the gap tier's bisection
+    (crash-heavy keys) or its multisection — carries a certificate the
+    checker accepts; valid keys carry none."""
+    from helpers import dup_versions
+    if case == "c5":
+        z = np.load(os.path.join(GOLDEN, "c5.npz"))
+        ops, off = z["ops"], z["key_off"]
+    elif case == "c2_crashes":
+        ops, off, _, _ = abi.synth(24, 1000, concurrency=20, p_info=0.05, p_anomaly=0.4,
+                                   seed=0x5EED0013)
+    elif case == "mixed_crash":
+        ops, off, _, _ = abi.synth(2000, 120, concurrency=12, p_info=0.2, info_frac=0.15,
+                                   p_anomaly=0.35, seed=51)
+    else:
+        ops, off, _, _ = abi.synth(600, 200, concurrency=10, p_anomaly=0.6, seed=52)
+        ops, off = pack_keys(dup_versions([ops[off[k]:off[k + 1]].tolist() for k in range(600)],
+                                          52, frac=0.7))
+    _, r, wit, kind, cert, cset = ctx.check(ops, off, witness=True, certificate=True)
+    certify(ops, off, r, wit, kind)
+    st = certify_invalid(ops, off, r, cert, cset, min_keys=3)
+    pinned = kind == abi.LC_WITNESS_PREFIX
+    assert (st[pinned] == oracle.CERT_OK).all(), [
+        (int(k), cert[k].tolist()) for k in np.nonzero(pinned & (st != oracle.CERT_OK))[0][:5]]
+    assert (cert[r["verdict"] != 0][:, 0] == abi.LC_CERT_NONE).all()
+    # the certificate outputs change nothing else
+    _, r2 = ctx.check(ops, off)
+    assert (r2 == r).all()
+
+
 def test_crash_leg_every_key_certified(ctx):
     """bench.py's crash_leg workload at full size: C2 (10,000 keys x 1,000
     ops, concurrency 20) with 5 % of writes/CAS crashed.  Every key goes to

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
         "lc_fx_open_rccl", "lc_fx_abort", "lc_fx_frontier"}
     for n in names:
         assert hasattr(lib, n), n
-    assert abi.lib().lc_abi_version() == 2
+    assert abi.lib().lc_abi_version() == 3
 
 
 def test_struct_sizes():
@@ -41,7 +41,7 @@ def test_struct_sizes():
     assert ctypes.sizeof(abi.LcOpts) == 40
     assert ctypes.sizeof(abi.LcSynthParams) == 56
     assert ctypes.sizeof(abi.LcStats) == 104
-    assert ctypes.sizeof(abi.LcAux) == 16
+    assert ctypes.sizeof(abi.LcAux) == 32
     assert ctypes.sizeof(abi.LcDeviceStats) == 56
     from jepsen.etcd_amd import fx
     assert ctypes.sizeof(fx.LcFxParams) == 40
