@@ -340,8 +340,12 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                                                d.d_jit2, d.d_status, want_wit ? wo.kind : nullptr,
                                                st));
       // the crash-light pass reads the list and its length from the device:
-      // no host round trip between the compaction and it
-      if (gap_on && !fused) {
+      // no host round trip between the compaction and it.  After the fused
+      // pass too: the keys it hands over are invalid or beyond the in-place
+      // decision, and the light pass names an invalid version-pinned key's
+      // first failure (check_kernel.hip, first_failure), so every path gives
+      // the same results
+      if (gap_on) {
         HIP_TRY(c, lcdev::launch_gap_light(d_ops, d_off, d.d_jit, n_keys, p, d_out, d.d_gap2,
                                            d.d_status, want_wit ? wo.wit : nullptr,
                                            want_wit ? wo.kind : nullptr, st));
@@ -351,18 +355,15 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                                 hipMemcpyDeviceToHost, st));
       HIP_TRY(c, hipStreamSynchronize(st));
       n_direct = d.h_status->n_jit2;
-      if (fused) {
-        d.use_fused = 4 * (int64_t)d.h_status->n_light > n_keys;
-        d.gap_ms = 0;
-        d.n_gap = d.h_status->n_light;
-        n_jit = d.h_status->n_jit;  // undecided: straight to the gap tier
-      } else if (gap_on) {
-        // most keys handed to the gap tier: the next call fuses the passes
-        d.use_fused = 2 * (int64_t)d.h_status->n_jit > n_keys;
+      if (gap_on) {
+        // fused: were most keys crash-light?  Else: most keys handed to the
+        // gap tier: the next call fuses the passes
+        d.use_fused = fused ? 4 * (int64_t)d.h_status->n_light > n_keys
+                            : 2 * (int64_t)d.h_status->n_jit > n_keys;
         light = true;
         HIP_TRY(c, hipEventElapsedTime(&ms, d.ef, d.el));
         d.gap_ms = ms;
-        d.n_gap = d.h_status->n_jit;
+        d.n_gap = fused ? d.h_status->n_light : d.h_status->n_jit;
         n_jit = d.h_status->n_gap2;  // what the gap tier proper still has to decide
         jit_list = d.d_gap2;
       } else {
