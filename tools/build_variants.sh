@@ -11,6 +11,7 @@ mkdir -p $out/obj
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c check_kernel.hip -o $out/obj/k.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c gap_tier.hip -o $out/obj/g.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c fx.hip -o $out/obj/f.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c cert.hip -o $out/obj/c.o
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC "$@" -x hip --offload-arch=gfx950 -DLC_BUILD_ID='"variant"' -c lincheck.cpp -o $out/obj/h.o
 g++ -O3 -std=c++17 -fPIC -c synth.cpp -o $out/obj/s.o
 g++ -O3 -std=c++17 -fPIC -c edn.cpp -o $out/obj/e.o

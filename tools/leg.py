@@ -1,7 +1,9 @@
 """Dev probe: run one bench.py leg's workload N times (for rocprofv3 passes
 that must see only that leg's kernels).
-  python tools/leg.py crash|model|hot|hotx [reps]
-crash: C2 with 5 % crashed writes/CAS (gap_light_kernel / gap_tier_kernel)
+  python tools/leg.py crash|model|hot|hotx|mixed|search|fx [reps]
+crash: C2 with 5 % crashed writes/CAS (fused_tier_kernel)
+mixed: C5, 1000 keys x 200 ops, 10 % anomalies (fast_tier_kernel, then
+       gap_light_kernel: the first-failure rule)
 model: cas-register model, 1000 keys x 1000 ops, concurrency 20 (lds_tier,
        hbm_coop_kernel<4>)
 hot / hotx: C4 at 20 % crashed, valid / invalid (gap_tier_kernel)
@@ -21,6 +23,8 @@ leg = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 if leg == "crash":
     ops, off, _, _ = abi.synth(10000, 1000, concurrency=20, p_info=0.05, seed=0x5EED0012)
+elif leg == "mixed":
+    ops, off, _, _ = abi.synth(1000, 200, concurrency=10, p_anomaly=0.1, seed=0x5EED0005)
 elif leg == "model":
     ops, off, _, _ = abi.synth(1000, 1000, concurrency=20, seed=7)
     ops = ops.copy()
