@@ -2444,6 +2444,23 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       decided = true;
       break;
     }
+    // LC_FX_DEBUG: the retirement AND kept incrementally (the insert and
+    // every level AND the masks they put into R, one atomic per workgroup)
+    // must equal the AND of R recomputed whole: a bit set that some
+    // configuration lacks would retire an op not linearized everywhere
+    if (debug && !multi() && nF) {
+      std::vector<Cfg> hR((size_t)nF);
+      FX_TRY(hipMemcpy(hR.data(), F, sizeof(Cfg) * (size_t)nF, hipMemcpyDeviceToHost));
+      unsigned long long whole = ~0ULL;
+      for (const Cfg &cf : hR) whole &= cf.mask;
+      if (whole != hCtr->andmask) {
+        err = "LC_FX_DEBUG: incremental retirement AND " + std::to_string(hCtr->andmask) +
+              " != AND of R " + std::to_string(whole) + " at the return of record " +
+              std::to_string(x);
+        return -EIO;
+      }
+      fprintf(stderr, "fx and-check ok x=%d nR=%lld\n", (int)x, (long long)nF);
+    }
     // retirement: ops linearized in every configuration free their slots
     const uint64_t all = occ & hCtr->andmask;
     if (debug)

@@ -75,6 +75,31 @@ def test_fx_matches_oracle_jitc(ranks, part_above):
 
 
 @pytest.mark.gpu
+def test_fx_incremental_retirement_and(monkeypatch, capfd):
+    """The retirement AND is kept incrementally (each workgroup of the insert
+    and of every level ANDs the masks it puts into R; no pass over R).  Under
+    LC_FX_DEBUG the engine recomputes the AND of R whole after every
+    replicated return and fails the check on any difference.  Version-less
+    keys whose returns start in the one-workgroup small-return kernel and
+    continue on the grid (kcur hand-off) across several batches, no counted
+    classes: every return checked, every result field equal to the oracle's
+    JITC."""
+    from jepsen.etcd_amd.fx import FrontierExchange
+    monkeypatch.setenv("LC_FX_DEBUG", "1")
+    monkeypatch.setenv("LC_FX_CLASSES", "0")
+    with FrontierExchange(device=0) as fx:
+        for n, conc, seed in ((700, 40, 81), (900, 40, 83), (1200, 36, 84)):
+            ops, off, _, _ = abi.synth(1, n, concurrency=conc, p_anomaly=0.0, seed=seed)
+            ops = ops.copy()
+            ops[:, 3] = -1
+            got = fx.check(ops)
+            _compare(got, _oracle(ops.tolist(), -1), (n, conc))
+            assert int(got["max_frontier"]) > 1024  # levels beyond the small kernel's cutoff
+    err = capfd.readouterr().err
+    assert err.count("fx and-check ok") > 500 and "LC_FX_DEBUG: incremental" not in err
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("transport", ["rccl", "hub"])
 def test_fx_self_exchange_matches_oracle(transport):
     """The multi-rank protocol with one rank exchanging with itself
