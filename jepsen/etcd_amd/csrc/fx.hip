@@ -129,7 +129,7 @@ struct Slot {
   uint64_t zob;              // Zobrist word of the op (0 for reads); class lane: members available
 };
 
-// Counted classes (one rank): crashed writes/CAS with equal (f, value,
+// Counted classes: crashed writes/CAS with equal (f, value,
 // expected, version) are interchangeable (their completion never arrived,
 // so their version stays nil — register.clj:64,71), and deadline order
 // linearizes them in call order, after every pending :ok member of the class.
@@ -159,6 +159,12 @@ struct Win {
   uint64_t fclear, fclose;
   int32_t rank, n_ranks;
   uint64_t fsub;   // one rank: class members retired since the last return (fields to subtract)
+  // ownership with counted classes (several ranks): the mask's slot bits, and
+  // per class the members retired (a field counts the members linearized
+  // beyond them), so the owner hashes a class by its absolute count
+  uint64_t slot_bits;
+  int32_t n_cls, pad_;
+  uint32_t cbase[kMaxCls];
   Slot s[kW];
 };
 
@@ -218,12 +224,19 @@ __device__ inline bool legal(const Slot &s, uint32_t ver, uint32_t val) {
 // linearized, retired ones included (kzob), and its state.  Retirement clears
 // a bit in every configuration and folds the op's word into kzob, so owners
 // never move; reads carry no word, so read closure never moves them either.
+// A counted class enters by its absolute member count (retired members plus
+// its field): retirement shrinks the field and grows cbase together, so it
+// moves no owner either.
 __device__ inline uint32_t owner_of(const Cfg &c, const Win &w) {
-  uint64_t z = w.kzob, m = c.mask;
+  uint64_t z = w.kzob, m = c.mask & w.slot_bits;
   while (m) {
     const int b = __builtin_ctzll(m);
     m &= m - 1;
     z ^= w.s[b].zob;
+  }
+  for (int k = 0; k < w.n_cls; k++) {
+    const uint64_t cnt = cls_get(c.mask, w.s[kClsLane0 + k].cls) + w.cbase[k];
+    if (cnt) z ^= mix64(((uint64_t)(k + 1) << 56) ^ cnt);
   }
   z ^= mix64(((uint64_t)c.ver << 32) | c.val);
   return (uint32_t)(mix64(z) % (uint64_t)w.n_ranks);
@@ -765,6 +778,15 @@ __global__ __launch_bounds__(256) void fx_clear_kernel(Cfg *list, int64_t n, uin
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     list[i].mask &= ~bits;
+}
+
+// Several ranks: retired class members leave every configuration's field at
+// once (fields are disjoint and each holds at least the retired count, so one
+// subtraction of the packed word borrows across no field).
+__global__ __launch_bounds__(256) void fx_sub_kernel(Cfg *list, int64_t n, uint64_t sub) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    list[i].mask -= sub;
 }
 
 // A read is called: linearize it at once wherever it is legal (closure).
@@ -1966,7 +1988,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     }
   };
 
-  // Counted classes (one rank; see kClsLane): crashed writes/CAS grouped by
+  // Counted classes (see kClsLane): crashed writes/CAS grouped by
   // (f, value, expected, version), each class a field wide enough for all of
   // its members in the key, placed just below the value-id bits; the slots
   // keep the bits below the fields.  LC_FX_CLASSES=0: one slot per crashed op.
@@ -1975,9 +1997,10 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   int64_t cls_called[kMaxCls] = {0}, cls_base[kMaxCls] = {0};
   int slot_max = kW;  // slots are bits [0, slot_max)
   uint64_t fsub = 0;  // one rank: class members retired since the last return
+  // (several ranks apply retirement at once: fx_clear_kernel / fx_sub_kernel)
   {
     const char *ce = getenv("LC_FX_CLASSES");
-    const bool want = !multi() && !(ce && ce[0] == '0');
+    const bool want = !(ce && ce[0] == '0');
     std::vector<int32_t> rep;
     for (int64_t i = 0; want && i < n; i++) {
       if (o[i].ret != LC_INF || o[i].f == LC_F_READ) continue;
@@ -2128,6 +2151,9 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
     w.fclose = fclose;
     w.fsub = fsub;
     fclear = fclose = fsub = 0;
+    w.slot_bits = n_cls ? (1ULL << slot_max) - 1 : ~0ULL;
+    w.n_cls = n_cls;
+    for (int c = 0; c < n_cls; c++) w.cbase[c] = (uint32_t)cls_base[c];
     if (multi()) FX_TRY(hipMemcpyAsync(dWin, &w, sizeof(Win), hipMemcpyHostToDevice, st));
     // mode switches (several ranks only)
     if (multi() && !part && nFglobal > part_above) {
@@ -2397,6 +2423,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       }
       if (!over && !timeout) {
         fx_and_kernel<<<grid_for(nF), 256, 0, st>>>(Rl, &dCtr->nR, dCtr, dExp);
+        if (n_cls) fx_cmin_kernel<<<grid_for(nF), 256, 0, st>>>(Rl, &dCtr->nR, dWin, dCtr);
         FX_TRY(hipGetLastError());
       }
       if (int er = sync_ctr()) return er;
@@ -2413,6 +2440,16 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       for (int b = 0; b < kW; b++)
         if (!v[1 + b]) gand |= 1ULL << b;
       hCtr->andmask = gand;
+      if (n_cls && !over && !timeout) {
+        // each class's smallest field over every rank's R: max of the negated
+        // local minima (a rank with R empty contributes nothing)
+        int64_t m[kMaxCls];
+        for (int c = 0; c < n_cls; c++)
+          m[c] = hCtr->cmin[c] == ~0ULL ? INT64_MIN : -(int64_t)hCtr->cmin[c];
+        FX_COLL(coll_allreduce(m, n_cls, LC_FX_MAX));
+        for (int c = 0; c < n_cls; c++)
+          hCtr->cmin[c] = m[c] == INT64_MIN ? ~0ULL : (unsigned long long)(-m[c]);
+      }
       break;
     }
     if (over) {
@@ -2485,15 +2522,23 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       for (int u = 0; u < kW; u++) before[u] &= ~all;
     }
     // counted classes: members every configuration has linearized retire
-    // (the fields shrink by as many, lazily, at the next split: fsub)
+    // (the fields shrink by as many: one rank lazily, at the next split —
+    // fsub; several ranks now, as cbase grows with them for owner_of)
+    uint64_t sub = 0;
     for (int c = 0; c < n_cls; c++) {
       const unsigned long long m = hCtr->cmin[c];
       if (m == 0 || m == ~0ULL) continue;
       Slot &cl = w.s[kClsLane0 + c];
       cls_base[c] += (int64_t)m;
       cl.zob -= m;
-      fsub += (uint64_t)m << cls_shift(cl.cls);
+      sub += (uint64_t)m << cls_shift(cl.cls);
       vbase += (uint32_t)m;
+    }
+    if (sub && !multi()) {
+      fsub += sub;
+    } else if (sub && nF) {
+      fx_sub_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, sub);
+      FX_TRY(hipGetLastError());
     }
   }
   // every rank reports the same totals

@@ -616,9 +616,9 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
 //
 // Keys left :unknown because more than LC_MAX_WINDOW ops were open at once
 // (crashed writes/CAS pile up in the tiers' windows) are searched again too,
-// by one-rank engines only (spread_ok false): there the crashed ops of a key
-// are counted per class instead of holding a window slot each (fx.hip,
-// "Counted classes").
+// the same way: there the crashed ops of a key are counted per class instead
+// of holding a window slot each (fx.hip, "Counted classes"; owner_of hashes a
+// class by its absolute count, so the multi-GPU engine partitions them too).
 //
 // A failure of the re-search (an allocation, say) is this key's alone: it
 // keeps the tiers' :unknown, the error text goes to lc_last_error, and the
@@ -626,8 +626,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
 // throws.
 int whole_gpu(lc_ctx *c, const std::vector<int64_t> &todo, const lc_opts *opts,
               const std::function<int(int64_t, std::vector<lc_op> &)> &fetch,
-              const std::function<int(int64_t, const lc_key_result &)> &store,
-              bool spread_ok = true) {
+              const std::function<int(int64_t, const lc_key_result &)> &store) {
   if (todo.empty()) return 0;
   std::vector<int> ids;  // the context's distinct GPUs
   for (const Dev &d : c->devs)
@@ -638,7 +637,7 @@ int whole_gpu(lc_ctx *c, const std::vector<int64_t> &todo, const lc_opts *opts,
     failed++;
     set_err(c, "LC_FLAG_WHOLE_GPU: key " + std::to_string(k) + " kept :unknown: " + what);
   };
-  if (spread_ok && nranks > 1 && todo.size() < (size_t)nranks) {
+  if (nranks > 1 && todo.size() < (size_t)nranks) {
     if (!c->fx_all && !c->fx_all_failed) {
       lc_fx_params fp{};
       fp.part_above = -1;
@@ -1184,7 +1183,7 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
       return 0;
     };
     rc = whole_gpu(c, todo, opts, fetch, store);
-    if (!rc) rc = whole_gpu(c, todo_w, opts, fetch, store, false);
+    if (!rc) rc = whole_gpu(c, todo_w, opts, fetch, store);
   }
   c->stats.n_keys = n_keys;
   c->stats.n_ops = key_off[n_keys] - key_off[0];
@@ -1281,7 +1280,7 @@ int lc_check_device_ex(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
       return hipMemcpy(d_out + k, &r, sizeof r, hipMemcpyHostToDevice) == hipSuccess ? 0 : -EIO;
     };
     rc = whole_gpu(c, todo, opts, fetch, store);
-    if (!rc) rc = whole_gpu(c, todo_w, opts, fetch, store, false);
+    if (!rc) rc = whole_gpu(c, todo_w, opts, fetch, store);
   }
   c->stats.kernel_ms = d.kernel_ms;
   c->stats.fast_kernel_ms = d.fast_ms;

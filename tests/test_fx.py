@@ -215,6 +215,63 @@ def test_fx_counted_classes_decide_crash_heavy_keys(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ranks,part_above", [(2, 0), (3, 0), (2, 2)])
+def test_fx_counted_classes_over_ranks(ranks, part_above):
+    """Counted classes on the multi-rank engine: a configuration's owner
+    hashes each class by its absolute count (members retired + its field),
+    which retirement leaves unchanged, and a class's retirement takes the
+    smallest field over every rank's R.  Crash-heavy mutex keys (frontiers
+    of a few configurations), every level partitioned (part_above=0) or
+    only returns above two configurations: every field equals the oracle's
+    JITC, with configurations actually exchanged."""
+    from jepsen.etcd_amd.fx import FrontierExchange
+    keys = _crash_heavy_mutex_keys(0xC1A57 + ranks, n=8)
+    ops, off = pack_keys(keys)
+    _, j = oracle.check(ops, off, algo=oracle.JITC, init_value=FREE, n_threads=8)
+    assert (j["verdict"] != -1).all()
+    o = abi.default_opts(init_value=FREE)
+    sent = part = 0
+    with FrontierExchange(device=0, virtual_ranks=ranks, part_above=part_above,
+                          repl_below=part_above // 2, table_log2=18) as fx:
+        for i, k in enumerate(keys):
+            got = fx.check(np.array(k, dtype=np.int64), o)
+            for f in FIELDS:
+                assert int(got[f]) == int(j[f][i]), (ranks, part_above, i, f, int(got[f]), int(j[f][i]))
+            st = fx.stats()
+            sent += st["sent_configs"]
+            part += st["part_returns"]
+    assert part > 0 and sent > 0
+
+
+@pytest.mark.gpu
+def test_whole_gpu_spreads_window_overflow_keys(monkeypatch, capfd):
+    """Fewer window-overflow keys than the context has devices: each one's
+    re-search spans every device (two device contexts on this box's GPU,
+    LC_VIRTUAL_DEVICES=2, run their two ranks in process; LC_FX_DEBUG names
+    the rank of every return), counted classes included, and the results
+    equal the oracle's JITC in every field."""
+    monkeypatch.setenv("LC_VIRTUAL_DEVICES", "2")
+    keys = _crash_heavy_mutex_keys(0xC1A58, n=6)
+    ops, off = pack_keys(keys)
+    with abi.Context(1) as ctx:
+        _, plain = ctx.check(ops, off, abi.default_opts(init_value=FREE))
+        over = np.flatnonzero(plain["reason"] == abi.LC_REASON_WINDOW_OVERFLOW)
+        assert len(over) >= 1
+        one = over[:1]  # one key: fewer than the two devices
+        sops, soff = pack_keys([keys[int(one[0])]])
+        monkeypatch.setenv("LC_FX_DEBUG", "1")
+        _, whole = ctx.check(sops, soff, abi.default_opts(init_value=FREE,
+                                                          flags=abi.LC_FLAG_WHOLE_GPU))
+        assert ctx.stats()["n_devices"] == 2
+    err = capfd.readouterr().err
+    assert "fx r1 ret" in err and "fx r0 ret" in err
+    _, j = oracle.check(sops, soff, algo=oracle.JITC, init_value=FREE)
+    for f in FIELDS:
+        assert (whole[f] == j[f]).all(), f
+    assert whole["verdict"][0] != -1
+
+
+@pytest.mark.gpu
 def test_whole_gpu_decides_window_overflow_keys():
     """lc_check's search tiers keep one window slot per open op
     (LC_MAX_WINDOW = 64): crash-heavy version-less keys come back :unknown
