@@ -380,19 +380,35 @@ __device__ inline void insert_rv(bool have, Cfg c, uint64_t xbit, const Tabs &t,
   wave_append(r == 1 && !toR, c, t.vdst, t.vcnt, t.list_cap, &ctr->overflow);
 }
 
-__global__ __launch_bounds__(256) void fx_insert_kernel(const Cfg *__restrict__ in, int64_t n,
-                                                        const Win *__restrict__ win, Tabs t,
-                                                        uint32_t epoch, Ctr *ctr) {
-  const uint64_t xbit = win->xbit;
-  const bool fix = win->fclear | win->fclose | win->fsub;
+// Counters of a return about to start: R and V empty, explored at `explored`
+// (the shards), levels from 0.
+__device__ inline void ctr_start(Ctr *ctr, unsigned long long explored) {
+  for (int i = 0; i < kExpShards; i++) ctr->exp[i * kExpStride] = i ? 0 : explored;
+  ctr->nR = ctr->nV = ctr->kcur = 0;
+  ctr->cnt[0] = ctr->cnt[1] = ctr->cnt[2] = 0;
+  ctr->levels = 0;
+  ctr->andmask = ~0ULL;
+  ctr->nsel = 0;
+  ctr->tfull = 0;
+  ctr->explored = explored;
+  for (int i = 0; i < 64; i++) ctr->cand[i] = 0;
+  for (int i = 0; i < kMaxCls; i++) ctr->cmin[i] = ~0ULL;
+}
+
+// Split F into R and V: the configurations that linearized the returning op
+// to R (its bit cleared), the others to V level 0.
+__device__ inline void split_into_rv(const Cfg *__restrict__ in, int64_t n, const Win &win, Tabs t,
+                                     uint32_t epoch, Ctr *ctr) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const uint64_t xbit = win.xbit;
+  const bool fix = win.fclear | win.fclose | win.fsub;
   uint64_t rand = ~0ULL;
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x; b < n; b += stride) {
     const int64_t i = b + threadIdx.x;
     const bool have = i < n;
     Cfg c{};
     if (have) c = in[i];
-    if (have && fix) fix_f(c, *win);
+    if (have && fix) fix_f(c, win);
     insert_rv(have, c, xbit, t, epoch, ctr, rand);
   }
   // the R entries' AND, one atomic per workgroup (ctr->andmask holds the
@@ -405,6 +421,40 @@ __global__ __launch_bounds__(256) void fx_insert_kernel(const Cfg *__restrict__ 
     const unsigned long long a = s_and[0] & s_and[1] & s_and[2] & s_and[3];
     if (a != ~0ULL) atomicAnd(&ctr->andmask, a);
   }
+}
+
+__global__ __launch_bounds__(256) void fx_insert_kernel(const Cfg *__restrict__ in, int64_t n,
+                                                        const Win *__restrict__ win, Tabs t,
+                                                        uint32_t epoch, Ctr *ctr) {
+  split_into_rv(in, n, *win, t, epoch, ctr);
+}
+
+// One rank's split at the start of a return by the grid: the window travels
+// as the argument (with `dwin` the first workgroup stores it for the levels
+// that follow), and the launch also prepares the NEXT return — the other
+// parity's counters, its one-word tables (`prep_words` entries) to EMPTY —
+// so that return needs no reset launch of its own (fx_reset_kernel: ≈4 µs of
+// each return on the oversized key).
+__global__ __launch_bounds__(256) void fx_split_kernel(const Cfg *__restrict__ in, int64_t n,
+                                                       const Win win, Win *dwin, Tabs t,
+                                                       uint32_t epoch, Ctr *ctr, Ctr *prep_ctr,
+                                                       unsigned long long *prep_tR,
+                                                       unsigned long long *prep_tV,
+                                                       int64_t prep_words) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (dwin && blockIdx.x == 0) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(&win);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(dwin);
+    for (int i = threadIdx.x; i < (int)(sizeof(Win) / 4); i += blockDim.x) dst[i] = src[i];
+  }
+  if (prep_ctr) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < prep_words; i += stride) {
+      prep_tR[i] = kEmpty;
+      prep_tV[i] = kEmpty;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr_start(prep_ctr, 0);
+  }
+  split_into_rv(in, n, win, t, epoch, ctr);
 }
 
 
@@ -840,15 +890,8 @@ __global__ __launch_bounds__(256) void fx_reset_kernel(Ctr *ctr, unsigned long l
     tagV[i] = fill;
   }
   if (blockIdx.x || threadIdx.x) return;
-  for (int i = 0; i < kExpShards; i++) exp[i * kExpStride] = i ? 0 : explored;
-  ctr->nR = ctr->nV = ctr->kcur = 0;
-  ctr->cnt[0] = ctr->cnt[1] = ctr->cnt[2] = 0;
-  ctr->andmask = ~0ULL;
-  ctr->nsel = 0;
-  ctr->tfull = 0;
-  ctr->explored = explored;
-  for (int i = 0; i < 64; i++) ctr->cand[i] = 0;
-  for (int i = 0; i < kMaxCls; i++) ctr->cmin[i] = ~0ULL;
+  (void)exp;
+  ctr_start(ctr, explored);
 }
 
 // ------------------------------------------------------------ the queue path
@@ -1480,6 +1523,15 @@ struct Rank {
   uint64_t tmask = 0;
   Win *dWin = nullptr, *hWin = nullptr;
   Ctr *dCtr = nullptr, *hCtr = nullptr;
+  // Returns alternate between two sets of counters and (one-word mode) two
+  // tables, so that a return can prepare the next one's (fx_split_kernel):
+  // dCtr = dCtrBase + par, the one-word tables of parity 1 are tagR2 / tagV2.
+  Ctr *dCtrBase = nullptr;
+  unsigned long long *tagR2 = nullptr, *tagV2 = nullptr;
+  int par = 0;
+  uint64_t dirtyC[2] = {0, 0};     // one-word tables: entries past this are EMPTY
+  bool prepped[2] = {false, false};  // counters reset and tables all EMPTY
+  unsigned long long exp_off = 0;  // added to the device's explored (prepared counters start at 0)
   unsigned long long *dExp = nullptr;  // explored shards
   Cfg *cand = nullptr;
   unsigned long long cand_cap = 0;  // per owner region
@@ -1507,13 +1559,13 @@ struct Rank {
 
   void release() {
     for (void *p : {(void *)F, (void *)Rl, (void *)Vl, (void *)tmp, (void *)tagR, (void *)tagV,
-                    (void *)keyR, (void *)keyV, (void *)dWin, (void *)dCtr, (void *)cand,
-                    (void *)sendb, (void *)recvb})
+                    (void *)tagR2, (void *)tagV2, (void *)keyR, (void *)keyV, (void *)dWin,
+                    (void *)dCtrBase, (void *)cand, (void *)sendb, (void *)recvb})
       if (p) (void)hipFree(p);
     F = Rl = Vl = tmp = keyR = keyV = cand = sendb = recvb = nullptr;
-    tagR = tagV = nullptr;
+    tagR = tagV = tagR2 = tagV2 = nullptr;
     dWin = nullptr;
-    dCtr = nullptr;
+    dCtr = dCtrBase = nullptr;
     dExp = nullptr;
     for (void *p : {(void *)qQ, (void *)qtab[0][0], (void *)qtab[0][1], (void *)qtab[1][0],
                     (void *)qtab[1][1], (void *)qctr})
@@ -1613,8 +1665,9 @@ struct Rank {
     FX_TRY(hipSetDevice(dev));
     FX_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     FX_TRY(hipMalloc(&dWin, sizeof(Win)));
-    FX_TRY(hipMalloc(&dCtr, sizeof(Ctr)));
-    FX_TRY(hipMemset(dCtr, 0, sizeof(Ctr)));
+    FX_TRY(hipMalloc(&dCtrBase, 2 * sizeof(Ctr)));
+    FX_TRY(hipMemset(dCtrBase, 0, 2 * sizeof(Ctr)));
+    dCtr = dCtrBase;
     dExp = &dCtr->exp[0];  // device address, not dereferenced here
     FX_TRY(hipHostMalloc(&hWin, sizeof(Win), hipHostMallocDefault));
     FX_TRY(hipHostMalloc(&hCtr, sizeof(Ctr), hipHostMallocDefault));
@@ -1654,7 +1707,7 @@ struct Rank {
     const uint64_t tcap = 1ULL << lg;
     if (list_cap >= need && tmask + 1 == tcap) return 0;
     for (void *p : {(void *)F, (void *)Rl, (void *)Vl, (void *)tmp, (void *)tagR, (void *)tagV,
-                    (void *)keyR, (void *)keyV})
+                    (void *)tagR2, (void *)tagV2, (void *)keyR, (void *)keyV})
       if (p) (void)hipFree(p);
     FX_TRY(hipMalloc(&F, need * sizeof(Cfg)));
     FX_TRY(hipMalloc(&Rl, need * sizeof(Cfg)));
@@ -1666,6 +1719,15 @@ struct Rank {
     FX_TRY(hipMalloc(&keyV, tcap * sizeof(Cfg)));
     FX_TRY(hipMemsetAsync(tagR, 0, tcap * 8, st));
     FX_TRY(hipMemsetAsync(tagV, 0, tcap * 8, st));
+    if (!multi()) {  // (several ranks reset every return: fx_reset_kernel)
+      FX_TRY(hipMalloc(&tagR2, tcap * 8));
+      FX_TRY(hipMalloc(&tagV2, tcap * 8));
+      FX_TRY(hipMemsetAsync(tagR2, 0xFF, tcap * 8, st));  // EMPTY
+      FX_TRY(hipMemsetAsync(tagV2, 0xFF, tcap * 8, st));
+    }
+    dirtyC[0] = tcap;  // zeroed: epoch tags, not EMPTY
+    dirtyC[1] = 0;
+    prepped[0] = prepped[1] = false;
     for (void *p : {(void *)qQ, (void *)qtab[0][0], (void *)qtab[0][1], (void *)qtab[1][0],
                     (void *)qtab[1][1]})
       if (p) (void)hipFree(p);
@@ -1706,8 +1768,8 @@ struct Rank {
     Tabs t;
     t.compact = compact;
     t.cshift = cur_cshift;
-    t.tagR = tagR;
-    t.tagV = tagV;
+    t.tagR = compact && par ? tagR2 : tagR;
+    t.tagV = compact && par ? tagV2 : tagV;
     t.keyR = keyR;
     t.keyV = keyV;
     t.listR = Rl;
@@ -1728,7 +1790,7 @@ struct Rank {
     FX_TRY(hipStreamSynchronize(st));
     unsigned long long e = 0;
     for (int i = 0; i < kExpShards; i++) e += hCtr->exp[i * kExpStride];
-    hCtr->explored = e;
+    hCtr->explored = e + exp_off;
     return 0;
   }
 
@@ -1948,8 +2010,14 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   // F = {(init state, nothing linearized)}
   Cfg init{0, (uint32_t)opts.init_version, (uint32_t)vid(opts.init_value)};
   FX_TRY(hipMemcpyAsync(F, &init, sizeof(Cfg), hipMemcpyHostToDevice, st));
-  FX_TRY(hipMemsetAsync(dCtr, 0, sizeof(Ctr), st));
+  FX_TRY(hipMemsetAsync(dCtrBase, 0, 2 * sizeof(Ctr), st));
   FX_TRY(hipStreamSynchronize(st));
+  par = 0;
+  dCtr = dCtrBase;
+  dExp = &dCtr->exp[0];
+  prepped[0] = prepped[1] = false;
+  exp_off = 0;
+  int64_t levels_total = 0;  // levels expanded (each return's counters count from 0)
   int64_t nF = 1, nFglobal = 1;
   bool part = false;
   int64_t max_frontier = 1;
@@ -1965,6 +2033,8 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   const bool debug = getenv("LC_FX_DEBUG") != nullptr;
   const int64_t tmul = getenv("LC_FX_TABLE_MUL") ? std::max(1, atoi(getenv("LC_FX_TABLE_MUL"))) : 4;
   const int64_t spad = getenv("LC_FX_SPEC_PAD") ? atoi(getenv("LC_FX_SPEC_PAD")) : 1;
+  // A/B switch (dev): LC_FX_PREP=0 resets every return by a launch of its own
+  const bool allow_prep = !(getenv("LC_FX_PREP") && getenv("LC_FX_PREP")[0] == '0');
   // queue path: the version every configuration of a return has before the
   // mutation slots its mask names (the initial one plus every mutation that
   // left the window linearized: returned, or retired)
@@ -2186,23 +2256,40 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       tlog = 12;
       while (tlog < tlog_full && (1LL << tlog) < guess) tlog++;
     }
+    dCtr = dCtrBase + par;
+    dExp = &dCtr->exp[0];
+    // the replicated return by the grid (not one workgroup, not the queue path)
+    const bool grid_ret = !part && !(qpath && !multi() && compact && !n_cls) &&
+                          !(nF <= kSmallF && last_work <= kSmallWork);
     for (int attempt = 0;; attempt++) {
       const Tabs tb = tabs(tlog, compact, -1);  // the split appends V level 0
       epoch++;
       if (compact) {
         tags_dirty = true;  // one-word tables start EMPTY: the reset fills this attempt's prefix
-      } else if (tags_dirty) {
-        // back to epoch tags after compact returns: no stale word may look live
-        FX_TRY(hipMemsetAsync(tagR, 0, (tmask + 1) * 8, st));
-        FX_TRY(hipMemsetAsync(tagV, 0, (tmask + 1) * 8, st));
-        tags_dirty = false;
+      } else {
+        dirtyC[0] = tmask + 1;  // tagR / tagV hold epoch tags
+        if (tags_dirty) {
+          // back to epoch tags after compact returns: no stale word may look live
+          FX_TRY(hipMemsetAsync(tagR, 0, (tmask + 1) * 8, st));
+          FX_TRY(hipMemsetAsync(tagV, 0, (tmask + 1) * 8, st));
+          tags_dirty = false;
+        }
       }
-      {
+      // the previous return prepared this one's counters and tables (one
+      // rank, one-word tables, first attempt): no reset launch
+      const bool use_prep = attempt == 0 && compact && grid_ret && prepped[par] && !multi();
+      prepped[par] = false;
+      levels_seen = 0;  // (the reset and the preparation count levels from 0)
+      if (use_prep) {
+        exp_off = explored_seen;
+      } else {
+        exp_off = 0;
         const int64_t words = compact ? (int64_t)1 << tlog : 0;
-        fx_reset_kernel<<<grid_for(words), 256, 0, st>>>(dCtr, explored_seen, dExp, tagR, tagV,
+        fx_reset_kernel<<<grid_for(words), 256, 0, st>>>(dCtr, explored_seen, dExp, tb.tagR, tb.tagV,
                                                           words, kEmpty, dWin, w, !multi());
         FX_TRY(hipGetLastError());
       }
+      if (compact) dirtyC[par] = std::max<uint64_t>(dirtyC[par], 1ULL << tlog);
       bool tfull = false;
       if (qpath && !multi() && compact && !n_cls) {
         // one launch per attempt (fx_return_kernel): split, queue, report
@@ -2291,8 +2378,19 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           k = (int64_t)hCtr->kcur;
           done = hCtr->tfull || hCtr->overflow || hCtr->cnt[k % 3] == 0;
         } else if (nF) {
-          fx_insert_kernel<<<grid_for(nF), 256, 0, st>>>(F, nF, dWin, tb, epoch, dCtr);
+          // one rank, one-word tables: the split also prepares the next
+          // return (the other parity's counters, its tables to EMPTY)
+          const int q = par ^ 1;
+          const bool prep = !multi() && compact && allow_prep;
+          const int64_t pw = prep ? (int64_t)dirtyC[q] : 0;
+          fx_split_kernel<<<std::max(grid_for(nF), grid_for(pw)), 256, 0, st>>>(
+              F, nF, w, use_prep ? dWin : nullptr, tb, epoch, dCtr, prep ? dCtrBase + q : nullptr,
+              q ? tagR2 : tagR, q ? tagV2 : tagV, pw);
           FX_TRY(hipGetLastError());
+          if (prep) {
+            dirtyC[q] = 0;
+            prepped[q] = true;
+          }
         }
         const int g = (int)std::max<int64_t>(16, std::min<int64_t>(kExpandWG, (std::max(nF, last_work) + 3) / 4));
         for (int batch = 0; !done; batch++) {
@@ -2319,6 +2417,10 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           if (hCtr->cnt[k % 3] == 0) break;  // the last level found nothing new
           spec_levels = std::min(spec_levels * 2, 64);
         }
+        // levels this attempt expanded (a redone attempt's count too)
+        const int64_t used = (int64_t)hCtr->levels - levels_seen;
+        levels_seen = (int64_t)hCtr->levels;
+        levels_total += used;
         const bool my_tfull = hCtr->tfull != 0;
         const bool my_redo = my_tfull && tlog < tlog_full;
         const bool my_over = my_tfull || hCtr->overflow ||
@@ -2345,8 +2447,6 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           over = my_over;
         }
         // next return: as many speculative levels as this one needed, plus one
-        const int64_t used = (int64_t)hCtr->levels - levels_seen;
-        levels_seen = (int64_t)hCtr->levels;
         spec_levels = (int)std::max<int64_t>(spad > 0 ? 2 : 1, std::min<int64_t>(64, used + spad));
         const unsigned long long ex = hCtr->explored;
         explored_repl += (int64_t)(ex - explored_seen);
@@ -2452,6 +2552,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
       }
       break;
     }
+    if (!multi()) par ^= 1;  // the next return takes the other counters and tables
     if (over) {
       result_unknown(res, LC_REASON_CONFIG_BUDGET);
       decided = true;
@@ -2551,7 +2652,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   res->configs_explored = 1 + explored_repl + tot_part;
   res->max_frontier = max_frontier;
   FX_TRY(hipStreamSynchronize(st));
-  stats.levels = (int64_t)hCtr->levels + stats.part_levels;
+  stats.levels = levels_total + stats.part_levels;
   stats.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (qdbg_time) {
     fprintf(stderr, "fxq: returns %lld redos %lld launches %lld launch us %.1f sync us %.1f total ms %.2f\n",

@@ -673,10 +673,10 @@ int whole_gpu(lc_ctx *c, const std::vector<int64_t> &todo, const lc_opts *opts,
     }
   }
   // key-parallel: engines per GPU, bounded by its free memory (lists and
-  // tables take up to ~288 B per configuration of the budget)
+  // tables take up to ~352 B per configuration of the budget, two one-word table sets included)
   const int64_t budget = opts && opts->max_configs_per_key > 0 ? opts->max_configs_per_key
                                                                 : kDefaultBudget;
-  const double per_engine = 288.0 * (double)(budget + 1) + (64 << 20);
+  const double per_engine = 352.0 * (double)(budget + 1) + (64 << 20);
   for (int id : ids) {
     int have = 0;
     for (const auto &e : c->fxs) have += e.second == id;
