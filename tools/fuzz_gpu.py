@@ -114,5 +114,27 @@ for rd in range(rounds):
         print("%-34s keys %5d decided %5d mismatches %d" % ("fx ranks %d r%d" % (ranks, rd),
                                                             len(keys), ndec, nbad), flush=True)
         bad_total += nbad
+    # crash-heavy mutex keys (more crashed acquires / releases than the window
+    # holds): counted classes, on one rank and on two with every level partitioned
+    from helpers import FREE
+    keys = [random_mutex(rng, rng.randrange(100, 300), p_info=0.4, p_perturb=0.5) for _ in range(10)]
+    kops, koff = pack_keys(keys)
+    _, o = oracle.check(kops, koff, algo=oracle.JITC, n_threads=16, init_value=FREE)
+    mo = abi.default_opts(init_value=FREE)
+    for ranks, pa in ((1, -1), (2, 0)):
+        nbad = ndec = 0
+        with FrontierExchange(device=0, virtual_ranks=ranks, part_above=pa, table_log2=18) as fx:
+            for k in range(len(keys)):
+                r = fx.check(kops[koff[k]:koff[k + 1]], mo)
+                if r["verdict"] == -1 or o["verdict"][k] == -1:
+                    nbad += int(r["verdict"] != o["verdict"][k])
+                    continue
+                ndec += 1
+                if any(int(r[f]) != int(o[f][k]) for f in fields):
+                    nbad += 1
+                    print("   fx class key", k, [int(r[f]) for f in fields], [int(o[f][k]) for f in fields])
+        print("%-34s keys %5d decided %5d mismatches %d" % ("fx classes ranks %d r%d" % (ranks, rd),
+                                                            len(keys), ndec, nbad), flush=True)
+        bad_total += nbad
 print("TOTAL mismatches", bad_total)
 sys.exit(1 if bad_total else 0)
