@@ -314,6 +314,10 @@ __device__ int gap_setup(const GapKey &g, const GapWs<SL> &w, uint32_t cut) {
     w.B[k] = kNever;
     w.Pin[k] = -1;
     w.Claim[k] = kAny;
+#ifdef GAP_SETUP_TOUCH  // A/B: also touch the arrays pass 1 writes first
+    w.Val[k] = 0;
+    w.PinExp[k] = kAny;
+#endif
   }
   if (tid == 0) {
     sh.flag = 0;
@@ -510,7 +514,7 @@ __device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int
   GapSh &sh = *g.sh;
 #ifdef GAP_PROFILE
   const uint64_t t0 = wall_clock64();
-  if (tid < 8) s_mprof[tid] = 0;
+  if (tid < 12) s_mprof[tid] = 0;
 #endif
   const int st = gap_setup<T, SL>(g, w, cut);
   if (st != GD_VALID) return st;
@@ -581,9 +585,9 @@ __device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int
   }
 #ifdef GAP_PROFILE
   if (tid == 0 && blockIdx.x < 2) {
-    printf("  matching wg %d: first-fits %llu augments %llu steps %llu failed %llu | cycles: first-fit %llu augment %llu fill %llu; cursor steps %llu\n",
+    printf("  matching wg %d: first-fits %llu augments %llu steps %llu failed %llu | cycles: first-fit %llu augment %llu fill %llu; cursor steps %llu; bfs visit iters %llu cycles %llu ops %llu\n",
            (int)blockIdx.x, s_mprof[0], s_mprof[1], s_mprof[2], s_mprof[3], s_mprof[4],
-           s_mprof[5], s_mprof[7], s_mprof[6]);
+           s_mprof[5], s_mprof[7], s_mprof[6], s_mprof[8], s_mprof[9], s_mprof[11]);
   }
   if (tid == 0 && blockIdx.x < 2)
     printf("gap_decide wg %d cut %u n %d G %d n_opt %d lds %d nodes %ld: setup %lu [clr %lu p1 %lu (ld %lu c %lu %lu %lu %lu) pre %lu p2 %lu smin %lu chk %lu gcmp %lu] compact %lu match %lu (x10ns)\n",

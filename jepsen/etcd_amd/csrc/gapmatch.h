@@ -148,7 +148,7 @@ __device__ __forceinline__ bool scan_chunk(const Cmp<L> &c, const int4 gp, int b
 // matching counters of this workgroup: first-fits, augments, augment steps,
 // failed augments, cycles (first-fit, augment, cursor steps, fill); LDS adds
 // whose result is unused (no wait inside the timed sections)
-__shared__ unsigned long long s_mprof[8];
+__shared__ unsigned long long s_mprof[12];
 #define MPROF(i, v) \
   do { if ((threadIdx.x & 63) == 0) atomicAdd(&s_mprof[i], (unsigned long long)(v)); } while (0)
 // cycles of a section (s_memtime), and the wave-max of a per-lane loop count
@@ -553,6 +553,111 @@ __device__ bool augment_cls(const Cmp<L> &c, int g0, const int4 gp0, int stamp, 
   }
 }
 
+// Augmenting path from the unmatched gap g0 by breadth-first search over the
+// class cursors (the default; GAP_DFS_AUG selects augment_cls).  The depth-
+// first search above visits one op per step, and each step is a chain of
+// wave reductions and LDS round trips (≈1,000 cycles on C4); here a dequeued
+// gap visits, in one lane-parallel loop, EVERY unvisited op it can reach —
+// the prefix of each compatible class up to its deadline, all matched (a free
+// one would have ended the search) — and queues their gaps.  Visits stay
+// prefixes of each class list, so every op is visited at most once and every
+// gap queued at most once, as in the depth-first search; the search fails
+// iff no augmenting path leaves g0 (Kuhn).  Per gap the queue (aSR) and the
+// gap it was reached from (aSG, indexed by gap); the path is flipped from its
+// free end back to g0.
+template <bool L>
+__device__ bool augment_bfs_cls(const Cmp<L> &c, int g0, const int4 gp0, int stamp, ClsSt &st) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const auto ops = c.ops();
+  st.p = 0;
+  cls_head(c, st, 0, &st.po, &st.pc);
+  int po2;        // the op after the visit cursor's, and its call: a lane
+  uint32_t pc2;   // visits two per round trip
+  cls_head(c, st, 1, &po2, &pc2);
+  if (lane == 0) c.at(aSR, 0) = g0;
+  match_fence<L>();
+  int qh = 0, qt = 1;
+  while (qh < qt) {
+    MPROF(2, 1);
+    const int g = uni(c.at(aSR, qh));
+    qh = uni(qh + 1);
+    const int4 gp = g == g0 ? gp0 : uni4(c.gaps()[g]);
+    // a free eligible op ends the path here (class heads, then pinned ops)
+    uint32_t fcall = cls_key(st, gp, st.fc);
+    int fop = st.fo;
+    if (st.any_pin) {
+      for (int q = uni(c.at(aPH, g)); q >= 0; q = uni(c.at(aPN, q))) {
+        const int4 op = uni4(ops[q]);
+        if (!elig(gp, op)) continue;
+        const int mq = uni(c.at(aMO, q));
+        if (mq == -1) {
+          if ((uint32_t)op.x < fcall) {
+            fcall = (uint32_t)op.x;
+            fop = q;
+          }
+        } else if (uni(c.at(aVis, q)) != stamp) {  // a pinned matched op: visit it
+          if (lane == 0) {
+            c.at(aVis, q) = stamp;
+            c.at(aSR, qt) = mq;
+            c.at(aSG, mq) = g;
+          }
+          qt = uni(qt + 1);
+        }
+      }
+    }
+    const uint32_t fbest = wave_min_u32(fcall);
+    if (fbest != kNever) {
+      int o = uni(__builtin_amdgcn_readlane(fop, first_lane(__ballot(fcall == fbest))));
+      if (lane == uni(c.at(aCls, o))) st.ma++;  // matched now, at or past its class's free cursor
+      match_fence<L>();
+      for (int gg = g;;) {  // flip: each gap of the path takes the op that reached its successor
+        const int o_old = uni(c.at(aMG, gg));
+        const int par = uni(c.at(aSG, gg));
+        if (lane == 0) {
+          c.at(aMG, gg) = o;
+          c.at(aMO, o) = gg;
+          if constexpr (L)
+            if (st.mgr) c.mgr()[o] = c.gaps()[gg];
+        }
+        match_fence<L>();
+        if (gg == g0) break;
+        o = o_old;
+        gg = par;
+      }
+      return true;
+    }
+    // visit every unvisited op of the compatible classes called before the
+    // deadline (all matched: no free one is eligible), queueing their gaps
+    const bool compat = cls_compat(st, gp);
+    MCLK0(tv);
+    for (;;) {
+      const bool a1 = compat & (st.pc < (uint32_t)gp.x);
+      const bool a2 = a1 & (pc2 < (uint32_t)gp.x);
+      const uint64_t m1 = __ballot(a1), m2 = __ballot(a2);
+      if (!m1) break;
+      MPROF(8, 1);
+      MPROF(11, __popcll(m1) + __popcll(m2));
+      if (a1) {
+        const int mo1 = c.at(aMO, st.po);
+        const int mo2 = a2 ? c.at(aMO, po2) : 0;
+        c.at(aSR, qt + lanes_below(m1)) = mo1;
+        c.at(aSG, mo1) = g;
+        if (a2) {
+          c.at(aSR, qt + __popcll(m1) + lanes_below(m2)) = mo2;
+          c.at(aSG, mo2) = g;
+        }
+        st.p += a2 ? 2 : 1;
+        cls_head(c, st, st.p, &st.po, &st.pc);
+        cls_head(c, st, st.p + 1, &po2, &pc2);
+      }
+      qt = uni(qt + __popcll(m1) + __popcll(m2));
+    }
+    MCLK1(tv, 9);
+    match_fence<L>();
+  }
+  return false;
+}
+
 // Fill every unmatched gap (first-fit, else an augmenting path).  False as
 // soon as one cannot be filled: no matching covers all gaps (once no path
 // leaves a gap, none ever will in Kuhn's algorithm).
@@ -594,7 +699,11 @@ __device__ bool fill(const Cmp<L> &c, int G, int n_opt, int *ff, int *stamp, Cls
       bool ok;
       MCLK0(ta);
       if constexpr (CM) {
+#ifdef GAP_DFS_AUG
         ok = augment_cls(c, gi, gp, *stamp, st);
+#else
+        ok = augment_bfs_cls(c, gi, gp, *stamp, st);
+#endif
       } else {
         ok = augment(c, gi, n_opt, *stamp);
       }
