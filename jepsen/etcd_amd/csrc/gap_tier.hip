@@ -63,7 +63,10 @@ namespace lcdev {
 namespace {
 
 constexpr int kGapThreads = 256;
-constexpr int kGapWaves = kGapThreads / kWave;
+// a few long keys' full decisions (GapJob::threads = 512): twice the waves
+// for the setup's record passes and scans; the matching stays on wave 0
+constexpr int kGapWideThreads = 512;
+constexpr int kGapWaves = kGapWideThreads / kWave;  // (per-wave slots of the shared words)
 constexpr int kGapArrays = 31;     // 32-bit arrays of `cap` entries per workgroup
 
 enum { F_NA = 1, F_INVALID = 2 };
@@ -87,11 +90,13 @@ constexpr int kSkelLdsBytes = 4 * kSkelArrays;  // per record; the matching foll
 constexpr int kMatchReserve = 8 << 10;           // LDS kept for the matching after a skeleton
 
 // Skeleton arrays are addressed through pointers typed by placement: LDS
-// (address space 3) when SL, global otherwise, so the setup compiles to ds_*
-// / global_* instructions rather than flat ones (a flat access waits on both
-// the LDS and the vector-memory counters, and flat atomics to LDS are slow).
+// (address space 3) when SL, global (1) otherwise, so the setup compiles to
+// ds_* / global_* instructions rather than flat ones (a flat access waits on
+// both the LDS and the vector-memory counters, and flat atomics to LDS are
+// slow).  (Round 4: the HBM placement was generic — flat — until then.)
 template <bool SL, class X>
-using WsP = std::conditional_t<SL, __attribute__((address_space(3))) X *, X *>;
+using WsP = std::conditional_t<SL, __attribute__((address_space(3))) X *,
+                               __attribute__((address_space(1))) X *>;
 
 template <bool SL>
 struct GapWs {
@@ -105,6 +110,25 @@ struct GapWs {
   WsP<SL, uint64_t> Mask;  // compaction ballots
   WsP<SL, int> Pre;        // compaction prefix counts
 };
+
+// load_raw (records.h) through a global-address-space pointer: global_*
+// loads where the generic pointer of a non-inlined function gave flat ones
+__device__ __forceinline__ Raw load_raw_g(const __attribute__((address_space(1))) lc_op *o, int i,
+                                          int n) {
+  Raw r;
+  if (i < n) {
+    const __attribute__((address_space(1))) long long *q =
+        reinterpret_cast<const __attribute__((address_space(1))) long long *>(o + i);
+    r.a = make_longlong2(q[0], q[1]);
+    r.b = make_longlong2(q[2], q[3]);
+    r.c = make_longlong2(q[4], q[5]);
+  } else {
+    r.a = make_longlong2(0, -1);
+    r.b = make_longlong2(-1, -1);
+    r.c = make_longlong2(-1, -1);  // call = ret = -1 marks "past the end"
+  }
+  return r;
+}
 
 struct GapSh {
   int flag, maxpos, maxread, n_opt, n_gap;
@@ -226,14 +250,19 @@ __device__ int mask_prefix(const GapWs<SL> &w, int nw, GapSh &sh) {
   return tot;
 }
 
+using GOp = const __attribute__((address_space(1))) lc_op;  // records in global memory
+
 struct GapKey {
-  const lc_op *kops;
+  GOp *kops;
   int n;
   int64_t base;  // call index of the key's first record
   int V0, init;
   int pref_budget;  // GapJob::pref_budget
-  GapSh *sh;
 };
+
+// The workgroup's shared words, at namespace scope so every access is a ds_*
+// instruction (through a pointer carried in GapKey they were flat ones).
+__shared__ GapSh s_gsh;
 
 // One record of the prefix at `cut`, classified.
 enum { K_NONE, K_READ, K_PIN, K_OPT };
@@ -304,7 +333,7 @@ constexpr int kSetupBatch = 4;  // record chunks whose loads are in flight toget
 template <int T, bool SL>
 __device__ int gap_setup(const GapKey &g, const GapWs<SL> &w, uint32_t cut) {
   const int tid = threadIdx.x, n = g.n, wv = tid / kWave, lane = tid & (kWave - 1);
-  GapSh &sh = *g.sh;
+  GapSh &sh = s_gsh;
   // Every wave must be done reading the previous decision's shared words
   // (sh.flag on its early-return paths, sh.maxret) before thread 0 resets
   // them: decisions follow each other without a barrier in the bisection.
@@ -328,6 +357,9 @@ __device__ int gap_setup(const GapKey &g, const GapWs<SL> &w, uint32_t cut) {
     sh.n_gap = 0;
   }
   __syncthreads();
+#if GAP_STOP_AT == 1  // dev timing builds (with GAP_STOP_SETUP): end the setup early
+  return GD_VALID;
+#endif
 #ifdef GAP_PROFILE
   if (tid == 0) sh.prof[0] = wall_clock64();
 #endif
@@ -345,7 +377,7 @@ __device__ int gap_setup(const GapKey &g, const GapWs<SL> &w, uint32_t cut) {
 #pragma unroll
         for (int b = 0; b < kSetupBatch; b++) {
           const int r = (c0 + b) * T + tid;
-          raw[b] = load_raw(g.kops, r, n);
+          raw[b] = load_raw_g(g.kops, r, n);
           pc[b] = (r > 0 && r < n) ? g.kops[r - 1].call : -1;
         }
       }
@@ -398,6 +430,9 @@ __device__ int gap_setup(const GapKey &g, const GapWs<SL> &w, uint32_t cut) {
       if (maxread >= 0) atomicMax(&sh.maxread, maxread);
       if (maxret) atomicMax(&sh.maxret, maxret);
       __syncthreads();
+#if GAP_STOP_AT == 2
+      return GD_VALID;
+#endif
 #ifdef GAP_PROFILE
     if (tid == 0) sh.prof[1] = wall_clock64();
 #endif
@@ -411,6 +446,9 @@ __device__ int gap_setup(const GapKey &g, const GapWs<SL> &w, uint32_t cut) {
   }
   if (flag) atomicOr(&sh.flag, flag);
   __syncthreads();
+#if GAP_STOP_AT == 3
+  return GD_VALID;
+#endif
 #ifdef GAP_PROFILE
     if (tid == 0) sh.prof[3] = wall_clock64();
 #endif
@@ -508,16 +546,30 @@ __device__ void gap_witness(const GapKey &g, const GapWs<SL> &w, const C *c, int
 // (this key's witness records), a valid decision also writes its
 // linearization (gap_witness).
 template <int T, bool SL>
-__device__ int gap_decide(const GapKey &g, const GapWs<SL> &w, uint32_t cut, int lds_bytes,
+__device__ int gap_decide(const GapKey &g_arg, const GapWs<SL> &w_arg, uint32_t cut, int lds_bytes,
                           int64_t *nodes, int *n_gaps, int32_t *wk) {
   const int tid = threadIdx.x;
-  GapSh &sh = *g.sh;
+  GapSh &sh = s_gsh;
+  // local copies: through the caller's references every field was reloaded
+  // from the caller's stack after each store the compiler could not rule out
+  // aliasing it (this function is not inlined)
+  const GapKey g = g_arg;
+  const GapWs<SL> w = w_arg;
 #ifdef GAP_PROFILE
+#ifdef GAP_WARM  // dev: a first setup pass whose result is dropped (cold-code cost)
+  const uint64_t tw = wall_clock64();
+  (void)gap_setup<T, SL>(g, w, cut);
+  __syncthreads();
+  if (tid == 0 && blockIdx.x < 2) printf("warm setup %lu (x10ns)\n", (unsigned long)(wall_clock64() - tw));
+#endif
   const uint64_t t0 = wall_clock64();
   if (tid < 12) s_mprof[tid] = 0;
 #endif
   const int st = gap_setup<T, SL>(g, w, cut);
   if (st != GD_VALID) return st;
+#ifdef GAP_STOP_SETUP  // dev timing build: every decision ends after its setup (verdicts meaningless)
+  return GD_VALID;
+#endif
 #ifdef GAP_PROFILE
   const uint64_t t1 = wall_clock64();
 #endif
@@ -632,11 +684,10 @@ __global__ __launch_bounds__(T) void gap_tier_kernel(
     const int32_t *__restrict__ keys, const KParams p, lc_key_result *__restrict__ out,
     int32_t *__restrict__ ws, const int64_t cap, int32_t *__restrict__ pass_keys,
     KStatus *__restrict__ status, const GapJob job) {
-  __shared__ GapSh sh;
+  GapSh &sh = s_gsh;
   const int64_t key_base = key_off[0];
   GapKey g;
   int32_t *const ws_hbm = ws + (size_t)blockIdx.x * kGapArrays * cap;
-  g.sh = &sh;
   g.V0 = p.init_ver;
   g.init = p.init_val;
   g.pref_budget = job.pref_budget;
@@ -655,7 +706,7 @@ __global__ __launch_bounds__(T) void gap_tier_kernel(
         pass_keys[atomicAdd(&status->n_jit2, 1)] = (int32_t)key;
       continue;
     }
-    g.kops = ops + (beg - key_base);
+    g.kops = (GOp *)(ops + (beg - key_base));
     g.n = (int)(end - beg);
     g.base = g.kops[0].call;
     // the skeleton goes to LDS when it fits with room for a small matching
@@ -861,11 +912,14 @@ hipError_t launch_gap_tier(const lc_op *d_ops, const int64_t *d_key_off, const i
                            int64_t cap, int32_t *d_pass_keys, KStatus *d_status,
                            const GapJob &job, hipStream_t stream) {
   if (job.n_tasks <= 0) return hipSuccess;
-  return job.threads == kWave
-             ? launch_gap_tier_t<kWave>(d_ops, d_key_off, d_keys, p, d_out, d_ws, n_wg, cap,
-                                        d_pass_keys, d_status, job, stream)
-             : launch_gap_tier_t<kGapThreads>(d_ops, d_key_off, d_keys, p, d_out, d_ws, n_wg, cap,
+  if (job.threads == kWave)
+    return launch_gap_tier_t<kWave>(d_ops, d_key_off, d_keys, p, d_out, d_ws, n_wg, cap,
+                                    d_pass_keys, d_status, job, stream);
+  if (job.threads == kGapWideThreads)
+    return launch_gap_tier_t<kGapWideThreads>(d_ops, d_key_off, d_keys, p, d_out, d_ws, n_wg, cap,
                                               d_pass_keys, d_status, job, stream);
+  return launch_gap_tier_t<kGapThreads>(d_ops, d_key_off, d_keys, p, d_out, d_ws, n_wg, cap,
+                                        d_pass_keys, d_status, job, stream);
 }
 
 int gap_tier_resident(int lds_bytes) {

@@ -638,17 +638,19 @@ __device__ bool augment_bfs_cls(const Cmp<L> &c, int g0, const int4 gp0, int sta
       MPROF(8, 1);
       MPROF(11, __popcll(m1) + __popcll(m2));
       if (a1) {
+        // the visited ops' gaps and the next two heads in flight together
+        // (the head loads are issued before the stores that wait for the gaps)
         const int mo1 = c.at(aMO, st.po);
         const int mo2 = a2 ? c.at(aMO, po2) : 0;
+        st.p += a2 ? 2 : 1;
+        cls_head(c, st, st.p, &st.po, &st.pc);
+        cls_head(c, st, st.p + 1, &po2, &pc2);
         c.at(aSR, qt + lanes_below(m1)) = mo1;
         c.at(aSG, mo1) = g;
         if (a2) {
           c.at(aSR, qt + __popcll(m1) + lanes_below(m2)) = mo2;
           c.at(aSG, mo2) = g;
         }
-        st.p += a2 ? 2 : 1;
-        cls_head(c, st, st.p, &st.po, &st.pc);
-        cls_head(c, st, st.p + 1, &po2, &pc2);
       }
       qt = uni(qt + __popcll(m1) + __popcll(m2));
     }

@@ -93,6 +93,8 @@ constexpr int kGapProbeMinLen = 1024;
 #endif
 constexpr int kGapWaveMaxLen = LC_GAP_WAVE_MAX_LEN;  // keys up to this long: one-wave gap-tier workgroups
 constexpr int64_t kGapWaveMinKeys = 1024;             // ... when there are more of them than this
+constexpr int64_t kGapWideMaxKeys = 64;    // at most this many keys for the gap tier ...
+constexpr int kGapWideMinLen = 2048;        // ... the longest of them this long: 512-thread workgroups
 
 struct Dev {
   int id = -1;
@@ -423,8 +425,13 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     job.wit = want_wit ? wo.wit : nullptr;
     job.wkind = want_wit ? wo.kind : nullptr;
     // short keys: one-wave workgroups (barriers nearly free, 4x the decisions
-    // in flight); longer keys: 256 threads share each decision's setup
-    job.threads = wave_wg ? 64 : 256;
+    // in flight); longer keys: 256 threads share each decision's setup; a
+    // few long keys (C4): 512, whose extra waves halve the setup's record
+    // passes (the matching is one wave either way)
+    const char *wide_env = getenv("LC_GAP_WIDE");  // A/B: 0 keeps 256
+    const bool wide_wg = !(wide_env && wide_env[0] == '0') && n_jit <= kGapWideMaxKeys &&
+                         d.h_status->max_len >= kGapWideMinLen;
+    job.threads = wave_wg ? 64 : wide_wg ? 512 : 256;
     // Bisect counterexamples in place unless the keys are long and few
     // enough for multisection rounds to pay (each round costs two launches
     // and a sync; a probe of a short key costs less than that).

@@ -2,9 +2,9 @@ set -o pipefail
 mkdir -p gpurun_out/r4b
 timeout -k 10 400 python -u -m pytest tests/test_gpu.py tests/test_gpu_witness.py -x -q --timeout 200 --timeout-method thread -m gpu -k "gap or c4 or crash or witness or fused or mixed or golden" > gpurun_out/r4b/c4_test.log 2>&1 || { tail -30 gpurun_out/r4b/c4_test.log; exit 1; }
 tail -1 gpurun_out/r4b/c4_test.log
-for v in "" dfs touch "" dfs touch; do
-  echo "variant ${v:-head}"
-  if [ -n "$v" ]; then export LINCHECK_LIB=tools/variants/$v/liblincheck.so; else unset LINCHECK_LIB; fi
+for v in ${VARS:-head stopsetup head stopsetup}; do
+  echo "variant $v"
+  if [ "$v" != head ]; then export LINCHECK_LIB=tools/variants/$v/liblincheck.so; else unset LINCHECK_LIB; fi
   timeout -k 10 120 python tools/gap_probe.py 3 C4,C4x,C4x1004 2>/dev/null | python -c "
 import sys,json
 r={}
@@ -14,7 +14,7 @@ for l in sys.stdin:
 print(r)" || exit 1
 done
 unset LINCHECK_LIB
-for v in prof proftouch; do
+for v in ${PROFV:-}; do
   LINCHECK_LIB=tools/variants/$v/liblincheck.so timeout -k 10 120 python tools/gap_probe.py 1 C4,C4x > gpurun_out/r4b/gp_$v.log 2>&1 || exit 1
   grep -E "matching wg 0|gap_decide wg 0" gpurun_out/r4b/gp_$v.log | head -4 | cut -c1-330
 done
