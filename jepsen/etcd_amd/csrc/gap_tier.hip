@@ -51,6 +51,7 @@
 // cannot decide (an :ok mutation without a version, a read [nil x], malformed
 // records, the branch budget) go on to the JIT tier.
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <type_traits>
 
@@ -890,16 +891,30 @@ size_t gap_tier_ws_bytes(int n_wg, int64_t cap) {
   return (size_t)n_wg * kGapArrays * (size_t)cap * sizeof(int32_t);
 }
 
+constexpr int kMaxGapDevices = 64;
+
 template <int T>
 hipError_t launch_gap_tier_t(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
                              const KParams &p, lc_key_result *d_out, int32_t *d_ws, int n_wg,
                              int64_t cap, int32_t *d_pass_keys, KStatus *d_status,
                              const GapJob &job, hipStream_t stream) {
   if (job.lds_bytes > (64 << 10)) {  // beyond the default dynamic-LDS limit (gfx950: 160 KB per CU)
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(gap_tier_kernel<T>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             job.lds_bytes);
-    if (e != hipSuccess) return e;
+    // once per device and kernel at the largest size asked for (a runtime
+    // call on the launch path of every decision otherwise)
+    static std::atomic<int> granted[kMaxGapDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxGapDevices ||
+        granted[dev].load(std::memory_order_relaxed) < job.lds_bytes) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(gap_tier_kernel<T>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               job.lds_bytes);
+      if (e != hipSuccess) return e;
+      if (dev >= 0 && dev < kMaxGapDevices) {
+        int cur = granted[dev].load(std::memory_order_relaxed);
+        while (cur < job.lds_bytes && !granted[dev].compare_exchange_weak(cur, job.lds_bytes)) {
+        }
+      }
+    }
   }
   hipLaunchKernelGGL(gap_tier_kernel<T>, dim3((unsigned)n_wg), dim3(T), (unsigned)job.lds_bytes,
                      stream, d_ops, d_key_off, d_keys, p, d_out, d_ws, cap, d_pass_keys, d_status,
