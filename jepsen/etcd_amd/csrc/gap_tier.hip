@@ -937,13 +937,15 @@ hipError_t launch_gap_tier(const lc_op *d_ops, const int64_t *d_key_off, const i
                                         d_pass_keys, d_status, job, stream);
 }
 
-int gap_tier_resident(int lds_bytes) {
-  const void *fn = reinterpret_cast<const void *>(gap_tier_kernel<kGapThreads>);
+int gap_tier_resident(int lds_bytes, int threads) {
+  const void *fn = threads == kGapWideThreads
+                       ? reinterpret_cast<const void *>(gap_tier_kernel<kGapWideThreads>)
+                       : reinterpret_cast<const void *>(gap_tier_kernel<kGapThreads>);
   if (lds_bytes > (64 << 10) &&
       hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) != hipSuccess)
     return 0;
   int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kGapThreads, (size_t)lds_bytes) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, (size_t)lds_bytes) !=
           hipSuccess ||
       hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)

@@ -186,7 +186,7 @@ struct GapJob {
 size_t gap_tier_ws_bytes(int n_wg, int64_t cap);
 // 256-thread gap-tier workgroups with lds_bytes of dynamic LDS the device
 // holds at once (0 if the runtime cannot tell)
-int gap_tier_resident(int lds_bytes);
+int gap_tier_resident(int lds_bytes, int threads);
 hipError_t launch_gap_tier(const lc_op *d_ops, const int64_t *d_key_off, const int32_t *d_keys,
                            const KParams &p, lc_key_result *d_out, int32_t *d_ws, int n_wg,
                            int64_t cap, int32_t *d_pass_keys, KStatus *d_status,

@@ -134,6 +134,15 @@ struct Dev {
   int32_t *h_handoff = nullptr;         // host-coherent flag: fast tier handed keys over
   int32_t *h_handoff_dev = nullptr;     // its device address
   bool status_dirty = true;             // d_status may be non-zero
+  // the handoff flags may be non-zero (the fast tier raised some and no
+  // compaction, which clears them, followed)
+  bool flags_dirty = true;
+  // A fused call that handed nothing over copies its status without waiting
+  // for it (the counts only choose the next call's pass and fill this call's
+  // n_gap_keys): the next call, or lc_last_stats, settles it (settle_status).
+  hipEvent_t es = nullptr;
+  bool st_pending = false;
+  int64_t st_keys = 0;
   void *d_ws = nullptr;
   size_t ws_cap = 0;
   int32_t *d_wit = nullptr;            // lc_check_ex: device copies of the lc_aux outputs
@@ -260,11 +269,23 @@ int run_certificates(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off
   return 0;
 }
 
+// A fused call's lazily copied status (Dev::st_pending): choose the next
+// call's pass from it and return the keys the crash-light decision took (the
+// call's n_gap), or -1 when nothing was pending.
+int64_t settle_status(Dev &d) {
+  if (!d.st_pending) return -1;
+  d.st_pending = false;
+  if (hipEventSynchronize(d.es) != hipSuccess) return 0;
+  d.use_fused = 4 * (int64_t)d.h_status->n_light > d.st_keys;
+  return d.h_status->n_light;
+}
+
 // Run the tiers for n_keys keys whose device arrays are in place.
 int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                int64_t n_keys, const lcdev::KParams &p,
                lc_key_result *d_out, hipStream_t st, int64_t flags,
                const WitOut &wo = WitOut()) {
+  (void)settle_status(d);  // before use_fused or h_status is read
   d.kernel_ms = d.hbm_ms = d.fast_ms = d.jit_ms = d.gap_ms = 0;
   d.n_hbm = d.n_jit = d.n_gap = 0;
   d.malformed = 0;
@@ -281,8 +302,9 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   const bool flags_new = d.flags_cap < sizeof(int32_t) * (size_t)n_keys || !d.d_flags;
   if (!rc) rc = ensure(c, &d.d_flags, &d.flags_cap, sizeof(int32_t) * (size_t)n_keys);
   if (rc) return rc;
-  if (flags_new || d.status_dirty)  // the flags are all-zero between clean calls
+  if (flags_new || d.flags_dirty)  // the flags are all-zero between calls that completed
     HIP_TRY(c, hipMemsetAsync(d.d_flags, 0, d.flags_cap, st));
+  d.flags_dirty = false;
   // With the gap tier on, the fast tier sends keys it can only pass on (no
   // version on an :ok mutation, a read [nil x], malformed) straight to the
   // JIT list d_jit2, which the gap tier then appends to.
@@ -314,6 +336,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     // the previous call on this device (LC_FUSED=0/1 forces it).
     const char *fenv = getenv("LC_FUSED");
     fused = gap_on && (fenv ? fenv[0] == '1' : d.use_fused);
+    d.flags_dirty = true;  // until the handoff (if any) is compacted
     if (fused)
       HIP_TRY(c, lcdev::launch_fused_tier(d_ops, d_off, n_keys, p, d_out, d.d_flags, d.d_status,
                                           d.h_handoff_dev, want_wit ? wo.wit : nullptr,
@@ -328,19 +351,22 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     n_jit = 0;
     jit_list = d.d_jit;
     const bool handed = __atomic_load_n(d.h_handoff, __ATOMIC_ACQUIRE) != 0;
+    if (!handed) d.flags_dirty = false;  // no key raised its flag
     if (fused && !handed) {
       // every key decided in the one pass: were most of them crash-light?
+      // (the answer picks the next call's pass; copied now, read later)
       HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                                 hipMemcpyDeviceToHost, st));
-      HIP_TRY(c, hipStreamSynchronize(st));
-      d.use_fused = 4 * (int64_t)d.h_status->n_light > n_keys;
-      d.n_gap = d.h_status->n_light;  // keys the crash-light decision took
+      HIP_TRY(c, hipEventRecord(d.es, st));
+      d.st_pending = true;
+      d.st_keys = n_keys;
       d.status_dirty = true;
     }
     if (handed) {
       HIP_TRY(c, lcdev::launch_handoff_compact(d.d_flags, d_off, n_keys, gap_on ? 1 : 0, d.d_jit,
                                                d.d_jit2, d.d_status, want_wit ? wo.kind : nullptr,
                                                st));
+      d.flags_dirty = false;  // the compaction clears every flag it reads
       // the crash-light pass reads the list and its length from the device:
       // no host round trip between the compaction and it.  After the fused
       // pass too: the keys it hands over are invalid or beyond the in-place
@@ -460,12 +486,16 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       // counterexamples of long keys: P probes per interval per round, over
       // the whole GPU
       job.mode = lcdev::kGapProbe;
-      job.threads = 256;
+      // the probes of a few long keys: 512-thread workgroups as for their full
+      // decisions (half as many probes per round; C4's interval still closes in
+      // two rounds)
+      const char *wp_env = getenv("LC_GAP_WIDE_PROBE");  // A/B: 0 keeps 256
+      job.threads = wide_wg && !(wp_env && wp_env[0] == '0') ? 512 : 256;
       job.lds_bytes = no_lds ? 0 : kGapLdsProbe;
       // as many probes as run at once: a round's time is its slowest batch
       // of resident workgroups, and a second batch doubles it for a few
       // more cuts (C4 invalid: 1,024 probes = two batches of 512 resident)
-      const int resident = lcdev::gap_tier_resident(job.lds_bytes);
+      const int resident = lcdev::gap_tier_resident(job.lds_bytes, job.threads);
       job.P = (resident / n_cex >= 2 ? std::min(resident, wg_cap) : wg_cap) / n_cex;
       job.n_tasks = n_cex * job.P;
       rc = ensure(c, reinterpret_cast<char **>(&d.d_gws), &d.gws_cap,
@@ -784,6 +814,7 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
           hipEventCreateWithFlags(&d.el, kEventFlags) != hipSuccess ||
           hipEventCreateWithFlags(&d.eh0, kEventFlags) != hipSuccess ||
           hipEventCreateWithFlags(&d.eh1, kEventFlags) != hipSuccess ||
+          hipEventCreateWithFlags(&d.es, kEventFlags) != hipSuccess ||
           hipMalloc(reinterpret_cast<void **>(&d.d_status), sizeof(lcdev::KStatus)) != hipSuccess ||
           hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess ||
           hipHostMalloc(reinterpret_cast<void **>(&d.h_handoff), sizeof(int32_t),
@@ -826,6 +857,8 @@ void lc_close(lc_ctx *c) {
     if (d.e1) (void)hipEventDestroy(d.e1);
     if (d.e2) (void)hipEventDestroy(d.e2);
     if (d.ef) (void)hipEventDestroy(d.ef);
+    for (hipEvent_t e : {d.eg, d.el, d.eh0, d.eh1, d.es})
+      if (e) (void)hipEventDestroy(e);
     if (d.d_jit) (void)hipFree(d.d_jit);
     if (d.d_jit2) (void)hipFree(d.d_jit2);
     if (d.d_flags) (void)hipFree(d.d_flags);
@@ -850,6 +883,11 @@ const char *lc_last_error(lc_ctx *c) { return c ? c->err.c_str() : "null context
 
 int lc_last_stats(lc_ctx *c, lc_stats *out) {
   if (!c || !out) return -EINVAL;
+  // the keys the crash-light decision took in a fused call, copied lazily
+  for (Dev &d : c->devs) {
+    const int64_t n = settle_status(d);
+    if (n > 0) c->stats.n_gap_keys += n;
+  }
   *out = c->stats;
   return 0;
 }
