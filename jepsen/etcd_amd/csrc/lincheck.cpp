@@ -360,7 +360,10 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       HIP_TRY(c, hipEventRecord(d.es, st));
       d.st_pending = true;
       d.st_keys = n_keys;
-      d.status_dirty = true;
+      // zeroed behind the copy now (while the host returns), not at the
+      // start of the next call
+      HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
+      d.status_dirty = false;
     }
     if (handed) {
       HIP_TRY(c, lcdev::launch_handoff_compact(d.d_flags, d_off, n_keys, gap_on ? 1 : 0, d.d_jit,
@@ -403,8 +406,10 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   }
   if (n_jit == 0 && n_direct == 0) {
     d.kernel_ms = d.fast_ms + d.gap_ms;
-    // after a handoff d_status is not zero: the next call clears it (async)
-    d.status_dirty = light;
+    // after a handoff d_status is not zero: cleared behind this call's work
+    // (the host has read it), not in front of the next call's
+    if (light) HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
+    d.status_dirty = false;
     return 0;
   }
   hipEvent_t before_jit = light ? d.el : d.ef;
