@@ -1393,7 +1393,7 @@ __global__ __launch_bounds__(kWave *kWavesPerWG) void lds_tier_kernel(
 #endif
 constexpr int kFastThreads = 256;
 constexpr int kFastWaves = kFastThreads / kWave;
-constexpr int kFastMax = 1024;
+constexpr int kFastMax = kFastMaxRecords;
 constexpr int kPer = kFastMax / kFastThreads;  // records per thread
 
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }

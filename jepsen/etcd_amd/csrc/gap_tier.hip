@@ -692,7 +692,8 @@ __global__ __launch_bounds__(T) void gap_tier_kernel(
   g.V0 = p.init_ver;
   g.init = p.init_val;
   g.pref_budget = job.pref_budget;
-  for (int t = blockIdx.x; t < job.n_tasks; t += gridDim.x) {
+  const int32_t n_tasks = job.n_tasks_dev ? min(job.n_tasks, *job.n_tasks_dev) : job.n_tasks;
+  for (int t = blockIdx.x; t < n_tasks; t += gridDim.x) {
     int ci = -1;  // counterexample index (probe / bisect)
     int64_t key;
     if (job.mode == kGapFull) {

@@ -18,6 +18,11 @@ struct KParams {
 };
 
 // Device-side status words, zeroed before every call.
+// Longest key the version-order tier and the crash-light pass decide (4
+// records per thread of a 256-thread workgroup); longer keys go on to the gap
+// tier proper.
+constexpr int kFastMaxRecords = 1024;
+
 struct KStatus {
   int32_t malformed;    // keys with LC_REASON_MALFORMED
   int32_t n_overflow;   // keys appended to the overflow list (LDS tier full)
@@ -182,6 +187,9 @@ struct GapJob {
   int32_t *probe;      // [n_cex * P] probe verdicts
   int32_t *wit;        // lc_aux witness (per record, indexed like the ops), or null
   int32_t *wkind;      // lc_aux witness kind (per key)
+  // kGapFull launched before the host has read the task count (lincheck.cpp,
+  // "launched early"): the count on the device, capped by n_tasks; or null
+  const int32_t *n_tasks_dev;
 };
 size_t gap_tier_ws_bytes(int n_wg, int64_t cap);
 // 256-thread gap-tier workgroups with lds_bytes of dynamic LDS the device

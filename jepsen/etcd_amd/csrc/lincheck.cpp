@@ -252,6 +252,19 @@ struct WitOut {
   int32_t *cert = nullptr;  // per key, 4 int32 (infeasibility certificates)
   int32_t *cset = nullptr;  // per record (HALL position sets)
   int64_t n_records = 0;
+  // (not an output) the shard's key offsets in host memory when the caller
+  // has them (lc_check_ex): the gap tier may then be launched early
+  const int64_t *h_off = nullptr;
+};
+
+// A gap-tier full-decision launch: its sizes and job (run_device).
+struct GapPlan {
+  int64_t gap_cap = 0;     // workspace entries per array per workgroup
+  size_t gap_per_wg = 0;
+  int wg_cap = 0, full_wg = 0;
+  bool wide_wg = false, no_lds = false;
+  size_t nk = 0;           // counterexample slots (the cex arrays' stride)
+  lcdev::GapJob job{};
 };
 
 // Infeasibility certificates for the invalid keys of a run_device call
@@ -316,6 +329,74 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
   d.status_dirty = true;
   float ms = 0;
+  // the gap tier's full-decision launch for keys up to max_len records long,
+  // nj of them at most (buffers ensured)
+  auto gap_plan = [&](int64_t max_len, int64_t nj, GapPlan &g) -> int {
+    g.gap_cap = (max_len + 2 + 3) & ~int64_t(3);  // 16-B records
+    g.gap_per_wg = lcdev::gap_tier_ws_bytes(1, g.gap_cap);
+    if (g.gap_per_wg > kGapWsBytes) return 0;  // (the caller checks)
+    g.wg_cap = (int)std::min<int64_t>(
+        (int64_t)kGapMaxWG, std::max<int64_t>(1, (int64_t)(kGapWsBytes / g.gap_per_wg)));
+    // many short keys: one-wave workgroups, four times as many decisions in
+    // flight (10k 200-op keys: 0.78 -> 0.45 ms); few keys are latency-bound
+    // and decide faster with 256 threads each (94 keys: 0.19 vs 0.145 ms)
+    const bool wave_wg = max_len <= kGapWaveMaxLen && nj > kGapWaveMinKeys;
+    g.full_wg = (int)std::min<int64_t>(nj, wave_wg ? 4 * (int64_t)g.wg_cap : g.wg_cap);
+    int rc2 = ensure(c, reinterpret_cast<char **>(&d.d_gws), &d.gws_cap,
+                     lcdev::gap_tier_ws_bytes(g.full_wg, g.gap_cap));
+    // counterexample intervals: key, lo, hi, gaps, state (int32), nodes
+    // (int64) per invalid key, and one int32 per probe workgroup
+    g.nk = (size_t)nj;
+    if (!rc2) rc2 = ensure(c, &d.d_cex, &d.cex_cap, g.nk * (5 * 4 + 8) + 4 * (size_t)g.wg_cap + 64);
+    if (rc2) return rc2;
+    lcdev::GapJob &job = g.job;
+    job = lcdev::GapJob{};
+    // LC_GAP_PREF_BUDGET (tests): a tiny budget sends every branching decision
+    // through the plain-order rerun
+    const char *pb_env = getenv("LC_GAP_PREF_BUDGET");
+    job.pref_budget = pb_env ? std::max(1, atoi(pb_env)) : lcdev::kGapPrefBudget;
+    const size_t nk = g.nk;
+    job.cex_nodes = reinterpret_cast<int64_t *>(d.d_cex);
+    job.cex_key = reinterpret_cast<int32_t *>(d.d_cex + 8 * nk);
+    job.cex_lo = reinterpret_cast<uint32_t *>(job.cex_key + nk);
+    job.cex_hi = job.cex_lo + nk;
+    job.cex_gaps = reinterpret_cast<int32_t *>(job.cex_hi + nk);
+    job.cex_state = job.cex_gaps + nk;
+    job.probe = job.cex_state + nk;
+    job.mode = lcdev::kGapFull;
+    job.n_tasks = (int32_t)nj;
+    const bool wants_wit = wo.wit && wo.kind;
+    job.wit = wants_wit ? wo.wit : nullptr;
+    job.wkind = wants_wit ? wo.kind : nullptr;
+    // short keys: one-wave workgroups (barriers nearly free, 4x the decisions
+    // in flight); longer keys: 256 threads share each decision's setup; a
+    // few long keys (C4): 512, whose extra waves halve the setup's record
+    // passes (the matching is one wave either way)
+    const char *wide_env = getenv("LC_GAP_WIDE");  // A/B: 0 keeps 256
+    g.wide_wg = !(wide_env && wide_env[0] == '0') && nj <= kGapWideMaxKeys &&
+                max_len >= kGapWideMinLen;
+    job.threads = wave_wg ? 64 : g.wide_wg ? 512 : 256;
+    // Bisect counterexamples in place unless the keys are long and few
+    // enough for multisection rounds to pay (each round costs two launches
+    // and a sync; a probe of a short key costs less than that).
+    job.bisect = max_len < kGapProbeMinLen || 2 * nj > g.wg_cap;
+    // LDS per workgroup: the longest key's skeleton (68 B per record) plus
+    // 8 KB for its matching when that stays within kGapSkelLdsMax (two
+    // workgroups per CU); else room for the matching alone (80 B per record
+    // plus its class table at worst), up to kGapLdsFull, or kGapLdsFew when
+    // there are few keys
+    const int64_t skel = 68 * g.gap_cap + (8 << 10);
+    const int64_t match_cap = nj <= kGapFewKeys ? kGapLdsFew : kGapLdsFull;
+    job.lds_bytes = (int)(skel <= kGapSkelLdsMax ? skel
+                                                 : std::min<int64_t>(match_cap, 80 * g.gap_cap + 1040));
+    // LC_GAP_LDS=0 (tests): keep every matching in the HBM workspace
+    const char *lds_env = getenv("LC_GAP_LDS");
+    g.no_lds = lds_env && lds_env[0] == '0';
+    if (g.no_lds) job.lds_bytes = 0;
+    return 0;
+  };
+  GapPlan early;              // the gap tier launched early (below), if it was
+  bool early_launched = false;
   bool light = false;  // the crash-light pass ran (its time is in gap_ms)
   bool fused = false;  // the version-order and crash-light decisions ran as one pass
   int64_t n_jit = n_keys;
@@ -381,6 +462,28 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                                            d.d_status, want_wit ? wo.wit : nullptr,
                                            want_wit ? wo.kind : nullptr, st));
         HIP_TRY(c, hipEventRecord(d.el, st));
+        // Launched early: a few keys, one longer than the light pass holds
+        // (kFastMaxRecords: it goes on to the gap tier proper) and the
+        // shard's offsets in host memory — the full decisions start right
+        // behind the light pass, sized from those offsets, their count read
+        // on the device (GapJob::n_tasks_dev), instead of after a host round
+        // trip for the status.  Same decisions, same results.
+        if (wo.h_off && n_keys <= kGapWideMaxKeys) {
+          int64_t ml = 0;
+          for (int64_t k = 0; k < n_keys; k++) ml = std::max<int64_t>(ml, wo.h_off[k + 1] - wo.h_off[k]);
+          const char *ee = getenv("LC_GAP_EARLY");  // A/B: 0 waits for the status
+          if (ml > lcdev::kFastMaxRecords && !(ee && ee[0] == '0')) {
+            if (int e = gap_plan(ml, n_keys, early)) return e;
+            if (early.gap_per_wg <= kGapWsBytes) {
+              early.job.n_tasks_dev = &d.d_status->n_gap2;
+              HIP_TRY(c, lcdev::launch_gap_tier(d_ops, d_off, d.d_gap2, p, d_out, d.d_gws,
+                                                early.full_wg, early.gap_cap, d.d_jit2, d.d_status,
+                                                early.job, st));
+              HIP_TRY(c, hipEventRecord(d.eg, st));
+              early_launched = true;
+            }
+          }
+        }
       }
       HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
                                 hipMemcpyDeviceToHost, st));
@@ -425,67 +528,21 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   } else if (gap_on) {
     // tier 1: gap matching for version-pinned keys (crashed writes/CAS, long
     // keys, invalid keys); what it cannot decide goes on to the JIT search
-    const int wg_cap = (int)std::min<int64_t>(
-        (int64_t)kGapMaxWG, std::max<int64_t>(1, (int64_t)(kGapWsBytes / gap_per_wg)));
-    // many short keys: one-wave workgroups, four times as many decisions in
-    // flight (10k 200-op keys: 0.78 -> 0.45 ms); few keys are latency-bound
-    // and decide faster with 256 threads each (94 keys: 0.19 vs 0.145 ms)
-    const bool wave_wg = d.h_status->max_len <= kGapWaveMaxLen && n_jit > kGapWaveMinKeys;
-    const int full_wg = (int)std::min<int64_t>(n_jit, wave_wg ? 4 * (int64_t)wg_cap : wg_cap);
-    rc = ensure(c, reinterpret_cast<char **>(&d.d_gws), &d.gws_cap,
-                lcdev::gap_tier_ws_bytes(full_wg, gap_cap));
-    // counterexample intervals: key, lo, hi, gaps, state (int32), nodes
-    // (int64) per invalid key, and one int32 per probe workgroup
-    const size_t nk = (size_t)n_jit;
-    if (!rc) rc = ensure(c, &d.d_cex, &d.cex_cap, nk * (5 * 4 + 8) + 4 * (size_t)wg_cap + 64);
-    if (rc) return rc;
-    lcdev::GapJob job{};
-    // LC_GAP_PREF_BUDGET (tests): a tiny budget sends every branching decision
-    // through the plain-order rerun
-    const char *pb_env = getenv("LC_GAP_PREF_BUDGET");
-    job.pref_budget = pb_env ? std::max(1, atoi(pb_env)) : lcdev::kGapPrefBudget;
-    job.cex_nodes = reinterpret_cast<int64_t *>(d.d_cex);
-    job.cex_key = reinterpret_cast<int32_t *>(d.d_cex + 8 * nk);
-    job.cex_lo = reinterpret_cast<uint32_t *>(job.cex_key + nk);
-    job.cex_hi = job.cex_lo + nk;
-    job.cex_gaps = reinterpret_cast<int32_t *>(job.cex_hi + nk);
-    job.cex_state = job.cex_gaps + nk;
-    job.probe = job.cex_state + nk;
-    job.mode = lcdev::kGapFull;
-    job.n_tasks = (int32_t)n_jit;
-    job.wit = want_wit ? wo.wit : nullptr;
-    job.wkind = want_wit ? wo.kind : nullptr;
-    // short keys: one-wave workgroups (barriers nearly free, 4x the decisions
-    // in flight); longer keys: 256 threads share each decision's setup; a
-    // few long keys (C4): 512, whose extra waves halve the setup's record
-    // passes (the matching is one wave either way)
-    const char *wide_env = getenv("LC_GAP_WIDE");  // A/B: 0 keeps 256
-    const bool wide_wg = !(wide_env && wide_env[0] == '0') && n_jit <= kGapWideMaxKeys &&
-                         d.h_status->max_len >= kGapWideMinLen;
-    job.threads = wave_wg ? 64 : wide_wg ? 512 : 256;
-    // Bisect counterexamples in place unless the keys are long and few
-    // enough for multisection rounds to pay (each round costs two launches
-    // and a sync; a probe of a short key costs less than that).
-    job.bisect = d.h_status->max_len < kGapProbeMinLen || 2 * n_jit > wg_cap;
-    // LDS per workgroup: the longest key's skeleton (68 B per record) plus
-    // 8 KB for its matching when that stays within kGapSkelLdsMax (two
-    // workgroups per CU); else room for the matching alone (80 B per record
-    // plus its class table at worst), up to kGapLdsFull, or kGapLdsFew when
-    // there are few keys
-    const int64_t skel = 68 * gap_cap + (8 << 10);
-    const int64_t match_cap = n_jit <= kGapFewKeys ? kGapLdsFew : kGapLdsFull;
-    job.lds_bytes = (int)(skel <= kGapSkelLdsMax ? skel
-                                                 : std::min<int64_t>(match_cap, 80 * gap_cap + 1040));
-    // LC_GAP_LDS=0 (tests): keep every matching in the HBM workspace
-    const char *lds_env = getenv("LC_GAP_LDS");
-    const bool no_lds = lds_env && lds_env[0] == '0';
-    if (no_lds) job.lds_bytes = 0;
-    HIP_TRY(c, lcdev::launch_gap_tier(d_ops, d_off, jit_list, p, d_out, d.d_gws,
-                                      full_wg, gap_cap, d.d_jit2,
-                                      d.d_status, job, st));
-    HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
-                              hipMemcpyDeviceToHost, st));
-    HIP_TRY(c, hipStreamSynchronize(st));
+    GapPlan g;
+    if (early_launched) {
+      g = early;  // launched behind the light pass; the status read since includes it
+    } else {
+      if (int e = gap_plan(d.h_status->max_len, n_jit, g)) return e;
+      HIP_TRY(c, lcdev::launch_gap_tier(d_ops, d_off, jit_list, p, d_out, d.d_gws, g.full_wg,
+                                        g.gap_cap, d.d_jit2, d.d_status, g.job, st));
+      HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
+                                hipMemcpyDeviceToHost, st));
+      HIP_TRY(c, hipStreamSynchronize(st));
+    }
+    lcdev::GapJob &job = g.job;
+    job.n_tasks_dev = nullptr;
+    const int wg_cap = g.wg_cap;
+    const bool wide_wg = g.wide_wg, no_lds = g.no_lds;
     const int32_t n_cex = d.h_status->n_cex;
     if (n_cex > 0) {
       // counterexamples of long keys: P probes per interval per round, over
@@ -535,10 +592,12 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                                           d.d_status, job, st));
       }
     }
-    HIP_TRY(c, hipEventRecord(d.eg, st));
-    HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
-                              hipMemcpyDeviceToHost, st));
-    HIP_TRY(c, hipStreamSynchronize(st));
+    if (!early_launched || n_cex > 0) {  // (launched early and done: the status is current)
+      HIP_TRY(c, hipEventRecord(d.eg, st));
+      HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
+                                hipMemcpyDeviceToHost, st));
+      HIP_TRY(c, hipStreamSynchronize(st));
+    }
     HIP_TRY(c, hipEventElapsedTime(&ms, d.ef, d.eg));
     d.gap_ms = ms;
     if (!light && !fused) d.n_gap = n_jit;
@@ -1161,6 +1220,7 @@ int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
       wo.cert = d.d_cert;
       wo.cset = d.d_cset;
     }
+    wo.h_off = key_off + a;
     r = run_device(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, nk, p,
                    d.d_out, d.stream, flags, wo);
     if (!r) r = run_certificates(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, nk, p,

@@ -281,3 +281,27 @@ def test_malformed_key_is_unknown_alone(ctx):
     assert r["reason"][0] == abi.LC_REASON_MALFORMED and ctx.stats()["n_malformed"] == 1
     _, o = oracle.check(ops[off[1]:], off[1:] - off[1], algo=oracle.JIT)
     assert (r["verdict"][1:] == o["verdict"]).all() and (r["fail_op"][1:] == o["fail_op"]).all()
+
+
+@pytest.mark.parametrize("seed", [61, 62])
+def test_gap_tier_early_launch_equal(ctx, monkeypatch, seed):
+    """A few long keys: the gap tier proper is launched right behind the
+    crash-light pass (sized from the host offsets, its task count read on the
+    device) instead of after a host round trip for the status.  Same results
+    and witnesses as the waiting launch, on valid and invalid long keys mixed
+    with short ones the light pass decides alone."""
+    lng, lo, _, _ = abi.synth(6, 2500, concurrency=30, p_info=0.2, info_frac=0.2,
+                              p_anomaly=0.5, seed=seed)
+    sht, so, _, _ = abi.synth(10, 60, concurrency=6, p_info=0.2, p_anomaly=0.3, seed=seed + 100)
+    keys = [lng[lo[k]:lo[k + 1]].tolist() for k in range(6)]
+    keys += [sht[so[k]:so[k + 1]].tolist() for k in range(10)]
+    ops, off = pack_keys(keys)
+    outs = []
+    for early in ("0", "1"):
+        monkeypatch.setenv("LC_GAP_EARLY", early)
+        _, r, wit, kind = ctx.check(ops, off, witness=True)
+        outs.append((r, wit, kind))
+    (a, wa, ka), (b, wb, kb) = outs
+    assert (a == b).all() and (ka == kb).all() and (wa == wb).all()
+    certify(ops, off, b, wb, kb)
+    assert (b["verdict"][:6] == 0).any() and (b["verdict"] == 1).any()
