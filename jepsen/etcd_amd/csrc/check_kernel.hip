@@ -33,6 +33,7 @@
 // same returns as knossos's, verdicts and counterexample prefixes are
 // unchanged, and the 2^k subsets of concurrent reads never materialise.
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <type_traits>
 
@@ -1391,6 +1392,12 @@ __global__ __launch_bounds__(kWave *kWavesPerWG) void lds_tier_kernel(
 #ifndef LC_FAST_DEV
 #define LC_FAST_DEV 0  // dev timing switches (tools/build_variants.sh); 0 in the product
 #endif
+// The version-order and fused kernels: one workgroup per key (0), or
+// persistent workgroups that issue the next key's loads while deciding a key
+// from LDS (1, fast_run; more VGPRs per thread, measured slower: DESIGN.md).
+#ifndef LC_PIPE
+#define LC_PIPE 0
+#endif
 constexpr int kFastThreads = 256;
 constexpr int kFastWaves = kFastThreads / kWave;
 constexpr int kFastMax = kFastMaxRecords;
@@ -1429,8 +1436,12 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // keys: 0.11 -> 0.67 ms), so a workgroup stores only if the device-side
 // any_handoff word still reads 0 (a few racing stores at most).
 __device__ __forceinline__ void fast_tier_handoff(int64_t key, int32_t *flags, KStatus *status,
-                                                  int32_t *h_handoff, bool jit_only = false) {
+                                                  int32_t *h_handoff, bool jit_only, int *raised) {
   flags[key] = jit_only ? 2 : 1;
+  // once per workgroup (the persistent kernels decide many keys each): the
+  // device-side word is read with every load in flight drained first
+  if (*raised) return;
+  *raised = 1;
   if (__hip_atomic_load(&status->any_handoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
     __hip_atomic_store(&status->any_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(h_handoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1441,36 +1452,59 @@ __device__ __forceinline__ void fast_tier_handoff(int64_t key, int32_t *flags, K
   }
 }
 
-// 14.4 KB of LDS per workgroup (7 workgroups per CU at 72 VGPRs).
+// 14.5 KB of LDS per workgroup (7 workgroups per CU at 72 VGPRs).
 // Index k of A/B is mutation position k (version V0+k+1):
 //   A[k] = max(call(m_k), calls of reads of version V0+k) + 1     (= L_k + 1)
 //   B[k] = min(ret(m_k),  rets of reads of version V0+k+1)        (= U_k)
-// Both are single LDS atomics per record.  Val/Own are plain stores: the
-// value and the key-relative record index of the mutation placed at k; a
-// second pass checks value claims and CAS expectations against Val, and a
-// mutation that finds another record's index in Own[k] shares its version
-// with it (two stores raced, one lost).  Per-wave summaries (counts, flags,
-// verdicts) go to per-wave slots, so there are no same-address atomics and
-// no slots to clear.
+// Both are single LDS atomics per record.  Val[k] is the value the state at
+// version V0+k+1 must hold, claimed with one LDS compare-and-swap from kAny
+// by every record that fixes it — the mutation placed at k (its value), the
+// reads of that version and a CAS pinned right after it (their values and
+// expectations): two different claims fail the key whatever order they land
+// in, so the value checks need no second pass over the records.  Own[k] is
+// the key-relative record index of the mutation placed at k (a plain store;
+// two mutations on one version leave a position unheld below the count of
+// placed ones, which the decision checks).  Per-wave summaries (counts,
+// flags, extents, verdicts) go to per-wave slots, so there are no
+// same-address atomics and no slots to clear.
 struct FastLds {
   uint32_t A[kFastMax + 4], B[kFastMax];  // 16-byte aligned rows (timing check)
-  int Val[kFastMax];
+  int Val[kFastMax + 4];       // kAny: nothing claimed (cleared with A/B)
   uint16_t Own[kFastMax + 4];  // 0xFFFF: no mutation placed (cleared with A/B)
-  uint32_t wsum[kFastWaves];  // per wave: mutations placed | inel << 16 | bad << 17
-  uint32_t wbad[kFastWaves];  // per wave: 1 if a CAS/read/timing condition failed
+  uint32_t wsum[kFastWaves];  // per wave: mutations placed | kSum* flags
+  uint32_t wext[kFastWaves];  // per wave: max(last placed position + 1, highest read version)
+  uint32_t wbad[kFastWaves];  // per wave: 1 if a hole or timing condition failed
   int wg[4 * kFastWaves];     // crash-light path: per-wave words (below)
+  // calls of each wave's first and last record per chunk: the order check
+  // across wave boundaries (lane 0's predecessor is another wave's lane 63)
+  uint32_t first_call[kPer][kFastWaves], last_call[kPer][kFastWaves];
+  int64_t base;  // the key's first call (thread 0 publishes it at the LDS init)
+  int raised;    // this workgroup has raised the handoff flag (thread 0 only)
 };
+
+// Pass 1's per-wave flags (FastLds::wsum, above the count of placed
+// mutations).  Any of the first five makes the key ineligible for the version
+// order; only kSumInel alone (crashed writes/CAS without a version) leaves it
+// to the crash-light decision.  kSumVbad: a value claim failed (the version
+// order finds the key invalid; the crash-light decision hands it over).
+constexpr uint32_t kSumInel = 1u << 16;    // crashed write/CAS, or an :ok one without a version
+constexpr uint32_t kSumBad = 1u << 17;     // a version no state reaches
+constexpr uint32_t kSumJit = 1u << 18;     // jit-only (malformed, unknown :f, [nil x] read, ...)
+constexpr uint32_t kSumGiveup = 1u << 19;  // a crashed write/CAS carrying a version
+constexpr uint32_t kSumOvf = 1u << 20;     // more crashed writes/CAS in a wave than its stash holds
+constexpr uint32_t kSumElig = 0x1Fu << 16;
+constexpr uint32_t kSumVbad = 1u << 21;
 
 // One thread's records of one key, as loaded (decoded only once they land).
 struct FastRecs {
   Raw w[kPer];
-  int64_t pc[kPer];  // wave-uniform (SGPRs): call of the record before lane 0's
 };
 
 // Issue every load of this thread's records without waiting: up to 4 x 48 B
-// per thread, 48 KB per workgroup in flight.  The order check takes the
-// previous record's call from the neighbouring lane; only lane 0 of a wave
-// loads it from memory.
+// per thread, 48 KB per workgroup in flight.  Vector loads only: a scalar
+// load in flight holds up every LDS wait (lgkmcnt) of the key the persistent
+// kernels decide meanwhile, so the order check takes lane 0's predecessor
+// from LDS (FastLds::last_call) and the key's first call arrives the same way.
 __device__ __forceinline__ void fast_issue(const lc_op *__restrict__ kops, int n, int tid,
                                            FastRecs &b) {
 #pragma unroll
@@ -1481,13 +1515,11 @@ __device__ __forceinline__ void fast_issue(const lc_op *__restrict__ kops, int n
       b.w[u].a = q[0];
       b.w[u].b = q[1];
       b.w[u].c = q[2];
+    } else {
+      // (defined either way: the persistent kernels' registers then carry no
+      // value of the key before across the loads)
+      b.w[u].a = b.w[u].b = b.w[u].c = make_longlong2(0, 0);
     }
-  }
-  const int w0 = __builtin_amdgcn_readfirstlane(tid & ~(kWave - 1));
-#pragma unroll
-  for (int u = 0; u < kPer; u++) {
-    const int r0 = w0 + u * kFastThreads;  // lane 0's record: a scalar load
-    b.pc[u] = (r0 > 0 && r0 < n) ? kops[r0 - 1].call : INT64_MIN;
   }
 }
 
@@ -1557,18 +1589,32 @@ __device__ __forceinline__ bool timing_fails(const FastLds &s, int M, int tid) {
 // positions); anything else — invalid (the gap tier bisects for the fail
 // op), more than kFgMaxGaps gaps or kFgMaxOps optional ops, a crashed op
 // that carries a version, the branch budget — is handed over as before.
-constexpr int kFgMaxGaps = 48;
-constexpr int kFgMaxOps = 96;
+#ifndef LC_FG_MAXGAPS
+#define LC_FG_MAXGAPS 48
+#endif
+#ifndef LC_FG_MAXOPS
+#define LC_FG_MAXOPS 96
+#endif
+constexpr int kFgMaxGaps = LC_FG_MAXGAPS;
+constexpr int kFgMaxOps = LC_FG_MAXOPS;
 // dynamic LDS: the matching region at its largest (gapmatch.h layout without
 // the class table: 16 B + 5 ints per gap, 16 B + 7 ints per op), then the
 // optional ops' record indices and the branch stack (gap, value)
 constexpr int kFgMatchBytes = 36 * kFgMaxGaps + 44 * kFgMaxOps;
 constexpr int kFgLdsBytes = kFgMatchBytes + 4 * kFgMaxOps + 8 * kFgMaxGaps;
+// Pass 1 stashes each wave's optional ops — (call, value, expectation or
+// kAny, record index), in record order — at the matching region's end, up to
+// kFgStash per wave (more: the key is handed over); the decision moves them
+// into place.  Inside the region, so the LDS per workgroup (and 7 per CU)
+// stays as it was.
+constexpr int kFgStash = 32;
+constexpr int kFgStashOff = kFgMatchBytes - 16 * kFgStash * 4;
+static_assert(kFgStashOff >= 0 && kFgStashOff % 16 == 0, "stash inside the matching region");
 
 // Exclusive suffix minimum over the workgroup's threads (those above this
 // one), with the wave totals through s.wg[8..11]; one barrier.
-__device__ __forceinline__ uint32_t fg_suffix_min_excl(uint32_t v, FastLds &s) {
-  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+__device__ __forceinline__ uint32_t fg_suffix_min_excl(uint32_t v, FastLds &s, int tid) {
+  const int lane = tid & (kWave - 1), w = __builtin_amdgcn_readfirstlane(tid / kWave);
   uint32_t incl = v;
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
@@ -1588,8 +1634,8 @@ __device__ __forceinline__ uint32_t fg_suffix_min_excl(uint32_t v, FastLds &s) {
 // Exclusive prefix sum over the workgroup's threads, wave totals through
 // s.wg[12..15]; *total = the sum.  Shares the caller's next barrier: the
 // caller reads the result only after one.
-__device__ __forceinline__ int fg_prefix_wave(int v, FastLds &s) {
-  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+__device__ __forceinline__ int fg_prefix_wave(int v, FastLds &s, int tid) {
+  const int lane = tid & (kWave - 1), w = __builtin_amdgcn_readfirstlane(tid / kWave);
   int incl = v;
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
@@ -1601,94 +1647,27 @@ __device__ __forceinline__ int fg_prefix_wave(int v, FastLds &s) {
 }
 
 // Returns true when the key was decided valid here; false: hand it over.
-// The records are read again (L2/MALL-hot: the workgroup loaded them just
-// before) rather than kept in registers across the branch: the version
-// order's pass 2 holds 4 x 48 B per thread, and keeping them live on this
-// path too would cost the kernel its 7-waves-per-SIMD occupancy.
-#ifndef LC_FG_REGS
-#define LC_FG_REGS 1  // decode the records from pass 1's registers (0: re-read them)
-#endif
-__device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, const FastRecs &b,
-                         const KParams &p, FastLds &s, lc_key_result *__restrict__ out,
-                         int32_t *__restrict__ wit, int32_t *__restrict__ kind) {
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-  const int64_t base_idx = kops[0].call;
-  const int V0 = p.init_ver, init = p.init_val;
-  // unheld positions start with no value requirement.  Thread t owns
-  // positions 4t..4t+3: one 8-byte / 16-byte LDS access per array instead of
-  // four lane-strided ones (4-way bank conflicts)
-  if (4 * tid < n) {
-    const uint2 own2 = reinterpret_cast<const uint2 *>(s.Own)[tid];
-    int4 v4 = reinterpret_cast<const int4 *>(s.Val)[tid];
-    if ((own2.x & 0xFFFF) == 0xFFFF) v4.x = kAny;
-    if ((own2.x >> 16) == 0xFFFF && 4 * tid + 1 < n) v4.y = kAny;
-    if ((own2.y & 0xFFFF) == 0xFFFF && 4 * tid + 2 < n) v4.z = kAny;
-    if ((own2.y >> 16) == 0xFFFF && 4 * tid + 3 < n) v4.w = kAny;
-    reinterpret_cast<int4 *>(s.Val)[tid] = v4;
+// Works from LDS alone: pass 1 (fast_key) already claimed the values, took
+// the extents and stashed the optional ops (kFgStash per wave, in record
+// order), so the records' registers are free for the next key's loads
+// (the persistent version-order / fused kernels) while this runs.
+// NM: mutations placed by pass 1 over the workgroup.
+__device__ __forceinline__ bool fast_gap(int64_t key, int n, int NM, const KParams &p, FastLds &s,
+                         lc_key_result *__restrict__ out, int32_t *__restrict__ wit,
+                         int32_t *__restrict__ kind, int tid) {
+  const int lane = tid & (kWave - 1), w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int init = p.init_val;
+  // a value claim failed: invalid (the gap tier names the fail op)
+  {
+    const uint4 ws = *reinterpret_cast<const uint4 *>(s.wsum);
+    if ((ws.x | ws.y | ws.z | ws.w) & kSumVbad) return false;
   }
-  __syncthreads();
-  // pass G1: duplicates, value claims, the extent M, optional ops per chunk
-  int maxpos = -1, maxread = 0, inv = 0, giveup = 0;
-  uint64_t optm[kPer];
-  auto claim = [&](int k, int v) {  // value v required at version V0+k+1 (k >= 0)
-    if (s.Own[k] != 0xFFFF) {
-      inv |= s.Val[k] != v;
-    } else {
-      const int old = atomicCAS(&s.Val[k], kAny, v);
-      inv |= (old != kAny) & (old != v);
-    }
-  };
-#if LC_FG_REGS
-#pragma unroll
-#else
-#pragma unroll 1
-#endif
-  for (int u = 0; u < kPer; u++) {
-    const int r = tid + u * kFastThreads;
-    bool opt = false;
-    if (r < n) {
-#if LC_FG_REGS
-      const Rec d = decode(b.w[u], base_idx);
-#else
-      const Rec d = decode(load_raw(kops, r, n), base_idx);
-#endif
-      if (d.f == LC_F_READ) {
-        if (d.ret != kNever && d.ver != -1) {  // (pass 1 handed [nil x] reads over)
-          const int k = d.ver - V0;
-          maxread = max(maxread, k);
-          if (d.val != -1) {
-            if (k == 0) inv |= d.val != init;
-            else claim(k - 1, d.val);
-          }
-        }
-      } else if (d.ret == kNever) {
-        opt = d.ver == -1;
-        giveup |= d.ver != -1;  // a crashed op pinned to a version: the gap tier's
-      } else {
-        const int pos = d.ver - V0 - 1;
-        maxpos = max(maxpos, pos);
-        inv |= s.Own[pos] != r;  // two mutations on one version
-        if (d.f == LC_F_CAS) {
-          if (pos == 0) inv |= d.exp != init;
-          else claim(pos - 1, d.exp);
-        }
-      }
-    }
-    optm[u] = __ballot(opt);
+  // extent M: past the last placed position and the highest read version
+  int M;
+  {
+    const uint4 we = *reinterpret_cast<const uint4 *>(s.wext);
+    M = (int)umax(umax(we.x, we.y), umax(we.z, we.w));
   }
-  // per wave: extent, flags, optional ops per chunk
-  const uint32_t wmax = wave_max_u32((uint32_t)max(maxpos + 1, maxread));
-  const bool wflag = __ballot(inv | giveup) != 0;
-  if (lane == 0) {
-    s.wg[w] = (int)(wmax | (wflag ? 0x80000000u : 0u));
-#pragma unroll
-    for (int u = 0; u < kPer; u++)
-      reinterpret_cast<uint8_t *>(&s.wg[4 + w])[u] = (uint8_t)__popcll(optm[u]);
-  }
-  __syncthreads();
-  const int4 w0 = *reinterpret_cast<const int4 *>(&s.wg[0]);
-  if ((w0.x | w0.y | w0.z | w0.w) < 0) return false;  // invalid or not this path's
-  const int M = max(max(w0.x, w0.y), max(w0.z, w0.w));
   // optional-op slots: chunk-major, then wave, then lane (= record order)
   int n_opt = 0;
 #pragma unroll
@@ -1696,6 +1675,13 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, con
 #pragma unroll
     for (int j = 0; j < kFastWaves; j++) n_opt += reinterpret_cast<const uint8_t *>(&s.wg[4 + j])[u];
   if (n_opt > kFgMaxOps) return false;
+  // this wave's stashed ops (one per lane) leave LDS before the compaction
+  // below can overwrite the stash (it lies at the matching region's end)
+  const uint32_t mycnt = (uint32_t)s.wg[4 + w];
+  const int mytot = (int)((mycnt & 0xFF) + ((mycnt >> 8) & 0xFF) + ((mycnt >> 16) & 0xFF) + (mycnt >> 24));
+  int4 mine = make_int4(0, 0, 0, 0);
+  if (lane < mytot)
+    mine = reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(lds_dyn) + kFgStashOff)[w * kFgStash + lane];
   // deadlines: Uh[k] = min(B[k..M-1]) for this thread's positions 4t..4t+3
   uint32_t bmin = kNever;
   int gapc = 0;
@@ -1711,8 +1697,8 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, con
       gapc += (k < M) && oo[j] == 0xFFFF;
     }
   }
-  const int gpre = fg_prefix_wave(gapc, s);
-  const uint32_t after = fg_suffix_min_excl(bmin, s);
+  const int gpre = fg_prefix_wave(gapc, s, tid);
+  const uint32_t after = fg_suffix_min_excl(bmin, s, tid);
   // (the barrier inside fg_suffix_min_excl also publishes s.wg[12..15])
   int G = 0, gbase = gpre;
 #pragma unroll
@@ -1724,6 +1710,9 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, con
   const bool tbad = __ballot(timing_fails(s, M, tid)) != 0;
   if (lane == 0) s.wbad[w] = tbad;
   if (G > kFgMaxGaps) return false;
+  // every placed mutation sits below M: M - G held positions for NM of them,
+  // fewer when two share a version (invalid)
+  if (M - G != NM) return false;
   // compact gaps and optional ops into the matching region (lds_dyn)
   Cmp<true> c;
   c.ws = nullptr;
@@ -1755,32 +1744,28 @@ __device__ bool fast_gap(int64_t key, int n, const lc_op *__restrict__ kops, con
       }
     }
   }
-  int obase = 0;
-#if LC_FG_REGS
+  if (lane < mytot) {
+    // stash item `lane` of this wave: chunk u where the wave's running count
+    // passes it; its slot = ops of earlier chunks + earlier waves' ops of u
+    int lo = 0, o = 0;
 #pragma unroll
-#else
-#pragma unroll 1
-#endif
-  for (int u = 0; u < kPer; u++) {
-    int my = obase;  // slots before this wave's ops of chunk u
+    for (int u = 0; u < kPer; u++) {
+      const int cu = (int)((mycnt >> (8 * u)) & 0xFF);
+      int before = 0, tot = 0;
 #pragma unroll
-    for (int j = 0; j < kFastWaves; j++) {
-      const int cnt = reinterpret_cast<const uint8_t *>(&s.wg[4 + j])[u];
-      my += j < w ? cnt : 0;
-      obase += cnt;
+      for (int j = 0; j < kFastWaves; j++) {
+        const int cnt = reinterpret_cast<const uint8_t *>(&s.wg[4 + j])[u];
+        before += j < w ? cnt : 0;
+        tot += cnt;
+      }
+      if (lane >= lo && lane < lo + cu) o += before + (lane - lo);
+      else if (lane >= lo + cu) o += tot;
+      lo += cu;
     }
-    if ((optm[u] >> lane) & 1) {
-      const int o = my + lanes_below(optm[u]);
-#if LC_FG_REGS
-      const Rec d = decode(b.w[u], base_idx);
-#else
-      const Rec d = decode(load_raw(kops, tid + u * kFastThreads, n), base_idx);
-#endif
-      c.ops()[o] = make_int4((int)d.call, d.val, d.f == LC_F_CAS ? d.exp : kAny, -1);
-      c.at(aMO, o) = -1;
-      c.at(aVis, o) = 0;
-      opt_rec[o] = tid + u * kFastThreads;
-    }
+    c.ops()[o] = make_int4(mine.x, mine.y, mine.z, -1);
+    c.at(aMO, o) = -1;
+    c.at(aVis, o) = 0;
+    opt_rec[o] = mine.w;
   }
   __syncthreads();
   {
@@ -2048,7 +2033,8 @@ struct FastSinks {
 enum { kModeFast = 0, kModeLight = 1, kModeFused = 2 };
 
 template <int MODE>
-__device__ __forceinline__ void fast_pass_on(int64_t key, const FastSinks &o, bool jit_only = false) {
+__device__ __forceinline__ void fast_pass_on(int64_t key, const FastSinks &o, int *raised,
+                                             bool jit_only = false) {
   if constexpr (MODE == kModeLight) {
     o.pass[atomicAdd(&o.status->n_gap2, 1)] = (int32_t)key;  // few: invalid / large keys
   } else {
@@ -2056,26 +2042,39 @@ __device__ __forceinline__ void fast_pass_on(int64_t key, const FastSinks &o, bo
     // or in the crash-light decision (fast_key)
     if constexpr (MODE == kModeFused)
       if (!jit_only) atomicAdd(&o.status->n_light, 1);
-    fast_tier_handoff(key, o.flags, o.status, o.h_handoff, jit_only);
+    fast_tier_handoff(key, o.flags, o.status, o.h_handoff, jit_only, raised);
   }
 }
 
 
 // Decide one key (records in b when 0 < n64 <= kFastMax) or hand it over.
 // Three barriers: after the LDS init, after pass 1, before thread 0 reads
-// the per-wave verdicts.
-template <int MODE>
+// the per-wave verdicts.  Pass 1 is the only pass over the records (value
+// claims are LDS compare-and-swaps, FastLds), so once it is done the
+// records' registers are free: `next()` — called once by every thread, there
+// or at once for a key with nothing to decide — lets the persistent kernels
+// issue the next key's loads into them while this key is decided from LDS.
+// The crash-light pass (kModeLight) keeps the records for first_failure.
+template <int MODE, typename Next>
 __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *__restrict__ kops,
                                          const FastRecs &b, const KParams &p, FastLds &s,
                                          lc_key_result *__restrict__ out, const FastSinks &o,
-                                         int32_t *__restrict__ wit) {
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+                                         int32_t *__restrict__ wit, Next &&next) {
+  // the thread index, opaque to the compiler: in the persistent kernels'
+  // loop everything derived from it (LDS addresses, lane masks) would
+  // otherwise be hoisted out and held in VGPRs across every key
+  int tid = threadIdx.x;
+#if LC_PIPE
+  asm volatile("" : "+v"(tid));
+#endif
+  const int lane = tid & (kWave - 1), w = __builtin_amdgcn_readfirstlane(tid / kWave);
   if (n64 <= 0 || n64 > kFastMax) {
+    next();
     if (tid == 0) {
       if (n64 == 0)
         out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 0};
       else
-        fast_pass_on<MODE>(key, o);
+        fast_pass_on<MODE>(key, o, &s.raised);
     }
     return;
   }
@@ -2085,38 +2084,78 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     int64_t x = 0;
 #pragma unroll
     for (int u = 0; u < kPer; u++)
-      x ^= b.w[u].a.x ^ b.w[u].a.y ^ b.w[u].b.x ^ b.w[u].b.y ^ b.w[u].c.x ^ b.w[u].c.y ^ b.pc[u];
+      x ^= b.w[u].a.x ^ b.w[u].a.y ^ b.w[u].b.x ^ b.w[u].b.y ^ b.w[u].c.x ^ b.w[u].c.y;
+    next();
     if (x == 0x123456789) out[key].configs_explored = x;
     if (tid == 0) out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
     return;
   }
 #endif
-  // thread t clears positions 4t..4t+3 of A and B (one 16-byte store each);
-  // A[kFastMax] (reads of the version after the last possible mutation) by
-  // thread 0
+  // thread t clears positions 4t..4t+3 of A, B, Own and Val (one 16-byte
+  // store each, 8 for Own); A[kFastMax] (reads of the version after the last
+  // possible mutation) by thread 0, which also publishes the key's first call
   if (4 * tid <= n) {
     reinterpret_cast<uint4 *>(s.A)[tid] = make_uint4(0, 0, 0, 0);  // nothing constrains t_k from below
     reinterpret_cast<uint4 *>(s.B)[tid] = make_uint4(kNever, kNever, kNever, kNever);
     reinterpret_cast<uint2 *>(s.Own)[tid] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    if (MODE != kModeFast || LC_PIPE)  // (claimed values start unclaimed)
+      reinterpret_cast<int4 *>(s.Val)[tid] = make_int4(kAny, kAny, kAny, kAny);
   }
-  if (tid == 0) s.A[kFastMax] = 0;
+#if LC_PIPE
+  if (tid == 0) {
+    s.A[kFastMax] = 0;
+    s.base = b.w[0].c.x;
+  }
   __syncthreads();
-  const int64_t base_idx = kops[0].call;
-  const int V0 = p.init_ver;
-  int inel = 0, bad = 0, nmut = 0, jit_only = 0;
-  // pass 1: place mutations, fold read intervals into A / B
+  const int64_t base_idx = s.base;
+#else
+  if (tid == 0) s.A[kFastMax] = 0;
+  const int64_t base_idx = kops[0].call;  // (a scalar load, beside the records')
+  __syncthreads();
+#endif
+  const int V0 = p.init_ver, init = p.init_val;
+  int inel = 0, bad = 0, nmut = 0, jit_only = 0, giveup = 0, vbad = 0;
+  int ext = 0;  // past the last placed position and the highest read version
+  int nopt = 0;        // this wave's optional ops so far (wave-uniform)
+  uint32_t optc = 0;   // per chunk, one byte each
+  int4 *stash = reinterpret_cast<int4 *>(reinterpret_cast<char *>(lds_dyn) + kFgStashOff) +
+                w * kFgStash;
+  // The version-order tier (one workgroup per key) keeps its records in
+  // registers through the decision: it stores each placed mutation's value
+  // and checks the claims in a second pass over the registers (measured ~2 %
+  // faster on C2 than the compare-and-swaps); the fused and light passes
+  // claim in pass 1 and free the records.
+  constexpr bool kTwoPass = MODE == kModeFast && !LC_PIPE;
+  auto claim = [&](int k, int v) {  // value v required at version V0+k+1 (k >= 0)
+    if constexpr (!kTwoPass) {
+      const int old = atomicCAS(&s.Val[k], kAny, v);
+      vbad |= (old != kAny) & (old != v);
+    }
+  };
+  // pass 1: place mutations, fold read intervals into A / B, claim values,
+  // stash crashed writes/CAS
 #pragma unroll
   for (int u = 0; u < kPer; u++) {
     const int r = tid + u * kFastThreads;
-    // previous record's call: lane-1's record of the same u, or for lane 0
-    // the scalar-loaded one
     const Raw &bw = b.w[u];
-    int64_t prev = __shfl_up(bw.c.x, 1);
-    if (lane == 0) prev = b.pc[u];
+
     bool placed = false;
+    // crashed writes/CAS without a version (a malformed one among them
+    // reserves a slot too: its key goes to the JIT tier, the stash unread)
+    uint64_t m = 0;
+    if constexpr (MODE != kModeFast)
+      m = __ballot(r < n && (bw.a.x == LC_F_WRITE || bw.a.x == LC_F_CAS) && bw.c.y == kInf &&
+                   bw.b.y == -1);
     if (r < n) {
       const Rec d = decode(bw, base_idx);
-      if (d.bad || d.f > LC_F_CAS || (r > 0 && prev >= bw.c.x)) {
+      // calls in order: the previous record's is lane-1's of the same u
+      // (lane 0's predecessor is checked after the barrier, from last_call).
+      // Key-relative 32-bit calls: exact when neither record is malformed,
+      // and a malformed one sends the key to the JIT tier anyway
+      const uint32_t prev = (uint32_t)__shfl_up((int)d.call, 1);
+      if (lane == 0) s.first_call[u][w] = d.call;
+      if (lane == kWave - 1) s.last_call[u][w] = d.call;
+      if (d.bad || d.f > LC_F_CAS || (lane > 0 && prev >= d.call)) {
         inel = jit_only = 1;  // the JIT tier reports malformed / unknown :f
       } else if (d.f == LC_F_READ) {
         if (d.ret != kNever && !(d.ver == -1 && d.val == -1)) {  // else never constrains
@@ -2128,13 +2167,23 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
               bad = 1;
             } else {
               atomicMax(&s.A[k], d.call + 1);
+              if constexpr (MODE != kModeFast) ext = max(ext, k);
               if (k > 0) atomicMin(&s.B[k - 1], d.ret);
+              if (d.val != -1) {
+                if (k == 0) vbad |= d.val != init;
+                else claim(k - 1, d.val);
+              }
             }
           }
         }
       } else if (d.ret == kNever || d.ver == -1) {
         inel = 1;  // crashed (the gap tier's case), or no version: order not pinned
         if (d.ret != kNever) jit_only = 1;
+        else if (d.ver != -1) giveup = 1;  // a crashed op pinned to a version: the gap tier's
+        else if constexpr (MODE != kModeFast) {
+          const int slot = nopt + lanes_below(m);
+          if (slot < kFgStash) stash[slot] = make_int4((int)d.call, d.val, d.f == LC_F_CAS ? d.exp : kAny, r);
+        }
       } else {
         const int pos = d.ver - V0 - 1;
         if (pos < 0 || pos >= n) {
@@ -2142,105 +2191,218 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
         } else {
           atomicMax(&s.A[pos], d.call + 1);
           atomicMin(&s.B[pos], d.ret);
-          s.Val[pos] = d.val;
           s.Own[pos] = (uint16_t)r;
+          if constexpr (kTwoPass) s.Val[pos] = d.val;
+          else claim(pos, d.val);
+          if constexpr (MODE != kModeFast) ext = max(ext, pos + 1);
+          if (d.f == LC_F_CAS) {
+            if (pos == 0) vbad |= d.exp != init;
+            else claim(pos - 1, d.exp);
+          }
           placed = true;
         }
       }
     }
     nmut += __popcll(__ballot(placed));
+    if constexpr (MODE != kModeFast) {
+      const int c = __popcll(m);
+      nopt += c;
+      optc |= (uint32_t)c << (8 * u);
+    }
   }
+  // the records are consumed: their registers take the next key's loads
+  if constexpr (MODE != kModeLight) next();
   // (ballots outside the lane-0 branch: they must see every lane)
-  // (the jit-only ballot only when something is ineligible: a uniform branch
-  // that a clean key never takes)
-  const uint32_t winel = __ballot(inel) ? (1u << 16) | (__ballot(jit_only) ? 1u << 18 : 0u) : 0u;
-  const uint32_t wsum = (uint32_t)nmut | winel | (__ballot(bad) ? 1u << 17 : 0u);
-  if (lane == 0) s.wsum[w] = wsum;
+  uint32_t fl = 0;
+  if (__ballot(inel | bad | vbad)) {  // a clean valid key skips the rest
+    fl = (__ballot(inel) ? kSumInel : 0u) | (__ballot(bad) ? kSumBad : 0u) |
+         (__ballot(jit_only) ? kSumJit : 0u) | (__ballot(giveup) ? kSumGiveup : 0u) |
+         (__ballot(vbad) ? kSumVbad : 0u) | (nopt > kFgStash ? kSumOvf : 0u);
+  }
+  // extents (the crash-light decision's M; the version order checks its
+  // tail from the tables instead)
+  uint32_t wext = 0;
+  if constexpr (MODE != kModeFast) wext = wave_max_u32((uint32_t)ext);
+  if (lane == 0) {
+    s.wsum[w] = (uint32_t)nmut | fl;
+    if constexpr (MODE != kModeFast) {
+      s.wext[w] = wext;
+      s.wg[4 + w] = (int)optc;
+    }
+  }
   __syncthreads();
-  const uint4 ws = *reinterpret_cast<const uint4 *>(s.wsum);
-  const uint32_t wor = ws.x | ws.y | ws.z | ws.w;
-  // M = mutations placed; M distinct positions all below M <=> positions
-  // 0..M-1 each held once (pass 2 checks both)
-  const int M = (int)((ws.x & 0xFFFF) + (ws.y & 0xFFFF) + (ws.z & 0xFFFF) + (ws.w & 0xFFFF));
-  if (wor >> 16) {  // ineligible or a version out of range: hand over
+  uint32_t wor;
+  int M;
+  {
+    const uint4 ws = *reinterpret_cast<const uint4 *>(s.wsum);
+    wor = ws.x | ws.y | ws.z | ws.w;
+    // M = mutations placed
+    M = (int)((ws.x & 0xFFFF) + (ws.y & 0xFFFF) + (ws.z & 0xFFFF) + (ws.w & 0xFFFF));
+  }
+  {
+    // the order check across wave boundaries: lane j < 16 takes the first
+    // record of (chunk j / 4, wave j % 4) against its predecessor's call
+    const int j = lane & 15, ju = j >> 2, jw = j & 3;
+    const int r0 = jw * kWave + ju * kFastThreads;
+    bool ob = false;
+    if (lane < 16 && r0 > 0 && r0 < n) {
+      const uint32_t pc = jw > 0 ? s.last_call[ju][jw - 1] : s.last_call[ju - 1][kFastWaves - 1];
+      ob = pc >= s.first_call[ju][jw];
+    }
+    if (__ballot(ob)) wor |= kSumInel | kSumJit;
+  }
+  if (wor & kSumElig) {  // ineligible or a version out of range: hand over
     // crash-light pass: crashed writes/CAS are the only obstacle
     if constexpr (MODE != kModeFast)
-      if ((wor >> 16) == 1 && fast_gap(key, n, kops, b, p, s, out, wit, o.kind)) {
+      if ((wor & kSumElig) == kSumInel && fast_gap(key, n, M, p, s, out, wit, o.kind, tid)) {
         if (MODE == kModeFused && tid == 0) atomicAdd(&o.status->n_light, 1);
         return;
       }
-    if (tid == 0) fast_pass_on<MODE>(key, o, (wor >> 18) & 1);
+    if (tid == 0) fast_pass_on<MODE>(key, o, &s.raised, (wor & kSumJit) != 0);
     return;
   }
   if constexpr (MODE == kModeLight) {
     // eligible here too: the version order found it invalid; name its first
     // failure in place (declined: the gap tier bisects)
     if (!first_failure(key, n, kops, b, p, s, out, wit, o.kind) && tid == 0)
-      fast_pass_on<MODE>(key, o);
+      fast_pass_on<MODE>(key, o, &s.raised);
     return;
   }
-  // pass 2: positions, duplicates, CAS expectations and read claims against
-  // the placed values
+  // the version order: positions 0..M-1 each held once (none below M
+  // unheld, none at or above M held), no read of a version past M (A[k] of
+  // k > M untouched: a read of version k, or a mutation at k, would have
+  // raised it), every claim agreed (pass 1), and the timing condition
+  const bool uni_bad = (wor & kSumVbad) != 0;
+  int hole = 0;
+  if constexpr (kTwoPass) {
+    // pass 2: positions, duplicates, CAS expectations and read claims
+    // against the placed values
 #pragma unroll
-  for (int u = 0; u < kPer; u++) {
-    const int r = tid + u * kFastThreads;
-    if (r >= n) continue;
-    const int f = (int)b.w[u].a.x, val = (int)b.w[u].a.y, exp = (int)b.w[u].b.x;
-    const int ver = (int)b.w[u].b.y;
-    if (f != LC_F_READ) {
-      const int pos = ver - V0 - 1;
-      if (pos >= M || s.Own[pos] != r) {
-        bad = 1;  // a gap below the last version, or a version held twice
-      } else if (f == LC_F_CAS && exp != (pos == 0 ? p.init_val : s.Val[pos - 1])) {
-        bad = 1;
+    for (int u = 0; u < kPer; u++) {
+      const int r = tid + u * kFastThreads;
+      if (r >= n) continue;
+      const int f = (int)b.w[u].a.x, val = (int)b.w[u].a.y, exp = (int)b.w[u].b.x;
+      const int ver = (int)b.w[u].b.y;
+      if (f != LC_F_READ) {
+        const int pos = ver - V0 - 1;
+        if (pos >= M || s.Own[pos] != r) {
+          hole = 1;  // a gap below the last version, or a version held twice
+        } else if (f == LC_F_CAS && exp != (pos == 0 ? init : s.Val[pos - 1])) {
+          hole = 1;
+        }
+      } else if (ver != -1 && b.w[u].c.y != kInf) {
+        const int k = ver - V0;
+        if (k > M)
+          hole = 1;  // a version no mutation wrote
+        else if (val != -1 && val != (k == 0 ? init : s.Val[k - 1]))
+          hole = 1;
       }
-    } else if (ver != -1 && b.w[u].c.y != kInf) {
-      const int k = ver - V0;
-      if (k > M)
-        bad = 1;  // a version no mutation wrote
-      else if (val != -1 && val != (k == 0 ? p.init_val : s.Val[k - 1]))
-        bad = 1;
+    }
+  } else if (4 * tid <= n) {
+    const uint2 own2 = reinterpret_cast<const uint2 *>(s.Own)[tid];
+    const uint4 a4 = reinterpret_cast<const uint4 *>(s.A)[tid];
+    const uint32_t oo[4] = {own2.x & 0xFFFF, own2.x >> 16, own2.y & 0xFFFF, own2.y >> 16};
+    const uint32_t aa[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int k = 4 * tid + j;
+      if (k < M) hole |= oo[j] == 0xFFFF;
+      else if (k < n) hole |= (oo[j] != 0xFFFF) | ((k > M) & (aa[j] != 0));
+      else if (k == n) hole |= (k > M) & (aa[j] != 0);
     }
   }
-  if (timing_fails(s, M, tid)) bad = 1;
-  const uint32_t wbad = __ballot(bad) ? 1u : 0u;
+  if (timing_fails(s, M, tid)) hole = 1;
+  const uint32_t wbad = __ballot(hole) ? 1u : 0u;
   if (lane == 0) s.wbad[w] = wbad;
   __syncthreads();
   // (the fused pass hands invalid keys over: the first-failure rule there
   // costs 5 VGPRs, 72 -> 77, and a wave per SIMD on crash-heavy batches)
   if (tid == 0) {
     const uint4 wb = *reinterpret_cast<const uint4 *>(s.wbad);
-    if (!(wb.x | wb.y | wb.z | wb.w))
+    if (!uni_bad && !(wb.x | wb.y | wb.z | wb.w))
       out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
     else
-      fast_pass_on<MODE>(key, o);
+      fast_pass_on<MODE>(key, o, &s.raised);
   }
 }
 
-// One workgroup per key.  (A persistent grid that issues key i+G's loads
-// before deciding key i measured slower, 0.113 -> 0.156 ms on C2: its two
-// register sets cut residency from 5 to 3 workgroups per CU, i.e. fewer
-// bytes in flight per CU than the hardware dispatcher keeps with 5.)
-__global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
-    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
-    const KParams p, lc_key_result *__restrict__ out,
-    int32_t *__restrict__ flags, KStatus *__restrict__ status,
-    int32_t *__restrict__ h_handoff) {
-  __shared__ FastLds s;
-  const int64_t key = blockIdx.x;
+// The version-order and fused kernels: persistent workgroups (as many as
+// are resident, lincheck.cpp sizes the grid), each deciding keys blockIdx.x,
+// + gridDim.x, ... .  A key's loads are issued while the key before it is
+// decided from LDS (fast_key's next()): one register set, the records in
+// flight during the decision instead of the decision and the loads taking
+// turns.  The next key's offsets come one key ahead, by vector loads (two
+// lanes) for the same reason as fast_issue's.
+template <int MODE>
+__device__ __forceinline__ void fast_run(const lc_op *__restrict__ ops,
+                                         const int64_t *__restrict__ key_off, int64_t n_keys,
+                                         const KParams &p, FastLds &s,
+                                         lc_key_result *__restrict__ out, const FastSinks &o) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int64_t off0 = key_off[0];
+  int64_t key = blockIdx.x;
+  if (key >= n_keys) return;
+  if (tid == 0) s.raised = 0;
+  int64_t beg = key_off[key], end = key_off[key + 1];
+  FastRecs r;
+  if (end - beg > 0 && end - beg <= kFastMax) fast_issue(ops + (beg - off0), (int)(end - beg), tid, r);
+  // the next key's offsets (lanes 0 and 1)
+  int64_t nx = key + gridDim.x;
+  int64_t offv = 0;
+  if (nx < n_keys && lane < 2) offv = key_off[nx + lane];
+  for (;;) {
+    int64_t nbeg = 0, nend = 0;
+    const int64_t nx2 = nx + gridDim.x;
+    auto next = [&]() {
+      nbeg = __shfl(offv, 0);
+      nend = __shfl(offv, 1);
+      const int64_t nn = nx < n_keys ? nend - nbeg : 0;
+      fast_issue(ops + (nbeg - off0), nn > 0 && nn <= kFastMax ? (int)nn : 0, tid, r);
+      if (nx2 < n_keys && lane < 2) offv = key_off[nx2 + lane];
+    };
+    fast_key<MODE>(key, end - beg, ops + (beg - off0), r, p, s, out, o,
+                   o.wit ? o.wit + (beg - off0) : nullptr, next);
+    if (nx >= n_keys) break;
+    key = nx;
+    beg = nbeg;
+    end = nend;
+    nx = nx2;
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void fast_one(const lc_op *__restrict__ ops,
+                                         const int64_t *__restrict__ key_off, int64_t key,
+                                         const KParams &p, FastLds &s,
+                                         lc_key_result *__restrict__ out, const FastSinks &o) {
   const int64_t beg = key_off[key], end = key_off[key + 1];
   const lc_op *kops = ops + (beg - key_off[0]);
   FastRecs r;
   if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
+  if (threadIdx.x == 0) s.raised = 0;
+  fast_key<MODE>(key, end - beg, kops, r, p, s, out, o,
+                 o.wit ? o.wit + (beg - key_off[0]) : nullptr, [] {});
+}
+
+__global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off, int64_t n_keys,
+    const KParams p, lc_key_result *__restrict__ out,
+    int32_t *__restrict__ flags, KStatus *__restrict__ status,
+    int32_t *__restrict__ h_handoff) {
+  __shared__ FastLds s;
   const FastSinks o{flags, status, h_handoff, nullptr, nullptr, nullptr};
-  fast_key<kModeFast>(key, end - beg, kops, r, p, s, out, o, nullptr);
+#if LC_PIPE
+  fast_run<kModeFast>(ops, key_off, n_keys, p, s, out, o);
+#else
+  fast_one<kModeFast>(ops, key_off, blockIdx.x, p, s, out, o);
+#endif
 }
 
 // Crash-light pass over the keys the version-order tier handed to the gap
 // tier (status->n_jit of them, written by the compaction launched just
 // before: no host round trip in between).  Same decision as the version-
 // order tier plus the in-place gap decision; what it cannot decide goes to
-// `pass` (status->n_gap2) for the gap tier.  Grid-stride over the list.
+// `pass` (status->n_gap2) for the gap tier.
 // 4 waves per SIMD (at most 128 VGPRs): left alone the compiler takes 138
 // (3 waves); 4 has no VGPR spills and decides bench.py's crash_leg in
 // 0.24 ms against 0.29 ms (5 and 6 waves spill: 0.33 / 0.36 ms).
@@ -2261,32 +2423,26 @@ __global__ __launch_bounds__(kFastThreads) LC_LIGHT_ATTR void gap_light_kernel(
   // VGPRs with SGPR spills, 4 waves per SIMD; one key each, 72 and 7.)
   const int t = blockIdx.x;
   if (t >= n_list) return;
-  const int64_t key = keys[t];
-  const int64_t beg = key_off[key], end = key_off[key + 1];
-  const lc_op *kops = ops + (beg - key_off[0]);
-  FastRecs r;
-  if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
-  fast_key<kModeLight>(key, end - beg, kops, r, p, s, out, o,
-                       o.wit ? o.wit + (beg - key_off[0]) : nullptr);
+  fast_one<kModeLight>(ops, key_off, keys[t], p, s, out, o);
 }
 
 // The version-order tier and the crash-light decision in one pass over every
-// key (kModeFused): one workgroup per key, as the version-order tier; keys it
-// does not decide are flagged for the same handoff compaction, and the gap
-// tier takes them without a crash-light pass.  The crash-light register
-// budget (4 waves per SIMD) — the host picks this kernel only for batches
-// where most keys carry crashed ops (lincheck.cpp).
-__global__ __launch_bounds__(kFastThreads) LC_LIGHT_ATTR void fused_tier_kernel(
-    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off, const KParams p,
-    lc_key_result *__restrict__ out, const FastSinks o) {
+// key (kModeFused), persistent as the version-order tier; keys it does not
+// decide are flagged for the same handoff compaction.  The crash-light
+// register budget — the host picks this kernel only for batches where most
+// keys carry crashed ops (lincheck.cpp).
+#ifndef LC_FUSED_WPE
+#define LC_FUSED_WPE LC_LIGHT_WPE
+#endif
+__global__ __launch_bounds__(kFastThreads) __attribute__((amdgpu_waves_per_eu(LC_FUSED_WPE, 8))) void fused_tier_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off, int64_t n_keys,
+    const KParams p, lc_key_result *__restrict__ out, const FastSinks o) {
   __shared__ FastLds s;
-  const int64_t key = blockIdx.x;
-  const int64_t beg = key_off[key], end = key_off[key + 1];
-  const lc_op *kops = ops + (beg - key_off[0]);
-  FastRecs r;
-  if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
-  fast_key<kModeFused>(key, end - beg, kops, r, p, s, out, o,
-                       o.wit ? o.wit + (beg - key_off[0]) : nullptr);
+#if LC_PIPE
+  fast_run<kModeFused>(ops, key_off, n_keys, p, s, out, o);
+#else
+  fast_one<kModeFused>(ops, key_off, blockIdx.x, p, s, out, o);
+#endif
 }
 
 // Workspace layout per wave: 3 regions of cap Cfg, 2 tables of 2*cap Cfg,
@@ -2545,13 +2701,36 @@ hipError_t launch_witness_init(const lc_op *d_ops, const int64_t *d_key_off, int
   return hipGetLastError();
 }
 
+// Resident workgroups of a persistent kernel on the current device (its
+// grid): occupancy per CU x CUs, cached per device and kernel.
+template <typename K>
+static int64_t resident_wgs(K kernel, int which, size_t dyn_lds) {
+  static std::atomic<int> cache[64][2];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int c = cache[dev][which].load(std::memory_order_relaxed);
+  if (c == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kFastThreads, dyn_lds) !=
+            hipSuccess || per_cu < 1)
+      per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 1;
+    c = per_cu * cus;
+    cache[dev][which].store(c, std::memory_order_relaxed);
+  }
+  return c;
+}
+
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_flags,
                             KStatus *d_status, int32_t *h_handoff, hipStream_t stream) {
   if (n_keys <= 0) return hipSuccess;
-  hipLaunchKernelGGL(fast_tier_kernel, dim3((unsigned)n_keys), dim3(kFastThreads), 0,
-                     stream, d_ops, d_key_off, p, d_out, d_flags, d_status, h_handoff);
+  const int64_t wgs = LC_PIPE ? std::min(n_keys, resident_wgs(fast_tier_kernel, 0, 0)) : n_keys;
+  hipLaunchKernelGGL(fast_tier_kernel, dim3((unsigned)wgs), dim3(kFastThreads), 0,
+                     stream, d_ops, d_key_off, n_keys, p, d_out, d_flags, d_status, h_handoff);
   return hipGetLastError();
 }
 
@@ -2561,8 +2740,10 @@ hipError_t launch_fused_tier(const lc_op *d_ops, const int64_t *d_key_off, int64
                              int32_t *d_witness_kind, hipStream_t stream) {
   if (n_keys <= 0) return hipSuccess;
   const FastSinks o{d_flags, d_status, h_handoff, nullptr, d_witness, d_witness_kind};
-  hipLaunchKernelGGL(fused_tier_kernel, dim3((unsigned)n_keys), dim3(kFastThreads),
-                     (unsigned)kFgLdsBytes, stream, d_ops, d_key_off, p, d_out, o);
+  const int64_t wgs =
+      LC_PIPE ? std::min(n_keys, resident_wgs(fused_tier_kernel, 1, kFgLdsBytes)) : n_keys;
+  hipLaunchKernelGGL(fused_tier_kernel, dim3((unsigned)wgs), dim3(kFastThreads),
+                     (unsigned)kFgLdsBytes, stream, d_ops, d_key_off, n_keys, p, d_out, o);
   return hipGetLastError();
 }
 
