@@ -45,6 +45,16 @@
 namespace lcdev {
 namespace {
 
+#ifdef LC_FG_PROF  // dev only: per-phase clocks of the fused pass, summed over keys
+__device__ unsigned long long g_fgp[8];
+__device__ unsigned int g_fgdone;
+#define FGP_T(i) uint64_t fgp_t##i = __builtin_amdgcn_s_memtime()
+#define FGP_ADD(i, a, b) if (threadIdx.x == 0) atomicAdd(&g_fgp[i], (unsigned long long)(fgp_t##b - fgp_t##a))
+#else
+#define FGP_T(i)
+#define FGP_ADD(i, a, b)
+#endif
+
 #ifdef HBM_PROFILE
 // Dev only (tools/build_variants.sh NAME -DHBM_PROFILE): per cooperative
 // return, by log2 of its larger set: returns, device ticks (100 MHz), LDS-
@@ -1091,7 +1101,7 @@ __device__ __forceinline__ ChunkMasks chunk_masks(const Rec &r, uint64_t fsv) {
 // Calls must strictly increase within a key: compare each record with its
 // predecessor (lane-1, or the previous chunk's last call for lane 0).
 __device__ __forceinline__ void check_order(Rec &r, uint32_t &last_call, int lane) {
-  const uint32_t prev = (uint32_t)__shfl_up((int)r.call, 1);
+  const uint32_t prev = (uint32_t)wave_shr1((int)r.call, 0);
   const bool first_key_rec = lane == 0 && last_call == kNever;
   const uint32_t p = lane == 0 ? last_call : prev;
   if (r.call != kNever && !first_key_rec && r.call <= p) r.bad = 1;
@@ -1615,15 +1625,9 @@ static_assert(kFgStashOff >= 0 && kFgStashOff % 16 == 0, "stash inside the match
 // one), with the wave totals through s.wg[8..11]; one barrier.
 __device__ __forceinline__ uint32_t fg_suffix_min_excl(uint32_t v, FastLds &s, int tid) {
   const int lane = tid & (kWave - 1), w = __builtin_amdgcn_readfirstlane(tid / kWave);
-  uint32_t incl = v;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_down((int)incl, o);
-    if (lane + o < kWave) incl = umin(incl, y);
-  }
+  uint32_t incl;
+  uint32_t excl = wave_suffix_min_excl(v, lane, kNever, &incl);
   if (lane == 0) s.wg[8 + w] = (int)incl;
-  uint32_t excl = (uint32_t)__shfl_down((int)incl, 1);
-  if (lane == kWave - 1) excl = kNever;
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kFastWaves; j++)
@@ -1636,12 +1640,7 @@ __device__ __forceinline__ uint32_t fg_suffix_min_excl(uint32_t v, FastLds &s, i
 // caller reads the result only after one.
 __device__ __forceinline__ int fg_prefix_wave(int v, FastLds &s, int tid) {
   const int lane = tid & (kWave - 1), w = __builtin_amdgcn_readfirstlane(tid / kWave);
-  int incl = v;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int y = __shfl_up(incl, o);
-    if (lane >= o) incl += y;
-  }
+  const int incl = wave_prefix_sum(v, lane);
   if (lane == kWave - 1) s.wg[12 + w] = incl;
   return incl - v;
 }
@@ -1699,6 +1698,7 @@ __device__ __forceinline__ bool fast_gap(int64_t key, int n, int NM, const KPara
   }
   const int gpre = fg_prefix_wave(gapc, s, tid);
   const uint32_t after = fg_suffix_min_excl(bmin, s, tid);
+  FGP_T(10);
   // (the barrier inside fg_suffix_min_excl also publishes s.wg[12..15])
   int G = 0, gbase = gpre;
 #pragma unroll
@@ -1768,6 +1768,7 @@ __device__ __forceinline__ bool fast_gap(int64_t key, int n, int NM, const KPara
     opt_rec[o] = mine.w;
   }
   __syncthreads();
+  FGP_T(11);
   {
     const uint4 tb = *reinterpret_cast<const uint4 *>(s.wbad);
     if (tb.x | tb.y | tb.z | tb.w) return false;
@@ -1788,6 +1789,9 @@ __device__ __forceinline__ bool fast_gap(int64_t key, int n, int NM, const KPara
       for (int gi = lane; gi < G; gi += kWave) wit[opt_rec[c.at(aMG, gi)]] = c.gaps()[gi].w;
   }
   __syncthreads();
+  FGP_T(12);
+  FGP_ADD(3, 10, 11);
+  FGP_ADD(4, 11, 12);
   if (G > 0) res = s.wg[0];
   if (res != GD_VALID) return false;
   if (tid == 0) {
@@ -1851,15 +1855,10 @@ __device__ __forceinline__ bool fast_gap(int64_t key, int n, int NM, const KPara
 // key was decided (result and, if wanted, its PREFIX witness written).
 __device__ __forceinline__ void suffix_min2_excl(uint32_t &a, uint32_t &b, FastLds &s) {
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  uint32_t ia = a, ib = b;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint32_t ya = (uint32_t)__shfl_down((int)ia, o), yb = (uint32_t)__shfl_down((int)ib, o);
-    if (lane + o < kWave) ia = umin(ia, ya), ib = umin(ib, yb);
-  }
+  uint32_t ia, ib;
+  uint32_t ea = wave_suffix_min_excl(a, lane, kNever, &ia);
+  uint32_t eb = wave_suffix_min_excl(b, lane, kNever, &ib);
   if (lane == 0) s.wg[8 + w] = (int)ia, s.wg[12 + w] = (int)ib;
-  uint32_t ea = (uint32_t)__shfl_down((int)ia, 1), eb = (uint32_t)__shfl_down((int)ib, 1);
-  if (lane == kWave - 1) ea = eb = kNever;
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kFastWaves; j++)
@@ -2079,6 +2078,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     return;
   }
   const int n = (int)n64;
+  FGP_T(0);
 #if LC_FAST_DEV == 2  // dev timing only: loads, no decision
   {
     int64_t x = 0;
@@ -2113,6 +2113,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
   const int64_t base_idx = kops[0].call;  // (a scalar load, beside the records')
   __syncthreads();
 #endif
+  FGP_T(1);
   const int V0 = p.init_ver, init = p.init_val;
   int inel = 0, bad = 0, nmut = 0, jit_only = 0, giveup = 0, vbad = 0;
   int ext = 0;  // past the last placed position and the highest read version
@@ -2152,7 +2153,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
       // (lane 0's predecessor is checked after the barrier, from last_call).
       // Key-relative 32-bit calls: exact when neither record is malformed,
       // and a malformed one sends the key to the JIT tier anyway
-      const uint32_t prev = (uint32_t)__shfl_up((int)d.call, 1);
+      const uint32_t prev = (uint32_t)wave_shr1((int)d.call, 0);
       if (lane == 0) s.first_call[u][w] = d.call;
       if (lane == kWave - 1) s.last_call[u][w] = d.call;
       if (d.bad || d.f > LC_F_CAS || (lane > 0 && prev >= d.call)) {
@@ -2231,6 +2232,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     }
   }
   __syncthreads();
+  FGP_T(2);
   uint32_t wor;
   int M;
   {
@@ -2251,11 +2253,25 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     }
     if (__ballot(ob)) wor |= kSumInel | kSumJit;
   }
+#ifdef LC_FG_STOP1  // dev timing only: the fused pass stops after pass 1
+  if (MODE == kModeFused) {
+    if (tid == 0) out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
+    return;
+  }
+#endif
   if (wor & kSumElig) {  // ineligible or a version out of range: hand over
     // crash-light pass: crashed writes/CAS are the only obstacle
     if constexpr (MODE != kModeFast)
       if ((wor & kSumElig) == kSumInel && fast_gap(key, n, M, p, s, out, wit, o.kind, tid)) {
         if (MODE == kModeFused && tid == 0) atomicAdd(&o.status->n_light, 1);
+#ifdef LC_FG_PROF
+        if (MODE == kModeFused) {
+          FGP_T(3);
+          FGP_ADD(0, 0, 1);
+          FGP_ADD(1, 1, 2);
+          FGP_ADD(2, 2, 3);
+        }
+#endif
         return;
       }
     if (tid == 0) fast_pass_on<MODE>(key, o, &s.raised, (wor & kSumJit) != 0);
@@ -2442,6 +2458,14 @@ __global__ __launch_bounds__(kFastThreads) __attribute__((amdgpu_waves_per_eu(LC
   fast_run<kModeFused>(ops, key_off, n_keys, p, s, out, o);
 #else
   fast_one<kModeFused>(ops, key_off, blockIdx.x, p, s, out, o);
+#endif
+#ifdef LC_FG_PROF
+  if (threadIdx.x == 0 && atomicAdd(&g_fgdone, 1u) == gridDim.x - 1) {
+    printf("fgprof keys-wg %u entry->init %llu init->pass1 %llu pass1->light %llu scans %llu match %llu\n",
+           gridDim.x, g_fgp[0], g_fgp[1], g_fgp[2], g_fgp[3], g_fgp[4]);
+    for (int i = 0; i < 8; i++) g_fgp[i] = 0;
+    g_fgdone = 0;
+  }
 #endif
 }
 

@@ -191,12 +191,7 @@ __device__ __forceinline__ void ws_min(P p, uint32_t v) {
 template <int T>
 __device__ __forceinline__ int block_excl_sum(int v, GapSh &sh, int *total) {
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  int incl = v;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int y = __shfl_up(incl, o);
-    if (lane >= o) incl += y;
-  }
+  const int incl = wave_prefix_sum(v, lane);
   if (lane == kWave - 1) sh.wtot[w] = incl;
   __syncthreads();
   int pre = 0, tot = 0;
@@ -214,20 +209,14 @@ __device__ __forceinline__ int block_excl_sum(int v, GapSh &sh, int *total) {
 template <int T>
 __device__ __forceinline__ uint32_t block_suffix_min_excl(uint32_t v, GapSh &sh) {
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  uint32_t incl = v;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_down((int)incl, o);
-    if (lane + o < kWave) incl = incl < y ? incl : y;
-  }
+  uint32_t incl;
+  const uint32_t excl = wave_suffix_min_excl(v, lane, kNever, &incl);
   if (lane == 0) sh.wtotu[w] = incl;
   __syncthreads();
   uint32_t post = kNever;
 #pragma unroll
   for (int j = 0; j < (T / kWave); j++)
     if (j > w) post = post < sh.wtotu[j] ? post : sh.wtotu[j];
-  uint32_t excl = (uint32_t)__shfl_down((int)incl, 1);
-  if (lane == kWave - 1) excl = kNever;
   __syncthreads();
   return post < excl ? post : excl;
 }
