@@ -687,10 +687,25 @@ __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ 
                                                         uint32_t epoch, Ctr *ctr, int64_t k,
                                                         int64_t lo_arg, int64_t hi_arg, Cfg *cbuf,
                                                         unsigned long long cand_cap) {
+  // The prologue's loads go out together — the level's size, the table-full
+  // flag and this thread's words of the window — one round trip to memory
+  // before the first configuration instead of three in a row (a level's
+  // launch is a chain of dependent round trips: DESIGN.md §7).
+  constexpr int kWinWords = (int)(sizeof(Win) / 4);
+  constexpr int kWinPer = (kWinWords + 255) / 256;
+  uint32_t wv[kWinPer];
+  const uint32_t *wsrc = reinterpret_cast<const uint32_t *>(gwin);
+#pragma unroll
+  for (int j = 0; j < kWinPer; j++) {
+    const int i = (int)threadIdx.x + j * 256;
+    wv[j] = i < kWinWords ? wsrc[i] : 0u;
+  }
+  const int64_t cnt = lo_arg < 0 ? (int64_t)ctr->cnt[k % 3] : 0;
+  const unsigned long long tfull = ctr->tfull;
   int64_t lo, hi;
   if (lo_arg < 0) {
     lo = 0;
-    hi = (int64_t)ctr->cnt[k % 3];
+    hi = cnt;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       ctr->cnt[(k + 2) % 3] = 0;
       if (hi) {
@@ -703,11 +718,18 @@ __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ 
     hi = hi_arg;
   }
   if (lo + (int64_t)blockIdx.x * (blockDim.x / kW) >= hi) return;
-  if (ctr->tfull) return;  // this attempt will be redone with a larger table
+  if (tfull) return;  // this attempt will be redone with a larger table
   __shared__ Win w;
   __shared__ Stage stg[4];
   __shared__ WgFlush wf;
-  load_win(w, gwin);
+  {
+    uint32_t *dst = reinterpret_cast<uint32_t *>(&w);
+#pragma unroll
+    for (int j = 0; j < kWinPer; j++) {
+      const int i = (int)threadIdx.x + j * 256;
+      if (i < kWinWords) dst[i] = wv[j];
+    }
+  }
   __syncthreads();
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kW;
   const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kW;
