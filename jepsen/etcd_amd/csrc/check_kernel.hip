@@ -1654,6 +1654,7 @@ __device__ __forceinline__ int fg_prefix_wave(int v, FastLds &s, int tid) {
 __device__ __forceinline__ bool fast_gap(int64_t key, int n, int NM, const KParams &p, FastLds &s,
                          lc_key_result *__restrict__ out, int32_t *__restrict__ wit,
                          int32_t *__restrict__ kind, int tid) {
+  FGP_T(17);
   const int lane = tid & (kWave - 1), w = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int init = p.init_val;
   // a value claim failed: invalid (the gap tier names the fail op)
@@ -1679,6 +1680,7 @@ __device__ __forceinline__ bool fast_gap(int64_t key, int n, int NM, const KPara
   const uint32_t mycnt = (uint32_t)s.wg[4 + w];
   const int mytot = (int)((mycnt & 0xFF) + ((mycnt >> 8) & 0xFF) + ((mycnt >> 16) & 0xFF) + (mycnt >> 24));
   int4 mine = make_int4(0, 0, 0, 0);
+  FGP_T(13);
   if (lane < mytot)
     mine = reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(lds_dyn) + kFgStashOff)[w * kFgStash + lane];
   // deadlines: Uh[k] = min(B[k..M-1]) for this thread's positions 4t..4t+3
@@ -1696,7 +1698,9 @@ __device__ __forceinline__ bool fast_gap(int64_t key, int n, int NM, const KPara
       gapc += (k < M) && oo[j] == 0xFFFF;
     }
   }
+  FGP_T(14);
   const int gpre = fg_prefix_wave(gapc, s, tid);
+  FGP_T(15);
   const uint32_t after = fg_suffix_min_excl(bmin, s, tid);
   FGP_T(10);
   // (the barrier inside fg_suffix_min_excl also publishes s.wg[12..15])
@@ -1792,12 +1796,16 @@ __device__ __forceinline__ bool fast_gap(int64_t key, int n, int NM, const KPara
   FGP_T(12);
   FGP_ADD(3, 10, 11);
   FGP_ADD(4, 11, 12);
+  FGP_ADD(5, 17, 13);
+  FGP_ADD(6, 13, 14);
   if (G > 0) res = s.wg[0];
   if (res != GD_VALID) return false;
   if (tid == 0) {
     out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, nodes, G};
     if (kind) kind[key] = LC_WITNESS_FULL;
   }
+  FGP_T(16);
+  FGP_ADD(7, 12, 16);
   return true;
 }
 
@@ -2040,7 +2048,7 @@ __device__ __forceinline__ void fast_pass_on(int64_t key, const FastSinks &o, in
     // fused: status->n_light counts the keys the gap procedure takes, here
     // or in the crash-light decision (fast_key)
     if constexpr (MODE == kModeFused)
-      if (!jit_only) atomicAdd(&o.status->n_light, 1);
+      if (!jit_only) atomicAdd(light_shard(o.status, key), 1);
     fast_tier_handoff(key, o.flags, o.status, o.h_handoff, jit_only, raised);
   }
 }
@@ -2253,6 +2261,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     }
     if (__ballot(ob)) wor |= kSumInel | kSumJit;
   }
+  FGP_T(4);
 #ifdef LC_FG_STOP1  // dev timing only: the fused pass stops after pass 1
   if (MODE == kModeFused) {
     if (tid == 0) out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
@@ -2263,7 +2272,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     // crash-light pass: crashed writes/CAS are the only obstacle
     if constexpr (MODE != kModeFast)
       if ((wor & kSumElig) == kSumInel && fast_gap(key, n, M, p, s, out, wit, o.kind, tid)) {
-        if (MODE == kModeFused && tid == 0) atomicAdd(&o.status->n_light, 1);
+        if (MODE == kModeFused && tid == 0) atomicAdd(light_shard(o.status, key), 1);
 #ifdef LC_FG_PROF
         if (MODE == kModeFused) {
           FGP_T(3);
@@ -2461,8 +2470,9 @@ __global__ __launch_bounds__(kFastThreads) __attribute__((amdgpu_waves_per_eu(LC
 #endif
 #ifdef LC_FG_PROF
   if (threadIdx.x == 0 && atomicAdd(&g_fgdone, 1u) == gridDim.x - 1) {
-    printf("fgprof keys-wg %u entry->init %llu init->pass1 %llu pass1->light %llu scans %llu match %llu\n",
-           gridDim.x, g_fgp[0], g_fgp[1], g_fgp[2], g_fgp[3], g_fgp[4]);
+    printf("fgprof keys-wg %u entry->init %llu init->pass1 %llu pass1->light %llu scans %llu match %llu "
+           "entry->stash %llu stash+deadlines %llu after-match %llu\n",
+           gridDim.x, g_fgp[0], g_fgp[1], g_fgp[2], g_fgp[3], g_fgp[4], g_fgp[5], g_fgp[6], g_fgp[7]);
     for (int i = 0; i < 8; i++) g_fgp[i] = 0;
     g_fgdone = 0;
   }

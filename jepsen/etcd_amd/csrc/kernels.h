@@ -36,8 +36,24 @@ struct KStatus {
   int32_t any_handoff;  // fast tier: some key was handed over (read before the host store)
   int32_t n_gap2;       // crash-light pass: keys it passes on to the gap tier
   int32_t hbm_next;     // HBM tiers: next list entry to claim (zeroed before each launch)
-  int32_t n_light;      // fused tier: keys that took the crash-light decision
+  int32_t n_light;      // fused tier: keys that took the crash-light decision (host: light_count)
+  // ... counted on the device in kLightShards counters 128 B apart, by key:
+  // one same-address device-scope atomic per key (10,000 on the crash leg)
+  // queued behind one another and held up the workgroups' stores and loads
+  // (fused pass 0.166 -> 0.121 ms without it)
+  int32_t n_light_sh[32 * 32];
 };
+constexpr int kLightShards = 32, kLightStride = 32;
+__host__ __device__ inline int32_t *light_shard(KStatus *s, int64_t key) {
+  return &s->n_light_sh[(key & (kLightShards - 1)) * kLightStride];
+}
+// The sum of the shards, into n_light (host, after the status copy).
+inline int32_t light_count(KStatus &s) {
+  int32_t n = 0;
+  for (int i = 0; i < kLightShards; i++) n += s.n_light_sh[i * kLightStride];
+  s.n_light = n;
+  return n;
+}
 
 constexpr int kWave = 64;
 constexpr int kWavesPerWG = 4;   // independent keys per 256-thread workgroup

@@ -289,8 +289,9 @@ int64_t settle_status(Dev &d) {
   if (!d.st_pending) return -1;
   d.st_pending = false;
   if (hipEventSynchronize(d.es) != hipSuccess) return 0;
-  d.use_fused = 4 * (int64_t)d.h_status->n_light > d.st_keys;
-  return d.h_status->n_light;
+  const int32_t n_light = lcdev::light_count(*d.h_status);
+  d.use_fused = 4 * (int64_t)n_light > d.st_keys;
+  return n_light;
 }
 
 // Run the tiers for n_keys keys whose device arrays are in place.
@@ -489,6 +490,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                                 hipMemcpyDeviceToHost, st));
       HIP_TRY(c, hipStreamSynchronize(st));
       n_direct = d.h_status->n_jit2;
+      if (fused) lcdev::light_count(*d.h_status);
       if (gap_on) {
         // fused: were most keys crash-light?  Else: most keys handed to the
         // gap tier: the next call fuses the passes
