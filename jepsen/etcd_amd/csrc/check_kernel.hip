@@ -2536,6 +2536,24 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
   }
 }
 
+// launch_status_settle (kernels.h): one workgroup.
+__global__ __launch_bounds__(256) void status_settle_kernel(KStatus *__restrict__ status,
+                                                            int32_t *__restrict__ h_light) {
+  const int tid = threadIdx.x;
+  int v = tid < kLightShards ? status->n_light_sh[tid * kLightStride] : 0;
+  if (tid < kWave) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (tid == 0) {
+      __hip_atomic_store(h_light, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+    }
+  }
+  __syncthreads();
+  uint32_t *w = reinterpret_cast<uint32_t *>(status);
+  for (int i = tid; i < (int)(sizeof(KStatus) / 4); i += 256) w[i] = 0;
+}
+
 // Build the handoff lists from the fast tier's per-key flags (and clear
 // them): one list reservation (atomicAdd) and one max per workgroup chunk.
 constexpr int kCompactThreads = 256;
@@ -2712,6 +2730,11 @@ __global__ __launch_bounds__(256) void witness_init_kernel(
 }
 
 }  // namespace
+
+hipError_t launch_status_settle(KStatus *d_status, int32_t *h_light, hipStream_t stream) {
+  hipLaunchKernelGGL(status_settle_kernel, dim3(1), dim3(256), 0, stream, d_status, h_light);
+  return hipGetLastError();
+}
 
 hipError_t launch_handoff_compact(int32_t *d_flags, const int64_t *d_key_off, int64_t n_keys,
                                   int route_direct, int32_t *d_jit_keys, int32_t *d_direct_keys,

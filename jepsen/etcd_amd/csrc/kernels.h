@@ -99,6 +99,10 @@ hipError_t launch_gap_light(const lc_op *d_ops, const int64_t *d_key_off, const 
                             int64_t max_keys, const KParams &p, lc_key_result *d_out,
                             int32_t *d_pass, KStatus *d_status, int32_t *d_witness,
                             int32_t *d_witness_kind, hipStream_t stream);
+// After a fused pass that handed nothing over: the crash-light key count
+// (the sum of the shards) to *h_light (mapped host memory), then *d_status
+// zeroed for the next call — one launch instead of a copy and a memset.
+hipError_t launch_status_settle(KStatus *d_status, int32_t *h_light, hipStream_t stream);
 // With witness_kind, every handed-over key's kind is reset to
 // LC_WITNESS_NONE (a later tier that certifies it sets it again).
 hipError_t launch_handoff_compact(int32_t *d_flags, const int64_t *d_key_off, int64_t n_keys,

@@ -131,7 +131,8 @@ struct Dev {
   int64_t n_jit = 0;
   lcdev::KStatus *d_status = nullptr;   // all-zero between calls
   lcdev::KStatus *h_status = nullptr;   // pinned: D2H copies of d_status
-  int32_t *h_handoff = nullptr;         // host-coherent flag: fast tier handed keys over
+  int32_t *h_handoff = nullptr;         // host-coherent: [0] fast tier handed keys over, [1] a fused
+                                        // pass's crash-light key count (status_settle_kernel)
   int32_t *h_handoff_dev = nullptr;     // its device address
   bool status_dirty = true;             // d_status may be non-zero
   // the handoff flags may be non-zero (the fast tier raised some and no
@@ -289,7 +290,7 @@ int64_t settle_status(Dev &d) {
   if (!d.st_pending) return -1;
   d.st_pending = false;
   if (hipEventSynchronize(d.es) != hipSuccess) return 0;
-  const int32_t n_light = lcdev::light_count(*d.h_status);
+  const int32_t n_light = __atomic_load_n(d.h_handoff + 1, __ATOMIC_ACQUIRE);  // (status_settle_kernel)
   d.use_fused = 4 * (int64_t)n_light > d.st_keys;
   return n_light;
 }
@@ -437,14 +438,12 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     if (fused && !handed) {
       // every key decided in the one pass: were most of them crash-light?
       // (the answer picks the next call's pass; copied now, read later)
-      HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus),
-                                hipMemcpyDeviceToHost, st));
+      // (one launch: the count to mapped host memory, d_status zeroed behind
+      // it now — while the host returns — not at the start of the next call)
+      HIP_TRY(c, lcdev::launch_status_settle(d.d_status, d.h_handoff_dev + 1, st));
       HIP_TRY(c, hipEventRecord(d.es, st));
       d.st_pending = true;
       d.st_keys = n_keys;
-      // zeroed behind the copy now (while the host returns), not at the
-      // start of the next call
-      HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
       d.status_dirty = false;
     }
     if (handed) {
@@ -883,7 +882,7 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
           hipEventCreateWithFlags(&d.es, kEventFlags) != hipSuccess ||
           hipMalloc(reinterpret_cast<void **>(&d.d_status), sizeof(lcdev::KStatus)) != hipSuccess ||
           hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess ||
-          hipHostMalloc(reinterpret_cast<void **>(&d.h_handoff), sizeof(int32_t),
+          hipHostMalloc(reinterpret_cast<void **>(&d.h_handoff), 2 * sizeof(int32_t),
                         hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
           hipHostGetDevicePointer(reinterpret_cast<void **>(&d.h_handoff_dev), d.h_handoff, 0) != hipSuccess) {
         c->devs.push_back(d);  // lc_close frees what was created
