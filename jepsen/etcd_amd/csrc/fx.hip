@@ -187,21 +187,33 @@ __device__ inline void fix_f(Cfg &c, const Win &w) {
 constexpr int kExpShards = 64;
 constexpr int kExpStride = 16;  // u64 per shard: 128 B
 
+// The same holds for every counter a level's workgroups all touch: on a
+// multi-XCD chip a device-scope atomic is executed past the XCD's L2, and
+// atomics on one 128-B line queue behind one another.  So the two list
+// reservations (R, the next level's V) sit on lines of their own, and the
+// retirement AND is sharded like `exp` (the host ANDs the shards: sync_ctr).
+constexpr int kAndShards = 16;
+
 struct Ctr {
-  unsigned long long nR, nV;    // R list size; V entries of the levels expanded so far
-  unsigned long long cnt[3];    // V levels, triple-buffered: level k is list k % 3
+  unsigned long long nV;        // V entries of the levels expanded so far
   unsigned long long kcur;      // fx_small_return_kernel: the first level it left unexpanded
   unsigned long long explored;  // successors generated (cumulative)
   unsigned long long levels;    // non-empty levels (cumulative)
-  unsigned long long andmask;   // AND of R's masks
+  unsigned long long andmask;   // AND of R's masks (host: the AND of `andm`, sync_ctr)
   unsigned long long overflow;  // a list ran out of room (the budget)
   unsigned long long nsel;      // filter output
   unsigned long long tfull;     // a table probe ran too long: redo the return with a larger table
-  unsigned long long pad[5];
-  unsigned long long cand[64];  // partitioned: candidates per owner rank
+  alignas(128) unsigned long long nR;      // R list size (reserved per workgroup)
+  alignas(128) unsigned long long cnt[3];  // V levels, triple-buffered: level k is list k % 3
+  alignas(128) unsigned long long cand[64];  // partitioned: candidates per owner rank
   unsigned long long cmin[kMaxCls];  // counted classes: the smallest field over R (retirement)
+  alignas(128) unsigned long long andm[kAndShards * kExpStride];  // AND of R's masks, sharded
   alignas(128) unsigned long long exp[kExpShards * kExpStride];  // explored, sharded
 };
+
+__device__ inline void and_into(Ctr *ctr, unsigned long long a) {
+  atomicAnd(&ctr->andm[(blockIdx.x % kAndShards) * kExpStride], a);
+}
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {
   x ^= x >> 33;
@@ -387,7 +399,7 @@ __device__ inline void ctr_start(Ctr *ctr, unsigned long long explored) {
   ctr->nR = ctr->nV = ctr->kcur = 0;
   ctr->cnt[0] = ctr->cnt[1] = ctr->cnt[2] = 0;
   ctr->levels = 0;
-  ctr->andmask = ~0ULL;
+  for (int i = 0; i < kAndShards; i++) ctr->andm[i * kExpStride] = ~0ULL;
   ctr->nsel = 0;
   ctr->tfull = 0;
   ctr->explored = explored;
@@ -419,7 +431,7 @@ __device__ inline void split_into_rv(const Cfg *__restrict__ in, int64_t n, cons
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned long long a = s_and[0] & s_and[1] & s_and[2] & s_and[3];
-    if (a != ~0ULL) atomicAnd(&ctr->andmask, a);
+    if (a != ~0ULL) and_into(ctr, a);
   }
 }
 
@@ -532,7 +544,7 @@ __device__ inline void wg_flush(WgFlush *wf, Stage *stg, int nr, int nv, unsigne
       te += wf->explored[k];
       ta &= wf->andm[k];
     }
-    if (ta != ~0ULL) atomicAnd(&ctr->andmask, ta);
+    if (ta != ~0ULL) and_into(ctr, ta);
     wf->base[0] = tr ? atomicAdd(&ctr->nR, tr) : 0;
     wf->base[1] = tv ? atomicAdd(t.vcnt, tv) : 0;
     if (te) atomicAdd(&t.exp[(blockIdx.x % kExpShards) * kExpStride], te);
@@ -819,7 +831,7 @@ __global__ __launch_bounds__(256) void fx_small_return_kernel(const Cfg *__restr
   unsigned long long a = ~0ULL;
   for (int64_t i = threadIdx.x; i < nR; i += blockDim.x) a &= t.listR[i].mask;
   a = wave_and(a);
-  if (__lane_id() == 0 && a != ~0ULL) atomicAnd(&ctr->andmask, a);
+  if (__lane_id() == 0 && a != ~0ULL) and_into(ctr, a);
   cls_min_over(w, t.listR, threadIdx.x, nR, blockDim.x, ctr);
   __syncthreads();
   if (threadIdx.x < kW) {
@@ -843,7 +855,7 @@ __global__ __launch_bounds__(256) void fx_and_kernel(const Cfg *__restrict__ lis
        i += (int64_t)gridDim.x * blockDim.x)
     a &= list[i].mask;
   a = wave_and(a);
-  if (__lane_id() == 0 && a != ~0ULL) atomicAnd(&ctr->andmask, a);
+  if (__lane_id() == 0 && a != ~0ULL) and_into(ctr, a);
 }
 
 __global__ __launch_bounds__(256) void fx_clear_kernel(Cfg *list, int64_t n, uint64_t bits) {
@@ -1813,6 +1825,9 @@ struct Rank {
     unsigned long long e = 0;
     for (int i = 0; i < kExpShards; i++) e += hCtr->exp[i * kExpStride];
     hCtr->explored = e + exp_off;
+    unsigned long long a = ~0ULL;
+    for (int i = 0; i < kAndShards; i++) a &= hCtr->andm[i * kExpStride];
+    hCtr->andmask = a;
     return 0;
   }
 
@@ -2420,7 +2435,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           // level add theirs): no pass over R unless counted classes need
           // their minima, which that pass recomputes whole
           if (n_cls && (small || batch)) {  // the reset set them for a first batch
-            FX_TRY(hipMemsetAsync(&dCtr->andmask, 0xFF, sizeof(unsigned long long), st));
+            FX_TRY(hipMemsetAsync(dCtr->andm, 0xFF, sizeof(dCtr->andm), st));
             FX_TRY(hipMemsetAsync(dCtr->cmin, 0xFF, sizeof(dCtr->cmin), st));
           }
           for (int l = 0; l < spec_levels; l++, k++)
