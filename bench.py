@@ -258,9 +258,11 @@ def main():
             line["c3_shards"] = c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream)
         line["c1_leg"] = c1_leg(ctx, abi)
         line["host_leg"] = host_leg(ctx, abi, ops, key_off, n_inv)
+        line["host_leg32"] = host_leg32(ctx, abi, ops, key_off)
         line["hot_key"] = hot_key(ctx, abi)
         line["search_leg"] = search_leg(ctx, abi, d_ops, d_off, d_out, my_keys, stream, n_ops)
         line["mixed_leg"] = mixed_leg(ctx, abi, dev, stream)
+        line["dropin_leg"] = dropin_leg(ctx, abi)
         line["model_leg"] = model_leg(ctx, abi)
         line["crash_leg"] = crash_leg(ctx, abi, dev, stream)
         line["oversized_key"] = oversized_key(ctx, abi)
@@ -349,17 +351,62 @@ def c1_leg(ctx, abi):
 
 def host_leg(ctx, abi, ops, key_off, n_inv):
     """The same C2 batch handed over as host buffers (lc_check: H2D copy of
-    the 480 MB of records, the kernels, D2H of the results), as a JVM caller
-    would: the PCIe-inclusive rate.  Never `value`; median of 3 calls."""
-    times = []
+    the 480 MB of records in chunks overlapped with the version-order tier,
+    D2H of the results), as a JVM caller would: the PCIe-inclusive rate.
+    Never `value`; median of 3 calls."""
+    times, profs = [], []
     for _ in range(4):
         t0 = time.perf_counter()
         _, r = ctx.check(ops, key_off)
         times.append(time.perf_counter() - t0)
-    t = float(np.median(times[1:]))
-    return {"workload": "C2 batch from host memory (lc_check)", "call_ms": t * 1e3,
+        profs.append(ctx.call_profile())
+    i = 1 + int(np.argsort(times[1:])[1])
+    t = times[i]
+    return {"workload": "C2 batch from host memory (lc_check, 48-byte records)", "call_ms": t * 1e3,
             "ops_per_s": int(key_off[-1]) / t, "h2d_gb_per_s": ops.nbytes / t / 1e9,
-            "valid": int((r["verdict"] == 1).sum())}
+            "profile": profs[i], "valid": int((r["verdict"] == 1).sum())}
+
+
+def host_leg32(ctx, abi, ops, key_off):
+    """The drop-in's rate (ABI 4): the C2 batch as 24-byte lc_op32 records
+    (what the JVM packer emits), lc_check32 from host memory — half the PCIe
+    bytes of lc_check, chunked copies overlapped with the widening and the
+    version-order tier.  Pageable, then page-locked (lc_host_register).
+    Results compared with lc_check's field for field.  lc_pack32 (narrowing
+    the 48-byte records on the host) is timed apart: a packer that emits
+    lc_op32 directly never runs it.  Never `value`; median of 3 calls."""
+    t0 = time.perf_counter()
+    o32, base = abi.pack32(ops, key_off)
+    pack_ms = (time.perf_counter() - t0) * 1e3
+    _, want = ctx.check(ops, key_off)
+    out = {"workload": "C2 batch from host memory as 24-byte records (lc_check32)",
+           "pack32_ms": pack_ms, "bytes": int(o32.nbytes)}
+    for mode in ("pageable", "registered"):
+        if mode == "registered":
+            t0 = time.perf_counter()
+            ctx.host_register(o32)
+            out["register_ms"] = (time.perf_counter() - t0) * 1e3
+        try:
+            times, profs, devs = [], [], []
+            for _ in range(4):
+                t0 = time.perf_counter()
+                _, r = ctx.check32(o32, key_off, base)
+                times.append(time.perf_counter() - t0)
+                profs.append(ctx.call_profile())
+                devs.append(ctx.device_stats())
+        finally:
+            if mode == "registered":
+                ctx.host_unregister(o32)
+        i = 1 + int(np.argsort(times[1:])[1])
+        t = times[i]
+        d = devs[i][0]
+        out[mode] = {"call_ms": t * 1e3, "ops_per_s": int(key_off[-1]) / t,
+                     "h2d_ms": d["h2d_ms"],
+                     "h2d_gb_per_s": d["h2d_bytes"] / (d["h2d_ms"] * 1e-3) / 1e9
+                     if d["h2d_ms"] > 0 else None,
+                     "profile": profs[i], "valid": int((r["verdict"] == 1).sum()),
+                     "result_mismatches_vs_lc_check": int((r != want).sum())}
+    return out
 
 
 def fanout_leg(abi, ops, key_off, world, local, calls=3):
@@ -371,7 +418,9 @@ def fanout_leg(abi, ops, key_off, world, local, calls=3):
     range, H2D time (HIP events), kernel time, wall time; aggregate H2D rate.
     A/B: the records as pageable memory, then page-locked by
     lc_host_register (DMA straight from the caller's buffer; registration
-    time reported).  Median of `calls` after one warm-up; not `value` (the
+    time reported); then the same as 24-byte records (lc_check32, ABI 4).
+    Each mode's lc_call_profile attributes the call's wall time (the split,
+    the threads' start and end, the join).  Median of `calls` after one warm-up; not `value` (the
     PCIe-inclusive rate).  Rehearsal on one GPU (LC_BENCH_DEVICE): N device
     contexts on that GPU (LC_VIRTUAL_DEVICES)."""
     rehearsal = bool(os.environ.get("LC_BENCH_DEVICE"))
@@ -393,28 +442,33 @@ def fanout_leg(abi, ops, key_off, world, local, calls=3):
         else:
             os.environ["LC_VIRTUAL_DEVICES"] = saved
     try:
-        for mode in ("pageable", "registered"):
-            if mode == "registered":
+        o32, base = abi.pack32(ops, key_off)
+        for mode in ("pageable", "registered", "pageable32", "registered32"):
+            buf = o32 if mode.endswith("32") else ops
+            if mode.startswith("registered"):
                 t0 = time.perf_counter()
-                ctx.host_register(ops)
-                out["register_ms"] = (time.perf_counter() - t0) * 1e3
+                ctx.host_register(buf)
+                out["register_ms" + ("32" if buf is o32 else "")] = (time.perf_counter() - t0) * 1e3
             try:
                 rows = []
                 for i in range(calls + 1):
                     t0 = time.perf_counter()
-                    _, r = ctx.check(ops, key_off)
+                    if buf is o32:
+                        _, r = ctx.check32(o32, key_off, base)
+                    else:
+                        _, r = ctx.check(ops, key_off)
                     ms = (time.perf_counter() - t0) * 1e3
                     if i:
-                        rows.append((ms, ctx.device_stats()))
+                        rows.append((ms, ctx.device_stats(), ctx.call_profile()))
                 rows.sort(key=lambda x: x[0])
-                ms, devs = rows[len(rows) // 2]
+                ms, devs, prof = rows[len(rows) // 2]
             finally:
-                if mode == "registered":
-                    ctx.host_unregister(ops)
+                if mode.startswith("registered"):
+                    ctx.host_unregister(buf)
             h2d = sum(d["h2d_bytes"] for d in devs)
             slow = max(d["h2d_ms"] for d in devs)
             out[mode] = {
-                "call_ms": ms, "n_devices": len(devs),
+                "call_ms": ms, "n_devices": len(devs), "profile": prof,
                 "ops_per_s": int(key_off[-1] - key_off[0]) / (ms * 1e-3),
                 "h2d_gb_per_s_aggregate": h2d / (slow * 1e-3) / 1e9 if slow > 0 else None,
                 "valid": int((r["verdict"] == 1).sum()),
@@ -519,6 +573,46 @@ def mixed_leg(ctx, abi, dev, stream):
             "unknown": int((res["verdict"] == -1).sum()),
             "ops_per_s": int(off[-1]) / (float(np.median(wall[1:])) * 1e-3),
             "verdict_or_fail_op_mismatches_vs_oracle": mism}
+
+
+def dropin_leg(ctx, abi):
+    """What a Jepsen user waits for on C5 (BASELINE configs[4]): the drop-in's
+    calls from host memory — lc_check32 with witnesses and infeasibility
+    certificates (lc_aux), then knossos's :configs for every invalid key in
+    one batched device search (lc_check_frontiers) — timed apart and
+    together; the configurations compared with the oracle's JITC frontier
+    on every invalid key.  Not part of `value`; median of 5 after a warm-up."""
+    import oracle
+    ops, off, _, _ = abi.synth(1000, 200, concurrency=10, p_anomaly=0.1, seed=0x5EED0005)
+    o32, base = abi.pack32(ops, off)
+    check_ms, cfg_ms, tot = [], [], []
+    for _ in range(6):
+        t0 = time.perf_counter()
+        _, r, wit, kind, cert, cset = ctx.check32(o32, off, base, witness=True, certificate=True)
+        t1 = time.perf_counter()
+        inv = np.nonzero(r["verdict"] == 0)[0]
+        parts = [ops[off[i]:off[i + 1]] for i in inv]
+        sub = np.zeros(len(inv) + 1, dtype=np.int64)
+        sub[1:] = np.cumsum([len(p) for p in parts])
+        cfgs = ctx.check_frontiers(np.concatenate(parts), sub, r["fail_op"][inv], 10)
+        t2 = time.perf_counter()
+        check_ms.append((t1 - t0) * 1e3)
+        cfg_ms.append((t2 - t1) * 1e3)
+        tot.append((t2 - t0) * 1e3)
+    bad = n_fallback = 0
+    for j, i in enumerate(inv):
+        if cfgs[j] is None:
+            n_fallback += 1
+            continue
+        want, n_want = oracle.frontier(parts[j], int(r["fail_op"][i]))
+        bad += int(len(cfgs[j]) != min(10, n_want) or any(c not in want for c in cfgs[j]))
+    med = lambda x: float(np.median(x[1:]))
+    return {"workload": "C5: 1000 keys x 200 ops, 10 % injected anomalies, host buffers",
+            "check32_with_witness_and_certificates_ms": med(check_ms),
+            "configs_ms": med(cfg_ms), "total_ms": med(tot), "invalid_keys": int(len(inv)),
+            "certified_kinds": int((cert[inv, 0] != 0).sum()),
+            "configs_keys_left_to_lc_fx_frontier": n_fallback,
+            "configs_mismatches_vs_oracle_frontier": bad}
 
 
 def crash_leg(ctx, abi, dev, stream):

@@ -28,7 +28,9 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 3  /* 3: lc_aux certificates, lc_device_stats, lc_host_register */
+#define LC_ABI_VERSION 4  /* 3: lc_aux certificates, lc_device_stats, lc_host_register;
+                             4: 24-byte lc_op32 records (lc_pack32, lc_check32,
+                             lc_check_device32), lc_last_call_profile */
 
 /* Op kinds: the three :f values of register.clj:98-100 (r / w / cas). */
 #define LC_F_READ  0
@@ -294,6 +296,89 @@ int lc_last_device_stats(lc_ctx *ctx, int32_t i, lc_device_stats *out);
  * Returns 0, -EINVAL, or -EIO (text in lc_last_error). */
 int lc_host_register(lc_ctx *ctx, const void *ptr, uint64_t bytes);
 int lc_host_unregister(lc_ctx *ctx, const void *ptr);
+
+/*
+ * ABI 4: the same op in 24 bytes.  The device reads every field of an lc_op
+ * as int32 (key-relative 32-bit indices, int32 values and
+ * versions), so half of the 48-byte record the JVM hands over crosses PCIe
+ * for nothing.  lc_op32 carries exactly what the device reads:
+ *
+ *  f, value, expected, version   as in lc_op (int32; LC_NIL = -1)
+ *  call, ret   history indices relative to the key's base (key_base[k],
+ *              any int64; the key's first call when packed by lc_pack32);
+ *              ret = LC_INF32 for :info / unterminated ops.
+ *
+ * Meaning: record r of key k stands for the lc_op
+ *   {f, value, expected, version, key_base[k] + call,
+ *    ret == LC_INF32 ? LC_INF : key_base[k] + ret}
+ * (all int32 fields sign-extended, call/ret zero-extended; key_base NULL =
+ * all zero), and lc_check32 returns exactly what lc_check returns for those
+ * records — fail_prefix_end included, as an absolute history index.
+ *
+ * lc_pack32 narrows lc_op records key by key with the device's own rules, so
+ * that lc_check32(lc_pack32(x)) == lc_check(x) field for field (witnesses and
+ * certificates too):
+ *   - key_base[k] = the key's first call, call/ret relative to it;
+ *   - a version outside [-1, 2^31-2] (one no state can reach) becomes
+ *     2^31-2, which no state reaches either (the device saturates it so);
+ *   - an :f outside read/write/cas becomes 3 (unknown :f);
+ *   - a record the device rejects as malformed (a value or expected id
+ *     outside [-1, 2^31-2], call < 0, ret <= call, a key spanning 2^32-1 or
+ *     more indices) gets value = -2, which keeps it malformed; its other
+ *     fields are kept modulo 2^32, which is all the device reads of them.
+ * A JVM (or any) packer may emit lc_op32 directly by the same rules (the
+ * Clojure shim does: INTEGRATION.md §2).
+ */
+typedef struct lc_op32 {
+  int32_t f;
+  int32_t value;
+  int32_t expected;
+  int32_t version;
+  uint32_t call;
+  uint32_t ret;
+} lc_op32;
+
+#define LC_INF32 0xFFFFFFFFu
+
+/* Narrow n_keys keys of lc_op records into out (indexed like ops: key k's
+ * records are out[key_off[k] .. key_off[k+1])) and key_base (n_keys entries).
+ * Host-only, multi-threaded for large batches; usable without a GPU.
+ * Returns 0 or -EINVAL (null buffers, key_off not monotone). */
+int lc_pack32(const lc_op *ops, const int64_t *key_off, int64_t n_keys, lc_op32 *out,
+              int64_t *key_base);
+
+/* lc_check_ex on 24-byte records from host memory (aux may be NULL; ops and
+ * key_off indexed as in lc_check, key_base per key or NULL).  Each
+ * device's key range is copied in chunks on a copy stream while the
+ * version-order tier decides the chunks already copied. */
+int lc_check32(lc_ctx *ctx, const lc_op32 *ops, const int64_t *key_off, const int64_t *key_base,
+               int64_t n_keys, const lc_opts *opts, lc_key_result *out, const lc_aux *aux);
+
+/* lc_check_device_ex on 24-byte records resident on the context's first GPU
+ * (d_key_base may be NULL). */
+int lc_check_device32(lc_ctx *ctx, const lc_op32 *d_ops, const int64_t *d_key_off,
+                      const int64_t *d_key_base, int64_t n_keys, const lc_opts *opts,
+                      lc_key_result *d_out, void *stream, const lc_aux *aux);
+
+/* Where the host wall time of the last lc_check / lc_check_ex / lc_check32
+ * call went (ABI 4): the argument checks, the split over devices, the start
+ * of the per-device threads, their ends, the frontier-exchange re-search
+ * (LC_FLAG_WHOLE_GPU), all as milliseconds since the call began. */
+typedef struct lc_call_profile {
+  double total_ms;          /* the whole call */
+  double checked_ms;        /* arguments checked, options converted */
+  double planned_ms;        /* keys split over the devices (plan_devices) */
+  double first_start_ms;    /* first per-device thread running */
+  double last_start_ms;     /* last per-device thread running */
+  double first_end_ms;      /* first per-device thread done (results copied back) */
+  double last_end_ms;       /* last per-device thread done */
+  double joined_ms;         /* every thread joined, statistics summed */
+  double whole_gpu_ms;      /* LC_FLAG_WHOLE_GPU re-search done (= joined_ms without it) */
+  int64_t n_devices;
+  int64_t n_chunks;         /* host-to-device chunks issued over all devices */
+} lc_call_profile;
+
+int lc_last_call_profile(lc_ctx *ctx, lc_call_profile *out);
 
 const char *lc_last_error(lc_ctx *ctx);
 void lc_close(lc_ctx *ctx);

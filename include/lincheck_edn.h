@@ -86,6 +86,12 @@ int64_t lc_edn_n_events(const lc_edn_history *h);  /* op maps read */
 const lc_op *lc_edn_ops(const lc_edn_history *h);
 const int64_t *lc_edn_key_off(const lc_edn_history *h);
 
+/* The same records as 24-byte lc_op32 (n_ops) and each key's base (n_keys):
+ * the inputs of lc_check32 (ABI 4), narrowed by lc_pack32's rules on the
+ * first call; valid until lc_edn_free.  NULL on a null history. */
+const lc_op32 *lc_edn_ops32(lc_edn_history *h);
+const int64_t *lc_edn_key_base(lc_edn_history *h);
+
 /* EDN text of key i as it first appeared (NUL-terminated). */
 const char *lc_edn_key(const lc_edn_history *h, int64_t key);
 

@@ -164,6 +164,23 @@ typedef struct lc_fx_config {
 int lc_fx_frontier(lc_fx *fx, const lc_op *ops, int64_t n, const lc_opts *opts, int64_t stop_op,
                    lc_fx_config *out, int32_t max, int32_t *n_out);
 
+/* ABI 4: the same for many keys in one call on an lc_check context (its
+ * first GPU).  Key k (records ops[key_off[k] .. key_off[k+1]), host memory)
+ * is searched on the device — one wavefront per key, the JIT search of the
+ * LDS tier, the same reductions as the frontier exchange — up to the :ok
+ * return of its record stop_op[k], and up to max_per_key configurations of
+ * the frontier that return expands go to out[k * max_per_key ...]:
+ * knossos's :configs of an invalid key whose stop_op is its fail_op
+ * (register.clj:110-111).  n_out[k] = configurations copied; 0 when
+ * stop_op's return is a no-op (the op was retired); -1 when the search could
+ * not get there on the LDS tier (a frontier beyond 128 configurations, more
+ * than LC_MAX_WINDOW open ops, the budget, an earlier failure, a stop_op that
+ * is not an :ok op): lc_fx_frontier decides those one by one.  Returns 0,
+ * -EINVAL, -ENOMEM or -EIO. */
+int lc_check_frontiers(lc_ctx *ctx, const lc_op *ops, const int64_t *key_off, int64_t n_keys,
+                       const int64_t *stop_op, const lc_opts *opts, lc_fx_config *out,
+                       int32_t max_per_key, int32_t *n_out);
+
 /* From another thread: stop a search in progress.  Every RCCL communicator
  * of the engine is aborted (ncclCommAbort), so ranks waiting in a collective
  * return and lc_fx_check fails; an RCCL engine is unusable afterwards.  For

@@ -45,6 +45,9 @@ LC_CERT_NONE, LC_CERT_DUP, LC_CERT_UNREACH, LC_CERT_CLAIMS, LC_CERT_PAIR, LC_CER
     LC_CERT_HALL = range(7)
 
 # lc_op: 6 x int64 (f, value, expected, version, call, ret); arrays are (n, 6).
+# lc_op32 (ABI 4): the same fields as 6 x 32 bits, arrays (n, 6) int32 with
+# call / ret holding the uint32 bit patterns (LC_INF32 = 0xFFFFFFFF reads -1).
+LC_INF32 = 0xFFFFFFFF
 OP_FIELDS = ("f", "value", "expected", "version", "call", "ret")
 RESULT_DTYPE = np.dtype([
     ("verdict", "<i4"), ("reason", "<i4"), ("fail_op", "<i8"),
@@ -75,6 +78,15 @@ class LcDeviceStats(ctypes.Structure):
                 ("key_begin", ctypes.c_int64), ("key_end", ctypes.c_int64),
                 ("h2d_bytes", ctypes.c_int64), ("h2d_ms", ctypes.c_double),
                 ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+
+
+class LcCallProfile(ctypes.Structure):
+    _fields_ = [("total_ms", ctypes.c_double), ("checked_ms", ctypes.c_double),
+                ("planned_ms", ctypes.c_double), ("first_start_ms", ctypes.c_double),
+                ("last_start_ms", ctypes.c_double), ("first_end_ms", ctypes.c_double),
+                ("last_end_ms", ctypes.c_double), ("joined_ms", ctypes.c_double),
+                ("whole_gpu_ms", ctypes.c_double), ("n_devices", ctypes.c_int64),
+                ("n_chunks", ctypes.c_int64)]
 
 
 class LcAux(ctypes.Structure):
@@ -140,6 +152,18 @@ def lib():
         L.lc_check_device_ex.argtypes = [vp, vp, vp, i64, ctypes.POINTER(LcOpts), vp, vp,
                                          ctypes.POINTER(LcAux)]
         L.lc_check_device_ex.restype = ctypes.c_int
+        L.lc_check32.argtypes = [vp, p, p, p, i64, ctypes.POINTER(LcOpts), p,
+                                 ctypes.POINTER(LcAux)]
+        L.lc_check32.restype = ctypes.c_int
+        L.lc_check_device32.argtypes = [vp, vp, vp, vp, i64, ctypes.POINTER(LcOpts), vp, vp,
+                                        ctypes.POINTER(LcAux)]
+        L.lc_check_device32.restype = ctypes.c_int
+        L.lc_pack32.argtypes = [p, p, i64, p, p]
+        L.lc_pack32.restype = ctypes.c_int
+        L.lc_check_frontiers.argtypes = [vp, p, p, i64, p, ctypes.POINTER(LcOpts), vp, i32, p]
+        L.lc_check_frontiers.restype = ctypes.c_int
+        L.lc_last_call_profile.argtypes = [vp, ctypes.POINTER(LcCallProfile)]
+        L.lc_last_call_profile.restype = ctypes.c_int
         L.lc_key_cost.argtypes = [p, p, i64, p]
         L.lc_key_cost.restype = ctypes.c_int
         L.lc_last_stats.argtypes = [vp, ctypes.POINTER(LcStats)]
@@ -191,6 +215,26 @@ def as_ops(ops):
     if a.ndim != 2 or a.shape[1] != 6:
         a = a.reshape(-1, 6)
     return a
+
+
+def as_ops32(ops32):
+    a = np.ascontiguousarray(ops32, dtype=np.int32)
+    if a.ndim != 2 or a.shape[1] != 6:
+        a = a.reshape(-1, 6)
+    return a
+
+
+def pack32(ops, key_off):
+    """lc_pack32 (ABI 4): (ops32 (n, 6) int32, key_base int64 per key), the
+    records narrowed by the device's own rules (include/lincheck.h)."""
+    ops = as_ops(ops)
+    key_off = np.ascontiguousarray(key_off, dtype=np.int64)
+    out = np.zeros((len(ops), 6), dtype=np.int32)
+    base = np.zeros(max(len(key_off) - 1, 0), dtype=np.int64)
+    rc = lib().lc_pack32(_ptr(ops), _ptr(key_off), len(key_off) - 1, _ptr(out), _ptr(base))
+    if rc != 0:
+        raise LcError(rc, "lc_pack32")
+    return out, base
 
 
 class LcError(RuntimeError):
@@ -258,6 +302,29 @@ class Context:
         if rc != 0:
             raise LcError(rc, self.last_error())
 
+    def _check_host(self, fn, ops, key_off, extra, opts, raise_on_error, witness, certificate):
+        key_off = np.ascontiguousarray(key_off, dtype=np.int64)
+        n_keys = len(key_off) - 1
+        out = np.zeros(max(n_keys, 0), dtype=RESULT_DTYPE)
+        o = opts if opts is not None else default_opts()
+        wit = kind = cert = cset = None
+        aux = None
+        if witness or certificate:
+            wit = np.full(len(ops), -3, dtype=np.int32)
+            kind = np.full(max(n_keys, 0), -3, dtype=np.int32)
+            if certificate:
+                cert = np.full((max(n_keys, 0), 4), -3, dtype=np.int32)
+                cset = np.zeros(len(ops), dtype=np.int32)
+            aux = ctypes.byref(LcAux(wit.ctypes.data, kind.ctypes.data,
+                                     cert.ctypes.data if certificate else None,
+                                     cset.ctypes.data if certificate else None))
+        rc = fn(self._h, _ptr(ops), _ptr(key_off), *extra, n_keys, ctypes.byref(o), _ptr(out), aux)
+        if rc != 0 and raise_on_error:
+            raise LcError(rc, self.last_error())
+        if certificate:
+            return rc, out, wit, kind, cert, cset
+        return (rc, out, wit, kind) if witness else (rc, out)
+
     def check(self, ops, key_off, opts=None, raise_on_error=True, witness=False,
               certificate=False):
         """Host-buffer check. Returns (rc, results structured array), or with
@@ -265,31 +332,53 @@ class Context:
         from lc_check_ex (include/lincheck.h, lc_aux); certificate=True adds
         the infeasibility certificates (int32[n_keys, 4]) and their position
         sets (int32 per record): (rc, results, witness, kind, cert, cert_set)."""
+        return self._check_host(lib().lc_check_ex, as_ops(ops), key_off, (), opts,
+                                raise_on_error, witness, certificate)
+
+    def check32(self, ops32, key_off, key_base=None, opts=None, raise_on_error=True,
+                witness=False, certificate=False):
+        """lc_check32 (ABI 4): 24-byte records from host memory ((n, 6) int32,
+        as pack32 makes them) and their key bases; returns as check()."""
+        ops32 = as_ops32(ops32)
+        base = None if key_base is None else np.ascontiguousarray(key_base, dtype=np.int64)
+        return self._check_host(lib().lc_check32, ops32, key_off, (_ptr(base),), opts,
+                                raise_on_error, witness, certificate)
+
+    def check_frontiers(self, ops, key_off, stop_ops, max_per_key=10, opts=None):
+        """lc_check_frontiers (include/lincheck_fx.h, ABI 4): for every key,
+        up to max_per_key configurations of its JIT frontier just before the
+        :ok return of record stop_ops[k], as (version, value id, pending
+        record indices) tuples — or None where the device search could not
+        get there (the caller's fallback: FrontierExchange.frontier)."""
+        from .fx import LcFxConfig
         ops = as_ops(ops)
         key_off = np.ascontiguousarray(key_off, dtype=np.int64)
         n_keys = len(key_off) - 1
-        out = np.zeros(max(n_keys, 0), dtype=RESULT_DTYPE)
+        stop = np.ascontiguousarray(stop_ops, dtype=np.int64)
+        assert len(stop) == n_keys
+        buf = (LcFxConfig * max(1, n_keys * max_per_key))()
+        n_out = np.zeros(max(n_keys, 1), dtype=np.int32)
         o = opts if opts is not None else default_opts()
-        if witness or certificate:
-            wit = np.full(len(ops), -3, dtype=np.int32)
-            kind = np.full(max(n_keys, 0), -3, dtype=np.int32)
-            cert = cset = None
-            if certificate:
-                cert = np.full((max(n_keys, 0), 4), -3, dtype=np.int32)
-                cset = np.zeros(len(ops), dtype=np.int32)
-            aux = LcAux(wit.ctypes.data, kind.ctypes.data,
-                        cert.ctypes.data if certificate else None,
-                        cset.ctypes.data if certificate else None)
-            rc = lib().lc_check_ex(self._h, _ptr(ops), _ptr(key_off), n_keys,
-                                   ctypes.byref(o), _ptr(out), ctypes.byref(aux))
-        else:
-            rc = lib().lc_check(self._h, _ptr(ops), _ptr(key_off), n_keys,
-                                ctypes.byref(o), _ptr(out))
-        if rc != 0 and raise_on_error:
+        rc = lib().lc_check_frontiers(self._h, _ptr(ops), _ptr(key_off), n_keys, _ptr(stop),
+                                      ctypes.byref(o), ctypes.cast(buf, ctypes.c_void_p),
+                                      max_per_key, _ptr(n_out))
+        if rc != 0:
             raise LcError(rc, self.last_error())
-        if certificate:
-            return rc, out, wit, kind, cert, cset
-        return (rc, out, wit, kind) if witness else (rc, out)
+        out = []
+        for k in range(n_keys):
+            n = int(n_out[k])
+            if n < 0:
+                out.append(None)
+                continue
+            out.append([(int(c.version), int(c.value), tuple(int(c.pending[j]) for j in range(c.n_pending)))
+                        for c in buf[k * max_per_key:k * max_per_key + n]])
+        return out
+
+    def call_profile(self):
+        """lc_last_call_profile: where the last host call's wall time went."""
+        pr = LcCallProfile()
+        lib().lc_last_call_profile(self._h, ctypes.byref(pr))
+        return {f: getattr(pr, f) for f, _ in LcCallProfile._fields_}
 
     def check_device(self, d_ops, d_key_off, n_keys, d_out, stream=None, opts=None,
                      d_witness=None, d_witness_kind=None):
@@ -308,6 +397,18 @@ class Context:
             raise LcError(rc, self.last_error())
         return rc
 
+
+    def check_device32(self, d_ops32, d_key_off, d_key_base, n_keys, d_out, stream=None,
+                       opts=None):
+        """lc_check_device32 (ABI 4): 24-byte records resident on the GPU."""
+        o = opts if opts is not None else default_opts()
+        rc = lib().lc_check_device32(self._h, ctypes.c_void_p(d_ops32), ctypes.c_void_p(d_key_off),
+                                     ctypes.c_void_p(d_key_base) if d_key_base else None, n_keys,
+                                     ctypes.byref(o), ctypes.c_void_p(d_out),
+                                     ctypes.c_void_p(stream) if stream else None, None)
+        if rc != 0:
+            raise LcError(rc, self.last_error())
+        return rc
 
     def bind_check_device(self, d_ops, d_key_off, n_keys, d_out, stream=None, opts=None,
                           stats=None):

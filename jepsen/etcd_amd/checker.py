@@ -23,10 +23,11 @@ timeline_dir set, the timeline half renders <dir>/independent/<k>/
 timeline.html on the host (timeline.py), as jepsen's timeline/html would.
 An invalid key's map also carries knossos's diagnostics (diagnostics.py):
 "previous-ok", "configs" and "final-paths" — from the search's own frontier
-just before the failing return (lc_fx_frontier, up to 10 configurations) for
-keys the frontier search decided, from the witness of the prefix before the
-failing return (lc_aux, with "last-op") for keys the version-order and gap
-tiers decided.
+just before the failing return (up to 10 configurations: one batched device
+search over every invalid key, lc_check_frontiers, and lc_fx_frontier for a
+key whose frontier outgrows it), and "last-op" from the witness of the prefix
+before the failing return (lc_aux) for keys the version-order and gap tiers
+decided.
 
 Errors: a key with malformed records is "unknown" alone (cause
 "malformed"), as jepsen.independent would lose only that key; unusable
@@ -38,9 +39,11 @@ import os
 from . import abi, diagnostics as D, history as H, linear_svg as LS, timeline as TL
 
 UNKNOWN = "unknown"
-# invalid keys the version-order / gap tiers decided get knossos's :configs
-# from a frontier re-search when they have at most this many crashed ops (the
-# frontier of a version-pinned key grows with its crashed ops only)
+# an invalid key the batched device search (lc_check_frontiers) could not
+# take, and which the version-order / gap tiers decided, is re-searched alone
+# (lc_fx_frontier) for knossos's :configs only when it has at most this many
+# crashed ops (the frontier of a version-pinned key grows with its crashed ops
+# only)
 FRONTIER_MAX_CRASHED = 16
 CERT_KINDS = {0: "none", 1: "dup", 2: "unreach", 3: "claims", 4: "pair", 5: "order", 6: "hall"}
 
@@ -144,10 +147,15 @@ class RegisterChecker:
         o = abi.default_opts(self.max_configs_per_key, m.version, init,
                              flags=abi.LC_FLAG_WHOLE_GPU if self.whole_gpu else 0,
                              time_budget_ms=self.time_budget_ms)
-        _, res, wit, kind, cert, cset = self._context().check(ops, key_off, o, witness=True,
-                                                              certificate=True)
+        # the drop-in's call (ABI 4): 24-byte records, what crosses PCIe
+        # (the JVM shim packs them directly; here lc_pack32 narrows the
+        # 48-byte pack by the same rules)
+        ops32, key_base = abi.pack32(ops, key_off)
+        _, res, wit, kind, cert, cset = self._context().check32(
+            ops32, key_off, key_base, o, witness=True, certificate=True)
+        cfgs_of = self._configs(ops, key_off, res, o)
         results = {}
-        n_frontier = 0  # frontier re-searches run for diagnostics in this call
+        n_fallback = 0  # one-key frontier re-searches run for diagnostics in this call
         for i, k in enumerate(keys):
             r = res[i]
             v = {1: True, 0: False}.get(int(r["verdict"]), UNKNOWN)
@@ -171,16 +179,21 @@ class RegisterChecker:
                 recs = ops[key_off[i]:key_off[i + 1]]
                 witnessed = m.name == "versioned-register" and kind[i] == abi.LC_WITNESS_PREFIX
                 # knossos's :configs are its search's frontier just before the
-                # failing return: re-run the frontier search up to there
-                # (lc_fx_frontier) for keys whose frontier stays small — any
-                # key the search decided, and witnessed keys with at most
-                # FRONTIER_MAX_CRASHED crashed ops — up to frontier_max_keys
-                # keys per call; beyond that, or if the re-search fails, the
-                # witness's one configuration (with "configs-error" saying why)
-                cfgs, err = None, None
-                if not witnessed or (n_frontier < self.frontier_max_keys and
-                                     int((recs[:, 5] == abi.LC_INF).sum()) <= FRONTIER_MAX_CRASHED):
-                    n_frontier += 1
+                # failing return: every invalid key's came from one batched
+                # device search (lc_check_frontiers, _configs); a key that
+                # search could not take (its frontier outgrew the LDS tier) is
+                # re-searched alone by the frontier exchange (lc_fx_frontier)
+                # — any key the search decided, and witnessed keys with at
+                # most FRONTIER_MAX_CRASHED crashed ops — at most
+                # frontier_max_keys such re-searches per call (the Clojure
+                # shim counts the same way); beyond that, or if the re-search
+                # fails, the witness's one configuration (with
+                # "configs-error" saying why)
+                cfgs, err = cfgs_of.get(i), None
+                if cfgs is None and n_fallback < self.frontier_max_keys and (
+                        not witnessed or
+                        int((recs[:, 5] == abi.LC_INF).sum()) <= FRONTIER_MAX_CRASHED):
+                    n_fallback += 1
                     try:
                         cfgs = self._frontier().frontier(recs, int(r["fail_op"]), D.MAX_ENTRIES, o)
                     except Exception as e:  # noqa: BLE001 — diagnostics only; the verdict stands
@@ -217,6 +230,21 @@ class RegisterChecker:
         return {"valid?": _merge_valid(r["valid?"] for r in results.values()),
                 "results": results,
                 "failures": [k for k, r in results.items() if r["valid?"] is False]}
+
+    def _configs(self, ops, key_off, res, opts):
+        """knossos's :configs of every invalid key in one device call
+        (lc_check_frontiers): {key index: [(version, value id, pending)]},
+        the keys the device search could not take left out."""
+        import numpy as np
+        inv = np.nonzero(res["verdict"] == abi.LC_INVALID)[0]
+        if self.frontier_max_keys <= 0 or len(inv) == 0:
+            return {}
+        parts = [ops[key_off[i]:key_off[i + 1]] for i in inv]
+        sub_off = np.zeros(len(inv) + 1, dtype=np.int64)
+        sub_off[1:] = np.cumsum([len(x) for x in parts])
+        got = self._context().check_frontiers(np.concatenate(parts), sub_off,
+                                              res["fail_op"][inv], D.MAX_ENTRIES, opts)
+        return {int(i): c for i, c in zip(inv, got) if c is not None}
 
     def _composed(self, k, linear, subs):
         """checker/compose's per-key map (register.clj:109-112)."""

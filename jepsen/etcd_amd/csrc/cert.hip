@@ -37,6 +37,7 @@
 // once); its arrays live in a workspace of 6 int32 per (record + 2) of the
 // batch.  Only run when the caller asks for certificates: this is a
 // diagnostics pass, not on any timed path.
+#include <algorithm>
 #include <climits>
 
 #include "kernels.h"
@@ -329,7 +330,20 @@ __global__ __launch_bounds__(kCertThreads) void cert_kernel(
   }
 }
 
+__global__ __launch_bounds__(256) void cert_none_kernel(int32_t *__restrict__ cert, int64_t n_keys) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_keys; k += stride)
+    reinterpret_cast<int4 *>(cert)[k] = make_int4(LC_CERT_NONE, -1, -1, 0);
+}
+
 }  // namespace
+
+hipError_t launch_cert_none(int32_t *d_cert, int64_t n_keys, hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  const int64_t wgs = std::min<int64_t>((n_keys + 255) / 256, 1024);
+  hipLaunchKernelGGL(cert_none_kernel, dim3((unsigned)wgs), dim3(256), 0, stream, d_cert, n_keys);
+  return hipGetLastError();
+}
 
 size_t cert_ws_bytes(int64_t n_records, int64_t n_keys) {
   return sizeof(int32_t) * (size_t)kCertArrays * (size_t)(n_records + 2 * n_keys + 2);

@@ -37,6 +37,7 @@
 #include <climits>
 #include <type_traits>
 
+#include "../../../include/lincheck_fx.h"
 #include "kernels.h"
 #include "records.h"
 #include "wave.h"
@@ -1109,10 +1110,67 @@ __device__ __forceinline__ void check_order(Rec &r, uint32_t &last_call, int lan
   if (l != kNever) last_call = l;
 }
 
+// lc_check_frontiers (knossos :configs): the search of check_key<.., true>
+// stops at the :ok return of record `stop` (key-relative return stop_ret) and
+// writes up to `max` configurations of the frontier that return expands; n
+// = configurations written, 0 when the op's return was a no-op (it had been
+// retired), -1 when the search ended before (an earlier failure, an
+// overflow, the budget).  Wave-uniform.
+struct DumpReq {
+  int stop;
+  uint32_t stop_ret;
+  lc_fx_config *out;
+  int max;
+  int n;
+};
+
+// The frontier just before a return: the lone configuration (every occupied
+// slot pending in it), or region rF's first min(nF, max) configurations;
+// one lane per configuration writes its state and its pending ops (slots
+// occupied and not linearized in it), sorted by record index.
 template <class Store>
+__device__ void dump_frontier(const Store &st, const Slot &sl, const Masks &mk, bool single,
+                              uint64_t fsv, int rF, int nF, DumpReq &dr, int lane) {
+  const int m = single ? 1 : min(nF, dr.max);
+  for (int j0 = 0; j0 < m; j0 += kWave) {
+    const int j = j0 + lane;
+    const bool act = j < m;
+    uint64_t lin = 0, sv = fsv;
+    if (!single && act) {
+      const Cfg c = st.get(rF, j);
+      lin = c.mask;
+      sv = c.sv;
+    }
+    const uint64_t pend = mk.occ & ~lin;
+    lc_fx_config *c = dr.out + (act ? j : 0);
+    int np = 0;
+    for (int t = 0; t < kWave; t++) {
+      if (!((mk.occ >> t) & 1)) continue;  // (uniform)
+      const int idx = rl32(sl.idx, t);
+      if (act && ((pend >> t) & 1)) c->pending[np++] = idx;
+    }
+    if (act) {
+      for (int a = 1; a < np; a++) {  // insertion sort, <= 64 entries
+        const int64_t v = c->pending[a];
+        int b = a - 1;
+        while (b >= 0 && c->pending[b] > v) {
+          c->pending[b + 1] = c->pending[b];
+          b--;
+        }
+        c->pending[b + 1] = v;
+      }
+      c->version = sv_ver(sv);
+      c->value = sv_val(sv);
+      c->n_pending = np;
+    }
+  }
+  dr.n = m;
+}
+
+template <class Store, bool kDump = false>
 __device__ void check_key(const lc_op *__restrict__ kops, const int n,
                           const KParams &p, Store &st, KeyOut &o,
-                          const int lane) {
+                          const int lane, DumpReq *dreq = nullptr) {
   o.verdict = LC_VALID;
   o.reason = LC_REASON_NONE;
   o.fail_op = -1;
@@ -1146,6 +1204,12 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
     // several are due at once.
     const uint64_t due = __ballot(sl.ret < ncall);
     if (due == 0) {
+      if constexpr (kDump) {
+        if (ncall > dreq->stop_ret) {  // (i >= n included) its return came and went:
+          dreq->n = 0;                 // the op had been retired
+          return;
+        }
+      }
       if (i >= n) break;  // no calls left, no pending returns
       // ------------------------------------------------------- call of op i
       const int li = i - base;
@@ -1233,6 +1297,16 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
     const uint64_t bs = 1ull << s;
     const int x_idx = rl32(sl.idx, s);
     const uint32_t nret = (uint32_t)rl32((int)sl.ret, s);
+    if constexpr (kDump) {
+      if (nret > dreq->stop_ret) {
+        dreq->n = 0;
+        return;
+      }
+      if (x_idx == dreq->stop) {
+        dump_frontier(st, sl, mk, single, fsv, rF, nF, *dreq, lane);
+        return;
+      }
+    }
     bool empty = false;
     if (single) {
       // x is pending (a linearized op would have been retired).  Chain walk:
@@ -1375,6 +1449,54 @@ __global__ __launch_bounds__(kWave *kWavesPerWG) void lds_tier_kernel(
       const int pos = atomicAdd(&status->n_overflow, 1);
       ovf_keys[pos] = (int32_t)key;
     }
+  }
+}
+
+// lc_check_frontiers: one wavefront per key runs the LDS tier's search up to
+// the :ok return of record stop_op[key] and writes the frontier that return
+// expands (knossos's :configs for an invalid key whose stop_op is its fail
+// op) to out[key * max ...]; n_out[key] as DumpReq::n.
+// One key's search up to the :ok return of its record stop (DumpReq); the
+// count written, or -1.
+template <class Store>
+__device__ int dump_key(const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
+                        int64_t key, int64_t stop, const KParams &p, Store &st,
+                        lc_fx_config *out, int max, int lane) {
+  const int64_t beg = key_off[key], end = key_off[key + 1];
+  DumpReq dr{(int)stop, kNever, out, max, -1};
+  if (end > beg && end - beg <= 0x7FFFFFFF && stop >= 0 && stop < end - beg) {
+    const lc_op *kops = ops + (beg - key_off[0]);
+    const int64_t b0 = kops[0].call, r = kops[stop].ret;
+    if (r != kInf && r - b0 >= 0 && r - b0 < (int64_t)kNever) {  // (an :ok op's return)
+      dr.stop_ret = (uint32_t)(r - b0);
+      KeyOut o;
+      check_key<Store, true>(kops, (int)(end - beg), p, st, o, lane, &dr);
+    }
+  }
+  return dr.n;
+}
+
+// lc_check_frontiers: one wavefront per key runs the LDS tier's search up to
+// the :ok return of record stop_op[key] and writes the frontier that return
+// expands (knossos's :configs for an invalid key whose stop_op is its fail
+// op) to out[key * max ...]; n_out[key] as DumpReq::n.  A key whose search
+// outgrows the LDS regions (-1) is listed in retry (count *n_retry) for
+// frontier_dump_hbm_kernel.
+__global__ __launch_bounds__(kWave *kWavesPerWG) void frontier_dump_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
+    const int64_t *__restrict__ stop_op, const int64_t n_keys, const KParams p,
+    lc_fx_config *__restrict__ out, const int max, int32_t *__restrict__ n_out,
+    int32_t *__restrict__ retry, int32_t *__restrict__ n_retry) {
+  __shared__ Cfg lds[kWavesPerWG][3][kLdsCap];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t key = (int64_t)blockIdx.x * kWavesPerWG + wid;
+  if (key >= n_keys) return;
+  LdsStore st{&lds[wid][0][0]};
+  const int n = dump_key(ops, key_off, key, stop_op[key], p, st, out + key * max, max, lane);
+  if (lane == 0) {
+    n_out[key] = n;
+    if (n < 0) retry[atomicAdd(n_retry, 1)] = (int32_t)key;
   }
 }
 
@@ -2536,6 +2658,35 @@ __global__ __launch_bounds__(kWave) void hbm_tier_kernel(
   }
 }
 
+// The same over HBM tables (the one-wave HBM tier's store, workspace of
+// hbm_wave_bytes(cap) per wave), for the listed keys, claimed one at a time.
+__global__ __launch_bounds__(kWave) void frontier_dump_hbm_kernel(
+    const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off,
+    const int64_t *__restrict__ stop_op, const int32_t *__restrict__ keys, const int32_t n_list,
+    const KParams p, char *__restrict__ ws, const int64_t cap, lc_fx_config *__restrict__ out,
+    const int max, int32_t *__restrict__ n_out, int32_t *__restrict__ next) {
+  const int lane = threadIdx.x;
+  char *w = ws + (size_t)blockIdx.x * hbm_wave_bytes(cap);
+  HbmStore st;
+  st.base = reinterpret_cast<Cfg *>(w);
+  st.tabs = st.base + 3 * cap;
+  st.tags = reinterpret_cast<uint32_t *>(st.tabs + 4 * cap);
+  st.cap = (int)cap;
+  st.tmask = st.tmask_full = (uint32_t)(2 * cap - 1);
+  hbm_zero_tags(st.tags, cap);
+  st.epoch = 0;
+  for (;;) {
+    int li = 0;
+    if (lane == 0) li = atomicAdd(next, 1);
+    li = uni(li);
+    if (li >= n_list) break;
+    const int64_t key = keys[li];
+    st.hint = 0;
+    const int n = dump_key(ops, key_off, key, stop_op[key], p, st, out + key * max, max, lane);
+    if (lane == 0) n_out[key] = n;
+  }
+}
+
 // launch_status_settle (kernels.h): one workgroup.
 __global__ __launch_bounds__(256) void status_settle_kernel(KStatus *__restrict__ status,
                                                             int32_t *__restrict__ h_light) {
@@ -2721,15 +2872,78 @@ __global__ __launch_bounds__(256) void witness_init_kernel(
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_records; r += stride) {
     const lc_op o = ops[r];
+    // a version no state reaches (outside (V0, kFieldMax): decode saturates
+    // the ones beyond int32 to kFieldMax) pins nothing, whatever its width
+    // (lc_pack32 narrows such versions to kFieldMax)
     const bool pinned = (o.f == LC_F_WRITE || o.f == LC_F_CAS) && o.ret != kInf &&
-                        o.version > (int64_t)V0 && o.version - V0 - 1 < (int64_t)INT_MAX;
+                        o.version > (int64_t)V0 && o.version < kFieldMax;
     wit[r] = pinned ? (int32_t)(o.version - V0 - 1) : -1;
   }
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_keys; k += stride)
     kind[k] = fast_on ? LC_WITNESS_FULL : LC_WITNESS_NONE;
 }
 
+// 24-byte records (lc_op32, ABI 4) into the 48-byte form every tier reads,
+// with the key's base added back to call / ret, so the tiers see exactly the
+// records lc_check would have been given (include/lincheck.h).  One
+// workgroup per key (grid.x = keys, grid.y splits long keys); 8-byte loads
+// (three per record), 16-byte stores (three per record).  HBM-bound:
+// 24 B read + 48 B written per record.
+__global__ __launch_bounds__(256) void widen32_kernel(const int2 *__restrict__ in,
+                                                      const int64_t *__restrict__ key_off,
+                                                      const int64_t *__restrict__ key_base,
+                                                      longlong2 *__restrict__ out) {
+  const int64_t k = blockIdx.x;
+  const int64_t off0 = key_off[0];
+  const int64_t b = key_off[k] - off0, e = key_off[k + 1] - off0;
+  const int64_t base = key_base ? key_base[k] : 0;
+  const int64_t step = (int64_t)blockDim.x * gridDim.y;
+  for (int64_t r = b + (int64_t)blockIdx.y * blockDim.x + threadIdx.x; r < e; r += step) {
+    const int2 fv = in[3 * r], ev = in[3 * r + 1], cr = in[3 * r + 2];
+    const uint32_t call = (uint32_t)cr.x, ret = (uint32_t)cr.y;
+    out[3 * r] = make_longlong2((int64_t)fv.x, (int64_t)fv.y);
+    out[3 * r + 1] = make_longlong2((int64_t)ev.x, (int64_t)ev.y);
+    out[3 * r + 2] = make_longlong2(base + (int64_t)call,
+                                    ret == LC_INF32 ? kInf : base + (int64_t)ret);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_frontier_dump(const lc_op *d_ops, const int64_t *d_key_off, const int64_t *d_stop,
+                                int64_t n_keys, const KParams &p, lc_fx_config *d_out, int max,
+                                int32_t *d_n_out, int32_t *d_retry, int32_t *d_n_retry,
+                                hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  const int64_t wgs = (n_keys + kWavesPerWG - 1) / kWavesPerWG;
+  hipLaunchKernelGGL(frontier_dump_kernel, dim3((unsigned)wgs), dim3(kWave * kWavesPerWG), 0, stream,
+                     d_ops, d_key_off, d_stop, n_keys, p, d_out, max, d_n_out, d_retry, d_n_retry);
+  return hipGetLastError();
+}
+
+hipError_t launch_frontier_dump_hbm(const lc_op *d_ops, const int64_t *d_key_off,
+                                    const int64_t *d_stop, const int32_t *d_keys, int32_t n_list,
+                                    const KParams &p, void *d_ws, int n_waves, int64_t cap,
+                                    lc_fx_config *d_out, int max, int32_t *d_n_out, int32_t *d_next,
+                                    hipStream_t stream) {
+  if (n_list <= 0) return hipSuccess;
+  hipLaunchKernelGGL(frontier_dump_hbm_kernel, dim3((unsigned)n_waves), dim3(kWave), 0, stream, d_ops,
+                     d_key_off, d_stop, d_keys, n_list, p, static_cast<char *>(d_ws), cap, d_out, max,
+                     d_n_out, d_next);
+  return hipGetLastError();
+}
+
+hipError_t launch_widen32(const lc_op32 *d_in, const int64_t *d_key_off, const int64_t *d_key_base,
+                          int64_t n_keys, int64_t max_len, lc_op *d_out, hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  if (n_keys > INT32_MAX) return hipErrorInvalidValue;
+  // keys longer than 1,024 records get more workgroups (C4's 5,000-op key)
+  const unsigned gy = (unsigned)std::min<int64_t>(64, std::max<int64_t>(1, (max_len + 1023) / 1024));
+  hipLaunchKernelGGL(widen32_kernel, dim3((unsigned)n_keys, gy), dim3(256), 0, stream,
+                     reinterpret_cast<const int2 *>(d_in), d_key_off, d_key_base,
+                     reinterpret_cast<longlong2 *>(d_out));
+  return hipGetLastError();
+}
 
 hipError_t launch_status_settle(KStatus *d_status, int32_t *h_light, hipStream_t stream) {
   hipLaunchKernelGGL(status_settle_kernel, dim3(1), dim3(256), 0, stream, d_status, h_light);

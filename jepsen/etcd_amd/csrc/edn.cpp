@@ -668,6 +668,10 @@ struct lc_edn_history {
   int64_t n_events = 0;
   std::vector<lc_op> ops;
   std::vector<int64_t> key_off;
+  // lc_op32 records (ABI 4) and key bases, made on first request
+  std::vector<lc_op32> ops32;
+  std::vector<int64_t> key_base;
+  bool packed32 = false;
   std::vector<std::string> keys;                  // display text
   std::vector<std::vector<std::string>> values;   // per key: display text by id
   std::vector<std::pair<size_t, size_t>> inv, comp;  // per record: op spans (comp beg == end: none)
@@ -958,6 +962,23 @@ int64_t lc_edn_n_ops(const lc_edn_history *h) { return h ? (int64_t)h->ops.size(
 int64_t lc_edn_n_events(const lc_edn_history *h) { return h ? h->n_events : 0; }
 const lc_op *lc_edn_ops(const lc_edn_history *h) { return h ? h->ops.data() : nullptr; }
 const int64_t *lc_edn_key_off(const lc_edn_history *h) { return h ? h->key_off.data() : nullptr; }
+
+// The 24-byte form lc_check32 takes (include/lincheck.h, ABI 4), narrowed by
+// lc_pack32's rules once, on first request.
+static int pack32(lc_edn_history *h) {
+  if (h->packed32) return 0;
+  const int64_t nk = (int64_t)h->key_off.size() - 1;
+  h->ops32.resize(std::max<size_t>(1, h->ops.size()));
+  h->key_base.resize(std::max<int64_t>(1, nk));
+  if (int rc = lc_pack32(h->ops.data(), h->key_off.data(), nk, h->ops32.data(), h->key_base.data()))
+    return rc;
+  h->packed32 = true;
+  return 0;
+}
+const lc_op32 *lc_edn_ops32(lc_edn_history *h) { return h && !pack32(h) ? h->ops32.data() : nullptr; }
+const int64_t *lc_edn_key_base(lc_edn_history *h) {
+  return h && !pack32(h) ? h->key_base.data() : nullptr;
+}
 
 const char *lc_edn_key(const lc_edn_history *h, int64_t key) {
   if (!h || key < 0 || key >= (int64_t)h->keys.size()) return nullptr;

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "../../../include/lincheck.h"
+#include "../../../include/lincheck_fx.h"
 
 namespace lcdev {
 
@@ -118,6 +119,30 @@ hipError_t launch_witness_init(const lc_op *d_ops, const int64_t *d_key_off, int
                                int64_t n_records, const KParams &p, int fast_on,
                                int32_t *d_witness, int32_t *d_witness_kind, hipStream_t stream);
 
+// lc_op32 records (ABI 4) widened into lc_op records for the tiers, the key's
+// base (d_key_base[k], or 0 when null) added to call / ret; d_in and d_out
+// point at the record of index d_key_off[0] (d_in 8-byte aligned, d_out
+// 16-byte).  max_len: the longest key's records (sizes the grid).
+hipError_t launch_widen32(const lc_op32 *d_in, const int64_t *d_key_off, const int64_t *d_key_base,
+                          int64_t n_keys, int64_t max_len, lc_op *d_out, hipStream_t stream);
+
+// lc_check_frontiers (include/lincheck_fx.h): the LDS tier's search per key
+// up to the :ok return of record d_stop[k], its frontier written to
+// d_out[k * max ...] (n per key in d_n_out: >= 0 written, -1 not reached).
+// Keys whose search outgrows the LDS regions are listed in d_retry (count
+// *d_n_retry, zero at launch) for launch_frontier_dump_hbm: the same search
+// over HBM tables of `cap` configurations (hbm_tier_ws_bytes(n_waves, cap)
+// of workspace; keys claimed from *d_next, zero at launch).
+hipError_t launch_frontier_dump(const lc_op *d_ops, const int64_t *d_key_off, const int64_t *d_stop,
+                                int64_t n_keys, const KParams &p, ::lc_fx_config *d_out, int max,
+                                int32_t *d_n_out, int32_t *d_retry, int32_t *d_n_retry,
+                                hipStream_t stream);
+hipError_t launch_frontier_dump_hbm(const lc_op *d_ops, const int64_t *d_key_off,
+                                    const int64_t *d_stop, const int32_t *d_keys, int32_t n_list,
+                                    const KParams &p, void *d_ws, int n_waves, int64_t cap,
+                                    ::lc_fx_config *d_out, int max, int32_t *d_n_out, int32_t *d_next,
+                                    hipStream_t stream);
+
 // LDS tier (JIT search): one wavefront per key, for the keys in d_keys
 // (n_keys of them), or for keys 0..n_keys-1 when d_keys is null.  In every
 // tier key_off is indexed by local key id and d_ops points at the record of
@@ -229,6 +254,9 @@ hipError_t launch_gap_narrow(const lc_op *d_ops, const int64_t *d_key_off, int32
 // of its records' slots of d_cset; other keys LC_CERT_NONE.  Workspace:
 // cert_ws_bytes(n_records, n_keys).
 size_t cert_ws_bytes(int64_t n_records, int64_t n_keys);
+// Every key {LC_CERT_NONE, -1, -1, 0} (what launch_certificates writes for a
+// key that is not LC_INVALID), for calls in which no key can be invalid.
+hipError_t launch_cert_none(int32_t *d_cert, int64_t n_keys, hipStream_t stream);
 hipError_t launch_certificates(const lc_op *d_ops, const int64_t *d_key_off, int64_t n_keys,
                                int64_t n_records, const KParams &p, const lc_key_result *d_out,
                                int32_t *d_ws, int32_t *d_cert, int32_t *d_cset,

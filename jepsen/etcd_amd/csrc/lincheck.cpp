@@ -162,6 +162,22 @@ struct Dev {
   bool use_fused = false;  // the next call takes the fused version-order + crash-light pass
   hipEvent_t eh0 = nullptr, eh1 = nullptr;  // around lc_check's host-to-device copies
   lc_device_stats last{};                   // this device's share of the last lc_check
+  // lc_check's host-to-device pipeline: the copy stream, one event per chunk
+  // (its records landed), the 24-byte staging records of lc_check32 /
+  // lc_check_device32 and the keys' bases
+  // (two copy streams, chunks alternating: two DMA engines read host memory
+  // at once; measured 52-53 GB/s with one, 57 GB/s with two on one GPU)
+  hipStream_t cst = nullptr, cst2 = nullptr;
+  std::vector<hipEvent_t> cev;
+  void *d_ops32 = nullptr;
+  size_t ops32_cap = 0;
+  int64_t *d_base = nullptr;
+  size_t base_cap = 0;
+  // some key of the last run_device call may be LC_INVALID (a key was handed
+  // over past the version-order tier, which decides valid keys only): the
+  // certificate pass runs only then
+  bool maybe_invalid = true;
+  double t_start = 0, t_end = 0;            // lc_call_profile: this thread's span (ms since the call began)
 };
 
 }  // namespace
@@ -179,6 +195,7 @@ struct lc_ctx {
   // lc_host_register: caller buffers page-locked for this context's devices
   std::vector<std::pair<const char *, uint64_t>> pinned;
   std::mutex pin_mu;
+  lc_call_profile prof{};  // lc_last_call_profile
 };
 
 namespace {
@@ -246,6 +263,33 @@ bool is_pinned(lc_ctx *c, const void *p, size_t n) {
   return false;
 }
 
+// lc_check's host-to-device pipeline on one device: the device's key range
+// cut into chunks of about kChunkBytes of records.  run_device calls
+// issue(i), which enqueues chunk i's record copy on the copy stream and
+// records ready[i]; the compute stream waits for that event, widens 24-byte
+// records (lc_check32), and runs the version-order (or fused) pass over the
+// chunk's keys while the copy engine moves the next chunk.  (A pageable copy
+// may block the issuing thread until it has landed; issuing each chunk's
+// copy right before its kernels keeps the overlap either way.)
+struct Chunks {
+  int n = 0;
+  std::vector<int64_t> k;   // key boundaries, n + 1, local to the device's range
+  std::vector<int64_t> r;   // record offsets of those keys from the range's first record
+  std::function<int(int)> issue;
+  const hipEvent_t *ready = nullptr;
+  const lc_op32 *d_ops32 = nullptr;  // staging records to widen into d_ops (null: 48-byte copies)
+  const int64_t *d_base = nullptr;   // key bases for the widening (null: 0)
+  int64_t max_len = 0;               // longest key (records)
+};
+// Chunks of kChunkBytes, the last ones halving down to kChunkTail: the
+// compute stream's tail after the last copy is one small chunk's widening and
+// version-order pass.  (Measured on C2's 240 MB of 24-byte records: 10
+// chunks of 24 MB 4.66 ms per call, 0.12 ms of it after the last copy; 29
+// chunks of 8 MB 5.2 ms — each pageable copy has a fixed cost.)
+constexpr size_t kChunkBytes = size_t(24) << 20;
+constexpr size_t kChunkTail = size_t(2) << 20;
+constexpr int kMaxChunks = 48;
+
 // Device-side lc_aux outputs of one run_device call (null: not wanted).
 struct WitOut {
   int32_t *wit = nullptr;   // per record, indexed like d_ops
@@ -256,6 +300,8 @@ struct WitOut {
   // (not an output) the shard's key offsets in host memory when the caller
   // has them (lc_check_ex): the gap tier may then be launched early
   const int64_t *h_off = nullptr;
+  // (not an output) lc_check's chunked copies, or null: the records are in place
+  const Chunks *chunks = nullptr;
 };
 
 // A gap-tier full-decision launch: its sizes and job (run_device).
@@ -274,6 +320,12 @@ int run_certificates(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off
                      const lcdev::KParams &p, const lc_key_result *d_out, hipStream_t st,
                      const WitOut &wo) {
   if (!wo.cert || !wo.cset || n_keys <= 0) return 0;
+  if (!d.maybe_invalid) {
+    // every key was decided by the version-order tier, which decides valid
+    // keys only: no certificate to find, every key LC_CERT_NONE
+    HIP_TRY(c, lcdev::launch_cert_none(wo.cert, n_keys, st));
+    return 0;
+  }
   if (int rc = ensure(c, reinterpret_cast<char **>(&d.d_cws), &d.cws_cap,
                       lcdev::cert_ws_bytes(wo.n_records, n_keys)))
     return rc;
@@ -404,14 +456,9 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   int64_t n_jit = n_keys;
   const int32_t *jit_list = nullptr;
   const bool want_wit = wo.wit && wo.kind;
-  if (want_wit)  // the version order is the witness of every key the fast tier decides
-    HIP_TRY(c, lcdev::launch_witness_init(d_ops, d_off, n_keys, wo.n_records, p,
-                                          !(flags & LC_FLAG_NO_FAST_PATH), wo.wit, wo.kind, st));
-  HIP_TRY(c, hipEventRecord(d.e0, st));
-  if (!(flags & LC_FLAG_NO_FAST_PATH)) {
-    // tier 0: version-order decision for every key; the rest go to the JIT.
-    // Only when some workgroup raised h_handoff is the count copied back.
-    __atomic_store_n(d.h_handoff, 0, __ATOMIC_RELEASE);
+  const bool fast_on = !(flags & LC_FLAG_NO_FAST_PATH);
+  d.maybe_invalid = true;
+  if (fast_on) {
     // Crash-heavy batches (most keys carry crashed writes/CAS: every key goes
     // on to the crash-light decision) take the fused pass, which reads each
     // key's records once for both decisions; others the version-order tier,
@@ -419,14 +466,51 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     // the previous call on this device (LC_FUSED=0/1 forces it).
     const char *fenv = getenv("LC_FUSED");
     fused = gap_on && (fenv ? fenv[0] == '1' : d.use_fused);
+    // Only when some workgroup raised h_handoff is the count copied back.
+    __atomic_store_n(d.h_handoff, 0, __ATOMIC_RELEASE);
     d.flags_dirty = true;  // until the handoff (if any) is compacted
+  }
+  // keys [k0, k0 + nk), records from r0 (relative to d_ops): the witness
+  // initialisation (the version order is the witness of every key the fast
+  // tier decides) and tier 0, the version-order decision (or the fused
+  // pass); the keys it cannot decide are flagged for the later tiers
+  auto first_pass = [&](int64_t k0, int64_t nk, int64_t r0, int64_t nrec) -> int {
+    const lc_op *o = d_ops + r0;
+    const int64_t *off = d_off + k0;
+    int32_t *wit = want_wit ? wo.wit + r0 : nullptr;
+    int32_t *kind = want_wit ? wo.kind + k0 : nullptr;
+    if (want_wit)
+      HIP_TRY(c, lcdev::launch_witness_init(o, off, nk, nrec, p, fast_on, wit, kind, st));
+    if (!fast_on) return 0;
     if (fused)
-      HIP_TRY(c, lcdev::launch_fused_tier(d_ops, d_off, n_keys, p, d_out, d.d_flags, d.d_status,
-                                          d.h_handoff_dev, want_wit ? wo.wit : nullptr,
-                                          want_wit ? wo.kind : nullptr, st));
+      HIP_TRY(c, lcdev::launch_fused_tier(o, off, nk, p, d_out + k0, d.d_flags + k0, d.d_status,
+                                          d.h_handoff_dev, wit, kind, st));
     else
-      HIP_TRY(c, lcdev::launch_fast_tier(d_ops, d_off, n_keys, p, d_out, d.d_flags,
-                                         d.d_status, d.h_handoff_dev, st));
+      HIP_TRY(c, lcdev::launch_fast_tier(o, off, nk, p, d_out + k0, d.d_flags + k0, d.d_status,
+                                         d.h_handoff_dev, st));
+    return 0;
+  };
+  HIP_TRY(c, hipEventRecord(d.e0, st));
+  if (const Chunks *ch = wo.chunks) {
+    // lc_check's pipeline: chunk i's copy is issued, the compute stream
+    // waits for it, widens it (24-byte records) and decides its keys while
+    // the copy engine moves chunk i + 1
+    for (int i = 0; i < ch->n; i++) {
+      if (int e = ch->issue(i)) return e;
+      HIP_TRY(c, hipStreamWaitEvent(st, ch->ready[i], 0));
+      const int64_t k0 = ch->k[i], nk = ch->k[i + 1] - k0;
+      const int64_t r0 = ch->r[i], nrec = ch->r[i + 1] - r0;
+      if (nk <= 0) continue;
+      if (ch->d_ops32)
+        HIP_TRY(c, lcdev::launch_widen32(ch->d_ops32 + r0, d_off + k0,
+                                         ch->d_base ? ch->d_base + k0 : nullptr, nk, ch->max_len,
+                                         const_cast<lc_op *>(d_ops) + r0, st));
+      if (int e = first_pass(k0, nk, r0, nrec)) return e;
+    }
+  } else if (int e = first_pass(0, n_keys, 0, wo.n_records)) {
+    return e;
+  }
+  if (fast_on) {
     HIP_TRY(c, hipEventRecord(d.ef, st));
     HIP_TRY(c, hipEventSynchronize(d.ef));
     HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.ef));
@@ -434,7 +518,12 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     n_jit = 0;
     jit_list = d.d_jit;
     const bool handed = __atomic_load_n(d.h_handoff, __ATOMIC_ACQUIRE) != 0;
-    if (!handed) d.flags_dirty = false;  // no key raised its flag
+    if (!handed) {
+      d.flags_dirty = false;  // no key raised its flag
+      // the version-order tier and the fused pass decide valid keys only
+      // (they hand invalid ones on for their counterexamples)
+      d.maybe_invalid = false;
+    }
     if (fused && !handed) {
       // every key decided in the one pass: were most of them crash-light?
       // (the answer picks the next call's pass; copied now, read later)
@@ -834,6 +923,452 @@ int whole_gpu(lc_ctx *c, const std::vector<int64_t> &todo, const lc_opts *opts,
   return 0;
 }
 
+// Per-key device cost in record-scan units (DESIGN.md §7).  The tier a key
+// lands in follows from its records alone (check_kernel.hip, fast_key):
+//   * version-order tier (every :ok mutation versioned, nothing crashed):
+//     one pass over the records, cost n;
+//   * gap tier (crashed writes/CAS, versions pinned): two skeleton passes,
+//     the matching and, for an invalid key, the bisection; measured ~6x the
+//     fast tier per record on C2 with 5 % crashed ops (crash_leg), plus the
+//     matching's share, which grows with the crashed ops;
+//   * frontier search (an :ok mutation or a read [nil x] without a version):
+//     the frontier grows with the open window w; measured (model_leg,
+//     tools/frontier_dist.py) ~1,600x the fast tier per record at
+//     concurrency 10 and ~4,700x at 20, i.e. ~12 w^2, and crashed ops
+//     multiply the configurations (capped: the search's budget bounds it).
+// Plus a fixed 64 per key (launch share, result write).
+// (Records of either width: lc_op, or lc_op32 with LC_INF32 for LC_INF.)
+inline bool rec_crashed(const lc_op32 &o) { return o.ret == LC_INF32; }
+inline int64_t rec_call(const lc_op &o) { return o.call; }
+inline int64_t rec_call(const lc_op32 &o) { return (int64_t)o.call; }
+inline int64_t rec_ret(const lc_op &o) { return o.ret; }
+inline int64_t rec_ret(const lc_op32 &o) { return o.ret == LC_INF32 ? LC_INF : (int64_t)o.ret; }
+// a crashed write/CAS, or an :ok op without a version that the version order
+// cannot pin (a mutation, or a read of a value)
+template <class Op>
+inline void rec_kind(const Op &o, bool *crashed_mut, bool *unpinned) {
+  const bool mut = o.f == LC_F_WRITE || o.f == LC_F_CAS;
+  *crashed_mut = mut && rec_crashed(o);
+  *unpinned = !rec_crashed(o) && o.version == (int32_t)LC_NIL &&
+              (mut || (o.f == LC_F_READ && o.value != (int32_t)LC_NIL));
+}
+inline void rec_kind(const lc_op &o, bool *crashed_mut, bool *unpinned) {
+  const bool mut = o.f == LC_F_WRITE || o.f == LC_F_CAS;
+  *crashed_mut = mut && o.ret == LC_INF;
+  *unpinned = o.ret != LC_INF && o.version == LC_NIL &&
+              (mut || (o.f == LC_F_READ && o.value != LC_NIL));
+}
+
+template <class Op>
+double key_cost(const Op *o, int64_t n) {
+  int64_t crashed = 0, unpinned = 0;
+  for (int64_t i = 0; i < n; i++) {
+    bool cm, un;
+    rec_kind(o[i], &cm, &un);
+    crashed += cm;
+    unpinned += un;
+  }
+  const double kOverhead = 64;
+  if (!unpinned && !crashed) return (double)n + kOverhead;
+  if (!unpinned) return (6.0 + 0.01 * (double)crashed) * (double)n + kOverhead;
+  // open window: the most ops called and not yet returned at once
+  std::vector<int64_t> rets;
+  rets.reserve((size_t)n);
+  for (int64_t i = 0; i < n; i++) rets.push_back(rec_ret(o[i]));
+  std::sort(rets.begin(), rets.end());
+  int64_t w = 0;
+  size_t j = 0;
+  for (int64_t i = 0; i < n; i++) {  // records are sorted by call
+    while (j < rets.size() && rets[j] < rec_call(o[i])) j++;
+    w = std::max<int64_t>(w, i + 1 - (int64_t)j);
+  }
+  const double blow = std::pow(2.0, (double)std::min<int64_t>(crashed, 12));
+  return (double)n * (1.0 + 12.0 * (double)w * (double)w) * blow + kOverhead;
+}
+
+
+// lc_check's own split over its devices: the same contiguous equal-cost cut
+// as lc_plan_partition, but a key is priced by all its records only when a
+// sample of them (every kSampleStride-th) shows it is not a clean
+// version-pinned key (a crashed write/CAS, an :ok op without a version);
+// otherwise it costs its record count, which is what lc_key_cost gives a
+// clean key.  And the sample itself is taken only when a first probe — the
+// same sample of every kKeyStride-th key — finds an irregular key: a batch
+// whose probe is clean is split by record count.  Pricing every record read
+// the whole batch on the host (480 MB for C2: several ms even on 16 threads)
+// before any copy could start; sampling every key still touched every page
+// (0.6-0.9 ms of a 5-ms call on the GPU box, tools/plan_probe.cpp); the
+// probe reads ~1/16 of them.  Only the split's balance, never a verdict,
+// depends on these estimates.
+constexpr int64_t kSampleStride = 64;
+constexpr int64_t kKeyStride = 16;
+template <class Op>
+bool irregular_sample(const Op *o, int64_t n) {
+  for (int64_t i = 0; i < n; i += kSampleStride) {
+    bool cm, un;
+    rec_kind(o[i], &cm, &un);
+    if (cm || un) return true;
+  }
+  return false;
+}
+
+template <class Op>
+void plan_devices(const Op *ops, const int64_t *key_off, int64_t n_keys, int nd,
+                  int64_t *bounds) {
+  std::vector<double> pre((size_t)n_keys + 1, 0.0);
+  bool any = false;
+  for (int64_t k = 0; k < n_keys && !any; k += kKeyStride)
+    any = irregular_sample(ops + key_off[k], key_off[k + 1] - key_off[k]);
+  auto price = [&](int64_t k0, int64_t k1) {
+    for (int64_t k = k0; k < k1; k++) {
+      const Op *o = ops + key_off[k];
+      const int64_t n = key_off[k + 1] - key_off[k];
+      pre[(size_t)k + 1] = any && irregular_sample(o, n) ? key_cost(o, n) : (double)n + 64.0;
+    }
+  };
+  const int nth = any ? (int)std::min<int64_t>(16, std::max<int64_t>(1, n_keys >> 10)) : 1;
+  if (nth <= 1) {
+    price(0, n_keys);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nth; t++) th.emplace_back(price, n_keys * t / nth, n_keys * (t + 1) / nth);
+    for (auto &x : th) x.join();
+  }
+  for (int64_t k = 0; k < n_keys; k++) pre[(size_t)k + 1] += pre[(size_t)k];
+  const double total = pre[(size_t)n_keys];
+  bounds[0] = 0;
+  int64_t k = 0;
+  for (int p = 1; p < nd; p++) {
+    const double goal = total * p / nd;
+    while (k < n_keys && pre[(size_t)k] < goal) k++;
+    bounds[p] = k;
+  }
+  bounds[nd] = n_keys;
+}
+
+// An lc_op32 record as the lc_op it stands for (include/lincheck.h, ABI 4).
+inline lc_op widen_op(const lc_op &o, int64_t) { return o; }
+inline lc_op widen_op(const lc_op32 &o, int64_t base) {
+  return lc_op{o.f, o.value, o.expected, o.version, base + (int64_t)o.call,
+               o.ret == LC_INF32 ? LC_INF : base + (int64_t)o.ret};
+}
+
+// lc_check_ex (48-byte lc_op) and lc_check32 (24-byte lc_op32, ABI 4) from
+// host memory: the keys split over the context's devices (plan_devices), one
+// host thread per device.  Per device, the key offsets (and lc_check32's key
+// bases) are copied first, then the records in chunks of about kChunkBytes
+// on the device's copy stream; the compute stream decides each chunk's keys
+// with the version-order (or fused) pass as soon as the chunk has landed
+// (run_device, Chunks), widening 24-byte records on the way, so the PCIe
+// copy of chunk i + 1 overlaps the kernels of chunk i.  The later tiers run
+// over the whole range once every chunk is in.  Results and lc_aux outputs
+// are copied back into the caller's arrays.  Per call, lc_call_profile keeps
+// where the host wall time went.
+template <class Op>
+int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *key_base,
+               int64_t n_keys, const lc_opts *opts, lc_key_result *out, const lc_aux *aux) {
+  constexpr bool k32 = sizeof(Op) == sizeof(lc_op32);
+  const auto t0 = std::chrono::steady_clock::now();
+  auto since = [&t0]() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  };
+  c->stats = lc_stats{};
+  c->prof = lc_call_profile{};
+  if (n_keys < 0 || (n_keys > 0 && (!ops || !key_off || !out))) {
+    set_err(c, "lc_check: null buffer or negative n_keys");
+    return -EINVAL;
+  }
+  if (n_keys == 0) return 0;
+  if (key_off[0] < 0) {
+    set_err(c, "lc_check: key_off[0] < 0");
+    return -EINVAL;
+  }
+  for (int64_t k = 0; k < n_keys; k++)
+    if (key_off[k + 1] < key_off[k]) {
+      set_err(c, "lc_check: key_off not monotone at key " + std::to_string(k));
+      return -EINVAL;
+    }
+  lcdev::KParams p;
+  int rc = opts_to_params(c, opts, &p);
+  if (rc) return rc;
+  const int64_t flags = opts ? opts->flags : 0;
+  const bool want_wit = aux && aux->witness && aux->witness_kind;
+  const bool want_cert = aux && aux->certificate;
+  const int nd = (int)c->devs.size();
+  c->prof.checked_ms = since();
+  std::vector<int64_t> bounds(nd + 1);
+  if (nd > 1) plan_devices(ops, key_off, n_keys, nd, bounds.data());
+  else bounds[0] = 0, bounds[1] = n_keys;
+  c->prof.planned_ms = since();
+  // the longest key (the widening's grid); C4's 5,000-op key takes more
+  // workgroups than a C2 key
+  int64_t max_len = 0;
+  if (k32)
+    for (int64_t k = 0; k < n_keys; k++) max_len = std::max(max_len, key_off[k + 1] - key_off[k]);
+
+  std::vector<int> rcs(nd, 0);
+  std::vector<int> nchunks(nd, 0);
+  auto work = [&](int di) {
+    Dev &d = c->devs[di];
+    d.t_start = since();
+    d.t_end = d.t_start;
+    const int64_t a = bounds[di], b = bounds[di + 1];
+    const int64_t nk = b - a;
+    const auto tw = std::chrono::steady_clock::now();
+    d.last = lc_device_stats{};
+    d.last.device = d.id;
+    d.last.key_begin = a;
+    d.last.key_end = b;
+    d.kernel_ms = 0;
+    if (nk <= 0) return;
+    if (hipSetDevice(d.id) != hipSuccess) {
+      rcs[di] = -EIO;
+      return;
+    }
+    const int64_t r0 = key_off[a], r1 = key_off[b];
+    const int64_t nrec = r1 - r0;
+    const size_t ops_bytes = sizeof(lc_op) * (size_t)nrec;  // on the device: 48-byte records
+    const size_t in_bytes = sizeof(Op) * (size_t)nrec;      // what crosses PCIe
+    int r = ensure(c, reinterpret_cast<char **>(&d.d_ops), &d.ops_cap, ops_bytes);
+    if (!r && k32) r = ensure(c, reinterpret_cast<char **>(&d.d_ops32), &d.ops32_cap, in_bytes);
+    if (!r && k32 && key_base) r = ensure(c, &d.d_base, &d.base_cap, sizeof(int64_t) * (size_t)nk);
+    if (!r) r = ensure(c, &d.d_off, &d.off_cap, sizeof(int64_t) * (size_t)(nk + 1));
+    if (!r) r = ensure(c, &d.d_out, &d.out_cap, sizeof(lc_key_result) * (size_t)nk);
+    if (!r && want_wit) r = ensure(c, &d.d_wit, &d.wit_cap, sizeof(int32_t) * (size_t)nrec);
+    if (!r && want_wit) r = ensure(c, &d.d_kind, &d.kind_cap, sizeof(int32_t) * (size_t)nk);
+    if (!r && want_cert) r = ensure(c, &d.d_cert, &d.cert_cap, 4 * sizeof(int32_t) * (size_t)nk);
+    if (!r && want_cert) r = ensure(c, &d.d_cset, &d.cset_cap, sizeof(int32_t) * (size_t)nrec);
+    if (r) {
+      rcs[di] = r;
+      return;
+    }
+    // chunks: contiguous key ranges of about kChunkBytes of input records,
+    // the last ones halving down to kChunkTail (cut at key boundaries)
+    Chunks ch;
+    std::vector<size_t> sizes;  // from the end of the range
+    for (size_t left = in_bytes, want = kChunkTail; left > 0 && (int)sizes.size() < kMaxChunks - 1;) {
+      const size_t take = std::min(left, want);
+      sizes.push_back(take);
+      left -= take;
+      want = std::min(kChunkBytes, 2 * want);
+    }
+    ch.k.push_back(0);
+    {
+      size_t sum = 0;
+      for (size_t z : sizes) sum += z;
+      int64_t rec_goal = (int64_t)((in_bytes - sum) / sizeof(Op));  // records before the next cut
+      for (size_t i = sizes.size(); i-- > 1;) {
+        rec_goal += (int64_t)(sizes[i] / sizeof(Op));
+        int64_t k = std::lower_bound(key_off + a, key_off + b, r0 + rec_goal) - (key_off + a);
+        if (k > ch.k.back() && k < nk) ch.k.push_back(k);
+      }
+    }
+    ch.k.push_back(nk);
+    ch.n = (int)ch.k.size() - 1;
+    for (int64_t k : ch.k) ch.r.push_back(key_off[a + k] - r0);
+    while ((int)d.cev.size() < ch.n) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        set_err(c, "hipEventCreateWithFlags failed");
+        rcs[di] = -EIO;
+        return;
+      }
+      d.cev.push_back(e);
+    }
+    ch.ready = d.cev.data();
+    ch.max_len = max_len;
+    if (k32) {
+      ch.d_ops32 = static_cast<const lc_op32 *>(d.d_ops32);
+      ch.d_base = key_base ? d.d_base : nullptr;
+    }
+    nchunks[di] = ch.n;
+    char *dst = static_cast<char *>(k32 ? d.d_ops32 : d.d_ops);
+    const char *src = reinterpret_cast<const char *>(ops + r0);
+    // the key offsets (and bases) lead; the compute stream waits for the
+    // first chunk's event, which follows them on the copy stream
+    hipError_t e = hipEventRecord(d.eh0, d.cst);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d.d_off, key_off + a, sizeof(int64_t) * (size_t)(nk + 1),
+                         hipMemcpyHostToDevice, d.cst);
+    if (e == hipSuccess && k32 && key_base)
+      e = hipMemcpyAsync(d.d_base, key_base + a, sizeof(int64_t) * (size_t)nk,
+                         hipMemcpyHostToDevice, d.cst);
+    if (e != hipSuccess) {
+      set_err(c, std::string("hipMemcpyAsync H2D: ") + hipGetErrorString(e));
+      rcs[di] = -EIO;
+      return;
+    }
+    // the second copy stream starts behind the offsets too
+    if (e == hipSuccess) e = hipEventRecord(d.cev[0], d.cst);
+    if (e == hipSuccess) e = hipStreamWaitEvent(d.cst2, d.cev[0], 0);
+    if (e != hipSuccess) {
+      set_err(c, std::string("hipStreamWaitEvent: ") + hipGetErrorString(e));
+      rcs[di] = -EIO;
+      return;
+    }
+    // Two copy streams, chunks alternating, the odd ones issued by a helper
+    // thread: a copy call returns only once the runtime has staged (pageable)
+    // or queued it, so one issuing thread left the link idle between copies —
+    // two device contexts copying at once moved 57 GB/s against 52-53 for one
+    // thread (tools/host32_probe.py)
+    auto copy = [&](int i) -> hipError_t {
+      const size_t o = sizeof(Op) * (size_t)ch.r[i];
+      const size_t bytes = sizeof(Op) * (size_t)(ch.r[i + 1] - ch.r[i]);
+      hipStream_t cs = i % 2 ? d.cst2 : d.cst;
+      hipError_t x = bytes ? hipMemcpyAsync(dst + o, src + o, bytes, hipMemcpyHostToDevice, cs)
+                           : hipSuccess;
+      if (x == hipSuccess) x = hipEventRecord(d.cev[(size_t)i], cs);
+      return x;
+    };
+    std::vector<std::atomic<int>> issued((size_t)ch.n);  // odd chunks: 1 issued, -1 failed
+    for (auto &f : issued) f.store(0);
+    std::atomic<bool> stop{false};
+    std::thread helper;
+    if (ch.n >= 4)
+      helper = std::thread([&] {
+        (void)hipSetDevice(d.id);
+        for (int i = 1; i < ch.n && !stop.load(std::memory_order_relaxed); i += 2)
+          issued[(size_t)i].store(copy(i) == hipSuccess ? 1 : -1, std::memory_order_release);
+      });
+    ch.issue = [&](int i) -> int {
+      hipError_t x = hipSuccess;
+      if (i % 2 == 0 || !helper.joinable()) {
+        x = copy(i);
+      } else {
+        int f;
+        while ((f = issued[(size_t)i].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+        if (f < 0) x = hipErrorUnknown;
+      }
+      if (x == hipSuccess && i == ch.n - 1) {
+        // both copy streams done
+        if (ch.n > 1) x = hipStreamWaitEvent(d.cst, d.cev[(size_t)i - 1], 0);
+        if (x == hipSuccess) x = hipStreamWaitEvent(d.cst, d.cev[(size_t)i], 0);
+        if (x == hipSuccess) x = hipEventRecord(d.eh1, d.cst);
+      }
+      if (x != hipSuccess) {
+        set_err(c, std::string("hipMemcpyAsync H2D: ") + hipGetErrorString(x));
+        return -EIO;
+      }
+      return 0;
+    };
+    auto join_helper = [&] {
+      stop.store(true);
+      if (helper.joinable()) helper.join();
+    };
+    d.last.h2d_bytes = (int64_t)(in_bytes + sizeof(int64_t) * (size_t)(nk + 1) +
+                                 (k32 && key_base ? sizeof(int64_t) * (size_t)nk : 0));
+    d.last.pinned = is_pinned(c, ops + r0, in_bytes);
+    WitOut wo;
+    wo.n_records = nrec;
+    if (want_wit) {
+      wo.wit = d.d_wit;
+      wo.kind = d.d_kind;
+    }
+    if (want_cert) {
+      wo.cert = d.d_cert;
+      wo.cset = d.d_cset;
+    }
+    wo.h_off = key_off + a;
+    wo.chunks = &ch;
+    r = run_device(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, nk, p, d.d_out, d.stream,
+                   flags, wo);
+    join_helper();
+    if (!r) r = run_certificates(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, nk, p,
+                                 d.d_out, d.stream, wo);
+    if (r) {
+      // the copy stream may still read the caller's buffer
+      (void)hipStreamSynchronize(d.cst);
+      (void)hipStreamSynchronize(d.cst2);
+      rcs[di] = r;
+      return;
+    }
+    e = hipMemcpyAsync(out + a, d.d_out, sizeof(lc_key_result) * (size_t)nk,
+                       hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess && want_wit && nrec)
+      e = hipMemcpyAsync(aux->witness + r0, d.d_wit, sizeof(int32_t) * (size_t)nrec,
+                         hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess && want_wit)
+      e = hipMemcpyAsync(aux->witness_kind + a, d.d_kind, sizeof(int32_t) * (size_t)nk,
+                         hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess && want_cert)
+      e = hipMemcpyAsync(aux->certificate + 4 * a, d.d_cert, 4 * sizeof(int32_t) * (size_t)nk,
+                         hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess && want_cert && aux->certificate_set && nrec)
+      e = hipMemcpyAsync(aux->certificate_set + r0, d.d_cset, sizeof(int32_t) * (size_t)nrec,
+                         hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
+    if (e != hipSuccess) {
+      set_err(c, std::string("hipMemcpyAsync D2H: ") + hipGetErrorString(e));
+      rcs[di] = -EIO;
+      return;
+    }
+    float hms = 0;
+    if (hipEventElapsedTime(&hms, d.eh0, d.eh1) == hipSuccess) d.last.h2d_ms = hms;
+    d.last.kernel_ms = d.kernel_ms;
+    d.last.total_ms = std::chrono::duration<double, std::milli>(
+                          std::chrono::steady_clock::now() - tw).count();
+    d.t_end = since();
+  };
+  if (nd == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int di = 0; di < nd; di++) th.emplace_back(work, di);
+    for (auto &t : th) t.join();
+  }
+  c->prof.first_start_ms = c->prof.first_end_ms = 1e300;
+  for (int di = 0; di < nd; di++) {
+    const Dev &d = c->devs[di];
+    if (rcs[di] && !rc) rc = rcs[di];
+    c->stats.kernel_ms += d.kernel_ms;
+    c->stats.fast_kernel_ms += d.fast_ms;
+    c->stats.jit_kernel_ms += d.jit_ms;
+    c->stats.n_jit_keys += d.n_jit;
+    c->stats.gap_kernel_ms += d.gap_ms;
+    c->stats.n_gap_keys += d.n_gap;
+    c->stats.hbm_kernel_ms += d.hbm_ms;
+    c->stats.n_hbm_keys += d.n_hbm;
+    c->stats.n_malformed += d.malformed;
+    c->prof.first_start_ms = std::min(c->prof.first_start_ms, d.t_start);
+    c->prof.last_start_ms = std::max(c->prof.last_start_ms, d.t_start);
+    c->prof.first_end_ms = std::min(c->prof.first_end_ms, d.t_end);
+    c->prof.last_end_ms = std::max(c->prof.last_end_ms, d.t_end);
+    c->prof.n_chunks += nchunks[di];
+  }
+  c->prof.joined_ms = since();
+  if (!rc && (flags & LC_FLAG_WHOLE_GPU)) {
+    std::vector<int64_t> todo, todo_w;
+    for (int64_t k = 0; k < n_keys; k++)
+      if (out[k].verdict == LC_UNKNOWN && out[k].reason == LC_REASON_CONFIG_BUDGET) todo.push_back(k);
+      else if (out[k].verdict == LC_UNKNOWN && out[k].reason == LC_REASON_WINDOW_OVERFLOW)
+        todo_w.push_back(k);
+    auto fetch = [&](int64_t k, std::vector<lc_op> &v) {
+      v.resize((size_t)(key_off[k + 1] - key_off[k]));
+      const int64_t base = key_base ? key_base[k] : 0;
+      for (size_t i = 0; i < v.size(); i++) v[i] = widen_op(ops[key_off[k] + (int64_t)i], base);
+      return 0;
+    };
+    auto store = [&](int64_t k, const lc_key_result &r) {
+      out[k] = r;
+      // re-decided by the frontier exchange: no certificate (cert.hip covers
+      // the tiers' decisions)
+      if (want_cert)
+        for (int j = 0; j < 4; j++) aux->certificate[4 * k + j] = j == 0 ? LC_CERT_NONE : j < 3 ? -1 : 0;
+      return 0;
+    };
+    rc = whole_gpu(c, todo, opts, fetch, store);
+    if (!rc) rc = whole_gpu(c, todo_w, opts, fetch, store);
+  }
+  c->prof.whole_gpu_ms = since();
+  c->stats.n_keys = n_keys;
+  c->stats.n_ops = key_off[n_keys] - key_off[0];
+  c->stats.n_devices = nd;
+  c->stats.total_ms = since();
+  c->prof.total_ms = c->stats.total_ms;
+  c->prof.n_devices = nd;
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -871,6 +1406,8 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
       d.id = i;
       if (hipSetDevice(i) != hipSuccess ||
           hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
+          hipStreamCreateWithFlags(&d.cst, hipStreamNonBlocking) != hipSuccess ||
+          hipStreamCreateWithFlags(&d.cst2, hipStreamNonBlocking) != hipSuccess ||
           hipEventCreateWithFlags(&d.e0, kEventFlags) != hipSuccess ||
           hipEventCreateWithFlags(&d.e1, kEventFlags) != hipSuccess ||
           hipEventCreateWithFlags(&d.e2, kEventFlags) != hipSuccess ||
@@ -934,11 +1471,15 @@ void lc_close(lc_ctx *c) {
     if (d.d_cert) (void)hipFree(d.d_cert);
     if (d.d_cset) (void)hipFree(d.d_cset);
     if (d.d_cws) (void)hipFree(d.d_cws);
-    if (d.eg) (void)hipEventDestroy(d.eg);
-    if (d.eh0) (void)hipEventDestroy(d.eh0);
-    if (d.eh1) (void)hipEventDestroy(d.eh1);
-    if (d.el) (void)hipEventDestroy(d.el);
     if (d.d_gap2) (void)hipFree(d.d_gap2);
+    if (d.d_ops32) (void)hipFree(d.d_ops32);
+    if (d.d_base) (void)hipFree(d.d_base);
+    for (hipEvent_t e : d.cev) (void)hipEventDestroy(e);
+    for (hipStream_t cs : {d.cst, d.cst2})
+      if (cs) {
+        (void)hipStreamSynchronize(cs);
+        (void)hipStreamDestroy(cs);
+      }
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
   delete c;
@@ -995,47 +1536,6 @@ int lc_host_unregister(lc_ctx *c, const void *ptr) {
   return -EINVAL;
 }
 
-// Per-key device cost in record-scan units (DESIGN.md §7).  The tier a key
-// lands in follows from its records alone (check_kernel.hip, fast_key):
-//   * version-order tier (every :ok mutation versioned, nothing crashed):
-//     one pass over the records, cost n;
-//   * gap tier (crashed writes/CAS, versions pinned): two skeleton passes,
-//     the matching and, for an invalid key, the bisection; measured ~6x the
-//     fast tier per record on C2 with 5 % crashed ops (crash_leg), plus the
-//     matching's share, which grows with the crashed ops;
-//   * frontier search (an :ok mutation or a read [nil x] without a version):
-//     the frontier grows with the open window w; measured (model_leg,
-//     tools/frontier_dist.py) ~1,600x the fast tier per record at
-//     concurrency 10 and ~4,700x at 20, i.e. ~12 w^2, and crashed ops
-//     multiply the configurations (capped: the search's budget bounds it).
-// Plus a fixed 64 per key (launch share, result write).
-static double key_cost(const lc_op *o, int64_t n) {
-  int64_t crashed = 0, unpinned = 0;
-  for (int64_t i = 0; i < n; i++) {
-    const bool mut = o[i].f == LC_F_WRITE || o[i].f == LC_F_CAS;
-    if (mut && o[i].ret == LC_INF) crashed++;
-    else if (o[i].ret != LC_INF && o[i].version == LC_NIL &&
-             (mut || (o[i].f == LC_F_READ && o[i].value != LC_NIL)))
-      unpinned++;
-  }
-  const double kOverhead = 64;
-  if (!unpinned && !crashed) return (double)n + kOverhead;
-  if (!unpinned) return (6.0 + 0.01 * (double)crashed) * (double)n + kOverhead;
-  // open window: the most ops called and not yet returned at once
-  std::vector<int64_t> rets;
-  rets.reserve((size_t)n);
-  for (int64_t i = 0; i < n; i++) rets.push_back(o[i].ret);
-  std::sort(rets.begin(), rets.end());
-  int64_t w = 0;
-  size_t j = 0;
-  for (int64_t i = 0; i < n; i++) {  // records are sorted by call
-    while (j < rets.size() && rets[j] < o[i].call) j++;
-    w = std::max<int64_t>(w, i + 1 - (int64_t)j);
-  }
-  const double blow = std::pow(2.0, (double)std::min<int64_t>(crashed, 12));
-  return (double)n * (1.0 + 12.0 * (double)w * (double)w) * blow + kOverhead;
-}
-
 int lc_key_cost(const lc_op *ops, const int64_t *key_off, int64_t n_keys, double *costs) {
   if (!ops || !key_off || !costs || n_keys < 0) return -EINVAL;
   for (int64_t k = 0; k < n_keys; k++) {
@@ -1088,225 +1588,31 @@ int lc_plan_partition(const lc_op *ops, const int64_t *key_off, int64_t n_keys,
   return 0;
 }
 
-// lc_check's own split over its devices: the same contiguous equal-cost cut
-// as lc_plan_partition, but a key is priced by all its records only when a
-// sample of them (every kSampleStride-th) shows it is not a clean
-// version-pinned key (a crashed write/CAS, an :ok op without a version);
-// otherwise it costs its record count, which is what lc_key_cost gives a
-// clean key.  Pricing every record reads the whole batch on the host (480 MB
-// for C2: several ms even on 16 threads) before any copy can start; the
-// sample reads one record in kSampleStride.  A key whose few irregular
-// records the sample misses is under-priced by at most its 6x gap-tier
-// factor: the split's balance, never a verdict, depends on it.
-constexpr int64_t kSampleStride = 32;
-static void plan_devices(const lc_op *ops, const int64_t *key_off, int64_t n_keys, int nd,
-                  int64_t *bounds) {
-  std::vector<double> pre((size_t)n_keys + 1, 0.0);
-  auto price = [&](int64_t k0, int64_t k1) {
-    for (int64_t k = k0; k < k1; k++) {
-      const lc_op *o = ops + key_off[k];
-      const int64_t n = key_off[k + 1] - key_off[k];
-      bool irregular = false;
-      for (int64_t i = 0; i < n && !irregular; i += kSampleStride) {
-        const bool mut = o[i].f == LC_F_WRITE || o[i].f == LC_F_CAS;
-        irregular = (mut && o[i].ret == LC_INF) ||
-                    (o[i].ret != LC_INF && o[i].version == LC_NIL &&
-                     (mut || (o[i].f == LC_F_READ && o[i].value != LC_NIL)));
-      }
-      pre[(size_t)k + 1] = irregular ? key_cost(o, n) : (double)n + 64.0;
-    }
-  };
-  const int nth = (int)std::min<int64_t>(16, std::max<int64_t>(1, n_keys >> 10));
-  if (nth <= 1) {
-    price(0, n_keys);
-  } else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < nth; t++) th.emplace_back(price, n_keys * t / nth, n_keys * (t + 1) / nth);
-    for (auto &x : th) x.join();
-  }
-  for (int64_t k = 0; k < n_keys; k++) pre[(size_t)k + 1] += pre[(size_t)k];
-  const double total = pre[(size_t)n_keys];
-  bounds[0] = 0;
-  int64_t k = 0;
-  for (int p = 1; p < nd; p++) {
-    const double goal = total * p / nd;
-    while (k < n_keys && pre[(size_t)k] < goal) k++;
-    bounds[p] = k;
-  }
-  bounds[nd] = n_keys;
-}
-
 int lc_check_ex(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
                 int64_t n_keys, const lc_opts *opts, lc_key_result *out, const lc_aux *aux) {
   if (!c) return -EINVAL;
-  const auto t0 = std::chrono::steady_clock::now();
-  c->stats = lc_stats{};
-  if (n_keys < 0 || (n_keys > 0 && (!ops || !key_off || !out))) {
-    set_err(c, "lc_check: null buffer or negative n_keys");
-    return -EINVAL;
-  }
-  if (n_keys == 0) return 0;
-  if (key_off[0] < 0) {
-    set_err(c, "lc_check: key_off[0] < 0");
-    return -EINVAL;
-  }
-  for (int64_t k = 0; k < n_keys; k++)
-    if (key_off[k + 1] < key_off[k]) {
-      set_err(c, "lc_check: key_off not monotone at key " + std::to_string(k));
-      return -EINVAL;
-    }
-  lcdev::KParams p;
-  int rc = opts_to_params(c, opts, &p);
-  if (rc) return rc;
-  const int64_t flags = opts ? opts->flags : 0;
-  const bool want_wit = aux && aux->witness && aux->witness_kind;
-  const bool want_cert = aux && aux->certificate;
-  const int nd = (int)c->devs.size();
-  std::vector<int64_t> bounds(nd + 1);
-  if (nd > 1) plan_devices(ops, key_off, n_keys, nd, bounds.data());
-  else bounds[0] = 0, bounds[1] = n_keys;
-
-  std::vector<int> rcs(nd, 0);
-  auto work = [&](int di) {
-    Dev &d = c->devs[di];
-    const int64_t a = bounds[di], b = bounds[di + 1];
-    const int64_t nk = b - a;
-    const auto tw = std::chrono::steady_clock::now();
-    d.last = lc_device_stats{};
-    d.last.device = d.id;
-    d.last.key_begin = a;
-    d.last.key_end = b;
-    d.kernel_ms = 0;
-    if (nk <= 0) return;
-    if (hipSetDevice(d.id) != hipSuccess) {
-      rcs[di] = -EIO;
-      return;
-    }
-    const int64_t r0 = key_off[a], r1 = key_off[b];
-    const int64_t nrec = r1 - r0;
-    const size_t ops_bytes = sizeof(lc_op) * (size_t)nrec;
-    int r = ensure(c, reinterpret_cast<char **>(&d.d_ops), &d.ops_cap, ops_bytes);
-    if (!r) r = ensure(c, &d.d_off, &d.off_cap, sizeof(int64_t) * (size_t)(nk + 1));
-    if (!r) r = ensure(c, &d.d_out, &d.out_cap, sizeof(lc_key_result) * (size_t)nk);
-    if (!r && want_wit) r = ensure(c, &d.d_wit, &d.wit_cap, sizeof(int32_t) * (size_t)nrec);
-    if (!r && want_wit) r = ensure(c, &d.d_kind, &d.kind_cap, sizeof(int32_t) * (size_t)nk);
-    if (!r && want_cert) r = ensure(c, &d.d_cert, &d.cert_cap, 4 * sizeof(int32_t) * (size_t)nk);
-    if (!r && want_cert) r = ensure(c, &d.d_cset, &d.cset_cap, sizeof(int32_t) * (size_t)nrec);
-    if (r) {
-      rcs[di] = r;
-      return;
-    }
-    hipError_t e = hipEventRecord(d.eh0, d.stream);
-    if (e == hipSuccess && ops_bytes)
-      e = hipMemcpyAsync(d.d_ops, ops + r0, ops_bytes, hipMemcpyHostToDevice,
-                         d.stream);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(d.d_off, key_off + a, sizeof(int64_t) * (size_t)(nk + 1),
-                         hipMemcpyHostToDevice, d.stream);
-    if (e == hipSuccess) e = hipEventRecord(d.eh1, d.stream);
-    d.last.h2d_bytes = (int64_t)(ops_bytes + sizeof(int64_t) * (size_t)(nk + 1));
-    d.last.pinned = is_pinned(c, ops + r0, ops_bytes);
-    if (e != hipSuccess) {
-      set_err(c, std::string("hipMemcpyAsync H2D: ") + hipGetErrorString(e));
-      rcs[di] = -EIO;
-      return;
-    }
-    WitOut wo;
-    wo.n_records = nrec;
-    if (want_wit) {
-      wo.wit = d.d_wit;
-      wo.kind = d.d_kind;
-    }
-    if (want_cert) {
-      wo.cert = d.d_cert;
-      wo.cset = d.d_cset;
-    }
-    wo.h_off = key_off + a;
-    r = run_device(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, nk, p,
-                   d.d_out, d.stream, flags, wo);
-    if (!r) r = run_certificates(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, nk, p,
-                                 d.d_out, d.stream, wo);
-    if (r) {
-      rcs[di] = r;
-      return;
-    }
-    e = hipMemcpyAsync(out + a, d.d_out, sizeof(lc_key_result) * (size_t)nk,
-                       hipMemcpyDeviceToHost, d.stream);
-    if (e == hipSuccess && want_wit && nrec)
-      e = hipMemcpyAsync(aux->witness + r0, d.d_wit, sizeof(int32_t) * (size_t)nrec,
-                         hipMemcpyDeviceToHost, d.stream);
-    if (e == hipSuccess && want_wit)
-      e = hipMemcpyAsync(aux->witness_kind + a, d.d_kind, sizeof(int32_t) * (size_t)nk,
-                         hipMemcpyDeviceToHost, d.stream);
-    if (e == hipSuccess && want_cert)
-      e = hipMemcpyAsync(aux->certificate + 4 * a, d.d_cert, 4 * sizeof(int32_t) * (size_t)nk,
-                         hipMemcpyDeviceToHost, d.stream);
-    if (e == hipSuccess && want_cert && aux->certificate_set && nrec)
-      e = hipMemcpyAsync(aux->certificate_set + r0, d.d_cset, sizeof(int32_t) * (size_t)nrec,
-                         hipMemcpyDeviceToHost, d.stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
-    if (e != hipSuccess) {
-      set_err(c, std::string("hipMemcpyAsync D2H: ") + hipGetErrorString(e));
-      rcs[di] = -EIO;
-      return;
-    }
-    float hms = 0;
-    if (hipEventElapsedTime(&hms, d.eh0, d.eh1) == hipSuccess) d.last.h2d_ms = hms;
-    d.last.kernel_ms = d.kernel_ms;
-    d.last.total_ms = std::chrono::duration<double, std::milli>(
-                          std::chrono::steady_clock::now() - tw).count();
-  };
-  if (nd == 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> th;
-    for (int di = 0; di < nd; di++) th.emplace_back(work, di);
-    for (auto &t : th) t.join();
-  }
-  for (int di = 0; di < nd; di++) {
-    if (rcs[di] && !rc) rc = rcs[di];
-    c->stats.kernel_ms += c->devs[di].kernel_ms;
-    c->stats.fast_kernel_ms += c->devs[di].fast_ms;
-    c->stats.jit_kernel_ms += c->devs[di].jit_ms;
-    c->stats.n_jit_keys += c->devs[di].n_jit;
-    c->stats.gap_kernel_ms += c->devs[di].gap_ms;
-    c->stats.n_gap_keys += c->devs[di].n_gap;
-    c->stats.hbm_kernel_ms += c->devs[di].hbm_ms;
-    c->stats.n_hbm_keys += c->devs[di].n_hbm;
-    c->stats.n_malformed += c->devs[di].malformed;
-  }
-  if (!rc && (flags & LC_FLAG_WHOLE_GPU)) {
-    std::vector<int64_t> todo, todo_w;
-    for (int64_t k = 0; k < n_keys; k++)
-      if (out[k].verdict == LC_UNKNOWN && out[k].reason == LC_REASON_CONFIG_BUDGET) todo.push_back(k);
-      else if (out[k].verdict == LC_UNKNOWN && out[k].reason == LC_REASON_WINDOW_OVERFLOW)
-        todo_w.push_back(k);
-    auto fetch = [&](int64_t k, std::vector<lc_op> &v) {
-      v.assign(ops + key_off[k], ops + key_off[k + 1]);
-      return 0;
-    };
-    auto store = [&](int64_t k, const lc_key_result &r) {
-      out[k] = r;
-      // re-decided by the frontier exchange: no certificate (cert.hip covers
-      // the tiers' decisions)
-      if (want_cert)
-        for (int j = 0; j < 4; j++) aux->certificate[4 * k + j] = j == 0 ? LC_CERT_NONE : j < 3 ? -1 : 0;
-      return 0;
-    };
-    rc = whole_gpu(c, todo, opts, fetch, store);
-    if (!rc) rc = whole_gpu(c, todo_w, opts, fetch, store);
-  }
-  c->stats.n_keys = n_keys;
-  c->stats.n_ops = key_off[n_keys] - key_off[0];
-  c->stats.n_devices = nd;
-  c->stats.total_ms = std::chrono::duration<double, std::milli>(
-                          std::chrono::steady_clock::now() - t0).count();
-  return rc;
+  return check_host(c, ops, key_off, nullptr, n_keys, opts, out, aux);
 }
 
 int lc_check(lc_ctx *c, const lc_op *ops, const int64_t *key_off,
              int64_t n_keys, const lc_opts *opts, lc_key_result *out) {
   return lc_check_ex(c, ops, key_off, n_keys, opts, out, nullptr);
+}
+
+int lc_check32(lc_ctx *c, const lc_op32 *ops, const int64_t *key_off, const int64_t *key_base,
+               int64_t n_keys, const lc_opts *opts, lc_key_result *out, const lc_aux *aux) {
+  if (!c) return -EINVAL;
+  if (reinterpret_cast<uintptr_t>(ops) % 4) {
+    set_err(c, "lc_check32: ops must be 4-byte aligned");
+    return -EINVAL;
+  }
+  return check_host(c, ops, key_off, key_base, n_keys, opts, out, aux);
+}
+
+int lc_last_call_profile(lc_ctx *c, lc_call_profile *out) {
+  if (!c || !out) return -EINVAL;
+  *out = c->prof;
+  return 0;
 }
 
 int lc_check_device_ex(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
@@ -1414,6 +1720,158 @@ int lc_check_device(lc_ctx *c, const lc_op *d_ops, const int64_t *d_key_off,
                     int64_t n_keys, const lc_opts *opts, lc_key_result *d_out,
                     void *stream) {
   return lc_check_device_ex(c, d_ops, d_key_off, n_keys, opts, d_out, stream, nullptr);
+}
+
+
+int lc_check_device32(lc_ctx *c, const lc_op32 *d_ops, const int64_t *d_key_off,
+                      const int64_t *d_key_base, int64_t n_keys, const lc_opts *opts,
+                      lc_key_result *d_out, void *stream, const lc_aux *aux) {
+  if (!c) return -EINVAL;
+  if (n_keys < 0 || (n_keys > 0 && (!d_ops || !d_key_off || !d_out))) {
+    set_err(c, "lc_check_device32: null buffer or negative n_keys");
+    return -EINVAL;
+  }
+  if (reinterpret_cast<uintptr_t>(d_ops) % 8) {
+    set_err(c, "lc_check_device32: ops must be 8-byte aligned");
+    return -EINVAL;
+  }
+  if (n_keys == 0) return lc_check_device_ex(c, nullptr, d_key_off, 0, opts, d_out, stream, aux);
+  Dev &d = c->devs[0];
+  HIP_TRY(c, hipSetDevice(d.id));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d.stream;
+  // the record count lives in device memory: key_off[n_keys] - key_off[0]
+  int64_t *ends = reinterpret_cast<int64_t *>(d.h_status);  // (pinned; free between calls)
+  HIP_TRY(c, hipMemcpyAsync(&ends[0], d_key_off, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(&ends[1], d_key_off + n_keys, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  const int64_t nrec = ends[1] - ends[0];
+  if (nrec < 0) {
+    set_err(c, "lc_check_device32: key_off[n_keys] < key_off[0]");
+    return -EINVAL;
+  }
+  if (int e = ensure(c, reinterpret_cast<char **>(&d.d_ops), &d.ops_cap, sizeof(lc_op) * (size_t)nrec))
+    return e;
+  // the grid's second dimension for long keys: sized from the mean length
+  // (any size is correct: each workgroup strides its key)
+  HIP_TRY(c, lcdev::launch_widen32(d_ops, d_key_off, d_key_base, n_keys, 4 * (nrec / n_keys + 1),
+                                   static_cast<lc_op *>(d.d_ops), st));
+  return lc_check_device_ex(c, static_cast<const lc_op *>(d.d_ops), d_key_off, n_keys, opts, d_out,
+                            stream, aux);
+}
+
+int lc_check_frontiers(lc_ctx *c, const lc_op *ops, const int64_t *key_off, int64_t n_keys,
+                       const int64_t *stop_op, const lc_opts *opts, lc_fx_config *out,
+                       int32_t max_per_key, int32_t *n_out) {
+  if (!c) return -EINVAL;
+  if (n_keys < 0 || max_per_key < 1 ||
+      (n_keys > 0 && (!ops || !key_off || !stop_op || !out || !n_out))) {
+    set_err(c, "lc_check_frontiers: null buffer, negative n_keys or max_per_key < 1");
+    return -EINVAL;
+  }
+  if (n_keys == 0) return 0;
+  if (key_off[0] < 0) {
+    set_err(c, "lc_check_frontiers: key_off[0] < 0");
+    return -EINVAL;
+  }
+  for (int64_t k = 0; k < n_keys; k++)
+    if (key_off[k + 1] < key_off[k]) {
+      set_err(c, "lc_check_frontiers: key_off not monotone at key " + std::to_string(k));
+      return -EINVAL;
+    }
+  lcdev::KParams p;
+  if (int rc = opts_to_params(c, opts, &p)) return rc;
+  Dev &d = c->devs[0];
+  HIP_TRY(c, hipSetDevice(d.id));
+  (void)settle_status(d);  // a fused call's status copy may still be pending
+  const int64_t r0 = key_off[0], nrec = key_off[n_keys] - r0;
+  const size_t cfg_bytes = sizeof(lc_fx_config) * (size_t)max_per_key * (size_t)n_keys;
+  // scratch: the records, offsets, stops and results share the context's
+  // lc_check buffers (a context is not re-entrant)
+  int e = ensure(c, reinterpret_cast<char **>(&d.d_ops), &d.ops_cap, sizeof(lc_op) * (size_t)nrec);
+  if (!e) e = ensure(c, &d.d_off, &d.off_cap, sizeof(int64_t) * (size_t)(2 * n_keys + 1));
+  if (!e) e = ensure(c, reinterpret_cast<char **>(&d.d_gws), &d.gws_cap, cfg_bytes);
+  if (!e) e = ensure(c, &d.d_jit, &d.jit_cap, sizeof(int32_t) * (size_t)n_keys);
+  if (!e) e = ensure(c, &d.d_jit2, &d.jit2_cap, sizeof(int32_t) * (size_t)n_keys);
+  if (e) return e;
+  int64_t *d_stop = d.d_off + (n_keys + 1);
+  lc_fx_config *d_cfg = reinterpret_cast<lc_fx_config *>(d.d_gws);
+  const lc_op *d_ops = static_cast<const lc_op *>(d.d_ops);
+  hipStream_t st = d.stream;
+  HIP_TRY(c, hipMemcpyAsync(d.d_ops, ops + r0, sizeof(lc_op) * (size_t)nrec, hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemcpyAsync(d.d_off, key_off, sizeof(int64_t) * (size_t)(n_keys + 1),
+                            hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemcpyAsync(d_stop, stop_op, sizeof(int64_t) * (size_t)n_keys, hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
+  d.status_dirty = true;
+  HIP_TRY(c, lcdev::launch_frontier_dump(d_ops, d.d_off, d_stop, n_keys, p, d_cfg, max_per_key, d.d_jit,
+                                         d.d_jit2, &d.d_status->n_overflow, st));
+  HIP_TRY(c, hipMemcpyAsync(d.h_status, d.d_status, sizeof(lcdev::KStatus), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  // keys whose search outgrew the LDS regions: again over HBM tables (the
+  // first HBM tier's 16k configurations per set), one wavefront per key
+  if (const int32_t n_retry = d.h_status->n_overflow) {
+    const int waves = std::min<int>(n_retry, 256);
+    if (!(e = ensure(c, reinterpret_cast<char **>(&d.d_ws), &d.ws_cap,
+                     lcdev::hbm_tier_ws_bytes(waves, kHbmCap[0]))))
+      HIP_TRY(c, lcdev::launch_frontier_dump_hbm(d_ops, d.d_off, d_stop, d.d_jit2, n_retry, p, d.d_ws,
+                                                 waves, kHbmCap[0], d_cfg, max_per_key, d.d_jit,
+                                                 &d.d_status->hbm_next, st));
+    else
+      return e;
+  }
+  HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
+  HIP_TRY(c, hipMemcpyAsync(n_out, d.d_jit, sizeof(int32_t) * (size_t)n_keys, hipMemcpyDeviceToHost, st));
+  // one copy of every key's slots (C5's 94 keys x 10: 0.5 MB) rather than one
+  // per key; slots past a key's count keep the device's scratch
+  HIP_TRY(c, hipMemcpyAsync(out, d_cfg, cfg_bytes, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  d.status_dirty = false;
+  return 0;
+}
+
+int lc_pack32(const lc_op *ops, const int64_t *key_off, int64_t n_keys, lc_op32 *out,
+              int64_t *key_base) {
+  if (n_keys < 0 || (n_keys > 0 && (!ops || !key_off || !out || !key_base))) return -EINVAL;
+  if (n_keys == 0) return 0;
+  if (key_off[0] < 0) return -EINVAL;
+  for (int64_t k = 0; k < n_keys; k++)
+    if (key_off[k + 1] < key_off[k]) return -EINVAL;
+  constexpr int64_t kFieldMax = 0x7FFFFFFE, kNever = 0xFFFFFFFFll;
+  // the device's decoding (records.h, decode) of a 48-byte record, applied
+  // here: what it reads of each field fits 32 bits
+  auto pack = [&](int64_t k0, int64_t k1) {
+    for (int64_t k = k0; k < k1; k++) {
+      const int64_t b = key_off[k], e = key_off[k + 1];
+      const int64_t base = e > b ? ops[b].call : 0;
+      key_base[k] = base;
+      for (int64_t i = b; i < e; i++) {
+        const lc_op &o = ops[i];
+        const int64_t rc = o.call - base, rr = o.ret - base;
+        const bool bad = o.value < -1 || o.value > kFieldMax || o.expected < -1 ||
+                         o.expected > kFieldMax || o.call < 0 || o.ret <= o.call || rc < 0 ||
+                         rc >= kNever || (o.ret != LC_INF && rr >= kNever);
+        lc_op32 &q = out[i];
+        q.f = o.f >= 0 && o.f <= LC_F_CAS ? (int32_t)o.f : 3;
+        q.value = bad ? -2 : (int32_t)o.value;  // -2: malformed, in either width
+        q.expected = (int32_t)o.expected;
+        q.version = o.version < -1 || o.version > kFieldMax ? (int32_t)kFieldMax : (int32_t)o.version;
+        q.call = (uint32_t)rc;
+        // (a malformed record's return may land on LC_INF32 modulo 2^32: it
+        // stays a return, which is what the witness initialisation reads)
+        q.ret = o.ret == LC_INF ? LC_INF32 : (uint32_t)rr == LC_INF32 ? LC_INF32 - 1 : (uint32_t)rr;
+      }
+    }
+  };
+  const int64_t n_rec = key_off[n_keys] - key_off[0];
+  const int nth = (int)std::min<int64_t>(16, std::max<int64_t>(1, std::min<int64_t>(n_keys, n_rec >> 18)));
+  if (nth <= 1) {
+    pack(0, n_keys);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nth; t++) th.emplace_back(pack, n_keys * t / nth, n_keys * (t + 1) / nth);
+    for (auto &x : th) x.join();
+  }
+  return 0;
 }
 
 }  // extern "C"

@@ -47,6 +47,10 @@ def _lib():
         L.lc_edn_ops.restype = vp
         L.lc_edn_key_off.argtypes = [vp]
         L.lc_edn_key_off.restype = vp
+        L.lc_edn_ops32.argtypes = [vp]
+        L.lc_edn_ops32.restype = vp
+        L.lc_edn_key_base.argtypes = [vp]
+        L.lc_edn_key_base.restype = vp
         L.lc_edn_key.argtypes = [vp, i64]
         L.lc_edn_key.restype = ctypes.c_char_p
         L.lc_edn_op_text.argtypes = [vp, i64, ctypes.c_int]
@@ -90,6 +94,18 @@ class EdnHistory:
             ctypes.cast(L.lc_edn_key_off(h), ctypes.POINTER(ctypes.c_int64)),
             shape=(self.n_keys + 1,)).copy()
         self.keys = [L.lc_edn_key(h, i).decode() for i in range(self.n_keys)]
+
+    def ops32(self):
+        """The records as lc_op32 ((n, 6) int32) and the keys' bases: what
+        lc_check32 takes (include/lincheck_edn.h, lc_edn_ops32)."""
+        L = _lib()
+        n = len(self.ops)
+        p32, pb = L.lc_edn_ops32(self._h), L.lc_edn_key_base(self._h)
+        o32 = np.ctypeslib.as_array(ctypes.cast(p32, ctypes.POINTER(ctypes.c_int32)),
+                                    shape=(max(n, 1) * 6,))[: n * 6].reshape(n, 6).copy()
+        base = np.ctypeslib.as_array(ctypes.cast(pb, ctypes.POINTER(ctypes.c_int64)),
+                                     shape=(max(self.n_keys, 1),))[: self.n_keys].copy()
+        return o32, base
 
     def op_text(self, rec, which=0):
         """EDN text of record rec's :invoke (0) or completion (1)."""
@@ -139,7 +155,9 @@ def check(src, device_mask=0, independent=True, ctx=None, opts=None, model="vers
     own = ctx is None
     ctx = ctx or abi.Context(device_mask)
     try:
-        rc, res = ctx.check(h.ops, h.key_off, opts=opts, raise_on_error=False)
+        # the drop-in's call: 24-byte records across PCIe (ABI 4)
+        o32, base = h.ops32()
+        rc, res = ctx.check32(o32, h.key_off, base, opts=opts, raise_on_error=False)
         if rc != 0:
             raise abi.LcError(rc, ctx.last_error())
     finally:

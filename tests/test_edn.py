@@ -30,6 +30,16 @@ def test_generated_history_matches_pack():
     assert h.n_events == len(hist)
 
 
+def test_ops32_are_lc_pack32_of_the_records():
+    """lc_edn_ops32 / lc_edn_key_base (ABI 4): the 24-byte records lc_check32
+    takes are lc_pack32's narrowing of the parsed 48-byte ones."""
+    hist, _ = synth.jepsen_history(30, 60, concurrency=6, p_info=0.05, p_anomaly=0.3, seed=17)
+    h = edn.read(edn.to_edn(hist))
+    o32, base = h.ops32()
+    want, wbase = abi.pack32(h.ops, h.key_off)
+    assert (o32 == want).all() and (base == wbase).all() and len(base) == h.n_keys
+
+
 def test_threads_do_not_change_the_result():
     hist, _ = synth.jepsen_history(60, 400, concurrency=20, p_info=0.02, seed=3)
     text = edn.to_edn(hist).encode()
