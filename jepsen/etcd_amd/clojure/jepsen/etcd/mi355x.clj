@@ -12,9 +12,11 @@
   The JVM side does the host preprocessing (client ops only, the independent
   per-key split, knossos-style invoke/completion pairing with :fail pairs
   dropped and :info ops pending forever, per-key value interning by Clojure
-  =) and packs one 48-byte lc_op record per operation into off-heap memory.
-  One lc_check call (JNA, liblincheck.so; C ABI in include/lincheck.h) then
-  decides every key on the MI355X GPUs of the control node.  The result has
+  =) and packs one 24-byte lc_op32 record per operation into off-heap memory
+  (ABI 4: the int32 fields the device reads, half the PCIe bytes of the
+  48-byte lc_op).  One lc_check32 call (JNA, liblincheck.so; C ABI in
+  include/lincheck.h) then decides every key on the MI355X GPUs of the
+  control node.  The result has
   jepsen.independent/checker's shape, and each key's entry has
   checker/compose's shape: {:valid? merged, :linear <the GPU verdict>,
   :timeline <jepsen's own timeline/html over that key's subhistory, written
@@ -27,12 +29,13 @@
     :checker (jepsen.etcd.mi355x/checker)
 
   An invalid key's :linear map carries knossos's diagnostics: :op,
-  :previous-ok, :configs and :final-paths — for keys the frontier search
-  decided, up to 10 configurations of that search's frontier just before
-  the failing return (lc_fx_frontier, include/lincheck_fx.h); for keys the
-  version-order and gap tiers decided, the one configuration the witness of
-  the prefix before the failing return names (lc_check_ex, lc_aux), with its
-  :last-op.  :final-paths step the reference's own model
+  :previous-ok, :configs and :final-paths — up to 10 configurations of the
+  JIT search's frontier just before the failing return, for every invalid
+  key from one batched device search (lc_check_frontiers,
+  include/lincheck_fx.h) and, for a key whose frontier outgrows it, from the
+  frontier exchange alone (lc_fx_frontier); for keys the version-order and
+  gap tiers decided, also the :last-op of the prefix witness (lc_aux); the
+  witness's one configuration stands in where no frontier could be had.  :final-paths step the reference's own model
   (jepsen.etcd.register/->VersionedRegister, register.clj:55-96) through
   knossos.model/step, so the messages are the model's own
   (jepsen/etcd_amd/diagnostics.py restates the same).  A key with malformed
@@ -50,7 +53,10 @@
 (def ^:const LC_NIL -1)
 (def ^:const LC_FLAG_WHOLE_GPU 8)  ; include/lincheck.h
 (def ^:const LC_INF Long/MAX_VALUE)
-(def ^:const op-bytes 48)
+(def ^:const op-bytes 48)      ; lc_op (the frontier searches)
+(def ^:const op32-bytes 24)    ; lc_op32 (lc_check32, ABI 4)
+(def ^:const field-max 0x7FFFFFFE)
+(def ^:const never 0xFFFFFFFF)
 (def ^:const result-bytes 40)
 
 (defonce ^:private lib
@@ -164,37 +170,91 @@
             [2 (intern (second v)) (intern (first v)) ver call ret]
             [f (intern v) LC_NIL ver call ret]))))))
 
+(defn- narrow
+  "One record [f v e ver call ret] as the six int32 words of an lc_op32, by
+  lc_pack32's rules (include/lincheck.h): call / ret relative to the key's
+  base (its first call), -1 (LC_INF32) for a pending op; a version no state
+  reaches becomes 2^31-2, an unknown :f 3, and a record the device rejects as
+  malformed keeps value -2 (the arithmetic wraps as the library's does)."
+  [^long base [f v e ver call ret]]
+  (let [f (long f), v (long v), e (long e), ver (long ver), call (long call), ret (long ret)
+        rc  (unchecked-subtract call base)
+        rr  (unchecked-subtract ret base)
+        inf (= ret LC_INF)
+        bad (or (< v -1) (> v field-max) (< e -1) (> e field-max) (neg? call) (<= ret call)
+                (neg? rc) (>= rc never) (and (not inf) (>= rr never)))
+        lo  (fn [^long x] (unchecked-int (bit-and x 0xFFFFFFFF)))]
+    [(if (<= 0 f 2) f 3)
+     (if bad -2 (unchecked-int v))
+     (unchecked-int e)
+     (if (or (< ver -1) (> ver field-max)) field-max ver)
+     (lo rc)
+     (cond inf -1                                        ; LC_INF32
+           (= (bit-and rr 0xFFFFFFFF) 0xFFFFFFFF) -2     ; LC_INF32 - 1
+           :else (lo rr))]))
+
+(defn- key-records
+  "One key's records [f v e ver call ret], values interned in record order
+  (so the ids are the ones its packing used), and its id -> value map."
+  [model d]
+  (let [intern (interner)
+        rs     (mapv #(record model intern %) d)]
+    [rs (intern)]))
+
 (defn- pack
-  "Packs all keys: returns [keys completed-per-key ^Memory ops ^Memory key-off
-  n-records values-per-key] (values: each key's id -> value map).  Records
-  are filled into one long[] and written to the off-heap buffer in a single
-  bulk copy."
+  "Packs all keys as 24-byte lc_op32 records: returns [keys completed-per-key
+  ^Memory ops ^Memory key-off ^Memory key-base n-records values-per-key]
+  (values: each key's id -> value map).  Records are filled into one int[]
+  and written to the off-heap buffer in a single bulk copy."
   [model subs]
   (let [keys  (vec (keys subs))
+        nk    (count keys)
         done  (mapv (fn [k] (complete (get subs k))) keys)
         n     (long (reduce + (map count done)))
-        arr   (long-array (* 6 n))
-        offs  (long-array (inc (count keys)))
+        arr   (int-array (* 6 n))
+        offs  (long-array (inc nk))
+        bases (long-array (max 1 nk))
         vals  (transient [])]
     (loop [ki 0, i 0]
       (aset offs ki i)
-      (when (< ki (count keys))
-        (let [intern (interner)
-              i'     (reduce (fn [^long i r]
-                               (let [[f v e ver call ret] (record model intern r)
-                                     b (* 6 i)]
-                                 (aset arr b (long f)) (aset arr (+ b 1) (long v))
-                                 (aset arr (+ b 2) (long e)) (aset arr (+ b 3) (long ver))
-                                 (aset arr (+ b 4) (long call)) (aset arr (+ b 5) (long ret))
-                                 (inc i)))
-                             i (nth done ki))]
-          (conj! vals (intern))
+      (when (< ki nk)
+        (let [[rs vm] (key-records model (nth done ki))
+              base    (if (seq rs) (long (nth (first rs) 4)) 0)
+              i'      (reduce (fn [^long i r]
+                                (let [w (narrow base r), b (* 6 i)]
+                                  (dotimes [j 6] (aset arr (+ b j) (unchecked-int (nth w j))))
+                                  (inc i)))
+                              i rs)]
+          (aset bases ki base)
+          (conj! vals vm)
           (recur (inc ki) i'))))
-    (let [ops (Memory. (max 1 (* op-bytes n)))
-          off (Memory. (* 8 (inc (count keys))))]
+    (let [ops (Memory. (max 1 (* op32-bytes n)))
+          off (Memory. (* 8 (inc nk)))
+          bm  (Memory. (* 8 (max 1 nk)))]
       (.write ops 0 arr 0 (alength arr))
       (.write off 0 offs 0 (alength offs))
-      [keys done ops off n (persistent! vals)])))
+      (.write bm 0 bases 0 (alength bases))
+      [keys done ops off bm n (persistent! vals)])))
+
+(defn- pack48
+  "The 48-byte lc_op records of some keys (the frontier searches take
+  them): [^Memory ops long[] key-off]."
+  [model done kis]
+  (let [rss  (mapv #(first (key-records model (nth done %))) kis)
+        n    (long (reduce + (map count rss)))
+        arr  (long-array (max 1 (* 6 n)))
+        offs (long-array (inc (count kis)))]
+    (loop [j 0, i 0]
+      (aset offs j i)
+      (when (< j (count kis))
+        (recur (inc j)
+               (reduce (fn [^long i r]
+                         (dotimes [x 6] (aset arr (+ (* 6 i) x) (long (nth r x))))
+                         (inc i))
+                       i (nth rss j)))))
+    (let [ops (Memory. (max 1 (* op-bytes n)))]
+      (.write ops 0 arr 0 (alength arr))
+      [ops offs])))
 
 ;; ---- knossos's invalid-analysis keys (diagnostics.py restates the same)
 
@@ -273,45 +333,85 @@
       (when-not (zero? rc) (throw (ex-info "lc_fx_open failed" {:rc rc})))
       (.getValue out))))
 
-(defn- frontier-analysis
-  ":configs — up to 10 configurations of the frontier search's own frontier
-  just before the failing return (lc_fx_frontier) — and :final-paths, for
-  keys the frontier search decided."
-  [model done ops k0 fail-op vals opts]
-  (let [n   (count done)
-        buf (Memory. (* 10 fx-config-bytes))
+(defn- configs-analysis
+  ":configs and :final-paths from [[version value-id pending-record-indices]
+  ...], a frontier search's configurations just before the failing return."
+  [model done fail-op vals configs]
+  (let [configs (for [[ver vid pending] configs]
+                  [ver (when (not= vid LC_NIL) (get vals vid vid)) pending])]
+    (cond-> {:configs (vec (for [[ver x pending] configs]
+                             {:model (if (= model :versioned-register)
+                                       {:version ver :value x}
+                                       {:value x})
+                              :pending (mapv #(:op (nth done %)) pending)}))}
+      (= model :versioned-register)
+      (assoc :final-paths
+             (final-paths done fail-op
+                          (for [[ver x pending] configs] [(ref-model ver x) nil pending]))))))
+
+(defn- read-configs
+  "n lc_fx_config structs from buf at byte offset b0."
+  [^Memory buf b0 n]
+  (vec (for [i (range n)
+             :let [b (+ b0 (* i fx-config-bytes))]]
+         [(.getLong buf b) (.getLong buf (+ b 8))
+          (vec (for [j (range (.getLong buf (+ b 16)))] (.getLong buf (+ b 24 (* 8 j)))))])))
+
+(defn- batched-configs
+  "knossos's :configs of every invalid key in one device call
+  (lc_check_frontiers, include/lincheck_fx.h): {:configs {key-index
+  configurations}, :ops ^Memory, :off long[], :at {key-index j}} — the keys the
+  device search could not take (a frontier beyond its tiers) are left out of
+  :configs; :ops / :off / :at hold their 48-byte records for lc_fx_frontier."
+  [model done inv o]
+  (let [kis         (mapv first inv)
+        [ops offs]  (pack48 model done kis)
+        nk          (count kis)
+        off         (doto (Memory. (* 8 (inc nk))) (.write 0 offs 0 (alength offs)))
+        stops       (long-array (map second inv))
+        stop        (doto (Memory. (* 8 (max 1 nk))) (.write 0 stops 0 (alength stops)))
+        buf         (Memory. (* (max 1 nk) 10 fx-config-bytes))
+        cnt         (Memory. (* 4 (max 1 nk)))
+        rc          (try
+                      (locking ctx
+                        (.invokeInt (fun "lc_check_frontiers")
+                                    (object-array [@ctx ops off (long nk) stop o buf (int 10) cnt])))
+                      ;; diagnostics only: the verdict stands whatever happens here
+                      (catch Exception e e))
+        ok?         (and (number? rc) (zero? rc))]
+    {:ops ops :off offs :at (zipmap kis (range))
+     :configs (if-not ok?
+                {}
+                (into {} (for [j (range nk)
+                               :let [c (.getInt cnt (* 4 j))]
+                               :when (>= c 0)]
+                           [(nth kis j) (read-configs buf (* j 10 fx-config-bytes) c)])))}))
+
+(defn- fx-frontier
+  "One key's frontier search alone, up to its failing return
+  (lc_fx_frontier): its configurations, or {:configs-error ...}."
+  [^Memory ops ^long k0 n fail-op opts]
+  (let [buf (Memory. (* 10 fx-config-bytes))
         cnt (Memory. 4)
         rc  (try
               (locking fx-engine
                 (.invokeInt (fun "lc_fx_frontier")
-                            (object-array [@fx-engine (.share ^Memory ops (* op-bytes k0))
+                            (object-array [@fx-engine (.share ops (* op-bytes k0))
                                            (long n) opts (long fail-op) buf (int 10) cnt])))
               ;; diagnostics only: the verdict stands whatever happens here
               (catch Exception e e))]
-    (if-not (and (number? rc) (zero? rc))
-      {:configs-error (if (number? rc) [:lc-fx-frontier rc] (str rc))}
-      (let [configs (for [i (range (.getInt cnt 0))
-                          :let [b   (* i fx-config-bytes)
-                                ver (.getLong buf b)
-                                vid (.getLong buf (+ b 8))
-                                np  (.getLong buf (+ b 16))
-                                x   (when (not= vid LC_NIL) (get vals vid vid))]]
-                      [ver x (vec (for [j (range np)] (.getLong buf (+ b 24 (* 8 j)))))])]
-        (cond-> {:configs (vec (for [[ver x pending] configs]
-                                 {:model (if (= model :versioned-register)
-                                           {:version ver :value x}
-                                           {:value x})
-                                  :pending (mapv #(:op (nth done %)) pending)}))}
-          (= model :versioned-register)
-          (assoc :final-paths
-                 (final-paths done fail-op
-                              (for [[ver x pending] configs] [(ref-model ver x) nil pending]))))))))
+    (if (and (number? rc) (zero? rc))
+      (read-configs buf 0 (.getInt cnt 0))
+      {:configs-error (if (number? rc) [:lc-fx-frontier rc] (str rc))})))
 
 (def ^:private cert-kinds {0 :none 1 :dup 2 :unreach 3 :claims 4 :pair 5 :order 6 :hall})
 
-;; invalid keys the version-order / gap tiers decided get :configs from a
-;; frontier re-search when they have at most this many crashed ops, up to
-;; frontier-max-keys such re-searches per check (checker.py: the same)
+;; an invalid key the batched device search could not take gets :configs from
+;; the frontier exchange alone when the frontier search decided it, or the
+;; version-order / gap tiers did and it has at most this many crashed ops; at
+;; most frontier-max-keys such searches per check (checker.py counts the same
+;; way: a search is counted when it runs, and runs while the count is below
+;; the cap)
 (def ^:private frontier-max-crashed 16)
 (def ^:private frontier-max-keys 1000)
 
@@ -324,12 +424,12 @@
   {2 :config-budget 3 :window-overflow 4 :malformed 5 :unknown-f 7 :time-budget})
 
 (defn- check-keys
-  "One lc_check_ex over subs {k [op ...]}: {k result-map}.  Malformed keys
-  come back :unknown one by one; lc_check_ex fails (and this throws, for
+  "One lc_check32 over subs {k [op ...]}: {k result-map}.  Malformed keys
+  come back :unknown one by one; lc_check32 fails (and this throws, for
   check-safe) only on unusable arguments or a GPU error."
   [model max-configs-per-key time-budget-ms flags subs]
-  (let [[keys done ops off n vals] (pack model subs)
-        n-frontier (atom 0)
+  (let [[keys done ops off base n vals] (pack model subs)
+        n-fallback (atom 0)
         nk   (count keys)
         out  (Memory. (* result-bytes nk))
         wit  (Memory. (max 4 (* 4 n)))
@@ -343,62 +443,73 @@
                (.setLong 16 max-configs-per-key)
                (.setLong 24 time-budget-ms) (.setLong 32 flags))
         rc   (locking ctx
-               (.invokeInt (fun "lc_check_ex")
-                           (object-array [@ctx ops off (long nk) o out aux])))]
+               (.invokeInt (fun "lc_check32")
+                           (object-array [@ctx ops off base (long nk) o out aux])))]
     (when-not (zero? rc)
-      (throw (ex-info "lc_check failed"
+      (throw (ex-info "lc_check32 failed"
                       {:rc rc :error (.invoke (fun "lc_last_error")
                                               String (object-array [@ctx]))})))
-    (into (array-map)
-          (for [ki (range nk)]
-            (let [b       (* ki result-bytes)
-                  verdict (.getInt out b)
-                  reason  (.getInt out (+ b 4))
-                  fail-op (.getLong out (+ b 8))
-                  fail-at (.getLong out (+ b 16))
-                  v       (case verdict 1 true 0 false :unknown)
-                  d       (nth done ki)
-                  k0      (.getLong off (* 8 ki))
-                  witness (when (and (false? v) (= model :versioned-register)
-                                     (= 2 (.getInt kind (* 4 ki))))  ; LC_WITNESS_PREFIX
-                            (vec (.getIntArray wit (* 4 k0) (count d))))]
-              [(nth keys ki)
-               (cond-> {:valid?   v
-                        :analyzer :mi355x
-                        :configs-explored (.getLong out (+ b 24))}
-                 (false? v)     (merge {:op (op-map (nth d fail-op))
-                                        :previous-ok (previous-ok d fail-at)
-                                        ;; why the prefix at the failing return has no
-                                        ;; linearization (include/lincheck.h LC_CERT_*)
-                                        :certificate
-                                        (let [c (.getIntArray cert (* 16 ki) 4)
-                                              kd (get cert-kinds (aget c 0) :none)
-                                              rec #(when (>= % 0) (op-map (nth d %)))]
-                                          (cond-> {:kind kd}
-                                            (#{:dup :unreach :claims :pair :order} kd)
-                                            (assoc :ops (vec (keep rec [(aget c 1) (aget c 2)])))
-                                            (= kd :hall)
-                                            (assoc :positions
-                                                   (vec (.getIntArray cset (* 4 k0) (aget c 3))))))}
-                                       (let [wa (when witness
-                                                  (witness-analysis d fail-op fail-at witness
-                                                                    [0 nil]))
-                                             ;; knossos's :configs: the frontier search's
-                                             ;; own, re-run up to the failing return, for
-                                             ;; keys whose frontier stays small
-                                             fa (when (or (nil? witness)
-                                                          (and (< (swap! n-frontier inc)
-                                                                  frontier-max-keys)
-                                                               (<= (count (filter
-                                                                           #(= LC_INF (:ret %)) d))
-                                                                   frontier-max-crashed)))
-                                                  (frontier-analysis model d ops k0 fail-op
-                                                                     (nth vals ki) o))]
-                                         (cond (and fa (:configs fa))
-                                               (cond-> fa (:last-op wa) (assoc :last-op (:last-op wa)))
-                                               wa (merge wa (select-keys fa [:configs-error]))
-                                               :else fa)))
-                 (= v :unknown) (assoc :error [:lincheck-reason (reasons reason reason)]))])))))
+    (let [inv (vec (for [ki (range nk)
+                         :let [b (* ki result-bytes)]
+                         :when (zero? (.getInt out b))]
+                     [ki (.getLong out (+ b 8))]))
+          bc  (when (seq inv) (batched-configs model done inv o))]
+      (into (array-map)
+            (for [ki (range nk)]
+              (let [b       (* ki result-bytes)
+                    verdict (.getInt out b)
+                    reason  (.getInt out (+ b 4))
+                    fail-op (.getLong out (+ b 8))
+                    fail-at (.getLong out (+ b 16))
+                    v       (case verdict 1 true 0 false :unknown)
+                    d       (nth done ki)
+                    k0      (.getLong off (* 8 ki))
+                    witnessed (and (false? v) (= model :versioned-register)
+                                   (= 2 (.getInt kind (* 4 ki))))  ; LC_WITNESS_PREFIX
+                    witness (when witnessed (vec (.getIntArray wit (* 4 k0) (count d))))]
+                [(nth keys ki)
+                 (cond-> {:valid?   v
+                          :analyzer :mi355x
+                          :configs-explored (.getLong out (+ b 24))}
+                   (false? v)     (merge {:op (op-map (nth d fail-op))
+                                          :previous-ok (previous-ok d fail-at)
+                                          ;; why the prefix at the failing return has no
+                                          ;; linearization (include/lincheck.h LC_CERT_*)
+                                          :certificate
+                                          (let [c (.getIntArray cert (* 16 ki) 4)
+                                                kd (get cert-kinds (aget c 0) :none)
+                                                rec #(when (>= % 0) (op-map (nth d %)))]
+                                            (cond-> {:kind kd}
+                                              (#{:dup :unreach :claims :pair :order} kd)
+                                              (assoc :ops (vec (keep rec [(aget c 1) (aget c 2)])))
+                                              (= kd :hall)
+                                              (assoc :positions
+                                                     (vec (.getIntArray cset (* 4 k0) (aget c 3))))))}
+                                         (let [wa (when witness
+                                                    (witness-analysis d fail-op fail-at witness
+                                                                      [0 nil]))
+                                               ;; knossos's :configs: the frontier search's
+                                               ;; own, up to the failing return — batched on
+                                               ;; the device, else this key alone
+                                               cs (or (get-in bc [:configs ki])
+                                                      (when (and (< @n-fallback frontier-max-keys)
+                                                                 (or (not witnessed)
+                                                                     (<= (count (filter
+                                                                                 #(= LC_INF (:ret %)) d))
+                                                                         frontier-max-crashed)))
+                                                        (swap! n-fallback inc)
+                                                        (fx-frontier (:ops bc)
+                                                                     (aget ^longs (:off bc)
+                                                                           (get (:at bc) ki))
+                                                                     (count d) fail-op o)))
+                                               fa (cond (vector? cs)
+                                                        (configs-analysis model d fail-op (nth vals ki) cs)
+                                                        (map? cs) cs)]
+                                           (cond (and fa (:configs fa))
+                                                 (cond-> fa (:last-op wa) (assoc :last-op (:last-op wa)))
+                                                 wa (merge wa (select-keys fa [:configs-error]))
+                                                 :else fa)))
+                   (= v :unknown) (assoc :error [:lincheck-reason (reasons reason reason)]))]))))))
 
 (defn linearizable
   "(checker/linearizable {:model m}) over the whole history, for the knossos
