@@ -115,28 +115,24 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ctx = abi.Context(device_mask=1 << local)
 
-    # one step = one lc_check_device call (+ its per-call stats), arguments
-    # converted once
-    step = ctx.bind_check_device(d_ops.data_ptr(), d_off.data_ptr(), my_keys,
-                                 d_out.data_ptr(), stream=stream.cuda_stream,
-                                 opts=abi.default_opts(), stats=abi.LcStats())
+    # one step = one lc_check_device call, arguments converted once.  The
+    # call returns on the version-order pass's follower signal (no event
+    # wait).  The pass is timed by HIP events on the launch stream on every
+    # TIME_EVERY-th step (each event record costs ~2 us of host time per
+    # call, so the other steps run with LC_FLAG_NO_TIMING); the event times
+    # are read after the loop (lc_last_totals), so no step waits for them
+    steps = bind_steps(ctx, abi, d_ops.data_ptr(), d_off.data_ptr(), my_keys, d_out.data_ptr(),
+                       stream.cuda_stream)
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        steps[i % TIME_EVERY != 0]()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
+    ctx.totals(reset=True)
     t0 = time.perf_counter()
-    kms, hms, fms, jms, gms, njit, cms = [], [], [], [], [], [], []
-    for _ in range(args.steps):
-        s = step()
-        kms.append(s.kernel_ms)
-        hms.append(s.hbm_kernel_ms)
-        fms.append(s.fast_kernel_ms)
-        jms.append(s.jit_kernel_ms)
-        gms.append(s.gap_kernel_ms)
-        njit.append(s.n_jit_keys)
-        cms.append(s.total_ms)
+    for i in range(args.steps):
+        steps[i % TIME_EVERY != 0]()
     torch.cuda.synchronize()
     # this rank's own K steps; the job time is the MAX of these over ranks
     # (reduce_run).  The trailing barrier closes the timed region on every
@@ -147,6 +143,13 @@ def main():
         dist.barrier()
     after_barrier = time.perf_counter() - t0
     elapsed = own
+    tot = ctx.totals(reset=True)
+    assert tot["calls"] == args.steps and tot["timed_calls"] >= 1, tot
+    last = ctx.stats()  # the last call's tiers (nothing has run since)
+    kms = [tot["kernel_ms"] / tot["timed_calls"]]
+    fms = [tot["fast_kernel_ms"] / tot["timed_calls"]]
+    hms, jms, gms = [last["hbm_kernel_ms"]], [last["jit_kernel_ms"]], [last["gap_kernel_ms"]]
+    njit = [last["n_jit_keys"]]
     res = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)[:my_keys]
     ranks = (D.gather_rows([rank, ka, kb, n_ops, own * 1e3 / args.steps,
                             float(np.mean(kms))])
@@ -243,7 +246,10 @@ def main():
         },
         "tiers": {"fast_kernel_ms": fast_ms, "gap_kernel_ms": gap_ms, "jit_kernel_ms": jit_ms,
                   "jit_keys": float(np.mean(njit)), "all_kernels_ms": kernel_ms,
-                  "c_call_ms": float(np.mean(cms))},
+                  "kernel_ms_source": "lc_last_totals: HIP events around the version-order "
+                                      "launch on the launch stream, every %d-th of the K timed "
+                                      "steps (%d of them; the others LC_FLAG_NO_TIMING), "
+                                      "mean" % (TIME_EVERY, tot["timed_calls"])},
         "verdicts": {"valid": n_valid, "invalid": n_invalid, "unknown": n_unknown},
         "hbm_tier_ms": float(np.mean(hms)),
         "cpu_baseline": None,
@@ -278,6 +284,19 @@ def main():
         dist.destroy_process_group()
 
 
+# every TIME_EVERY-th timed step records HIP events around the version-order
+# pass (their host cost kept out of the other steps: LC_FLAG_NO_TIMING)
+TIME_EVERY = 4
+
+
+def bind_steps(ctx, abi, d_ops, d_off, n_keys, d_out, stream):
+    """[timed step, untimed step]: lc_check_device with the arguments
+    converted once, with and without LC_FLAG_NO_TIMING."""
+    return [ctx.bind_check_device(d_ops, d_off, n_keys, d_out, stream=stream,
+                                  opts=abi.default_opts(flags=f))
+            for f in (0, abi.LC_FLAG_NO_TIMING)]
+
+
 def c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream, steps=200, warmup=20):
     """A one-GPU predictor of BASELINE configs[2] (C3): the same C2 batch cut
     by lc_plan_partition into 1, 2, 4 and 8 shards, and each shard timed as
@@ -296,19 +315,19 @@ def c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream, steps=200, warm
             a, b = int(bounds[p]), int(bounds[p + 1])
             outb = torch.zeros(max(b - a, 1) * abi.RESULT_DTYPE.itemsize, dtype=torch.uint8,
                                device=dev)
-            step = ctx.bind_check_device(d_ops.data_ptr() + int(key_off[a] - key_off[0]) * 48,
-                                         d_off.data_ptr() + a * 8, b - a, outb.data_ptr(),
-                                         stream=stream.cuda_stream, opts=abi.default_opts(),
-                                         stats=abi.LcStats())
-            for _ in range(warmup):
-                step()
+            st2 = bind_steps(ctx, abi, d_ops.data_ptr() + int(key_off[a] - key_off[0]) * 48,
+                             d_off.data_ptr() + a * 8, b - a, outb.data_ptr(), stream.cuda_stream)
+            for i in range(warmup):
+                st2[i % TIME_EVERY != 0]()
             torch.cuda.synchronize()
+            ctx.totals(reset=True)
             t0 = time.perf_counter()
-            kms = []
-            for _ in range(steps):
-                kms.append(step().kernel_ms)
+            for i in range(steps):
+                st2[i % TIME_EVERY != 0]()
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3 / steps
+            tot = ctx.totals(reset=True)
+            kms = [tot["kernel_ms"] / max(1, tot["timed_calls"])]
             res = np.frombuffer(outb.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)[:b - a]
             shard_ms.append({"keys": [a, b], "ms_per_step": ms, "kernel_ms": float(np.mean(kms)),
                              "valid": int((res["verdict"] == 1).sum())})

@@ -86,6 +86,10 @@ typedef struct lc_opts {
 #define LC_FLAG_NO_FAST_PATH 2  /* skip the version-order and gap tiers: JIT search for every key */
 #define LC_FLAG_NO_GAP_TIER  4  /* skip the gap-matching tier: keys the version-order tier
                                    hands over go straight to the JIT search */
+#define LC_FLAG_NO_TIMING   16  /* ABI 4, lc_check_device: no HIP events around the version-
+                                   order pass (each costs ~2 us of host time per call); its
+                                   time is then not measured (lc_last_stats 0, not counted
+                                   by lc_last_totals) */
 #define LC_FLAG_WHOLE_GPU    8  /* every entry point: a key the tiers leave :unknown at the
                                    configuration budget is searched again by the frontier
                                    exchange (include/lincheck_fx.h), whose budget bounds each
@@ -256,7 +260,11 @@ int lc_check_ex(lc_ctx *ctx, const lc_op *ops, const int64_t *key_off,
 
 /* Same, with ops / key_off / out already resident in device memory of the
  * context's first GPU; `stream` is a hipStream_t (NULL: the context's own).
- * Synchronous with respect to the host. */
+ * Returns when every key is decided: d_out is complete for work ordered
+ * after the call on `stream` (another stream reads it after synchronising
+ * `stream`: a call that every key's version-order pass decided returns on
+ * the pass's completion signal, a few microseconds before the kernel
+ * retires; ABI 4). */
 int lc_check_device(lc_ctx *ctx, const lc_op *d_ops, const int64_t *d_key_off,
                     int64_t n_keys, const lc_opts *opts,
                     lc_key_result *d_out, void *stream);
@@ -268,6 +276,21 @@ int lc_check_device_ex(lc_ctx *ctx, const lc_op *d_ops, const int64_t *d_key_off
                        void *stream, const lc_aux *aux);
 
 int lc_last_stats(lc_ctx *ctx, lc_stats *out);
+
+/* ABI 4: sums over the calls since the last reset (reset != 0 zeroes them
+ * after the read).  lc_check_device returns as soon as the version-order (or
+ * fused) pass signals that every key is decided, before the kernel has
+ * retired; the pass's HIP-event time is read afterwards — here, by
+ * lc_last_stats, or at the next call — so a loop that times calls reads the
+ * device time of all of them at once without waiting inside the loop. */
+typedef struct lc_totals {
+  int64_t calls;           /* run on the context's devices (one per device per call) */
+  int64_t timed_calls;     /* those whose pass was timed (without LC_FLAG_NO_TIMING) */
+  double fast_kernel_ms;   /* the version-order / fused pass (HIP events on the launch stream) */
+  double kernel_ms;        /* every tier */
+} lc_totals;
+
+int lc_last_totals(lc_ctx *ctx, lc_totals *out, int32_t reset);
 
 /* Per-device share of the most recent lc_check / lc_check_ex call (the
  * multi-GPU fan-out: one host thread and one HIP stream per device, each over

@@ -40,6 +40,7 @@ LC_FLAG_NO_HBM_RETRY = 1
 LC_FLAG_NO_FAST_PATH = 2
 LC_FLAG_NO_GAP_TIER = 4
 LC_FLAG_WHOLE_GPU = 8
+LC_FLAG_NO_TIMING = 16
 LC_WITNESS_NONE, LC_WITNESS_FULL, LC_WITNESS_PREFIX = 0, 1, 2
 LC_CERT_NONE, LC_CERT_DUP, LC_CERT_UNREACH, LC_CERT_CLAIMS, LC_CERT_PAIR, LC_CERT_ORDER, \
     LC_CERT_HALL = range(7)
@@ -87,6 +88,11 @@ class LcCallProfile(ctypes.Structure):
                 ("last_end_ms", ctypes.c_double), ("joined_ms", ctypes.c_double),
                 ("whole_gpu_ms", ctypes.c_double), ("n_devices", ctypes.c_int64),
                 ("n_chunks", ctypes.c_int64)]
+
+
+class LcTotals(ctypes.Structure):
+    _fields_ = [("calls", ctypes.c_int64), ("timed_calls", ctypes.c_int64),
+                ("fast_kernel_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double)]
 
 
 class LcAux(ctypes.Structure):
@@ -162,6 +168,8 @@ def lib():
         L.lc_pack32.restype = ctypes.c_int
         L.lc_check_frontiers.argtypes = [vp, p, p, i64, p, ctypes.POINTER(LcOpts), vp, i32, p]
         L.lc_check_frontiers.restype = ctypes.c_int
+        L.lc_last_totals.argtypes = [vp, ctypes.POINTER(LcTotals), i32]
+        L.lc_last_totals.restype = ctypes.c_int
         L.lc_last_call_profile.argtypes = [vp, ctypes.POINTER(LcCallProfile)]
         L.lc_last_call_profile.restype = ctypes.c_int
         L.lc_key_cost.argtypes = [p, p, i64, p]
@@ -373,6 +381,13 @@ class Context:
             out.append([(int(c.version), int(c.value), tuple(int(c.pending[j]) for j in range(c.n_pending)))
                         for c in buf[k * max_per_key:k * max_per_key + n]])
         return out
+
+    def totals(self, reset=False):
+        """lc_last_totals (ABI 4): calls and device time summed since the last
+        reset, every pending event read first."""
+        t = LcTotals()
+        lib().lc_last_totals(self._h, ctypes.byref(t), 1 if reset else 0)
+        return {f: getattr(t, f) for f, _ in LcTotals._fields_}
 
     def call_profile(self):
         """lc_last_call_profile: where the last host call's wall time went."""

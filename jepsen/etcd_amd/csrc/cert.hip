@@ -34,9 +34,11 @@
 // in tests/cert_ref.py and checks it on the oracle's own failing prefixes).
 //
 // One 256-thread workgroup per key of the call (those not invalid leave at
-// once); its arrays live in a workspace of 6 int32 per (record + 2) of the
-// batch.  Only run when the caller asks for certificates: this is a
-// diagnostics pass, not on any timed path.
+// once); its arrays live in a workspace of kCertSlots int32 per (record + 2)
+// of the batch.  Run when the caller asks for certificates and some key can
+// be invalid (a call whose version-order pass decided every key has none:
+// lincheck.cpp, run_certificates); the drop-ins ask for them on every call
+// (dropin_leg in bench.py times it on C5).
 #include <algorithm>
 #include <climits>
 
@@ -48,15 +50,20 @@ namespace lcdev {
 namespace {
 
 constexpr int kCertThreads = 256;
-constexpr int kCertArrays = 6;
+// Workspace per (record + 2) of the batch, in int32 slots: seven int32
+// arrays, two uint64 arrays (two slots each) and the candidate list (int4,
+// four slots); the stride is a multiple of 4 so the wide arrays stay aligned.
+constexpr int kCertSlots = 7 + 2 * 2 + 4;
 constexpr int kFree = INT_MIN;  // no value fixed
 
 struct CertSh {
   int n_mut, m_need, n_gap, n_cand;
   unsigned long long best;  // a stage's lowest (a+1, b+1) pair found
   int pos;                  // a stage's lowest position found
-  int ra, rb;               // ORDER: the two records
-  int wmin[kCertThreads / kWave];
+  int rb;                   // PAIR: the lowest consumer
+  int n_u;                  // HALL: unpinned candidates listed
+  unsigned long long wmin[kCertThreads / kWave];
+  int cnt[kCertThreads];    // HALL: per-thread candidate counts, then their prefix
 };
 
 __device__ __forceinline__ void cert_write(int32_t *c, int kind, int a, int b, int x) {
@@ -64,6 +71,12 @@ __device__ __forceinline__ void cert_write(int32_t *c, int kind, int a, int b, i
   c[1] = a;
   c[2] = b;
   c[3] = x;
+}
+
+__device__ __forceinline__ unsigned long long shfl_down64(unsigned long long v, int o) {
+  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, o);
+  const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), o);
+  return ((unsigned long long)hi << 32) | lo;
 }
 
 __global__ __launch_bounds__(kCertThreads) void cert_kernel(
@@ -87,26 +100,34 @@ __global__ __launch_bounds__(kCertThreads) void cert_kernel(
   const int64_t cut64 = res[key].fail_prefix_end - base;
   const uint32_t cut = cut64 < 0 ? 0u : cut64 >= (int64_t)kNever ? kNever - 1 : (uint32_t)cut64;
   const int V0 = p.init_ver, init = p.init_val;
-  // this key's arrays, positions 0..n+1 (ws_stride int32 per array)
+  // this key's arrays, positions / records 0..n+1 (ws_stride slots per int32 array)
   const int64_t off = rb + 2 * key;
   int *held_rec = ws + off;                  // lowest required mutation pinned at k
   int *held_cnt = ws + ws_stride + off;      // how many; for an open position: its one candidate
   int *claim_rec = ws + 2 * ws_stride + off; // lowest required read of version V0+k with a value
-  uint32_t *lo_call = reinterpret_cast<uint32_t *>(ws + 3 * ws_stride + off);  // max call + 1; then marks
-  uint32_t *uh = reinterpret_cast<uint32_t *>(ws + 4 * ws_stride + off);       // min ret; suffix minimum
-  int *cnt = ws + 5 * ws_stride + off;       // open positions: candidate count
+  int *cnt = ws + 3 * ws_stride + off;       // open positions: candidate count
+  int *mark = ws + 4 * ws_stride + off;      // records: a candidate of some open position
+  int *pin_head = ws + 5 * ws_stride + off;  // positions: pending :ok mutations pinned there (list)
+  int *pin_next = ws + 6 * ws_stride + off;  // records: the next of that list
+  // bounds with the record that sets them: (call + 1) << 32 | r, max; ret << 32 | r, min
+  unsigned long long *lo64 = reinterpret_cast<unsigned long long *>(ws + 7 * ws_stride) + off;
+  unsigned long long *uh64 = reinterpret_cast<unsigned long long *>(ws + 9 * ws_stride) + off;
+  int4 *ulist = reinterpret_cast<int4 *>(ws + 11 * ws_stride) + off;  // HALL: unpinned candidates
+  constexpr unsigned long long kUhNone = ((unsigned long long)kNever << 32) | 0xFFFFFFFFull;
   for (int k = tid; k <= n + 1; k += kCertThreads) {
     held_rec[k] = INT_MAX;
     held_cnt[k] = 0;
     claim_rec[k] = INT_MAX;
-    lo_call[k] = 0;
-    uh[k] = kNever;
     cnt[k] = -1;
+    mark[k] = 0;
+    pin_head[k] = -1;
+    lo64[k] = 0;
+    uh64[k] = kUhNone;
   }
   if (tid == 0) {
-    sh.n_mut = sh.m_need = sh.n_gap = sh.n_cand = 0;
+    sh.n_mut = sh.m_need = sh.n_gap = sh.n_cand = sh.n_u = 0;
     sh.best = ~0ull;
-    sh.pos = sh.ra = sh.rb = INT_MAX;
+    sh.pos = sh.rb = INT_MAX;
     cert_write(c, LC_CERT_NONE, -1, -1, 0);
   }
   __syncthreads();
@@ -138,6 +159,8 @@ __global__ __launch_bounds__(kCertThreads) void cert_kernel(
   for (int r = tid; r < n; r += kCertThreads) {
     const Rec d = rec(r);
     if (!req(d) || d.ver == -1 || d.bad) continue;
+    const unsigned long long lo = ((unsigned long long)(d.call + 1) << 32) | (uint32_t)r;
+    const unsigned long long hi = ((unsigned long long)d.ret << 32) | (uint32_t)r;
     if (is_mut(d)) {
       const int pos = d.ver - V0 - 1;
       if (pos < 0 || pos + 1 > n_mut) {
@@ -146,8 +169,8 @@ __global__ __launch_bounds__(kCertThreads) void cert_kernel(
       }
       atomicAdd(&held_cnt[pos], 1);
       atomicMin(&held_rec[pos], r);
-      atomicMax(&lo_call[pos], d.call + 1);
-      atomicMin(&uh[pos], d.ret);
+      atomicMax(&lo64[pos], lo);
+      atomicMin(&uh64[pos], hi);
       need = max(need, pos + 1);
     } else if (d.f == LC_F_READ) {
       const int k = d.ver - V0;
@@ -156,8 +179,8 @@ __global__ __launch_bounds__(kCertThreads) void cert_kernel(
         continue;
       }
       if (d.val != -1) atomicMin(&claim_rec[k], r);
-      atomicMax(&lo_call[k], d.call + 1);
-      if (k > 0) atomicMin(&uh[k - 1], d.ret);
+      atomicMax(&lo64[k], lo);
+      if (k > 0) atomicMin(&uh64[k - 1], hi);
       need = max(need, k);
     }
   }
@@ -211,52 +234,88 @@ __global__ __launch_bounds__(kCertThreads) void cert_kernel(
     if (tid == 0) cert_write(c, LC_CERT_PAIR, q == 0 ? -1 : held_rec[q - 1], sh.rb, q);
     return;
   }
-  // ORDER: the suffix minimum of the upper bounds, then a lower bound above it
+  // ORDER: the suffix minimum of the upper bounds, then a lower bound above
+  // it; each bound carries the record that sets it (a record
+  // found by matching timestamps could be an unrelated op's)
   const int L = M + 1;  // indices 0..M (reads of the last version bound index M from below)
   {
     const int per = (L + kCertThreads - 1) / kCertThreads;
     const int k0 = min(tid * per, L), k1 = min(k0 + per, L);
-    uint32_t loc = kNever;
-    for (int k = k0; k < k1; k++) loc = umin(loc, uh[k]);
+    unsigned long long loc = kUhNone;
+    for (int k = k0; k < k1; k++) loc = min(loc, uh64[k]);
     const int lane = tid & (kWave - 1), wv = tid / kWave;
-    uint32_t incl = loc;
+    unsigned long long incl = loc;
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_down((int)incl, o);
-      if (lane + o < kWave) incl = umin(incl, y);
+      const unsigned long long y = shfl_down64(incl, o);
+      if (lane + o < kWave) incl = min(incl, y);
     }
-    if (lane == 0) sh.wmin[wv] = (int)incl;
-    uint32_t run = (uint32_t)__shfl_down((int)incl, 1);
-    if (lane == kWave - 1) run = kNever;
+    if (lane == 0) sh.wmin[wv] = incl;
+    unsigned long long run = shfl_down64(incl, 1);
+    if (lane == kWave - 1) run = kUhNone;
     __syncthreads();
-    for (int j = wv + 1; j < kCertThreads / kWave; j++) run = umin(run, (uint32_t)sh.wmin[j]);
+    for (int j = wv + 1; j < kCertThreads / kWave; j++) run = min(run, sh.wmin[j]);
     for (int k = k1 - 1; k >= k0; k--) {
-      run = umin(run, uh[k]);
-      uh[k] = run;
+      run = min(run, uh64[k]);
+      uh64[k] = run;
     }
   }
   __syncthreads();
-  for (int k = tid; k < L; k += kCertThreads)
-    if (lo_call[k] != 0 && lo_call[k] - 1 > uh[k]) atomicMin(&sh.pos, k);
+  for (int k = tid; k < L; k += kCertThreads) {
+    const uint32_t lo = (uint32_t)(lo64[k] >> 32);  // call + 1, 0: none
+    if (lo != 0 && lo - 1 > (uint32_t)(uh64[k] >> 32)) atomicMin(&sh.pos, k);
+  }
   __syncthreads();
   if (sh.pos != INT_MAX) {
     // a: the op whose call is the lower bound, b: the op whose return is the
-    // upper bound (calls and returns are distinct events)
+    // upper bound
     const int j = sh.pos;
-    for (int r = tid; r < n; r += kCertThreads) {
-      const Rec d = rec(r);
-      if (!req(d)) continue;
-      if (d.call + 1 == lo_call[j]) atomicMin(&sh.ra, r);
-      if (d.ret == uh[j]) atomicMin(&sh.rb, r);
-    }
-    __syncthreads();
-    if (tid == 0) cert_write(c, LC_CERT_ORDER, sh.ra, sh.rb, 0);
+    if (tid == 0)
+      cert_write(c, LC_CERT_ORDER, (int)(uint32_t)lo64[j], (int)(uint32_t)uh64[j], 0);
     return;
   }
-  // the open positions (needed, held by no required op) and their candidates
-  uint32_t *mark = lo_call;
-  for (int k = tid; k <= n + 1; k += kCertThreads) mark[k] = 0;
+  // The open positions (needed, held by no required op) and their
+  // candidates: the mutations of P without a version, listed once in call
+  // order (each thread takes a contiguous run of records, their counts
+  // prefix-summed), and the pending :ok mutations pinned to the position
+  // (linked per position).  An open position scans the list only up to its
+  // deadline: O(open positions x candidates called before it) instead of a
+  // pass over every record per position.
+  {
+    const int per = (n + kCertThreads - 1) / kCertThreads;
+    const int r0 = min(tid * per, n), r1 = min(r0 + per, n);
+    int u = 0;
+    for (int r = r0; r < r1; r++) {
+      const Rec d = rec(r);
+      if (!in_p(d) || !is_mut(d) || d.bad) continue;
+      if (d.ver == -1) {
+        u++;
+      } else if (!req(d)) {
+        const int g = d.ver - V0 - 1;
+        if (g >= 0 && g <= n) pin_next[r] = atomicExch(&pin_head[g], r);
+      }
+    }
+    sh.cnt[tid] = u;
+    __syncthreads();
+    if (tid == 0) {
+      int acc = 0;
+      for (int t = 0; t < kCertThreads; t++) {
+        const int x = sh.cnt[t];
+        sh.cnt[t] = acc;
+        acc += x;
+      }
+      sh.n_u = acc;
+    }
+    __syncthreads();
+    int at = sh.cnt[tid];
+    for (int r = r0; r < r1; r++) {
+      const Rec d = rec(r);
+      if (in_p(d) && is_mut(d) && !d.bad && d.ver == -1)
+        ulist[at++] = make_int4((int)d.call, d.val, d.f == LC_F_CAS ? d.exp : kFree, r);
+    }
+  }
   __syncthreads();
+  const int n_u = sh.n_u;
   int n_gap = 0;
   for (int g = tid; g < M; g += kCertThreads) {
     if (held_rec[g] != INT_MAX) continue;
@@ -274,13 +333,20 @@ __global__ __launch_bounds__(kCertThreads) void cert_kernel(
     if (g == 0) before = init;
     else if (held_rec[g - 1] != INT_MAX) before = (int)kops[held_rec[g - 1]].value;
     else if (claim_rec[g] != INT_MAX) before = (int)kops[claim_rec[g]].value;
-    const uint32_t dl = uh[g];
+    const uint32_t dl = (uint32_t)(uh64[g] >> 32);
     int k = 0, one = -1;
-    if (!clash)
-      for (int x = 0; x < n; x++) {
+    if (!clash) {
+      for (int j = 0; j < n_u; j++) {
+        const int4 e = ulist[j];
+        if ((uint32_t)e.x >= dl) break;  // (call order)
+        if (e.z != kFree && before != kFree && e.z != before) continue;
+        if (want != kFree && e.y != want) continue;
+        k++;
+        one = e.w;
+        mark[e.w] = 1;
+      }
+      for (int x = pin_head[g]; x >= 0; x = pin_next[x]) {
         const Rec d = rec(x);
-        if (!in_p(d) || !is_mut(d) || d.bad || (req(d) && d.ver != -1)) continue;
-        if (d.ver != -1 && d.ver - V0 - 1 != g) continue;
         if (d.call >= dl) continue;
         if (d.f == LC_F_CAS && before != kFree && d.exp != before) continue;
         if (want != kFree && d.val != want) continue;
@@ -288,6 +354,7 @@ __global__ __launch_bounds__(kCertThreads) void cert_kernel(
         one = x;
         mark[x] = 1;
       }
+    }
     cnt[g] = k;
     held_cnt[g] = one;
     if (k == 0) atomicMin(&sh.pos, g);
@@ -345,8 +412,13 @@ hipError_t launch_cert_none(int32_t *d_cert, int64_t n_keys, hipStream_t stream)
   return hipGetLastError();
 }
 
+// (the stride, records + 2 per key, rounded up to a multiple of 4)
+static int64_t cert_stride(int64_t n_records, int64_t n_keys) {
+  return (n_records + 2 * n_keys + 2 + 3) & ~int64_t(3);
+}
+
 size_t cert_ws_bytes(int64_t n_records, int64_t n_keys) {
-  return sizeof(int32_t) * (size_t)kCertArrays * (size_t)(n_records + 2 * n_keys + 2);
+  return sizeof(int32_t) * (size_t)kCertSlots * (size_t)cert_stride(n_records, n_keys);
 }
 
 hipError_t launch_certificates(const lc_op *d_ops, const int64_t *d_key_off, int64_t n_keys,
@@ -354,7 +426,7 @@ hipError_t launch_certificates(const lc_op *d_ops, const int64_t *d_key_off, int
                                int32_t *d_ws, int32_t *d_cert, int32_t *d_cset,
                                hipStream_t stream) {
   if (n_keys <= 0) return hipSuccess;
-  const int64_t stride = n_records + 2 * n_keys + 2;
+  const int64_t stride = cert_stride(n_records, n_keys);
   hipLaunchKernelGGL(cert_kernel, dim3((unsigned)n_keys), dim3(kCertThreads), 0, stream, d_ops,
                      d_key_off, p, d_out, d_ws, stride, d_cert, d_cset);
   return hipGetLastError();

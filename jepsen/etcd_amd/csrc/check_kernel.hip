@@ -2531,6 +2531,11 @@ __device__ __forceinline__ void fast_one(const lc_op *__restrict__ ops,
                  o.wit ? o.wit + (beg - key_off[0]) : nullptr, [] {});
 }
 
+// launch_done_signal (kernels.h): the follower of a pass launch.
+__global__ void done_signal_kernel(uint32_t *h_done, uint32_t seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(h_done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
     const lc_op *__restrict__ ops, const int64_t *__restrict__ key_off, int64_t n_keys,
     const KParams p, lc_key_result *__restrict__ out,
@@ -2942,6 +2947,11 @@ hipError_t launch_widen32(const lc_op32 *d_in, const int64_t *d_key_off, const i
   hipLaunchKernelGGL(widen32_kernel, dim3((unsigned)n_keys, gy), dim3(256), 0, stream,
                      reinterpret_cast<const int2 *>(d_in), d_key_off, d_key_base,
                      reinterpret_cast<longlong2 *>(d_out));
+  return hipGetLastError();
+}
+
+hipError_t launch_done_signal(uint32_t *h_done, uint32_t seq, hipStream_t stream) {
+  hipLaunchKernelGGL(done_signal_kernel, dim3(1), dim3(64), 0, stream, h_done, seq);
   return hipGetLastError();
 }
 

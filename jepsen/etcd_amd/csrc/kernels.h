@@ -77,6 +77,12 @@ constexpr int kLdsCap = 128;     // configurations per LDS region (3 regions/wav
 // the launch 0.16 ms.)
 // (A grid-wide "last workgroup" counter instead costs 10k same-address
 // atomics per launch: measured 0.115 -> 0.345 ms.)
+// The follower of a version-order / fused pass launch on the same stream:
+// one thread stores seq to *h_done (host-mapped) once the pass has retired
+// (stream order).  The host spins on that word instead of recording events
+// around the launch and waiting on the second: an empty 1,250-workgroup
+// launch took 10.1 us per step this way against 15.0 (tools/doorbell_probe.hip).
+hipError_t launch_done_signal(uint32_t *h_done, uint32_t seq, hipStream_t stream);
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_flags,

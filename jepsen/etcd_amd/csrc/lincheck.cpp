@@ -178,6 +178,13 @@ struct Dev {
   // certificate pass runs only then
   bool maybe_invalid = true;
   double t_start = 0, t_end = 0;            // lc_call_profile: this thread's span (ms since the call began)
+  // The version-order / fused pass's follower signal (kernels.h
+  // launch_done_signal): a host-mapped word the host spins on instead of
+  // waiting for an event; the pass's HIP-event time is read later
+  // (timing_pending)
+  uint32_t *h_done = nullptr, *h_done_dev = nullptr;
+  uint32_t seq = 0;
+  bool timing_pending = false;
 };
 
 }  // namespace
@@ -196,6 +203,7 @@ struct lc_ctx {
   std::vector<std::pair<const char *, uint64_t>> pinned;
   std::mutex pin_mu;
   lc_call_profile prof{};  // lc_last_call_profile
+  lc_totals totals{};      // lc_last_totals
 };
 
 namespace {
@@ -347,12 +355,54 @@ int64_t settle_status(Dev &d) {
   return n_light;
 }
 
+// A call that returned on the completion signal: its pass's HIP-event time,
+// read once the kernel has retired (now, if it has not yet), into the
+// device's statistics and the context's totals.  Before the events are
+// recorded again, and by lc_last_stats / lc_last_totals.
+void settle_timing(lc_ctx *c, Dev &d) {
+  if (!d.timing_pending) return;
+  d.timing_pending = false;
+  float ms = 0;
+  if (hipEventSynchronize(d.ef) == hipSuccess && hipEventElapsedTime(&ms, d.e0, d.ef) == hipSuccess) {
+    d.fast_ms = ms;
+    d.kernel_ms = ms;
+    c->totals.timed_calls++;
+    c->totals.fast_kernel_ms += ms;
+    c->totals.kernel_ms += ms;
+  }
+}
+
+// Wait for the pass's follower signal (seq in *h_done): spin, checking the
+// stream every 1,024 rounds; past 2 ms (or once the stream is idle, which
+// cannot happen before the word) synchronise the stream instead.  Returns 0,
+// or -EIO on a stream error.
+int wait_done(lc_ctx *c, Dev &d, uint32_t seq, hipStream_t st) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1;; i++) {
+    if (__atomic_load_n(d.h_done, __ATOMIC_ACQUIRE) == seq) return 0;
+    if ((i & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) return 0;
+      if (q != hipErrorNotReady) {
+        set_err(c, std::string("fast tier: ") + hipGetErrorString(q));
+        return -EIO;
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+        HIP_TRY(c, hipStreamSynchronize(st));
+        return 0;
+      }
+    }
+  }
+}
+
 // Run the tiers for n_keys keys whose device arrays are in place.
 int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                int64_t n_keys, const lcdev::KParams &p,
                lc_key_result *d_out, hipStream_t st, int64_t flags,
                const WitOut &wo = WitOut()) {
   (void)settle_status(d);  // before use_fused or h_status is read
+  settle_timing(c, d);     // before e0 / ef are recorded again
+  c->totals.calls++;
   d.kernel_ms = d.hbm_ms = d.fast_ms = d.jit_ms = d.gap_ms = 0;
   d.n_hbm = d.n_jit = d.n_gap = 0;
   d.malformed = 0;
@@ -474,6 +524,11 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   // initialisation (the version order is the witness of every key the fast
   // tier decides) and tier 0, the version-order decision (or the fused
   // pass); the keys it cannot decide are flagged for the later tiers
+  // A call with one pass launch (no chunks) returns on the pass's follower
+  // signal (kernels.h launch_done_signal) instead of an event wait; with
+  // LC_FLAG_NO_TIMING it records no events around the pass either.
+  const bool signal = !wo.chunks && fast_on && n_keys > 0;
+  const bool timing = !signal || !(flags & LC_FLAG_NO_TIMING);
   auto first_pass = [&](int64_t k0, int64_t nk, int64_t r0, int64_t nrec) -> int {
     const lc_op *o = d_ops + r0;
     const int64_t *off = d_off + k0;
@@ -490,7 +545,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                                          d.h_handoff_dev, st));
     return 0;
   };
-  HIP_TRY(c, hipEventRecord(d.e0, st));
+  if (timing) HIP_TRY(c, hipEventRecord(d.e0, st));
   if (const Chunks *ch = wo.chunks) {
     // lc_check's pipeline: chunk i's copy is issued, the compute stream
     // waits for it, widens it (24-byte records) and decides its keys while
@@ -511,13 +566,29 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     return e;
   }
   if (fast_on) {
-    HIP_TRY(c, hipEventRecord(d.ef, st));
-    HIP_TRY(c, hipEventSynchronize(d.ef));
-    HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.ef));
-    d.fast_ms = ms;
+    if (timing) HIP_TRY(c, hipEventRecord(d.ef, st));
+    if (signal) {
+      HIP_TRY(c, lcdev::launch_done_signal(d.h_done_dev, ++d.seq, st));
+      if (int e = wait_done(c, d, d.seq, st)) return e;
+    } else {
+      HIP_TRY(c, hipEventSynchronize(d.ef));
+    }
     n_jit = 0;
     jit_list = d.d_jit;
     const bool handed = __atomic_load_n(d.h_handoff, __ATOMIC_ACQUIRE) != 0;
+    if (signal && !handed) {
+      // every key decided: the pass's event time (if any) is read later
+      d.timing_pending = timing;
+    } else {
+      if (!timing) {
+        // the later tiers' times are measured from here (the pass untimed)
+        HIP_TRY(c, hipEventRecord(d.e0, st));
+        HIP_TRY(c, hipEventRecord(d.ef, st));
+      }
+      HIP_TRY(c, hipEventSynchronize(d.ef));
+      HIP_TRY(c, hipEventElapsedTime(&ms, d.e0, d.ef));
+      d.fast_ms = ms;
+    }
     if (!handed) {
       d.flags_dirty = false;  // no key raised its flag
       // the version-order tier and the fused pass decide valid keys only
@@ -599,6 +670,11 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   }
   if (n_jit == 0 && n_direct == 0) {
     d.kernel_ms = d.fast_ms + d.gap_ms;
+    if (!d.timing_pending && timing) {
+      c->totals.timed_calls++;
+      c->totals.fast_kernel_ms += d.fast_ms;
+      c->totals.kernel_ms += d.kernel_ms;
+    }
     // after a handoff d_status is not zero: cleared behind this call's work
     // (the host has read it), not in front of the next call's
     if (light) HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
@@ -783,6 +859,11 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
   HIP_TRY(c, hipStreamSynchronize(st));
   d.status_dirty = false;
+  if (timing) {
+    c->totals.timed_calls++;
+    c->totals.fast_kernel_ms += d.fast_ms;
+  }
+  c->totals.kernel_ms += d.kernel_ms + d.hbm_ms;
   return 0;
 }
 
@@ -1421,7 +1502,10 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
           hipHostMalloc(reinterpret_cast<void **>(&d.h_status), sizeof(lcdev::KStatus), 0) != hipSuccess ||
           hipHostMalloc(reinterpret_cast<void **>(&d.h_handoff), 2 * sizeof(int32_t),
                         hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-          hipHostGetDevicePointer(reinterpret_cast<void **>(&d.h_handoff_dev), d.h_handoff, 0) != hipSuccess) {
+          hipHostGetDevicePointer(reinterpret_cast<void **>(&d.h_handoff_dev), d.h_handoff, 0) != hipSuccess ||
+          hipHostMalloc(reinterpret_cast<void **>(&d.h_done), 64,
+                        hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+          hipHostGetDevicePointer(reinterpret_cast<void **>(&d.h_done_dev), d.h_done, 0) != hipSuccess) {
         c->devs.push_back(d);  // lc_close frees what was created
         lc_close(c);
         return -ENODEV;
@@ -1455,6 +1539,7 @@ void lc_close(lc_ctx *c) {
     if (d.d_status) (void)hipFree(d.d_status);
     if (d.h_status) (void)hipHostFree(d.h_status);
     if (d.h_handoff) (void)hipHostFree(d.h_handoff);
+    if (d.h_done) (void)hipHostFree(d.h_done);
     if (d.e0) (void)hipEventDestroy(d.e0);
     if (d.e1) (void)hipEventDestroy(d.e1);
     if (d.e2) (void)hipEventDestroy(d.e2);
@@ -1489,12 +1574,27 @@ const char *lc_last_error(lc_ctx *c) { return c ? c->err.c_str() : "null context
 
 int lc_last_stats(lc_ctx *c, lc_stats *out) {
   if (!c || !out) return -EINVAL;
+  // a call that returned on the completion signal: its pass's event time
+  // (single-device calls only take that path)
+  if (c->devs[0].timing_pending) {
+    settle_timing(c, c->devs[0]);
+    c->stats.fast_kernel_ms = c->devs[0].fast_ms;
+    c->stats.kernel_ms = c->devs[0].kernel_ms;
+  }
   // the keys the crash-light decision took in a fused call, copied lazily
   for (Dev &d : c->devs) {
     const int64_t n = settle_status(d);
     if (n > 0) c->stats.n_gap_keys += n;
   }
   *out = c->stats;
+  return 0;
+}
+
+int lc_last_totals(lc_ctx *c, lc_totals *out, int32_t reset) {
+  if (!c || !out) return -EINVAL;
+  for (Dev &d : c->devs) settle_timing(c, d);
+  *out = c->totals;
+  if (reset) c->totals = lc_totals{};
   return 0;
 }
 

@@ -25,25 +25,29 @@ def main():
     with abi.Context(device_mask=1) as ctx:
         for nk in (1, 1250, 2500, 5000, 10000):
             out = torch.zeros(nk * abi.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-            st = abi.LcStats()
-            step = ctx.bind_check_device(d_ops.data_ptr(), d_off.data_ptr(), nk, out.data_ptr(),
-                                         stream=stream.cuda_stream, opts=abi.default_opts(), stats=st)
-            for _ in range(20):
-                step()
-            torch.cuda.synchronize()
-            wall, call, kern = [], [], []
-            t_all = time.perf_counter()
-            for _ in range(steps):
-                t0 = time.perf_counter()
-                step()
-                wall.append((time.perf_counter() - t0) * 1e6)
-                call.append(st.total_ms * 1e3)
-                kern.append(st.fast_kernel_ms * 1e3)
-            t_all = (time.perf_counter() - t_all) * 1e6 / steps
-            print(json.dumps({"keys": nk, "us_per_step": round(t_all, 2),
-                              "wall_us_med": round(float(np.median(wall)), 2),
-                              "c_call_us_med": round(float(np.median(call)), 2),
-                              "kernel_us_med": round(float(np.median(kern)), 2)}), flush=True)
+            for every in (1, 4, 0):  # timed steps: every step, every 4th, none
+                fl = [0, abi.LC_FLAG_NO_TIMING]
+                steps_ = [ctx.bind_check_device(d_ops.data_ptr(), d_off.data_ptr(), nk, out.data_ptr(),
+                                                stream=stream.cuda_stream, opts=abi.default_opts(flags=f))
+                          for f in fl]
+                pick = (lambda i: 0 if i % every == 0 else 1) if every else (lambda i: 1)
+                for i in range(20):
+                    steps_[pick(i)]()
+                torch.cuda.synchronize()
+                ctx.totals(reset=True)
+                wall = []
+                t_all = time.perf_counter()
+                for i in range(steps):
+                    t0 = time.perf_counter()
+                    steps_[pick(i)]()
+                    wall.append((time.perf_counter() - t0) * 1e6)
+                t_all = (time.perf_counter() - t_all) * 1e6 / steps
+                tot = ctx.totals(reset=True)
+                print(json.dumps({"keys": nk, "timed_every": every, "us_per_step": round(t_all, 2),
+                                  "wall_us_med": round(float(np.median(wall)), 2),
+                                  "kernel_us_mean": round(tot["fast_kernel_ms"] * 1e3 /
+                                                          max(1, tot["timed_calls"]), 2)}),
+                      flush=True)
 
 
 if __name__ == "__main__":
