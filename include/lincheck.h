@@ -221,8 +221,23 @@ typedef struct lc_aux {
  *                    records]: each needed by a required op and held by none,
  *                    and fewer ops of P can hold any of them than c (Hall's
  *                    condition fails for the gap matching).
+ *   LC_CERT_PROOF    (ABI 4) c tokens in certificate_set[0 .. c): a case
+ *                    analysis over who holds the open positions (needed, no
+ *                    required holder), for infeasibility only the gap
+ *                    matching's branching finds.  token = kind << 30 | a << 15
+ *                    | b: FORCE (1) — position a has exactly one op able to
+ *                    hold it under the choices so far, op b, which then holds
+ *                    it; BRANCH (2) — position a has exactly b such ops, and b
+ *                    sub-proofs follow, one per op in record order, each
+ *                    assuming that op holds a; EMPTY (3) — no op can hold
+ *                    position a.  A proof is FORCE* then BRANCH or EMPTY.
+ *                    "Able" is HALL's list of conditions, plus: an op chosen
+ *                    at a+1 that is a CAS fixes the value a's holder writes,
+ *                    one chosen at a-1 the value a CAS at a expects, and a
+ *                    chosen op holds no other position.  Keys and positions
+ *                    below 2^15.
  * LC_CERT_NONE: no certificate (valid or :unknown keys, keys only a search
- * decided where none of these applies).  oracle/witness.c checks them from
+ * decided where none of these applies).  oracle/cert.c checks them from
  * the records alone (tests/).
  */
 #define LC_CERT_NONE    0
@@ -232,6 +247,7 @@ typedef struct lc_aux {
 #define LC_CERT_PAIR    4
 #define LC_CERT_ORDER   5
 #define LC_CERT_HALL    6
+#define LC_CERT_PROOF   7
 
 typedef struct lc_ctx lc_ctx;
 

@@ -43,7 +43,7 @@ LC_FLAG_WHOLE_GPU = 8
 LC_FLAG_NO_TIMING = 16
 LC_WITNESS_NONE, LC_WITNESS_FULL, LC_WITNESS_PREFIX = 0, 1, 2
 LC_CERT_NONE, LC_CERT_DUP, LC_CERT_UNREACH, LC_CERT_CLAIMS, LC_CERT_PAIR, LC_CERT_ORDER, \
-    LC_CERT_HALL = range(7)
+    LC_CERT_HALL, LC_CERT_PROOF = range(8)
 
 # lc_op: 6 x int64 (f, value, expected, version, call, ret); arrays are (n, 6).
 # lc_op32 (ABI 4): the same fields as 6 x 32 bits, arrays (n, 6) int32 with

@@ -45,7 +45,8 @@ UNKNOWN = "unknown"
 # crashed ops (the frontier of a version-pinned key grows with its crashed ops
 # only)
 FRONTIER_MAX_CRASHED = 16
-CERT_KINDS = {0: "none", 1: "dup", 2: "unreach", 3: "claims", 4: "pair", 5: "order", 6: "hall"}
+CERT_KINDS = {0: "none", 1: "dup", 2: "unreach", 3: "claims", 4: "pair", 5: "order", 6: "hall",
+              7: "proof"}
 
 
 class VersionedRegister:
@@ -176,6 +177,10 @@ class RegisterChecker:
                 elif ck == "hall":
                     out["certificate"]["positions"] = [
                         int(x) for x in cset[key_off[i]:key_off[i] + int(cert[i][3])]]
+                elif ck == "proof":  # the case splits: (position, cases) in preorder
+                    out["certificate"]["splits"] = [
+                        ((int(x) & 0xFFFFFFFF) >> 15 & 0x7FFF, int(x) & 0x7FFF)
+                        for x in cset[key_off[i]:key_off[i] + int(cert[i][3])]]
                 recs = ops[key_off[i]:key_off[i + 1]]
                 witnessed = m.name == "versioned-register" and kind[i] == abi.LC_WITNESS_PREFIX
                 # knossos's :configs are its search's frontier just before the

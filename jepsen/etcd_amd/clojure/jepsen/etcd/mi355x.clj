@@ -404,7 +404,7 @@
       (read-configs buf 0 (.getInt cnt 0))
       {:configs-error (if (number? rc) [:lc-fx-frontier rc] (str rc))})))
 
-(def ^:private cert-kinds {0 :none 1 :dup 2 :unreach 3 :claims 4 :pair 5 :order 6 :hall})
+(def ^:private cert-kinds {0 :none 1 :dup 2 :unreach 3 :claims 4 :pair 5 :order 6 :hall 7 :proof})
 
 ;; an invalid key the batched device search could not take gets :configs from
 ;; the frontier exchange alone when the frontier search decided it, or the
@@ -484,7 +484,13 @@
                                               (assoc :ops (vec (keep rec [(aget c 1) (aget c 2)])))
                                               (= kd :hall)
                                               (assoc :positions
-                                                     (vec (.getIntArray cset (* 4 k0) (aget c 3))))))}
+                                                     (vec (.getIntArray cset (* 4 k0) (aget c 3))))
+                                              ;; the case splits, [position cases] in preorder
+                                              (= kd :proof)
+                                              (assoc :splits
+                                                     (mapv (fn [t] [(bit-and (bit-shift-right t 15) 0x7FFF)
+                                                                    (bit-and t 0x7FFF)])
+                                                           (.getIntArray cset (* 4 k0) (aget c 3))))))}
                                          (let [wa (when witness
                                                     (witness-analysis d fail-op fail-at witness
                                                                       [0 nil]))

@@ -389,12 +389,189 @@ __global__ __launch_bounds__(kCertThreads) void cert_kernel(
   for (int x = tid; x < n; x += kCertThreads) u += mark[x] != 0;
   atomicAdd(&sh.n_cand, u);
   __syncthreads();
-  if (sh.n_gap > sh.n_cand && tid == 0) {
-    int i = 0;
-    for (int g = 0; g < M; g++)
-      if (held_rec[g] == INT_MAX) ks[i++] = g;
-    cert_write(c, LC_CERT_HALL, -1, -1, i);
+  if (sh.n_gap > sh.n_cand) {
+    if (tid == 0) {
+      int i = 0;
+      for (int g = 0; g < M; g++)
+        if (held_rec[g] == INT_MAX) ks[i++] = g;
+      cert_write(c, LC_CERT_HALL, -1, -1, i);
+    }
+    return;
   }
+  // Infeasibility only a search finds: a PROOF — its case splits; the
+  // forced choices between them and the empty positions that close each
+  // case are re-derived by the checker's propagation (tests/cert_ref.py
+  // prove, oracle/cert.c proof_ok) — searched by wave 0 (the other waves
+  // are done).
+  if (tid >= kWave) return;
+  // the arrays free by now: the open positions' list (cnt), the assumed
+  // holder per position (held_cnt), the assumed ops (mark), the log of
+  // assumed positions and the case-split frames (lo64's slots)
+  int *glist = cnt, *asg = held_cnt, *used = mark;
+  int *logp = reinterpret_cast<int *>(lo64);
+  int4 *frames = reinterpret_cast<int4 *>(logp + ((n + 2 + 3) & ~3));
+  const int n_frames = (n + 2) / 4;
+  int ng = 0;  // the open positions, in order
+  for (int g = 0; g < M; g++)
+    if (held_rec[g] == INT_MAX) {
+      if (tid == 0) glist[ng] = g;
+      ng++;
+    }
+  for (int k = tid; k <= n + 1; k += kWave) {
+    asg[k] = -1;
+    used[k] = 0;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (ng < 1 || n > 0x7FFF || M > 0x7FFF) return;
+  // candidates of open position g under the assumptions: their count and
+  // the lowest record index above `after` (one lane, sequential)
+  long long work = 0;
+  auto cands = [&](int g, int after, int *first) -> int {
+    int want = kFree, before = kFree;
+    if (held_rec[g + 1] != INT_MAX && kops[held_rec[g + 1]].f == LC_F_CAS)
+      want = (int)kops[held_rec[g + 1]].expected;
+    if (claim_rec[g + 1] != INT_MAX) {
+      const int v = (int)kops[claim_rec[g + 1]].value;
+      if (want != kFree && want != v) return 0;
+      want = v;
+    }
+    if (g + 1 < M && asg[g + 1] >= 0 && kops[asg[g + 1]].f == LC_F_CAS) {
+      const int v = (int)kops[asg[g + 1]].expected;
+      if (want != kFree && want != v) return 0;
+      want = v;
+    }
+    if (g == 0) before = init;
+    else if (held_rec[g - 1] != INT_MAX) before = (int)kops[held_rec[g - 1]].value;
+    else if (claim_rec[g] != INT_MAX) before = (int)kops[claim_rec[g]].value;
+    else if (asg[g - 1] >= 0) before = (int)kops[asg[g - 1]].value;
+    const uint32_t dl = (uint32_t)(uh64[g] >> 32);
+    int k = 0, lo = INT_MAX;
+    for (int j = 0; j < n_u; j++) {
+      const int4 e = ulist[j];
+      if ((uint32_t)e.x >= dl) break;
+      work++;
+      if (used[e.w] || e.w <= after) continue;
+      if (e.z != kFree && before != kFree && e.z != before) continue;
+      if (want != kFree && e.y != want) continue;
+      k++;
+      lo = min(lo, e.w);
+    }
+    for (int x = pin_head[g]; x >= 0; x = pin_next[x]) {
+      work++;
+      if (used[x] || x <= after) continue;
+      const lc_op &y = kops[x];
+      if ((uint32_t)(y.call - base) >= dl) continue;
+      if (y.f == LC_F_CAS && before != kFree && (int)y.expected != before) continue;
+      if (want != kFree && (int)y.value != want) continue;
+      k++;
+      lo = min(lo, x);
+    }
+    *first = lo;
+    return k;
+  };
+  auto token = [](int kind, int a, int b) { return (int32_t)(((uint32_t)kind << 30) | ((uint32_t)a << 15) | (uint32_t)b); };
+  auto assign = [&](int g, int x, int &nlog) {  // (lane 0 writes; all lanes keep the counts)
+    if (tid == 0) {
+      asg[g] = x;
+      used[x] = 1;
+      logp[nlog] = g;
+    }
+    nlog++;
+  };
+  auto sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  constexpr int kNodes = 2048;                       // as tests/cert_ref.py PROOF_NODES
+  constexpr long long kWork = 1ll << 22;             // candidate checks per lane
+  // frames of the open case splits: (position, cases << 16 | case index,
+  // log length before the split's own assumption, the op assumed in the
+  // current case)
+  int T = 0, nlog = 0, sp = 0, nodes = 0;
+  bool ok = false;
+  for (;;) {
+    // at the current assumptions: an open position with no candidate (the
+    // lowest), else one with one (the lowest), else the fewest
+    if (++nodes > kNodes) break;
+    int best_e = INT_MAX, best_f = INT_MAX, best_fx = -1, best_b = INT_MAX, best_bk = INT_MAX;
+    int any = 0;
+    for (int i = tid; i < ng; i += kWave) {
+      const int g = glist[i];
+      if (asg[g] >= 0) continue;
+      any = 1;
+      int f;
+      const int k = cands(g, -1, &f);
+      if (k == 0) best_e = min(best_e, g);
+      else if (k == 1 && g < best_f) best_f = g, best_fx = f;
+      else if (k < best_bk || (k == best_bk && g < best_b)) best_bk = k, best_b = g;
+    }
+    if (__ballot(work > kWork)) break;
+    if (!__ballot(any)) break;  // every open position held: no contradiction here
+    const int e = wave_min_i32(best_e);
+    if (e != INT_MAX) {
+      // this case is closed (the checker re-derives that: no token): back to
+      // the innermost split with a case left
+      bool resumed = false;
+      while (sp > 0) {
+        const int4 fr = frames[sp - 1];
+        // undo the assumptions made inside the case, then the case's own
+        while (nlog > fr.z) {
+          nlog--;
+          if (tid == 0) {
+            const int g = logp[nlog];
+            used[asg[g]] = 0;
+            asg[g] = -1;
+          }
+        }
+        sync();
+        const int k = fr.y >> 16, i = fr.y & 0xFFFF;
+        if (i + 1 < k) {
+          // the next case: the lowest candidate above the one just closed
+          int x = INT_MAX;
+          if (tid == 0) cands(fr.x, fr.w, &x);
+          x = uni(x);
+          if (x == INT_MAX) break;  // (cannot happen: the split counted its cases)
+          if (tid == 0) frames[sp - 1] = make_int4(fr.x, (k << 16) | (i + 1), fr.z, x);
+          assign(fr.x, x, nlog);
+          sync();
+          resumed = true;
+          break;
+        }
+        sp--;  // every case of this split closed: the case around it is too
+      }
+      if (resumed) continue;
+      ok = sp == 0;
+      break;
+    }
+    const int f = wave_min_i32(best_f);
+    if (f != INT_MAX) {
+      // forced (the checker re-derives it: no token)
+      const int x = uni(__shfl(best_fx, __builtin_ctzll(__ballot(best_f == f))));
+      assign(f, x, nlog);
+      sync();
+      continue;
+    }
+    // a case split at the position with the fewest candidates (the lowest
+    // position among equals), its first case the lowest candidate
+    const int bk = wave_min_i32(best_bk);
+    const int b = wave_min_i32(best_bk == bk ? best_b : INT_MAX);
+    if (sp >= n_frames || bk > 0x7FFF || T >= n) break;
+    int x = INT_MAX;
+    if (tid == 0) cands(b, -1, &x);
+    x = uni(x);
+    if (tid == 0) {
+      ks[T] = token(2, b, bk);
+      frames[sp] = make_int4(b, bk << 16, nlog, x);
+    }
+    T++;
+    sp++;
+    assign(b, x, nlog);
+    sync();
+  }
+  if (ok && tid == 0) cert_write(c, LC_CERT_PROOF, -1, -1, T);
 }
 
 __global__ __launch_bounds__(256) void cert_none_kernel(int32_t *__restrict__ cert, int64_t n_keys) {

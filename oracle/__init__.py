@@ -131,7 +131,8 @@ def check_witness(ops, key_off, witness, kind, results=None, init_version=0, ini
 
 
 CERT_OK, CERT_NONE, CERT_BAD = 1, 0, -1
-CERT_KINDS = {0: "none", 1: "dup", 2: "unreach", 3: "claims", 4: "pair", 5: "order", 6: "hall"}
+CERT_KINDS = {0: "none", 1: "dup", 2: "unreach", 3: "claims", 4: "pair", 5: "order", 6: "hall",
+              7: "proof"}
 
 
 def check_certificate(ops, key_off, cert, cert_set, results, init_version=0, init_value=-1,

@@ -32,6 +32,15 @@
  *            before a was called.
  *   HALL     c needed positions no required op holds, fewer ops of P able
  *            to hold any of them (the necessary conditions below) than c.
+ *   PROOF    a case analysis over who holds the open positions: the case
+ *            splits a search needed (every op able to hold a position, one
+ *            case each), the forced choices in between re-derived here by
+ *            propagation (a position exactly one op can hold), each case
+ *            ending at a position no remaining op can hold — "able" under
+ *            the choices made so far (an op assumed next to a position
+ *            fixes the value it writes or expects; an assumed op holds
+ *            nothing else).  Sound because each position needed and held by
+ *            no required op is held by one of its candidates.
  *
  * "Able to hold position p" (cand) is a set of NECESSARY conditions on the
  * op x that holds a needed position p no required op holds: x is a mutation
@@ -90,10 +99,21 @@ static int64_t value_before(const pfx_t *P, int64_t p, int *det) {
   return 0;
 }
 
+/* Assumptions of a PROOF certificate: asg[p] = the op assumed to hold open
+ * position p (-1: none), used[x] = op x holds some assumed position. */
+typedef struct {
+  int64_t *asg;          /* M entries */
+  unsigned char *used;   /* n entries */
+} assume_t;
+
 /* cand(p), for a needed position no required op holds: the number of ops
  * able to hold it; *one = the op when there is exactly one; mark[x] set for
- * each (may be NULL). */
-static int64_t cand(const pfx_t *P, int64_t p, int64_t *one, unsigned char *mark) {
+ * each (may be NULL); list[] the ops in record order (may be NULL).  Under
+ * assumptions A (may be NULL): an op assumed at p+1 that is a CAS fixes the
+ * value p must write, one assumed at p-1 the value before p, and an op
+ * assumed anywhere holds nothing else. */
+static int64_t cand_a(const pfx_t *P, int64_t p, int64_t *one, unsigned char *mark,
+                      const assume_t *A, int64_t *list) {
   const lc_op *o = P->o;
   /* deadline: returns of the required ops whose points follow t_p */
   int64_t dl = LC_INF;
@@ -105,7 +125,11 @@ static int64_t cand(const pfx_t *P, int64_t p, int64_t *one, unsigned char *mark
       if (y->ret < dl) dl = y->ret;
   }
   int det;
-  const int64_t before = value_before(P, p, &det);
+  int64_t before = value_before(P, p, &det);
+  if (A && !det && p >= 1 && A->asg[p - 1] >= 0) {
+    det = 1;
+    before = o[A->asg[p - 1]].value;
+  }
   /* the value the holder of p must write: claimed by the required reads of
    * version V0+p+1, expected by a required CAS at p+1 (two different: none) */
   int has_want = 0, clash = 0;
@@ -125,6 +149,12 @@ static int64_t cand(const pfx_t *P, int64_t p, int64_t *one, unsigned char *mark
     has_want = 1;
     want = v;
   }
+  if (A && p + 1 < P->M && A->asg[p + 1] >= 0 && o[A->asg[p + 1]].f == LC_F_CAS) {
+    const int64_t v = o[A->asg[p + 1]].expected;
+    if (has_want && v != want) clash = 1;
+    has_want = 1;
+    want = v;
+  }
   if (clash) return 0;
   int64_t cnt = 0;
   for (int64_t j = 0; j < P->n; j++) {
@@ -134,11 +164,17 @@ static int64_t cand(const pfx_t *P, int64_t p, int64_t *one, unsigned char *mark
     if (x->call >= dl) continue;
     if (x->f == LC_F_CAS && det && x->expected != before) continue;
     if (has_want && x->value != want) continue;
+    if (A && A->used[j]) continue;
     if (mark) mark[j] = 1;
     if (one) *one = j;
+    if (list) list[cnt] = j;
     cnt++;
   }
   return cnt;
+}
+
+static int64_t cand(const pfx_t *P, int64_t p, int64_t *one, unsigned char *mark) {
+  return cand_a(P, p, one, mark, NULL, NULL);
 }
 
 /* Position p is needed by a required op and held by none. */
@@ -154,6 +190,71 @@ static int forced_at(const pfx_t *P, int64_t i, int64_t p) {
   if (!open_gap(P, p)) return 0;
   int64_t one = -1;
   return cand(P, p, &one, NULL) == 1 && one == i;
+}
+
+/* A PROOF certificate's proof, from token *at on (include/lincheck.h
+ * LC_CERT_PROOF).  Forced choices are derived, not listed: the open
+ * positions are propagated — a position no op can hold under the choices so
+ * far closes the case; else the lowest position exactly one op can hold is
+ * assumed held by it, and again — and only where propagation stops does the
+ * next token name a case split, BRANCH(g, k): g open and unassigned with
+ * exactly k >= 2 candidates, whose k sub-proofs follow, one per candidate in
+ * record order, each assuming it holds g.  (As a SAT proof checker's unit
+ * propagation: deterministic deduction, no search.)  Every assumption is
+ * undone before returning.  1: the (sub)proof holds. */
+static int proof_ok(const pfx_t *P, const int32_t *tok, int64_t len, int64_t *at, assume_t *A,
+                    int64_t *scratch, int depth) {
+  if (depth > 64) return 0;
+  int64_t *forced = scratch + (int64_t)depth * 2 * (P->n + 2);  /* this level's assumptions */
+  int64_t *list = forced + (P->n + 2);
+  int64_t nf = 0;
+  int ok = 0;
+  for (;;) {
+    /* propagate: an empty position closes the case; else the lowest forced */
+    int64_t fp = -1, fo = -1, empty = 0;
+    for (int64_t p = 0; p < P->M; p++) {
+      if (A->asg[p] >= 0 || !open_gap(P, p)) continue;
+      int64_t one = -1;
+      const int64_t k = cand_a(P, p, &one, NULL, A, NULL);
+      if (k == 0) {
+        empty = 1;
+        break;
+      }
+      if (k == 1 && fp < 0) fp = p, fo = one;
+    }
+    if (empty) {
+      ok = 1;
+      break;
+    }
+    if (fp >= 0) {
+      A->asg[fp] = fo;
+      A->used[fo] = 1;
+      forced[nf++] = fp;
+      continue;
+    }
+    /* a case split, named by the next token */
+    if (*at >= len) break;
+    const uint32_t t = (uint32_t)tok[(*at)++];
+    const int64_t g = (t >> 15) & 0x7FFF, k = t & 0x7FFF;
+    if ((t >> 30) != 2 || !open_gap(P, g) || A->asg[g] >= 0 || k < 2) break;
+    if (cand_a(P, g, NULL, NULL, A, list) != k) break;
+    ok = 1;
+    for (int64_t i = 0; i < k && ok; i++) {
+      const int64_t x = list[i];
+      A->asg[g] = x;
+      A->used[x] = 1;
+      ok = proof_ok(P, tok, len, at, A, scratch, depth + 1);
+      A->asg[g] = -1;
+      A->used[x] = 0;
+    }
+    break;
+  }
+  while (nf > 0) {
+    const int64_t p = forced[--nf];
+    A->used[A->asg[p]] = 0;
+    A->asg[p] = -1;
+  }
+  return ok;
 }
 
 static int check_cert(const lc_op *o, int64_t n, const int32_t *c, const int32_t *cset,
@@ -250,6 +351,29 @@ static int check_cert(const lc_op *o, int64_t n, const int32_t *c, const int32_t
       free(mark);
       free(seen);
       if (good && u < cnt) return ORACLE_CERT_OK;
+      break;
+    }
+    case LC_CERT_PROOF: {
+      const int64_t len = c[3];
+      if (len < 0 || len > n || !cset || P.M < 1) break;
+      int64_t *asg = (int64_t *)malloc(sizeof(int64_t) * (size_t)P.M);
+      unsigned char *used = (unsigned char *)calloc((size_t)n, 1);
+      int64_t *scratch = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n + 2) * 2 * 66);
+      if (!asg || !used || !scratch) {
+        free(asg);
+        free(used);
+        free(scratch);
+        return -ENOMEM;
+      }
+      for (int64_t p = 0; p < P.M; p++) asg[p] = -1;
+      assume_t A = {asg, used};
+      int64_t at = 0;
+      /* the whole proof, and nothing after it */
+      const int ok = proof_ok(&P, cset, len, &at, &A, scratch, 0) && at == len;
+      free(asg);
+      free(used);
+      free(scratch);
+      if (ok) return ORACLE_CERT_OK;
       break;
     }
     default:

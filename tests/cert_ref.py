@@ -10,10 +10,24 @@ find(recs, cut) -> (kind, a, b, c, positions)."""
 INF = (1 << 63) - 1
 NIL = -1
 R, W, C = 0, 1, 2
-NONE, DUP, UNREACH, CLAIMS, PAIR, ORDER, HALL = range(7)
+NONE, DUP, UNREACH, CLAIMS, PAIR, ORDER, HALL, PROOF = range(8)
+# PROOF tokens (include/lincheck.h LC_CERT_PROOF): kind << 30 | a << 15 | b
+FORCE, BRANCH, EMPTY = 1, 2, 3
+PROOF_NODES = 2048  # search budget (the device finder's, cert.hip)
 
 
-def find(recs, cut, v0=0, init=-1):
+def tok(kind, a, b=0):
+    """One proof token as the int32 the certificate set holds."""
+    x = (kind << 30) | (a << 15) | b
+    return x - (1 << 32) if x >= (1 << 31) else x
+
+
+def untok(t):
+    t &= 0xFFFFFFFF
+    return t >> 30, (t >> 15) & 0x7FFF, t & 0x7FFF
+
+
+def find(recs, cut, v0=0, init=-1, proof=True):
     n = len(recs)
     inp = [r[4] <= cut for r in recs]
     req = [inp[i] and recs[i][5] <= cut for i in range(n)]
@@ -137,4 +151,91 @@ def find(recs, cut, v0=0, init=-1):
         union.update(cands[p])
     if len(union) < len(gaps):
         return (HALL, -1, -1, len(gaps), gaps)
+    # Infeasibility that only a search finds (a choice at one open position
+    # fixes the value or uses the op another one needs): a proof by forced
+    # choices and case splits over the candidates (LC_CERT_PROOF), as the
+    # device's finder searches for it (cert.hip, prove)
+    toks = prove(recs, gaps, held, claim, inp, req, mut, pin, pos, v0, init) if proof else None
+    if toks is not None and len(toks) <= n and max(gaps) < 1 << 15 and n <= 1 << 15:
+        return (PROOF, -1, -1, len(toks), toks)
     return (NONE, -1, -1, 0, [])
+
+
+def prove(recs, gaps, held, claim, inp, req, mut, pin, pos, v0, init, budget=PROOF_NODES):
+    """The proof's tokens — one BRANCH(position, cases) per case split, in
+    preorder — or None (a complete consistent assignment exists, or the
+    search ran over its budget).  Between splits the open positions are
+    propagated (the checker re-derives this): a position with no candidate
+    closes the case, else the lowest one with exactly one is assumed held by
+    it; a split is taken at the open position with the fewest candidates
+    (the lowest among equals), its cases in increasing record order."""
+    n = len(recs)
+    dl, base_before, base_wants, S = {}, {}, {}, {}
+    for p in gaps:
+        d = INF
+        for i in range(n):
+            if req[i] and ((pin[i] and pos[i] > p) or (recs[i][0] == R and recs[i][3] != NIL and
+                                                        recs[i][3] - v0 - 1 >= p)):
+                d = min(d, recs[i][5])
+        dl[p] = d
+        if p == 0:
+            base_before[p] = (True, init)
+        elif p - 1 in held:
+            base_before[p] = (True, recs[held[p - 1]][1])
+        elif p in claim:
+            base_before[p] = (True, recs[claim[p]][1])
+        else:
+            base_before[p] = (False, None)
+        w = set()
+        if p + 1 in claim:
+            w.add(recs[claim[p + 1]][1])
+        if p + 1 in held and recs[held[p + 1]][0] == C:
+            w.add(recs[held[p + 1]][2])
+        base_wants[p] = w
+        S[p] = [x for x in range(n) if inp[x] and mut[x] and not (req[x] and pin[x]) and
+                (not pin[x] or pos[x] == p) and recs[x][4] < d]
+
+    def cands(p, asg, used):
+        wants = set(base_wants[p])
+        if p + 1 in asg and recs[asg[p + 1]][0] == C:
+            wants.add(recs[asg[p + 1]][2])
+        if len(wants) > 1:
+            return []
+        det, bv = base_before[p]
+        if not det and p - 1 in asg:
+            det, bv = True, recs[asg[p - 1]][1]
+        return [x for x in S[p] if x not in used and not (recs[x][0] == C and det and recs[x][2] != bv)
+                and not (wants and recs[x][1] not in wants)]
+
+    nodes = [0]
+
+    def search(asg, used):
+        nodes[0] += 1
+        if nodes[0] > budget:
+            return None
+        asg, used = dict(asg), set(used)
+        while True:
+            open_ = [p for p in gaps if p not in asg]
+            if not open_:
+                return None  # every open position held: no contradiction here
+            cs = {p: cands(p, asg, used) for p in open_}
+            if any(not cs[p] for p in open_):
+                return []    # the case closes
+            one = [p for p in open_ if len(cs[p]) == 1]
+            if one:          # forced (the checker re-derives it)
+                p = one[0]
+                asg[p] = cs[p][0]
+                used.add(cs[p][0])
+                continue
+            p = min(open_, key=lambda q: (len(cs[q]), q))
+            out = [tok(BRANCH, p, len(cs[p]))]
+            for o in cs[p]:
+                a2 = dict(asg)
+                a2[p] = o
+                sub = search(a2, used | {o})
+                if sub is None:
+                    return None
+                out += sub
+            return out
+
+    return search({}, set())

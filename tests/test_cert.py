@@ -8,13 +8,14 @@ checker accepts it from the records alone.  Here: the finder's restatement
 oracle's own failing prefixes, and no certificate at all — the finder's, or
 random ones — is ever accepted on a prefix the oracle finds linearizable
 (the prefix just before each failing return, and valid keys' histories)."""
+import os
 import random
 
 import numpy as np
 
 import oracle
 import cert_ref
-from helpers import INF, dup_versions, pack_keys, tiny_batch
+from helpers import GOLDEN, INF, dup_versions, pack_keys, tiny_batch
 from jepsen.etcd_amd import abi
 
 
@@ -28,6 +29,9 @@ def _sets():
         ops, off, _, _ = abi.synth(nk, n, concurrency=conc, p_info=pi, p_anomaly=pa, seed=seed)
         out.append((name, [ops[off[k]:off[k + 1]].tolist() for k in range(nk)]))
     out.append(("dup", dup_versions(out[1][1], 34, frac=0.8)))
+    z = np.load(os.path.join(GOLDEN, "branch.npz"))
+    out.append(("branch", [z["ops"][z["key_off"][k]:z["key_off"][k + 1]].tolist()
+                           for k in range(len(z["key_off"]) - 1)]))
     return out
 
 
@@ -76,7 +80,7 @@ def test_certificates_of_the_oracles_failing_prefixes():
         for k in np.nonzero(inv)[0]:
             kinds[oracle.CERT_KINDS[int(cert[4 * k])]] = kinds.get(oracle.CERT_KINDS[int(cert[4 * k])], 0) + 1
     assert total > 900, (total, kinds)
-    assert {"dup", "pair", "order", "hall", "claims", "unreach"} <= set(kinds), kinds
+    assert {"dup", "pair", "order", "hall", "claims", "unreach", "proof"} <= set(kinds), kinds
 
 
 def test_no_certificate_passes_on_a_linearizable_prefix():
@@ -118,11 +122,13 @@ def test_no_certificate_passes_on_a_linearizable_prefix():
             base = 0
             for i, recs in enumerate(keys):
                 n = max(1, len(recs))
-                kind = rng.randrange(1, 7)
-                c = rng.randrange(0, n) if kind != 6 else rng.randrange(1, n + 1)
+                kind = rng.randrange(1, 8)
+                c = rng.randrange(0, n) if kind < 6 else rng.randrange(1, n + 1)
                 rc[4 * i: 4 * i + 4] = (kind, rng.randrange(-1, n), rng.randrange(0, n), c)
                 for g in range(len(recs)):
-                    rs[base + g] = rng.randrange(0, n + 1)
+                    rs[base + g] = (rng.randrange(0, n + 1) if kind != 7 else
+                                    cert_ref.tok(rng.randrange(1, 4), rng.randrange(0, n + 1),
+                                                 rng.randrange(0, n)))
                 base += len(recs)
             st = oracle.check_certificate(ops, off, rc, rs, _res(lin_cut))
             assert not (use & (st == oracle.CERT_OK)).any(), (name, trial)
@@ -153,3 +159,61 @@ def test_tampered_certificates_are_rejected():
         assert st[0] == want, (c, st[0])
     got = cert_ref.find([tuple(r) for r in recs], 5)
     assert got[0] == cert_ref.ORDER and got[1:3] == (2, 1)
+
+
+def test_branch_fixture_needs_and_gets_a_proof():
+    """tests/golden/branch.npz (make_branch.py): invalid version-pinned keys
+    whose failing prefix no fixed certificate kind covers — the fixed
+    stages alone find nothing — get an LC_CERT_PROOF the checker accepts.
+    The oracle's verdicts and failing returns are the fixture's."""
+    z = np.load(os.path.join(GOLDEN, "branch.npz"))
+    ops, off = z["ops"], z["key_off"]
+    keys = [ops[off[k]:off[k + 1]].tolist() for k in range(len(off) - 1)]
+    _, j = oracle.check(ops, off, algo=oracle.JITC, n_threads=8)
+    assert (j["verdict"] == 0).all() and (j["fail_op"] == z["fail_op"]).all()
+    assert (j["fail_prefix_end"] == z["fail_prefix_end"]).all()
+    cuts = z["fail_prefix_end"]
+    for i, recs in enumerate(keys):
+        assert cert_ref.find([tuple(r) for r in recs], int(cuts[i]), proof=False)[0] == cert_ref.NONE
+    cert, cset = _certs(keys, cuts)
+    assert (cert[0::4] == cert_ref.PROOF).all()
+    st = oracle.check_certificate(ops, off, cert, cset, _res(cuts))
+    assert (st == oracle.CERT_OK).all(), np.nonzero(st != oracle.CERT_OK)[0][:5]
+
+
+def test_tampered_proofs_are_rejected():
+    """Every proof of the branch fixture, tampered: cut short, a case split
+    counting one case fewer or more or of another kind, a token too many
+    — the checker rejects each (it follows the proof step by step).  The
+    finder's proofs themselves: most are propagation alone (no token)."""
+    z = np.load(os.path.join(GOLDEN, "branch.npz"))
+    ops, off = z["ops"], z["key_off"]
+    keys = [ops[off[k]:off[k + 1]].tolist() for k in range(len(off) - 1)]
+    cuts = z["fail_prefix_end"]
+    cert, cset = _certs(keys, cuts)
+    n_checked = 0
+    lens = []
+    for i in range(len(keys)):
+        c, b = int(cert[4 * i + 3]), int(off[i])
+        toks = [int(x) for x in cset[b:b + c]]
+        lens.append(c)
+        variants = [toks + [cert_ref.tok(cert_ref.BRANCH, 0, 2)]]
+        if c > 0:
+            variants.append(toks[:-1])
+        for t in range(c):
+            kind, a, x = cert_ref.untok(toks[t])
+            # (a split at another position may be another valid proof: not here)
+            for v in (cert_ref.tok(kind, a, x - 1), cert_ref.tok(kind, a, x + 1),
+                      cert_ref.tok(cert_ref.FORCE, a, x)):
+                variants.append(toks[:t] + [v] + toks[t + 1:])
+        for v in variants:
+            if len(v) > len(keys[i]) or v == toks:
+                continue
+            one = np.zeros(len(keys[i]), dtype=np.int32)
+            one[:len(v)] = v
+            st = oracle.check_certificate(np.array(keys[i], dtype=np.int64), np.array([0, len(keys[i])]),
+                                          np.array([cert_ref.PROOF, -1, -1, len(v)], dtype=np.int32),
+                                          one, _res(np.array([cuts[i]])))
+            assert st[0] == oracle.CERT_BAD, (i, toks, v)
+            n_checked += 1
+    assert n_checked > 100 and max(lens) >= 1, (n_checked, lens)

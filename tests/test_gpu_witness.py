@@ -132,6 +132,24 @@ def test_invalid_keys_certified(ctx, case):
     assert (r2 == r).all()
 
 
+def test_branch_fixture_certified(ctx):
+    """tests/golden/branch.npz: invalid keys whose failing prefix only a
+    search over who holds the open positions refutes (no fixed certificate
+    kind covers them).  The device's verdicts and fail ops are the
+    fixture's, and its finder proves each one (LC_CERT_PROOF) by a proof
+    oracle/cert.c checks step by step."""
+    z = np.load(os.path.join(GOLDEN, "branch.npz"))
+    ops, off = z["ops"], z["key_off"]
+    _, r, wit, kind, cert, cset = ctx.check(ops, off, witness=True, certificate=True)
+    assert (r["verdict"] == 0).all() and (r["fail_op"] == z["fail_op"]).all()
+    assert (r["fail_prefix_end"] == z["fail_prefix_end"]).all()
+    certify(ops, off, r, wit, kind)
+    st = certify_invalid(ops, off, r, cert, cset, min_keys=100)
+    assert (st == oracle.CERT_OK).all(), [(int(k), cert[k].tolist())
+                                          for k in np.nonzero(st != oracle.CERT_OK)[0][:5]]
+    assert (cert[:, 0] == abi.LC_CERT_PROOF).sum() >= 100
+
+
 def test_crash_leg_every_key_certified(ctx):
     """bench.py's crash_leg workload at full size: C2 (10,000 keys x 1,000
     ops, concurrency 20) with 5 % of writes/CAS crashed.  Every key goes to
