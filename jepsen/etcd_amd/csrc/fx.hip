@@ -211,6 +211,24 @@ struct Ctr {
   alignas(128) unsigned long long exp[kExpShards * kExpStride];  // explored, sharded
 };
 
+// What the host reads of Ctr after a batch (sync_ctr): the counters, the
+// shards already summed / ANDed, written by fx_report_kernel into host-mapped
+// memory with `seq` last, so that the host spins on one word instead of a
+// device-to-host copy and a stream synchronisation (≈3 µs of copy on the
+// device plus the host's wake-up, per batch).
+struct Rep {
+  unsigned long long nV, kcur, explored, levels, andmask, overflow, nsel, tfull, nR;
+  unsigned long long cnt[3];
+  unsigned long long cand[64];
+  unsigned long long cmin[kMaxCls];
+  alignas(64) unsigned int seq;
+};
+
+// One wave: lane i sums explored shard i (64 of them), ANDs AND shard i (16),
+// copies owner count i and class minimum i; lane 0 the scalars; then a
+// system-scope release and `seq`.
+__global__ __launch_bounds__(64) void fx_report_kernel(const Ctr *__restrict__ c, Rep *r, unsigned int seq);
+
 __device__ inline void and_into(Ctr *ctr, unsigned long long a) {
   atomicAnd(&ctr->andm[(blockIdx.x % kAndShards) * kExpStride], a);
 }
@@ -360,6 +378,42 @@ __device__ inline unsigned long long wave_and(unsigned long long v) {
   return v;
 }
 
+__device__ inline unsigned long long wave_sum(unsigned long long v) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, off), hi = __shfl_xor((uint32_t)(v >> 32), off);
+    v += ((unsigned long long)hi << 32) | lo;
+  }
+  return v;
+}
+
+static_assert(kExpShards == 64 && kAndShards <= 64 && kMaxCls <= 64, "one lane per shard");
+
+__global__ __launch_bounds__(64) void fx_report_kernel(const Ctr *__restrict__ c, Rep *r, unsigned int seq) {
+  const int i = threadIdx.x;
+  const unsigned long long e = wave_sum(c->exp[i * kExpStride]);
+  const unsigned long long q = wave_sum(c->exp[i * kExpStride + 1]);
+  const unsigned long long a = wave_and(i < kAndShards ? c->andm[i * kExpStride] : ~0ULL);
+  r->cand[i] = c->cand[i];
+  if (i < kMaxCls) r->cmin[i] = c->cmin[i];
+  if (i < 3) r->cnt[i] = c->cnt[i];
+  if (i == 0) {
+    r->nV = c->nV + q;
+    r->kcur = c->kcur;
+    r->explored = e;
+    r->levels = c->levels;
+    r->andmask = a;
+    r->overflow = c->overflow;
+    r->nsel = c->nsel;
+    r->tfull = c->tfull;
+    r->nR = c->nR;
+  }
+  __syncthreads();
+  if (i == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(&r->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Wave-aggregated append of the lanes in `take` (each with its own c).
 __device__ inline void wave_append(bool take, const Cfg &c, Cfg *list, unsigned long long *count,
                                    unsigned long long cap, unsigned long long *overflow) {
@@ -395,7 +449,10 @@ __device__ inline void insert_rv(bool have, Cfg c, uint64_t xbit, const Tabs &t,
 // Counters of a return about to start: R and V empty, explored at `explored`
 // (the shards), levels from 0.
 __device__ inline void ctr_start(Ctr *ctr, unsigned long long explored) {
-  for (int i = 0; i < kExpShards; i++) ctr->exp[i * kExpStride] = i ? 0 : explored;
+  for (int i = 0; i < kExpShards; i++) {
+    ctr->exp[i * kExpStride] = i ? 0 : explored;
+    ctr->exp[i * kExpStride + 1] = 0;  // second-hop configurations (nV's part kept here)
+  }
   ctr->nR = ctr->nV = ctr->kcur = 0;
   ctr->cnt[0] = ctr->cnt[1] = ctr->cnt[2] = 0;
   ctr->levels = 0;
@@ -479,10 +536,12 @@ __global__ __launch_bounds__(256) void fx_split_kernel(const Cfg *__restrict__ i
 // flush of up to kStage entries instead of one per configuration expanded —
 // the list counters are the only same-address atomics of a level.
 constexpr int kStage = 128;
+constexpr int kHop2 = 64;  // most successors a wave expands itself in a level launch
 struct Stage {
   Cfg r[kStage];
   Cfg v[kStage];
   Cfg s[64];  // successors gathered from several configurations, inserted together
+  Cfg q[2][kHop2];  // new successors this wave expands in the same launch (later hops)
 };
 
 __device__ inline void stage_flush(Cfg *buf, int &n, Cfg *list, unsigned long long *count,
@@ -519,28 +578,31 @@ __device__ inline void stage_put(bool isnew, bool toR, const Cfg &c, Stage *stg,
 // writes its own.  Every wave of the workgroup must call it.
 struct WgFlush {
   int n[4][2];
+  int nq[4];
   unsigned long long base[2];
   unsigned long long explored[4];
   unsigned long long andm[4];
 };
 
-__device__ inline void wg_flush(WgFlush *wf, Stage *stg, int nr, int nv, unsigned long long explored,
-                                uint64_t rand, const Tabs &t, Ctr *ctr) {
+__device__ inline void wg_flush(WgFlush *wf, Stage *stg, int nr, int nv, int nq,
+                                unsigned long long explored, uint64_t rand, const Tabs &t, Ctr *ctr) {
   const int w = threadIdx.x / kW, lane = __lane_id();
   rand = wave_and(rand);
   if (lane == 0) {
     wf->n[w][0] = nr;
     wf->n[w][1] = nv;
+    wf->nq[w] = nq;
     wf->explored[w] = explored;
     wf->andm[w] = rand;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     const int nw = blockDim.x / kW;
-    unsigned long long tr = 0, tv = 0, te = 0, ta = ~0ULL;
+    unsigned long long tr = 0, tv = 0, te = 0, ta = ~0ULL, tq = 0;
     for (int k = 0; k < nw; k++) {
       tr += wf->n[k][0];
       tv += wf->n[k][1];
+      tq += wf->nq[k];
       te += wf->explored[k];
       ta &= wf->andm[k];
     }
@@ -548,6 +610,7 @@ __device__ inline void wg_flush(WgFlush *wf, Stage *stg, int nr, int nv, unsigne
     wf->base[0] = tr ? atomicAdd(&ctr->nR, tr) : 0;
     wf->base[1] = tv ? atomicAdd(t.vcnt, tv) : 0;
     if (te) atomicAdd(&t.exp[(blockIdx.x % kExpShards) * kExpStride], te);
+    if (tq) atomicAdd(&t.exp[(blockIdx.x % kExpShards) * kExpStride + 1], tq);
   }
   __syncthreads();
   unsigned long long br = wf->base[0], bv = wf->base[1];
@@ -574,12 +637,24 @@ __device__ inline void wg_flush(WgFlush *wf, Stage *stg, int nr, int nv, unsigne
 // Read closure: the reads a successor's state makes legal are, for reads
 // without a version, fixed by the value this lane's op writes (rv_me, once
 // per launch); only reads that name a version are tested per successor.
+// Later hops (replicated mode, `hops` > 0): up to `hop2` of the new
+// successors a wave finds that stay in V are expanded by that wave in the
+// same launch instead of going to the next level's list, and up to `hop2` of
+// theirs, `hops` times, so a launch covers up to 1 + `hops` levels of the
+// search.  A configuration is still expanded exactly
+// once (the one whose insert found it new does it, whenever), so the
+// configurations explored and the frontiers are those of one level per
+// launch; the levels' lists are then work queues whose entries may differ in
+// depth.
 __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch, Ctr *ctr,
                                     int64_t lo, int64_t hi, int64_t wave, int64_t nwaves,
                                     Cfg *cbuf, unsigned long long cand_cap, Stage *stg,
-                                    WgFlush *wf) {
+                                    WgFlush *wf, int hop2 = 0, int hops = 0) {
   const int lane = __lane_id();
   int nr = 0, nv = 0;  // staged entries (wave-uniform)
+  int nq = 0;          // configurations kept for the next hop, in stg->q[qb] (wave-uniform)
+  int qb = 0;
+  int nkept = 0;       // configurations the later hops expanded
   const Slot me = w.s[lane];
   const uint64_t bit = 1ULL << lane;
   const uint64_t muts = w.occ & ~w.reads;
@@ -623,6 +698,7 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
     const int64_t n = hi - lo;
     const int64_t chunk = std::min<int64_t>(kW, std::max<int64_t>(1, (n + nwaves - 1) / nwaves));
     int ns = 0;
+    int room = hops ? hop2 : 0;  // places left for the next hop
     auto insert_stash = [&]() {
       __builtin_amdgcn_wave_barrier();
       const bool have = lane < ns;
@@ -635,8 +711,29 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
       if (have) x = any_insert(t, toR, epoch, sc);
       if (x == -1) atomicOr(&ctr->tfull, 1ULL);
       if (x == 1 && toR) rand &= sc.mask;
-      stage_put(x == 1, toR, sc, stg, nr, nv, t, ctr);
+      bool keep = false;
+      if (room) {
+        const uint64_t mk = __ballot(x == 1 && !toR);
+        const int r = __popcll(mk & below);
+        keep = x == 1 && !toR && r < room;
+        if (keep) stg->q[qb][nq + r] = sc;
+        const int took = min(__popcll(mk), room);
+        nq += took;
+        room -= took;
+      }
+      stage_put(x == 1 && !keep, toR, sc, stg, nr, nv, t, ctr);
       ns = 0;
+    };
+    auto expand_one = [&](const Cfg &c) {
+      bool cand;
+      Cfg sc;
+      succ(c, cand, sc);
+      const uint64_t m = __ballot(cand);
+      const int k = __popcll(m);
+      explored += k;
+      if (ns + k > kW) insert_stash();
+      if (cand) stg->s[ns + __popcll(m & below)] = sc;
+      ns += k;
     };
     for (int64_t base = lo + wave * chunk; base < hi; base += nwaves * chunk) {
       const int cnt = (int)std::min<int64_t>(chunk, hi - base);
@@ -648,18 +745,25 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
                  __shfl((uint32_t)mine.mask, j);
         c.ver = __shfl(mine.ver, j);
         c.val = __shfl(mine.val, j);
-        bool cand;
-        Cfg sc;
-        succ(c, cand, sc);
-        const uint64_t m = __ballot(cand);
-        const int k = __popcll(m);
-        explored += k;
-        if (ns + k > kW) insert_stash();
-        if (cand) stg->s[ns + __popcll(m & below)] = sc;
-        ns += k;
+        expand_one(c);
       }
     }
     if (ns) insert_stash();
+    for (int h = 1; h <= hops && nq; h++) {
+      // hop h + 1: the kept configurations (their new successors kept again
+      // while hops are left, else to the lists)
+      const int n = nq, cur = qb;
+      nkept += n;
+      qb ^= 1;
+      nq = 0;
+      room = h < hops ? hop2 : 0;
+      __builtin_amdgcn_wave_barrier();
+      for (int j = 0; j < n; j++) {
+        const Cfg c = stg->q[cur][j];
+        expand_one(c);
+      }
+      if (ns) insert_stash();
+    }
   } else {
     for (int64_t i = lo + wave; i < hi; i += nwaves) {
       const Cfg c = t.vsrc[i];
@@ -679,7 +783,7 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
       }
     }
   }
-  wg_flush(wf, stg, nr, nv, explored, rand, t, ctr);
+  wg_flush(wf, stg, nr, nv, nkept, explored, rand, t, ctr);
 }
 
 __device__ inline void load_win(Win &w, const Win *gwin) {
@@ -698,7 +802,8 @@ __device__ inline void load_win(Win &w, const Win *gwin) {
 __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ gwin, Tabs t,
                                                         uint32_t epoch, Ctr *ctr, int64_t k,
                                                         int64_t lo_arg, int64_t hi_arg, Cfg *cbuf,
-                                                        unsigned long long cand_cap) {
+                                                        unsigned long long cand_cap, int hop2,
+                                                        int hops) {
   // The prologue's loads go out together — the level's size, the table-full
   // flag and this thread's words of the window — one round trip to memory
   // before the first configuration instead of three in a row (a level's
@@ -745,7 +850,8 @@ __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ 
   __syncthreads();
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kW;
   const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kW;
-  expand_range(w, t, epoch, ctr, lo, hi, wave, nwaves, cbuf, cand_cap, &stg[threadIdx.x / kW], &wf);
+  expand_range(w, t, epoch, ctr, lo, hi, wave, nwaves, cbuf, cand_cap, &stg[threadIdx.x / kW], &wf,
+               hop2, hops);
 }
 
 
@@ -1557,6 +1663,9 @@ struct Rank {
   uint64_t tmask = 0;
   Win *dWin = nullptr, *hWin = nullptr;
   Ctr *dCtr = nullptr, *hCtr = nullptr;
+  Rep *hRep = nullptr, *dRep = nullptr;  // host-mapped (sync_ctr)
+  unsigned int rep_seq = 0;
+  bool copy_sync = false;  // LC_FX_COPY_SYNC=1 (A/B): the copy and stream synchronisation instead
   // Returns alternate between two sets of counters and (one-word mode) two
   // tables, so that a return can prepare the next one's (fx_split_kernel):
   // dCtr = dCtrBase + par, the one-word tables of parity 1 are tagR2 / tagV2.
@@ -1611,8 +1720,10 @@ struct Rank {
     qrep = qrep_dev = nullptr;
     if (hWin) (void)hipHostFree(hWin);
     if (hCtr) (void)hipHostFree(hCtr);
+    if (hRep) (void)hipHostFree(hRep);
     hWin = nullptr;
     hCtr = nullptr;
+    hRep = dRep = nullptr;
     list_cap = 0;
     if (nc) {
       if (nc->d) (void)hipFree(nc->d);
@@ -1705,6 +1816,11 @@ struct Rank {
     dExp = &dCtr->exp[0];  // device address, not dereferenced here
     FX_TRY(hipHostMalloc(&hWin, sizeof(Win), hipHostMallocDefault));
     FX_TRY(hipHostMalloc(&hCtr, sizeof(Ctr), hipHostMallocDefault));
+    FX_TRY(hipHostMalloc(&hRep, sizeof(Rep), hipHostMallocMapped | hipHostMallocCoherent));
+    FX_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&dRep), hRep, 0));
+    std::memset(hRep, 0, sizeof(Rep));
+    rep_seq = 0;
+    copy_sync = getenv("LC_FX_COPY_SYNC") && getenv("LC_FX_COPY_SYNC")[0] == '1';
     std::memset(hWin, 0, sizeof(Win));
     if (const char *q = getenv("LC_FX_QUEUE")) qpath = q[0] == '1';
     if (const char *q = getenv("LC_FXQ_G")) qdbg_g = atoi(q);
@@ -1819,11 +1935,48 @@ struct Rank {
   }
 
   // Ctr to the host; its explored is the sum of the shards.
+  // The report kernel writes the counters to host-mapped memory, `seq` last;
+  // the host spins on it (checking the stream every 1,024 rounds, so that an
+  // error ends the wait; past 20 ms it synchronises the stream instead).
   int sync_ctr() {
+    if (!copy_sync) {
+      const unsigned int s = ++rep_seq;
+      fx_report_kernel<<<1, 64, 0, st>>>(dCtr, dRep, s);
+      FX_TRY(hipGetLastError());
+      const auto t0 = std::chrono::steady_clock::now();
+      for (uint32_t i = 1; __atomic_load_n(&hRep->seq, __ATOMIC_ACQUIRE) != s; i++) {
+        if (i & 1023) continue;
+        const hipError_t q = hipStreamQuery(st);
+        if (q != hipSuccess && q != hipErrorNotReady) FX_TRY(q);
+        if (q == hipSuccess && __atomic_load_n(&hRep->seq, __ATOMIC_ACQUIRE) != s) {
+          err = "counter report lost";
+          return -EIO;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20))
+          FX_TRY(hipStreamSynchronize(st));
+      }
+      const Rep &r = *hRep;
+      hCtr->nV = r.nV;
+      hCtr->kcur = r.kcur;
+      hCtr->explored = r.explored + exp_off;
+      hCtr->levels = r.levels;
+      hCtr->andmask = r.andmask;
+      hCtr->overflow = r.overflow;
+      hCtr->nsel = r.nsel;
+      hCtr->tfull = r.tfull;
+      hCtr->nR = r.nR;
+      for (int i = 0; i < 3; i++) hCtr->cnt[i] = r.cnt[i];
+      for (int i = 0; i < 64; i++) hCtr->cand[i] = r.cand[i];
+      for (int i = 0; i < kMaxCls; i++) hCtr->cmin[i] = r.cmin[i];
+      return 0;
+    }
     FX_TRY(hipMemcpyAsync(hCtr, dCtr, sizeof(Ctr), hipMemcpyDeviceToHost, st));
     FX_TRY(hipStreamSynchronize(st));
     unsigned long long e = 0;
-    for (int i = 0; i < kExpShards; i++) e += hCtr->exp[i * kExpStride];
+    for (int i = 0; i < kExpShards; i++) {
+      e += hCtr->exp[i * kExpStride];
+      hCtr->nV += hCtr->exp[i * kExpStride + 1];
+    }
     hCtr->explored = e + exp_off;
     unsigned long long a = ~0ULL;
     for (int i = 0; i < kAndShards; i++) a &= hCtr->andm[i * kExpStride];
@@ -1867,7 +2020,7 @@ struct Rank {
     FX_TRY(hipMemsetAsync(dCtr->cand, 0, sizeof(unsigned long long) * P, st));
     if (b > a) {
       const int g = (int)std::max<int64_t>(1, std::min<int64_t>(kExpandWG, (b - a + 3) / 4));
-      fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tb, epoch, dCtr, 0, a, b, cand, cand_cap);
+      fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tb, epoch, dCtr, 0, a, b, cand, cand_cap, 0, 0);
       FX_TRY(hipGetLastError());
     }
     std::vector<int64_t> sc(P), rc(P);
@@ -2070,6 +2223,10 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   const bool debug = getenv("LC_FX_DEBUG") != nullptr;
   const int64_t tmul = getenv("LC_FX_TABLE_MUL") ? std::max(1, atoi(getenv("LC_FX_TABLE_MUL"))) : 4;
   const int64_t spad = getenv("LC_FX_SPEC_PAD") ? atoi(getenv("LC_FX_SPEC_PAD")) : 1;
+  // second-hop places per wave of a level launch (LC_FX_HOP2, 0..kHop2)
+  const int hop2 = getenv("LC_FX_HOP2") ? std::max(0, std::min(kHop2, atoi(getenv("LC_FX_HOP2")))) : 32;
+  // later hops per level launch (LC_FX_HOPS; 0: one level per launch)
+  const int hops = hop2 ? (getenv("LC_FX_HOPS") ? std::max(0, std::min(16, atoi(getenv("LC_FX_HOPS")))) : 8) : 0;
   // A/B switch (dev): LC_FX_PREP=0 resets every return by a launch of its own
   const bool allow_prep = !(getenv("LC_FX_PREP") && getenv("LC_FX_PREP")[0] == '0');
   // queue path: the version every configuration of a return has before the
@@ -2440,7 +2597,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           }
           for (int l = 0; l < spec_levels; l++, k++)
             fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tabs(tlog, compact, k), epoch, dCtr, k, -1, -1,
-                                                nullptr, 0);
+                                                nullptr, 0, hop2, hops);
           if (n_cls) {
             const int ga = grid_for((int64_t)std::max(nF, last_work));
             fx_and_kernel<<<ga, 256, 0, st>>>(Rl, &dCtr->nR, dCtr, dExp);
