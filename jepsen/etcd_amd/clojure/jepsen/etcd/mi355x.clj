@@ -65,9 +65,15 @@
 
 (defn- fun ^Function [name] (.getFunction ^NativeLibrary @lib name))
 
+(def ^:const abi-min 4)  ; lc_check32 / lc_check_frontiers (include/lincheck.h LC_ABI_VERSION)
+
 (defonce ^:private ctx
   (delay
-    (let [out (PointerByReference.)
+    (let [abi (.invokeInt (fun "lc_abi_version") (object-array []))
+          _   (when (< abi abi-min)
+                (throw (ex-info "liblincheck.so is older than this shim's ABI"
+                                {:abi abi :need abi-min})))
+          out (PointerByReference.)
           rc  (.invokeInt (fun "lc_open") (object-array [(int 0) out]))]
       (when-not (zero? rc)
         (throw (ex-info "lc_open failed: no usable GPU (no CPU fallback)"

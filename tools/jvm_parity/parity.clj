@@ -22,6 +22,15 @@
 ;; verdict mismatch.  (Knossos's reported :op can legitimately differ from the
 ;; canonical first failing return when its WGL analyzer wins the race, so op
 ;; differences are reported but do not fail the run.)
+;;
+;; With MI355X_SHIM set to this repo's jepsen/etcd_amd/clojure/jepsen/etcd/
+;; mi355x.clj (and LINCHECK_LIB to the built liblincheck.so, ABI >= 4 — the
+;; shim checks lc_abi_version), the drop-in runs on the same history too:
+;; (jepsen.etcd.mi355x/checker {:timeline? false}), i.e. lc_check32 plus
+;; lc_check_frontiers for the invalid keys' :configs.  Its verdicts must equal
+;; the expected ones on every key (the drop-in never answers :unknown on these
+;; fixtures), its invalid keys' :op :index the expected failing completion, and
+;; every key knossos decides must get the same verdict from both.
 (ns mi355x.parity
   (:require [clojure.edn :as edn]
             [clojure.java.io :as io]
@@ -52,6 +61,35 @@
     (f ops)
     ops))
 
+(def ^:private dropin
+  (delay (when-let [shim (System/getenv "MI355X_SHIM")]
+           (load-file shim)
+           ((requiring-resolve 'jepsen.etcd.mi355x/checker) {:timeline? false}))))
+
+(defn- check-dropin
+  "The drop-in on the same history: its verdicts and fail ops against the
+  expected ones, and against knossos's where knossos decided.  True when
+  there is no mismatch (or no shim)."
+  [name hist expected res]
+  (if-let [chk @dropin]
+    (let [t0   (System/nanoTime)
+          dres (checker/check chk {:name (str "mi355x-dropin-" name)} (as-history hist) {})
+          secs (/ (- (System/nanoTime) t0) 1e9)
+          rows (for [[k {:keys [valid? op-index]}] expected]
+                 (let [d (get-in dres [:results k])
+                       r (get-in res [:results k :valid?])]
+                   {:key k :want valid? :got (:valid? d) :knossos r
+                    :op-want op-index :op-got (get-in d [:linear :op :index])}))
+          bad  (filter #(or (not= (:want %) (:got %))
+                            (and (false? (:want %)) (not= (:op-want %) (:op-got %)))
+                            (and (boolean? (:knossos %)) (not= (:knossos %) (:got %))))
+                       rows)]
+      (println (format "%s: drop-in %d keys, %d mismatches (verdict, fail op or vs knossos), %.2f s"
+                       name (count rows) (count bad) secs))
+      (doseq [m (take 10 bad)] (println "  drop-in mismatch" m))
+      (empty? bad))
+    true))
+
 (defn- check-file [dir name]
   (let [hist     (read-history (io/file dir (str name ".edn.gz")))
         expected (edn/read-string (slurp (io/file dir (str name ".expected.edn"))))
@@ -72,7 +110,7 @@
     (println (format "%s: %d keys, %d verdict mismatches, %d knossos :unknown, %d op differences, %.1f s"
                      name (count rows) (count mismatch) (count unknown) (count op-diff) secs))
     (doseq [m (take 10 mismatch)] (println "  mismatch" m))
-    (empty? mismatch)))
+    (and (empty? mismatch) (check-dropin name hist expected res))))
 
 (let [[dir & names] *command-line-args*
       names (or (seq names) ["kat" "c1" "tiny" "c5" "info"])
