@@ -1666,6 +1666,12 @@ struct Rank {
   Rep *hRep = nullptr, *dRep = nullptr;  // host-mapped (sync_ctr)
   unsigned int rep_seq = 0;
   bool copy_sync = false;  // LC_FX_COPY_SYNC=1 (A/B): the copy and stream synchronisation instead
+  // LC_FX_HOSTPROF (dev): host time between counter reports (launching, the
+  // host's books) against time spinning for them, per check
+  bool hostprof = false;
+  double hp_host = 0, hp_wait = 0, hp_split = 0, hp_expand = 0;
+  long long hp_syncs = 0, hp_nsplit = 0, hp_nexpand = 0;
+  std::chrono::steady_clock::time_point hp_mark;
   // Returns alternate between two sets of counters and (one-word mode) two
   // tables, so that a return can prepare the next one's (fx_split_kernel):
   // dCtr = dCtrBase + par, the one-word tables of parity 1 are tagR2 / tagV2.
@@ -1821,6 +1827,7 @@ struct Rank {
     std::memset(hRep, 0, sizeof(Rep));
     rep_seq = 0;
     copy_sync = getenv("LC_FX_COPY_SYNC") && getenv("LC_FX_COPY_SYNC")[0] == '1';
+    hostprof = getenv("LC_FX_HOSTPROF") != nullptr;
     std::memset(hWin, 0, sizeof(Win));
     if (const char *q = getenv("LC_FX_QUEUE")) qpath = q[0] == '1';
     if (const char *q = getenv("LC_FXQ_G")) qdbg_g = atoi(q);
@@ -1944,6 +1951,10 @@ struct Rank {
       fx_report_kernel<<<1, 64, 0, st>>>(dCtr, dRep, s);
       FX_TRY(hipGetLastError());
       const auto t0 = std::chrono::steady_clock::now();
+      if (hostprof) {
+        hp_host += std::chrono::duration<double, std::micro>(t0 - hp_mark).count();
+        hp_syncs++;
+      }
       for (uint32_t i = 1; __atomic_load_n(&hRep->seq, __ATOMIC_ACQUIRE) != s; i++) {
         if (i & 1023) continue;
         const hipError_t q = hipStreamQuery(st);
@@ -1968,6 +1979,10 @@ struct Rank {
       for (int i = 0; i < 3; i++) hCtr->cnt[i] = r.cnt[i];
       for (int i = 0; i < 64; i++) hCtr->cand[i] = r.cand[i];
       for (int i = 0; i < kMaxCls; i++) hCtr->cmin[i] = r.cmin[i];
+      if (hostprof) {
+        hp_mark = std::chrono::steady_clock::now();
+        hp_wait += std::chrono::duration<double, std::micro>(hp_mark - t0).count();
+      }
       return 0;
     }
     FX_TRY(hipMemcpyAsync(hCtr, dCtr, sizeof(Ctr), hipMemcpyDeviceToHost, st));
@@ -2116,6 +2131,7 @@ void result_unknown(lc_key_result *r, int reason) {
 
 int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result *res) {
   const auto t0 = std::chrono::steady_clock::now();
+  hp_mark = t0;
   std::memset(&stats, 0, sizeof(stats));
   lc_opts opts;
   if (opts_in) {
@@ -2577,10 +2593,15 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           const int q = par ^ 1;
           const bool prep = !multi() && compact && allow_prep;
           const int64_t pw = prep ? (int64_t)dirtyC[q] : 0;
+          const auto ts0 = std::chrono::steady_clock::now();
           fx_split_kernel<<<std::max(grid_for(nF), grid_for(pw)), 256, 0, st>>>(
               F, nF, w, use_prep ? dWin : nullptr, tb, epoch, dCtr, prep ? dCtrBase + q : nullptr,
               q ? tagR2 : tagR, q ? tagV2 : tagV, pw);
           FX_TRY(hipGetLastError());
+          if (hostprof) {
+            hp_split += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - ts0).count();
+            hp_nsplit++;
+          }
           if (prep) {
             dirtyC[q] = 0;
             prepped[q] = true;
@@ -2595,9 +2616,14 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
             FX_TRY(hipMemsetAsync(dCtr->andm, 0xFF, sizeof(dCtr->andm), st));
             FX_TRY(hipMemsetAsync(dCtr->cmin, 0xFF, sizeof(dCtr->cmin), st));
           }
+          const auto te0 = std::chrono::steady_clock::now();
           for (int l = 0; l < spec_levels; l++, k++)
             fx_expand_kernel<<<g, 256, 0, st>>>(dWin, tabs(tlog, compact, k), epoch, dCtr, k, -1, -1,
                                                 nullptr, 0, hop2, hops);
+          if (hostprof) {
+            hp_expand += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - te0).count();
+            hp_nexpand += spec_levels;
+          }
           if (n_cls) {
             const int ga = grid_for((int64_t)std::max(nF, last_work));
             fx_and_kernel<<<ga, 256, 0, st>>>(Rl, &dCtr->nR, dCtr, dExp);
@@ -2848,6 +2874,14 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   FX_TRY(hipStreamSynchronize(st));
   stats.levels = levels_total + stats.part_levels;
   stats.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (hostprof) {
+    fprintf(stderr, "fx hostprof: total %.2f ms, reports %lld, host between reports %.2f ms, waiting %.2f ms; "
+            "split launches %lld %.2f ms, expand launches %lld %.2f ms\n",
+            stats.total_ms, hp_syncs, hp_host * 1e-3, hp_wait * 1e-3, hp_nsplit, hp_split * 1e-3, hp_nexpand,
+            hp_expand * 1e-3);
+    hp_host = hp_wait = hp_split = hp_expand = 0;
+    hp_syncs = hp_nsplit = hp_nexpand = 0;
+  }
   if (qdbg_time) {
     fprintf(stderr, "fxq: returns %lld redos %lld launches %lld launch us %.1f sync us %.1f total ms %.2f\n",
             (long long)stats.returns, (long long)stats.redos, (long long)qt_n, qt_launch, qt_sync,
