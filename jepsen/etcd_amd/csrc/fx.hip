@@ -649,7 +649,7 @@ __device__ inline void wg_flush(WgFlush *wf, Stage *stg, int nr, int nv, int nq,
 __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch, Ctr *ctr,
                                     int64_t lo, int64_t hi, int64_t wave, int64_t nwaves,
                                     Cfg *cbuf, unsigned long long cand_cap, Stage *stg,
-                                    WgFlush *wf, int hop2 = 0, int hops = 0) {
+                                    WgFlush *wf, int hop2 = 0, int hops = 0, bool from_f = false) {
   const int lane = __lane_id();
   int nr = 0, nv = 0;  // staged entries (wave-uniform)
   int nq = 0;          // configurations kept for the next hop, in stg->q[qb] (wave-uniform)
@@ -739,6 +739,19 @@ __device__ inline void expand_range(const Win &w, const Tabs &t, uint32_t epoch,
       const int cnt = (int)std::min<int64_t>(chunk, hi - base);
       Cfg mine{};
       if (lane < cnt) mine = t.vsrc[base + lane];
+      if (from_f) {
+        // the frontier itself (fx_split_expand_kernel): each configuration,
+        // with the updates since the last return, is inserted as a successor
+        // would be — to R if it linearized the returning op, else to V, where
+        // a new one is kept and expanded below like any kept successor
+        if (lane < cnt) {
+          fix_f(mine, w);
+          stg->s[lane] = mine;
+        }
+        ns = cnt;
+        insert_stash();
+        continue;
+      }
       for (int j = 0; j < cnt; j++) {
         Cfg c;
         c.mask = ((uint64_t)__shfl((uint32_t)(mine.mask >> 32), j) << 32) |
@@ -854,6 +867,53 @@ __global__ __launch_bounds__(256) void fx_expand_kernel(const Win *__restrict__ 
                hop2, hops);
 }
 
+
+// A return's split and its first levels in one launch (one rank): the
+// frontier F, with the updates since the last return applied, goes to R (it
+// linearized the returning op) or V (dedup tables as the split's); a new V
+// configuration is kept and expanded in the same launch up to `hops` levels
+// deep (expand_range's later hops), and what does not fit goes to V level 0,
+// which the batch's level launches take on.  Like fx_split_kernel it stores
+// the window for the level launches (dwin) and prepares the next return's
+// counters and tables (prep_*): one launch instead of the split and the
+// return's first level launch, and no list round trip for the configurations
+// it expands itself.
+__global__ __launch_bounds__(256) void fx_split_expand_kernel(const Cfg *__restrict__ F, int64_t nF,
+                                                              const Win win, Win *dwin, Tabs t,
+                                                              uint32_t epoch, Ctr *ctr, Ctr *prep_ctr,
+                                                              unsigned long long *prep_tR,
+                                                              unsigned long long *prep_tV,
+                                                              int64_t prep_words, int hop2, int hops) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (dwin && blockIdx.x == 0) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(&win);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(dwin);
+    for (int i = threadIdx.x; i < (int)(sizeof(Win) / 4); i += blockDim.x) dst[i] = src[i];
+  }
+  if (prep_ctr) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < prep_words; i += stride) {
+      prep_tR[i] = kEmpty;
+      prep_tV[i] = kEmpty;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr_start(prep_ctr, 0);
+  }
+  if ((int64_t)blockIdx.x * (blockDim.x / kW) >= nF) return;  // (workgroup-uniform)
+  __shared__ Win w;
+  __shared__ Stage stg[4];
+  __shared__ WgFlush wf;
+  {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(&win);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(&w);
+    for (int i = threadIdx.x; i < (int)(sizeof(Win) / 4); i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kW;
+  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kW;
+  Tabs tf = t;
+  tf.vsrc = const_cast<Cfg *>(F);
+  expand_range(w, tf, epoch, ctr, 0, nF, wave, nwaves, nullptr, 0, &stg[threadIdx.x / kW], &wf, hop2,
+               hops, true);
+}
 
 // Counted classes: the smallest field of each class over list[lo, hi) (this
 // thread strided by `step`), into ctr->cmin (retirement of the members every
@@ -2243,6 +2303,10 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
   const int hop2 = getenv("LC_FX_HOP2") ? std::max(0, std::min(kHop2, atoi(getenv("LC_FX_HOP2")))) : 32;
   // later hops per level launch (LC_FX_HOPS; 0: one level per launch)
   const int hops = hop2 ? (getenv("LC_FX_HOPS") ? std::max(0, std::min(16, atoi(getenv("LC_FX_HOPS")))) : 8) : 0;
+  // the split and the first levels in one launch (one rank; LC_FX_MERGE=0:
+  // fx_split_kernel, then the level launches)
+  const bool merge_on = !multi() && hops > 0 && !(getenv("LC_FX_MERGE") && getenv("LC_FX_MERGE")[0] == '0');
+  const int64_t mpad = getenv("LC_FX_MERGE_PAD") ? std::max(0, atoi(getenv("LC_FX_MERGE_PAD"))) : 0;
   // A/B switch (dev): LC_FX_PREP=0 resets every return by a launch of its own
   const bool allow_prep = !(getenv("LC_FX_PREP") && getenv("LC_FX_PREP")[0] == '0');
   // queue path: the version every configuration of a return has before the
@@ -2579,6 +2643,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
         // (or for what it leaves) speculative batches of levels over the
         // grid, one sync per batch
         const bool small = nF <= kSmallF && last_work <= kSmallWork;
+        const bool merge = merge_on && !small;
         int64_t k = 0;  // the next V level to expand
         bool done = false;
         if (small) {
@@ -2594,9 +2659,17 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           const bool prep = !multi() && compact && allow_prep;
           const int64_t pw = prep ? (int64_t)dirtyC[q] : 0;
           const auto ts0 = std::chrono::steady_clock::now();
-          fx_split_kernel<<<std::max(grid_for(nF), grid_for(pw)), 256, 0, st>>>(
-              F, nF, w, use_prep ? dWin : nullptr, tb, epoch, dCtr, prep ? dCtrBase + q : nullptr,
-              q ? tagR2 : tagR, q ? tagV2 : tagV, pw);
+          if (merge) {
+            // one rank: the split and the return's first levels in one launch
+            const int gm = (int)std::max<int64_t>(16, std::min<int64_t>(kExpandWG, (std::max(nF, last_work) + 3) / 4));
+            fx_split_expand_kernel<<<std::max(gm, grid_for(pw)), 256, 0, st>>>(
+                F, nF, w, use_prep ? dWin : nullptr, tb, epoch, dCtr, prep ? dCtrBase + q : nullptr,
+                q ? tagR2 : tagR, q ? tagV2 : tagV, pw, hop2, hops);
+          } else {
+            fx_split_kernel<<<std::max(grid_for(nF), grid_for(pw)), 256, 0, st>>>(
+                F, nF, w, use_prep ? dWin : nullptr, tb, epoch, dCtr, prep ? dCtrBase + q : nullptr,
+                q ? tagR2 : tagR, q ? tagV2 : tagV, pw);
+          }
           FX_TRY(hipGetLastError());
           if (hostprof) {
             hp_split += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - ts0).count();
@@ -2608,6 +2681,9 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           }
         }
         const int g = (int)std::max<int64_t>(16, std::min<int64_t>(kExpandWG, (std::max(nF, last_work) + 3) / 4));
+        // the merged launch may have expanded the whole return: its first
+        // batch may launch no level (spec_levels 0, then the count of V level 0)
+        if (!merge || small || !nF) spec_levels = std::max(spec_levels, 1);
         for (int batch = 0; !done; batch++) {
           // ctr->andmask is the AND of R as it grows (the insert and every
           // level add theirs): no pass over R unless counted classes need
@@ -2635,7 +2711,7 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
               (int64_t)(hCtr->nR + hCtr->nV + hCtr->cnt[k % 3]) > budget)
             break;
           if (hCtr->cnt[k % 3] == 0) break;  // the last level found nothing new
-          spec_levels = std::min(spec_levels * 2, 64);
+          spec_levels = std::min(std::max(1, spec_levels * 2), 64);
         }
         // levels this attempt expanded (a redone attempt's count too)
         const int64_t used = (int64_t)hCtr->levels - levels_seen;
@@ -2667,7 +2743,10 @@ int Rank::check(const lc_op *o, int64_t n, const lc_opts *opts_in, lc_key_result
           over = my_over;
         }
         // next return: as many speculative levels as this one needed, plus one
-        spec_levels = (int)std::max<int64_t>(spad > 0 ? 2 : 1, std::min<int64_t>(64, used + spad));
+        // (merged launches: plus LC_FX_MERGE_PAD, default 0: none when the merged
+        // launch finished the last return)
+        spec_levels = merge_on ? (int)std::min<int64_t>(64, used + mpad)
+                               : (int)std::max<int64_t>(spad > 0 ? 2 : 1, std::min<int64_t>(64, used + spad));
         const unsigned long long ex = hCtr->explored;
         explored_repl += (int64_t)(ex - explored_seen);
         explored_seen = ex;
