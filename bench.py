@@ -262,6 +262,7 @@ def main():
     if rank == 0 and not args.bare:
         if world == 1:  # first, in the timed loop's own state (no leg has run on the context yet)
             line["c3_shards"] = c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream)
+            line["resident32_leg"] = resident32_leg(ctx, abi, ops, key_off, d_ops, d_off, dev, stream)
         line["c1_leg"] = c1_leg(ctx, abi)
         line["host_leg"] = host_leg(ctx, abi, ops, key_off, n_inv)
         line["host_leg32"] = host_leg32(ctx, abi, ops, key_off)
@@ -340,6 +341,56 @@ def c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream, steps=200, warm
     for o in out:
         o["implied_speedup"] = base / o["implied_ms_per_step"]
     return out
+
+
+def resident32_leg(ctx, abi, ops, key_off, d_ops, d_off, dev, stream, steps=200, warmup=20):
+    """The same C2 batch as 24-byte lc_op32 records resident in HBM — the
+    format the JVM drop-in and the EDN reader hand over (ABI 4, lc_pack32's
+    output) — decided by lc_check_device32, which reads them as they are
+    (fast_tier32_kernel; a key handed to the later tiers would be widened
+    then), timed as the main loop times lc_check_device (every TIME_EVERY-th
+    step with HIP events).  Every result field is compared with the 48-byte
+    path's.  Not part of `value`, which stays on the 48-byte records of
+    SURVEY §8(b)'s boundary."""
+    import torch
+    n_keys = len(key_off) - 1
+    n_rec = int(key_off[-1] - key_off[0])
+    t0 = time.perf_counter()
+    o32, base = abi.pack32(ops, key_off)
+    pack_ms = (time.perf_counter() - t0) * 1e3
+    d32 = torch.from_numpy(np.ascontiguousarray(o32)).to(dev)
+    d_base = torch.from_numpy(np.ascontiguousarray(base)).to(dev)
+    nb = max(n_keys, 1) * abi.RESULT_DTYPE.itemsize
+    out32 = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    out48 = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    st = [ctx.bind_check_device32(d32.data_ptr(), d_off.data_ptr(), d_base.data_ptr(), n_keys,
+                                  out32.data_ptr(), stream=stream.cuda_stream,
+                                  opts=abi.default_opts(flags=f))
+          for f in (0, abi.LC_FLAG_NO_TIMING)]
+    for i in range(warmup):
+        st[i % TIME_EVERY != 0]()
+    torch.cuda.synchronize()
+    ctx.totals(reset=True)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        st[i % TIME_EVERY != 0]()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    tot = ctx.totals(reset=True)
+    kms = tot["fast_kernel_ms"] / max(1, tot["timed_calls"])
+    ctx.check_device(d_ops.data_ptr(), d_off.data_ptr(), n_keys, out48.data_ptr(),
+                     stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    r32 = np.frombuffer(out32.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)[:n_keys]
+    r48 = np.frombuffer(out48.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)[:n_keys]
+    algo = 24 * n_rec + ALGO_BYTES_PER_KEY * n_keys
+    return {"workload": "the C2 batch as 24-byte lc_op32 records resident in HBM (lc_check_device32)",
+            "ms_per_step": ms, "ops_per_s": n_rec / (ms * 1e-3), "kernel": "fast_tier32_kernel",
+            "kernel_ms": kms, "algorithmic_bytes_per_launch": algo,
+            "achieved_gb_per_s": algo / (kms * 1e-3) / 1e9 if kms > 0 else None,
+            "frac_of_hbm_peak": algo / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS if kms > 0 else None,
+            "pack32_ms": pack_ms, "valid": int((r32["verdict"] == 1).sum()),
+            "result_mismatches_vs_48_byte": int((r32 != r48).sum())}
 
 
 def c1_leg(ctx, abi):

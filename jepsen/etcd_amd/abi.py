@@ -425,6 +425,26 @@ class Context:
             raise LcError(rc, self.last_error())
         return rc
 
+    def bind_check_device32(self, d_ops32, d_key_off, d_key_base, n_keys, d_out, stream=None,
+                            opts=None):
+        """lc_check_device32 (ABI 4) with its arguments converted once, as
+        bind_check_device: 24-byte records resident on the device."""
+        L = lib()
+        o = opts if opts is not None else default_opts()
+        args = (self._h, ctypes.c_void_p(d_ops32), ctypes.c_void_p(d_key_off),
+                ctypes.c_void_p(d_key_base) if d_key_base else None, ctypes.c_int64(n_keys),
+                ctypes.byref(o), ctypes.c_void_p(d_out),
+                ctypes.c_void_p(stream) if stream else None, None)
+        fn = L.lc_check_device32
+
+        def call():
+            rc = fn(*args)
+            if rc != 0:
+                raise LcError(rc, self.last_error())
+
+        call._keep = (o,)
+        return call
+
     def bind_check_device(self, d_ops, d_key_off, n_keys, d_out, stream=None, opts=None,
                           stats=None):
         """check_device with its arguments converted once: returns a

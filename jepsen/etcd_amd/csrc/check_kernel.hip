@@ -1655,6 +1655,51 @@ __device__ __forceinline__ void fast_issue(const lc_op *__restrict__ kops, int n
   }
 }
 
+// The same records as lc_op32 (ABI 4): one thread's 24-byte records as
+// loaded — (f, value), (expected, version), (call, ret) — widened to the
+// 48-byte form only as pass 1 reads each (rec_raw), so the registers in
+// flight are half the 48-byte path's.  rec_raw widens exactly as
+// widen32_kernel does (the key's base re-added, LC_INF32 -> kInf), so every
+// decision equals the one on widened records.
+struct Raw32 {
+  int2 a, b, c;
+};
+struct FastRecs32 {
+  Raw32 w[kPer];
+};
+
+__device__ __forceinline__ void fast_issue(const lc_op32 *__restrict__ kops, int n, int tid,
+                                           FastRecs32 &b) {
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int r = tid + u * kFastThreads;
+    if (r < n) {
+      const int2 *q = reinterpret_cast<const int2 *>(kops + r);
+      b.w[u].a = q[0];
+      b.w[u].b = q[1];
+      b.w[u].c = q[2];
+    } else {
+      b.w[u].a = b.w[u].b = b.w[u].c = make_int2(0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ const Raw &rec_raw(const FastRecs &b, int u, int64_t) { return b.w[u]; }
+__device__ __forceinline__ Raw rec_raw(const FastRecs32 &b, int u, int64_t kbase) {
+  const Raw32 &q = b.w[u];
+  Raw r;
+  r.a = make_longlong2((int64_t)q.a.x, (int64_t)q.a.y);
+  r.b = make_longlong2((int64_t)q.b.x, (int64_t)q.b.y);
+  const uint32_t call = (uint32_t)q.c.x, ret = (uint32_t)q.c.y;
+  r.c = make_longlong2(kbase + (int64_t)call, ret == LC_INF32 ? kInf : kbase + (int64_t)ret);
+  return r;
+}
+// the key's first call (decode's base), a scalar load beside the records'
+__device__ __forceinline__ int64_t first_call(const lc_op *__restrict__ k, int64_t) { return k[0].call; }
+__device__ __forceinline__ int64_t first_call(const lc_op32 *__restrict__ k, int64_t kbase) {
+  return kbase + (int64_t)k[0].call;
+}
+
 // Timing condition max(A[0..k]) - 1 < B[k] for every position k < M (A holds
 // L + 1).  Thread t owns positions 4t..4t+3 (16-byte LDS reads).  The max
 // over earlier positions is: a DPP row scan, the row totals (v_readlane), and
@@ -2184,9 +2229,9 @@ __device__ __forceinline__ void fast_pass_on(int64_t key, const FastSinks &o, in
 // or at once for a key with nothing to decide — lets the persistent kernels
 // issue the next key's loads into them while this key is decided from LDS.
 // The crash-light pass (kModeLight) keeps the records for first_failure.
-template <int MODE, typename Next>
-__device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *__restrict__ kops,
-                                         const FastRecs &b, const KParams &p, FastLds &s,
+template <int MODE, typename Next, class Op = lc_op, class Recs = FastRecs>
+__device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__restrict__ kops,
+                                         int64_t kbase, const Recs &b, const KParams &p, FastLds &s,
                                          lc_key_result *__restrict__ out, const FastSinks &o,
                                          int32_t *__restrict__ wit, Next &&next) {
   // the thread index, opaque to the compiler: in the persistent kernels'
@@ -2240,7 +2285,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
   const int64_t base_idx = s.base;
 #else
   if (tid == 0) s.A[kFastMax] = 0;
-  const int64_t base_idx = kops[0].call;  // (a scalar load, beside the records')
+  const int64_t base_idx = first_call(kops, kbase);  // (a scalar load, beside the records')
   __syncthreads();
 #endif
   FGP_T(1);
@@ -2268,7 +2313,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
 #pragma unroll
   for (int u = 0; u < kPer; u++) {
     const int r = tid + u * kFastThreads;
-    const Raw &bw = b.w[u];
+    auto &&bw = rec_raw(b, u, kbase);
 
     bool placed = false;
     // crashed writes/CAS without a version (a malformed one among them
@@ -2428,8 +2473,9 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
     for (int u = 0; u < kPer; u++) {
       const int r = tid + u * kFastThreads;
       if (r >= n) continue;
-      const int f = (int)b.w[u].a.x, val = (int)b.w[u].a.y, exp = (int)b.w[u].b.x;
-      const int ver = (int)b.w[u].b.y;
+      auto &&bw = rec_raw(b, u, kbase);
+      const int f = (int)bw.a.x, val = (int)bw.a.y, exp = (int)bw.b.x;
+      const int ver = (int)bw.b.y;
       if (f != LC_F_READ) {
         const int pos = ver - V0 - 1;
         if (pos >= M || s.Own[pos] != r) {
@@ -2437,7 +2483,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const lc_op *
         } else if (f == LC_F_CAS && exp != (pos == 0 ? init : s.Val[pos - 1])) {
           hole = 1;
         }
-      } else if (ver != -1 && b.w[u].c.y != kInf) {
+      } else if (ver != -1 && bw.c.y != kInf) {
         const int k = ver - V0;
         if (k > M)
           hole = 1;  // a version no mutation wrote
@@ -2507,7 +2553,7 @@ __device__ __forceinline__ void fast_run(const lc_op *__restrict__ ops,
       fast_issue(ops + (nbeg - off0), nn > 0 && nn <= kFastMax ? (int)nn : 0, tid, r);
       if (nx2 < n_keys && lane < 2) offv = key_off[nx2 + lane];
     };
-    fast_key<MODE>(key, end - beg, ops + (beg - off0), r, p, s, out, o,
+    fast_key<MODE>(key, end - beg, ops + (beg - off0), 0, r, p, s, out, o,
                    o.wit ? o.wit + (beg - off0) : nullptr, next);
     if (nx >= n_keys) break;
     key = nx;
@@ -2527,7 +2573,25 @@ __device__ __forceinline__ void fast_one(const lc_op *__restrict__ ops,
   FastRecs r;
   if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
   if (threadIdx.x == 0) s.raised = 0;
-  fast_key<MODE>(key, end - beg, kops, r, p, s, out, o,
+  fast_key<MODE>(key, end - beg, kops, 0, r, p, s, out, o,
+                 o.wit ? o.wit + (beg - key_off[0]) : nullptr, [] {});
+}
+
+// fast_one over lc_op32 records (the native 24-byte pass, kernels *32 below)
+template <int MODE>
+__device__ __forceinline__ void fast_one32(const lc_op32 *__restrict__ ops,
+                                           const int64_t *__restrict__ key_off,
+                                           const int64_t *__restrict__ key_base, int64_t key,
+                                           const KParams &p, FastLds &s,
+                                           lc_key_result *__restrict__ out, const FastSinks &o) {
+  static_assert(!LC_PIPE, "the 24-byte pass reads its base per key, not from LDS (LC_PIPE)");
+  const int64_t beg = key_off[key], end = key_off[key + 1];
+  const lc_op32 *kops = ops + (beg - key_off[0]);
+  const int64_t kbase = key_base ? key_base[key] : 0;
+  FastRecs32 r;
+  if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
+  if (threadIdx.x == 0) s.raised = 0;
+  fast_key<MODE>(key, end - beg, kops, kbase, r, p, s, out, o,
                  o.wit ? o.wit + (beg - key_off[0]) : nullptr, [] {});
 }
 
@@ -2548,6 +2612,19 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
 #else
   fast_one<kModeFast>(ops, key_off, blockIdx.x, p, s, out, o);
 #endif
+}
+
+// The version-order tier over lc_op32 records (lc_check32 / lc_check_device32
+// without lc_aux outputs): the same decision on half the bytes; a key it
+// hands over is decided by the later tiers on the records widened then.
+__global__ __launch_bounds__(kFastThreads) void fast_tier32_kernel(
+    const lc_op32 *__restrict__ ops, const int64_t *__restrict__ key_off,
+    const int64_t *__restrict__ key_base, int64_t n_keys, const KParams p,
+    lc_key_result *__restrict__ out, int32_t *__restrict__ flags, KStatus *__restrict__ status,
+    int32_t *__restrict__ h_handoff) {
+  __shared__ FastLds s;
+  const FastSinks o{flags, status, h_handoff, nullptr, nullptr, nullptr};
+  if ((int64_t)blockIdx.x < n_keys) fast_one32<kModeFast>(ops, key_off, key_base, blockIdx.x, p, s, out, o);
 }
 
 // Crash-light pass over the keys the version-order tier handed to the gap
@@ -2604,6 +2681,15 @@ __global__ __launch_bounds__(kFastThreads) __attribute__((amdgpu_waves_per_eu(LC
     g_fgdone = 0;
   }
 #endif
+}
+
+// The fused pass over lc_op32 records (as fast_tier32_kernel)
+__global__ __launch_bounds__(kFastThreads) __attribute__((amdgpu_waves_per_eu(LC_FUSED_WPE, 8))) void fused_tier32_kernel(
+    const lc_op32 *__restrict__ ops, const int64_t *__restrict__ key_off,
+    const int64_t *__restrict__ key_base, int64_t n_keys, const KParams p,
+    lc_key_result *__restrict__ out, const FastSinks o) {
+  __shared__ FastLds s;
+  if ((int64_t)blockIdx.x < n_keys) fast_one32<kModeFused>(ops, key_off, key_base, blockIdx.x, p, s, out, o);
 }
 
 // Workspace layout per wave: 3 regions of cap Cfg, 2 tables of 2*cap Cfg,
@@ -3025,6 +3111,25 @@ hipError_t launch_fused_tier(const lc_op *d_ops, const int64_t *d_key_off, int64
       LC_PIPE ? std::min(n_keys, resident_wgs(fused_tier_kernel, 1, kFgLdsBytes)) : n_keys;
   hipLaunchKernelGGL(fused_tier_kernel, dim3((unsigned)wgs), dim3(kFastThreads),
                      (unsigned)kFgLdsBytes, stream, d_ops, d_key_off, n_keys, p, d_out, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_fast_tier32(const lc_op32 *d_ops, const int64_t *d_key_off, const int64_t *d_key_base,
+                              int64_t n_keys, const KParams &p, lc_key_result *d_out, int32_t *d_flags,
+                              KStatus *d_status, int32_t *h_handoff, hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fast_tier32_kernel, dim3((unsigned)n_keys), dim3(kFastThreads), 0, stream, d_ops,
+                     d_key_off, d_key_base, n_keys, p, d_out, d_flags, d_status, h_handoff);
+  return hipGetLastError();
+}
+
+hipError_t launch_fused_tier32(const lc_op32 *d_ops, const int64_t *d_key_off, const int64_t *d_key_base,
+                               int64_t n_keys, const KParams &p, lc_key_result *d_out, int32_t *d_flags,
+                               KStatus *d_status, int32_t *h_handoff, hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  const FastSinks o{d_flags, d_status, h_handoff, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL(fused_tier32_kernel, dim3((unsigned)n_keys), dim3(kFastThreads),
+                     (unsigned)kFgLdsBytes, stream, d_ops, d_key_off, d_key_base, n_keys, p, d_out, o);
   return hipGetLastError();
 }
 

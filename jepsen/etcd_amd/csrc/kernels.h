@@ -92,6 +92,15 @@ hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
 // are flagged for the handoff compaction (as launch_fast_tier), and go to the
 // gap tier without a crash-light pass.  status->n_light counts the keys that
 // took the crash-light decision.
+// The version-order tier / fused pass over lc_op32 records (ABI 4) with the
+// keys' bases (null: 0), no witnesses: same decisions as on the widened
+// records; the keys they hand over need the 48-byte records (launch_widen32).
+hipError_t launch_fast_tier32(const lc_op32 *d_ops, const int64_t *d_key_off, const int64_t *d_key_base,
+                              int64_t n_keys, const KParams &p, lc_key_result *d_out, int32_t *d_flags,
+                              KStatus *d_status, int32_t *h_handoff, hipStream_t stream);
+hipError_t launch_fused_tier32(const lc_op32 *d_ops, const int64_t *d_key_off, const int64_t *d_key_base,
+                               int64_t n_keys, const KParams &p, lc_key_result *d_out, int32_t *d_flags,
+                               KStatus *d_status, int32_t *h_handoff, hipStream_t stream);
 hipError_t launch_fused_tier(const lc_op *d_ops, const int64_t *d_key_off, int64_t n_keys,
                              const KParams &p, lc_key_result *d_out, int32_t *d_flags,
                              KStatus *d_status, int32_t *h_handoff, int32_t *d_witness,

@@ -310,6 +310,13 @@ struct WitOut {
   const int64_t *h_off = nullptr;
   // (not an output) lc_check's chunked copies, or null: the records are in place
   const Chunks *chunks = nullptr;
+  // (not an output) the first pass over lc_op32 records (lc_check32 /
+  // lc_check_device32 without lc_aux outputs): ops32 and the keys' bases
+  // (null: 0), indexed like d_ops / d_off; `widen` fills the 48-byte records
+  // the later tiers read (and names them) once a key is handed over
+  const lc_op32 *ops32 = nullptr;
+  const int64_t *base32 = nullptr;
+  std::function<int(const lc_op **)> widen;
 };
 
 // A gap-tier full-decision launch: its sizes and job (run_device).
@@ -370,6 +377,13 @@ void settle_timing(lc_ctx *c, Dev &d) {
     c->totals.fast_kernel_ms += ms;
     c->totals.kernel_ms += ms;
   }
+}
+
+// LC_NATIVE32=0 (A/B): 24-byte records are widened before the first pass, as
+// in the first ABI-4 build, instead of decided as they are
+bool native32_off() {
+  const char *e = getenv("LC_NATIVE32");
+  return e && e[0] == '0';
 }
 
 // Wait for the pass's follower signal (seq in *h_done): spin, checking the
@@ -530,8 +544,18 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   const bool signal = !wo.chunks && fast_on && n_keys > 0;
   const bool timing = !signal || !(flags & LC_FLAG_NO_TIMING);
   auto first_pass = [&](int64_t k0, int64_t nk, int64_t r0, int64_t nrec) -> int {
-    const lc_op *o = d_ops + r0;
     const int64_t *off = d_off + k0;
+    if (wo.ops32) {  // the native 24-byte pass (no lc_aux outputs)
+      const int64_t *base = wo.base32 ? wo.base32 + k0 : nullptr;
+      if (fused)
+        HIP_TRY(c, lcdev::launch_fused_tier32(wo.ops32 + r0, off, base, nk, p, d_out + k0,
+                                              d.d_flags + k0, d.d_status, d.h_handoff_dev, st));
+      else
+        HIP_TRY(c, lcdev::launch_fast_tier32(wo.ops32 + r0, off, base, nk, p, d_out + k0,
+                                             d.d_flags + k0, d.d_status, d.h_handoff_dev, st));
+      return 0;
+    }
+    const lc_op *o = d_ops + r0;
     int32_t *wit = want_wit ? wo.wit + r0 : nullptr;
     int32_t *kind = want_wit ? wo.kind + k0 : nullptr;
     if (want_wit)
@@ -556,7 +580,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       const int64_t k0 = ch->k[i], nk = ch->k[i + 1] - k0;
       const int64_t r0 = ch->r[i], nrec = ch->r[i + 1] - r0;
       if (nk <= 0) continue;
-      if (ch->d_ops32)
+      if (ch->d_ops32 && !wo.ops32)
         HIP_TRY(c, lcdev::launch_widen32(ch->d_ops32 + r0, d_off + k0,
                                          ch->d_base ? ch->d_base + k0 : nullptr, nk, ch->max_len,
                                          const_cast<lc_op *>(d_ops) + r0, st));
@@ -607,6 +631,9 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       d.status_dirty = false;
     }
     if (handed) {
+      // the native 24-byte pass: the later tiers read 48-byte records
+      if (wo.widen)
+        if (int e = wo.widen(&d_ops)) return e;
       HIP_TRY(c, lcdev::launch_handoff_compact(d.d_flags, d_off, n_keys, gap_on ? 1 : 0, d.d_jit,
                                                d.d_jit2, d.d_status, want_wit ? wo.kind : nullptr,
                                                st));
@@ -1351,6 +1378,18 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
     }
     wo.h_off = key_off + a;
     wo.chunks = &ch;
+    if (k32 && !want_wit && !want_cert && !(flags & LC_FLAG_NO_FAST_PATH) && !native32_off()) {
+      // decided from the 24-byte records; widened only if a key is handed over
+      wo.ops32 = static_cast<const lc_op32 *>(d.d_ops32);
+      wo.base32 = key_base ? d.d_base : nullptr;
+      wo.widen = [&](const lc_op **out) -> int {
+        HIP_TRY(c, lcdev::launch_widen32(static_cast<const lc_op32 *>(d.d_ops32), d.d_off,
+                                         key_base ? d.d_base : nullptr, nk, max_len,
+                                         static_cast<lc_op *>(d.d_ops), d.stream));
+        *out = static_cast<const lc_op *>(d.d_ops);
+        return 0;
+      };
+    }
     r = run_device(c, d, static_cast<const lc_op *>(d.d_ops), d.d_off, nk, p, d.d_out, d.stream,
                    flags, wo);
     join_helper();
@@ -1839,6 +1878,55 @@ int lc_check_device32(lc_ctx *c, const lc_op32 *d_ops, const int64_t *d_key_off,
   Dev &d = c->devs[0];
   HIP_TRY(c, hipSetDevice(d.id));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d.stream;
+  const int64_t flags = opts ? opts->flags : 0;
+  if (!(aux && (aux->witness || aux->certificate)) &&
+      !(flags & (LC_FLAG_NO_FAST_PATH | LC_FLAG_WHOLE_GPU)) && !native32_off()) {
+    // decided from the 24-byte records as they are; the 48-byte form (and
+    // the record count it needs, read from device memory) only if a key is
+    // handed over to the later tiers
+    lcdev::KParams p;
+    if (int rc = opts_to_params(c, opts, &p)) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    c->stats = lc_stats{};
+    WitOut wo;
+    wo.ops32 = d_ops;
+    wo.base32 = d_key_base;
+    wo.widen = [&](const lc_op **out) -> int {
+      int64_t *ends = reinterpret_cast<int64_t *>(d.h_status);  // (pinned; read before any later status copy)
+      HIP_TRY(c, hipMemcpyAsync(&ends[0], d_key_off, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      HIP_TRY(c, hipMemcpyAsync(&ends[1], d_key_off + n_keys, sizeof(int64_t), hipMemcpyDeviceToHost,
+                                st));
+      HIP_TRY(c, hipStreamSynchronize(st));
+      const int64_t nrec = ends[1] - ends[0];
+      if (nrec < 0) {
+        set_err(c, "lc_check_device32: key_off[n_keys] < key_off[0]");
+        return -EINVAL;
+      }
+      if (int e = ensure(c, reinterpret_cast<char **>(&d.d_ops), &d.ops_cap,
+                         sizeof(lc_op) * (size_t)std::max<int64_t>(nrec, 1)))
+        return e;
+      HIP_TRY(c, lcdev::launch_widen32(d_ops, d_key_off, d_key_base, n_keys, 4 * (nrec / n_keys + 1),
+                                       static_cast<lc_op *>(d.d_ops), st));
+      *out = static_cast<const lc_op *>(d.d_ops);
+      return 0;
+    };
+    int rc = run_device(c, d, nullptr, d_key_off, n_keys, p, d_out, st, flags, wo);
+    c->stats.kernel_ms = d.kernel_ms;
+    c->stats.fast_kernel_ms = d.fast_ms;
+    c->stats.jit_kernel_ms = d.jit_ms;
+    c->stats.n_jit_keys = d.n_jit;
+    c->stats.gap_kernel_ms = d.gap_ms;
+    c->stats.n_gap_keys = d.n_gap;
+    c->stats.hbm_kernel_ms = d.hbm_ms;
+    c->stats.n_hbm_keys = d.n_hbm;
+    c->stats.n_malformed = d.malformed;
+    c->stats.n_keys = n_keys;
+    c->stats.n_ops = -1;
+    c->stats.n_devices = 1;
+    c->stats.total_ms = std::chrono::duration<double, std::milli>(
+                            std::chrono::steady_clock::now() - t0).count();
+    return rc;
+  }
   // the record count lives in device memory: key_off[n_keys] - key_off[0]
   int64_t *ends = reinterpret_cast<int64_t *>(d.h_status);  // (pinned; free between calls)
   HIP_TRY(c, hipMemcpyAsync(&ends[0], d_key_off, sizeof(int64_t), hipMemcpyDeviceToHost, st));

@@ -267,3 +267,44 @@ def test_check32_fan_out_over_devices(monkeypatch):
     assert (got == want).all() and (got48 == want).all()
     assert prof["n_devices"] == 3 and prof["n_chunks"] >= 3
     assert prof["last_end_ms"] <= prof["joined_ms"] <= prof["total_ms"]
+
+
+@pytest.mark.gpu
+def test_check32_native_pass_equals_check(ctx):
+    """Without lc_aux outputs lc_check32 decides the 24-byte records as they
+    are (fast_tier32_kernel / fused_tier32_kernel), widening them only when a
+    key is handed over: every result field equals lc_check's on the golden
+    fixtures, batches through every tier (clean, crash-light via both passes,
+    invalid, C4-long, version-less) and the malformed keys."""
+    batches = []
+    for name in ("c1", "c5", "info", "tiny"):
+        z = np.load(os.path.join(GOLDEN, name + ".npz"))
+        batches.append((name, z["ops"], z["key_off"]))
+    for name, kw in (("clean", dict(n_keys=2000, ops_per_key=400, concurrency=20, seed=21)),
+                     ("c5", dict(n_keys=1000, ops_per_key=200, concurrency=10, p_anomaly=0.1,
+                                 seed=0x5EED0005)),
+                     ("crash", dict(n_keys=2000, ops_per_key=300, concurrency=20, p_info=0.05, seed=12)),
+                     ("c4", dict(n_keys=2, ops_per_key=5000, concurrency=50, p_info=0.2,
+                                 info_frac=0.2, p_anomaly=1.0, seed=1007))):
+        kw = dict(kw)
+        ops, off, _, _ = abi.synth(kw.pop("n_keys"), kw.pop("ops_per_key"), **kw)
+        batches.append((name, ops, off))
+    ops, off, _, _ = abi.synth(200, 150, concurrency=8, p_info=0.02, p_anomaly=0.3, seed=14)
+    ops = ops.copy()
+    ops[:, 3] = abi.LC_NIL
+    batches.append(("version-less", ops, off))
+    W, R = 1, 0
+    ops, off = pack_keys([[[W, 1, -1, 1, 5, 6], [W, 2, -1, 2, 3, 4]], [[1, 1, -1, 1, 5, 5]],
+                          [[1, 1 << 40, -1, 1, 0, 1]], [[7, 1, -1, 1, 0, 1]],
+                          [[W, 1, -1, 1, 0, 1], [W, 2, -1, 2, 2, 3], [R, 1, -1, 1, 4, 5]],
+                          [[W, 1, -1, 1, 0, 1], [R, 1, -1, 1 << 40, 2, 3]], [[W, 1, -1, -7, 0, 1]],
+                          [[W, 1, -1, 1, 0, 1], [W, 2, -1, 2, 1 << 33, (1 << 33) + 1]],
+                          [[W, 1, -1, 1, 0, 1]]])
+    batches.append(("malformed", ops, off))
+    for name, ops, off in batches:
+        o32, base = abi.pack32(ops, off)
+        for _ in range(2):  # a crash batch's second call takes the fused pass
+            _, want = ctx.check(ops, off, raise_on_error=False)
+            _, got = ctx.check32(o32, off, base, raise_on_error=False)
+            bad = np.nonzero(want != got)[0]
+            assert len(bad) == 0, (name, [(int(k), want[k].tolist(), got[k].tolist()) for k in bad[:5]])
