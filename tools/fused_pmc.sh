@@ -6,9 +6,9 @@ O=$R/gpurun_out/pmc_fused
 mkdir -p $O
 export TMPDIR=/tmp LC_FUSED=1
 cd /tmp
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $O/a -o a --output-format csv -- python3 $R/tools/leg.py crash 3 > $O/a.log 2>&1
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $O/a -o a --output-format csv -- python3 $R/tools/leg.py crashdev 3 > $O/a.log 2>&1
 echo pass a
-timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_SALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT -d $O/b -o b --output-format csv -- python3 $R/tools/leg.py crash 3 > $O/b.log 2>&1
+timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_SALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT -d $O/b -o b --output-format csv -- python3 $R/tools/leg.py crashdev 3 > $O/b.log 2>&1
 echo pass b
 python3 - <<'PY'
 import csv,glob,collections
