@@ -823,6 +823,9 @@ __device__ int match_branch_m(const Cmp<L> &c, int G, int n_opt, P brPos, P brVa
     MCLK0(tn);
     const bool filled = fill<L, CM>(c, G, n_opt, &ff, &stamp, st);
     MCLK1(tn, 7);
+#ifdef GAP_ONE_FILL  // dev timing build: every decision ends after its first fill (verdicts meaningless)
+    return filled ? GD_VALID : GD_INVALID;
+#endif
     if (filled) {
       // the matching ignored CAS expectations after free gaps: check them.
       // PREF: every violation whose expected value some eligible op writes
