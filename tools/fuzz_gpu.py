@@ -1,6 +1,7 @@
 """Dev: broad differential fuzz, GPU vs the oracle, over random histories:
 tiny random keys (brute-force sized), synthetic register keys across crash and
-anomaly rates and concurrencies, version-stripped keys (cas-register), mutex
+anomaly rates and concurrencies (each also as 24-byte records through lc_check32,
+field for field against the 48-byte call), version-stripped keys (cas-register), mutex
 and cas-register record generators, and the frontier exchange (one and three
 ranks) on version-less keys.  Prints mismatches; exits 1 on any.
     python tools/fuzz_gpu.py [rounds]"""
@@ -27,6 +28,11 @@ def compare(tag, ops, off, opts=None, algo=oracle.JITC, budget=1 << 18):
     global bad_total
     with abi.Context(device_mask=1) as ctx:
         _, g = ctx.check(ops, off, opts)
+        # the same batch as 24-byte records (lc_check32's native pass): every
+        # result field equal to the 48-byte call's
+        o32, b32 = abi.pack32(ops, off)
+        _, g32 = ctx.check32(o32, off, b32, opts)
+    n32 = int((g32 != g).sum())
     _, o = oracle.check(ops, off, algo=algo, n_threads=16, max_configs=budget,
                         init_version=opts.init_version if opts is not None else 0,
                         init_value=opts.init_value if opts is not None else -1)
@@ -36,12 +42,12 @@ def compare(tag, ops, off, opts=None, algo=oracle.JITC, budget=1 << 18):
         diff |= g["fail_op"] != o["fail_op"]
     bad = np.nonzero(known & diff)[0]
     gpu_unknown = int(((g["verdict"] == -1) & (o["verdict"] != -1)).sum())
-    print("%-34s keys %5d decided %5d gpu-only-unknown %3d mismatches %d (%.0fs)"
-          % (tag, len(off) - 1, int(known.sum()), gpu_unknown, len(bad), time.time() - t_start),
+    print("%-34s keys %5d decided %5d gpu-only-unknown %3d mismatches %d 32-bit %d (%.0fs)"
+          % (tag, len(off) - 1, int(known.sum()), gpu_unknown, len(bad), n32, time.time() - t_start),
           flush=True)
     for k in bad[:5]:
         print("   key", int(k), "gpu", g[k].tolist(), "oracle", int(o["verdict"][k]), int(o["fail_op"][k]))
-    bad_total += len(bad)
+    bad_total += len(bad) + n32
 
 
 for rd in range(rounds):
