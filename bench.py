@@ -405,6 +405,13 @@ def c1_leg(ctx, abi):
         t0 = time.perf_counter()
         _, r = ctx.check(ops, off)
         times.append((time.perf_counter() - t0) * 1e3)
+    # the drop-in's call: the same records as 24-byte lc_op32 (packed before)
+    o32, base = abi.pack32(ops, off)
+    times32 = []
+    for _ in range(6):
+        t0 = time.perf_counter()
+        _, r32 = ctx.check32(o32, off, base)
+        times32.append((time.perf_counter() - t0) * 1e3)
     best = None
     for name, algo in (("jit", oracle.JIT), ("wgl", oracle.WGL)):
         t0 = time.perf_counter()
@@ -414,6 +421,8 @@ def c1_leg(ctx, abi):
             best = (name, dt, o)
     return {"workload": "C1: 100 keys x 200 ops, concurrency 10 (host buffers)",
             "gpu_call_ms": float(np.median(times[1:])),
+            "gpu_call32_ms": float(np.median(times32[1:])),
+            "check32_result_mismatches": int((r32 != r).sum()),
             "cpu_oracle_ms": best[1], "cpu_oracle": best[0] + ", 1 thread",
             "valid": int((r["verdict"] == 1).sum()),
             "verdict_mismatches_vs_oracle": int((r["verdict"] != best[2]["verdict"]).sum())}
