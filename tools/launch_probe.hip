@@ -1,4 +1,5 @@
 // Dev probe: host-side cost of submitting one kernel launch, by launch API
+// (and a captured two-kernel graph against the two launches)
 // and argument size (the frontier exchange submits two launches per return,
 // the first with its ~2.7 KB window by value).  Batches of 200 launches of a
 // one-workgroup kernel are enqueued and timed on the host, then the stream is
@@ -69,5 +70,22 @@ int main() {
         hipExtLaunchKernelGGL(k_small, dim3(1), dim3(64), 0, st, nullptr, nullptr, 0, d, i);
       }))
     return 1;
+  // a captured graph of two launches (a step's pass and its follower) against
+  // the two launches themselves
+  if (run("two <<<>>> launches", [&](int i) {
+        k_small<<<1, 64, 0, st>>>(d, i);
+        k_small<<<1, 64, 0, st>>>(d + 4, i);
+      }))
+    return 1;
+  hipGraph_t g;
+  hipGraphExec_t ge;
+  CK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+  k_small<<<1, 64, 0, st>>>(d, 1);
+  k_small<<<1, 64, 0, st>>>(d + 4, 1);
+  CK(hipStreamEndCapture(st, &g));
+  CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  if (run("hipGraphLaunch (2 kernels)", [&](int) { (void)hipGraphLaunch(ge, st); })) return 1;
+  CK(hipGraphExecDestroy(ge));
+  CK(hipGraphDestroy(g));
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
