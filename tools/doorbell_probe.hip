@@ -92,6 +92,25 @@ __global__ void flag_k(uint32_t *h_done, uint32_t *ctr, int *out, uint32_t s) {
   }
 }
 
+// the same without the per-workgroup release and with relaxed counters: the
+// last workgroup alone fences (system scope) before its host store
+__global__ void flag_relaxed_k(uint32_t *h_done, uint32_t *ctr, int *out, uint32_t s) {
+  const int nshard = (int)min((unsigned)kShards, gridDim.x);
+  const int shard = blockIdx.x % nshard;
+  const uint32_t per = gridDim.x / nshard + (shard < (int)(gridDim.x % nshard) ? 1 : 0);
+  if (threadIdx.x == 0) {
+    out[blockIdx.x] = (int)s;
+    const uint32_t v = __hip_atomic_fetch_add(ctr + shard * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    if (v % per == 0) {
+      const uint32_t t = __hip_atomic_fetch_add(ctr + kShards * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+      if (t % (uint32_t)nshard == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(h_done, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
 __global__ void follow_k(uint32_t *h_done, uint32_t s) {
   if (threadIdx.x == 0) __hip_atomic_store(h_done, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -128,7 +147,7 @@ int main() {
   int khz = 100000;
   (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
   const int N = 500;
-  for (int grid : {1, 1250, 1792}) {
+  for (int grid : {1, 1250, 1792, 10000}) {
     printf("grid %4d launch ...\n", grid);
     // launch + events + event sync (lc_check_device today)
     for (int w = 0; w < 50; w++) hipLaunchKernelGGL(empty_k, dim3(grid), dim3(256), 0, st, d_out);
@@ -158,6 +177,21 @@ int main() {
     t1 = std::chrono::steady_clock::now();
     CK(hipStreamSynchronize(st));
     printf("grid %4d launch+kernel flag spin: %.2f us\n", grid,
+           std::chrono::duration<double, std::micro>(t1 - t0).count() / N);
+    // the same, relaxed counters, one fence by the last workgroup
+    CK(hipMemset(ctr, 0, 4 * (kShards + 1) * 32));
+    *(volatile uint32_t *)h_done = 0;
+    t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1; i <= (uint32_t)N; i++) {
+      hipLaunchKernelGGL(flag_relaxed_k, dim3(grid), dim3(256), 0, st, hd_dev, ctr, d_out, i);
+      if (!spin_until(h_done, i)) {
+        printf("grid %4d relaxed flag: request %u not seen in 100 ms (h_done %u)\n", grid, i, *h_done);
+        break;
+      }
+    }
+    t1 = std::chrono::steady_clock::now();
+    CK(hipStreamSynchronize(st));
+    printf("grid %4d launch+relaxed kernel flag spin: %.2f us\n", grid,
            std::chrono::duration<double, std::micro>(t1 - t0).count() / N);
     // launch, then a one-thread follower kernel writes the host flag (it
     // starts once the first kernel has retired, in stream order)
