@@ -185,6 +185,10 @@ struct Dev {
   uint32_t *h_done = nullptr, *h_done_dev = nullptr;
   uint32_t seq = 0;
   bool timing_pending = false;
+  // lc_check's small calls from pageable memory: inputs and outputs pass
+  // through this pinned buffer (kStageMax)
+  char *h_stage = nullptr;
+  size_t stage_cap = 0;
 };
 
 }  // namespace
@@ -297,6 +301,12 @@ struct Chunks {
 constexpr size_t kChunkBytes = size_t(24) << 20;
 constexpr size_t kChunkTail = size_t(2) << 20;
 constexpr int kMaxChunks = 48;
+// A call whose pageable inputs and outputs fit in kStageMax bytes copies them
+// through the device's pinned staging buffer (a memcpy on the host, then a
+// DMA from pinned memory): the runtime's pageable path costs tens of
+// microseconds per copy, which small calls (C1, C4, C5) pay in full.
+// LC_STAGE=0 (A/B): the pageable copies.
+constexpr size_t kStageMax = size_t(8) << 20;
 
 // Device-side lc_aux outputs of one run_device call (null: not wanted).
 struct WitOut {
@@ -1250,6 +1260,37 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
       rcs[di] = r;
       return;
     }
+    // small pageable calls: inputs (offsets, bases, records) and outputs
+    // (results, lc_aux arrays) through the pinned staging buffer
+    auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const bool pinned = is_pinned(c, ops + r0, in_bytes);
+    const size_t off_bytes = sizeof(int64_t) * (size_t)(nk + 1);
+    const size_t base_bytes = k32 && key_base ? sizeof(int64_t) * (size_t)nk : 0;
+    const size_t out_bytes =
+        up(sizeof(lc_key_result) * (size_t)nk) +
+        (want_wit ? up(sizeof(int32_t) * (size_t)nrec) + up(sizeof(int32_t) * (size_t)nk) : 0) +
+        (want_cert ? up(4 * sizeof(int32_t) * (size_t)nk) + up(sizeof(int32_t) * (size_t)nrec) : 0);
+    const size_t stage_need = up(off_bytes) + up(base_bytes) + up(in_bytes) + out_bytes;
+    const char *stage_env = getenv("LC_STAGE");
+    // (not with lc_aux outputs: the drop-in's C5 call with witnesses and
+    // certificates measured 0.05-0.1 ms slower staged)
+    const bool stage = !pinned && !want_wit && !want_cert && stage_need <= kStageMax &&
+                       !(stage_env && stage_env[0] == '0');
+    if (stage && d.stage_cap < stage_need) {
+      if (d.h_stage) (void)hipHostFree(d.h_stage);
+      d.h_stage = nullptr;
+      d.stage_cap = 0;
+      if (hipHostMalloc(reinterpret_cast<void **>(&d.h_stage), kStageMax, 0) != hipSuccess) {
+        set_err(c, "hipHostMalloc (staging) failed");
+        rcs[di] = -ENOMEM;
+        return;
+      }
+      d.stage_cap = kStageMax;
+    }
+    char *st_off = stage ? d.h_stage : nullptr;
+    char *st_base = stage ? st_off + up(off_bytes) : nullptr;
+    char *st_ops = stage ? st_base + up(base_bytes) : nullptr;
+    char *st_out = stage ? st_ops + up(in_bytes) : nullptr;
     // chunks: contiguous key ranges of about kChunkBytes of input records,
     // the last ones halving down to kChunkTail (cut at key boundaries)
     Chunks ch;
@@ -1295,12 +1336,17 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
     // the key offsets (and bases) lead; the compute stream waits for the
     // first chunk's event, which follows them on the copy stream
     hipError_t e = hipEventRecord(d.eh0, d.cst);
+    const void *src_off = key_off + a, *src_base = k32 && key_base ? key_base + a : nullptr;
+    if (stage) {
+      std::memcpy(st_off, src_off, off_bytes);
+      if (base_bytes) std::memcpy(st_base, src_base, base_bytes);
+      src_off = st_off;
+      src_base = st_base;
+    }
     if (e == hipSuccess)
-      e = hipMemcpyAsync(d.d_off, key_off + a, sizeof(int64_t) * (size_t)(nk + 1),
-                         hipMemcpyHostToDevice, d.cst);
-    if (e == hipSuccess && k32 && key_base)
-      e = hipMemcpyAsync(d.d_base, key_base + a, sizeof(int64_t) * (size_t)nk,
-                         hipMemcpyHostToDevice, d.cst);
+      e = hipMemcpyAsync(d.d_off, src_off, off_bytes, hipMemcpyHostToDevice, d.cst);
+    if (e == hipSuccess && base_bytes)
+      e = hipMemcpyAsync(d.d_base, src_base, base_bytes, hipMemcpyHostToDevice, d.cst);
     if (e != hipSuccess) {
       set_err(c, std::string("hipMemcpyAsync H2D: ") + hipGetErrorString(e));
       rcs[di] = -EIO;
@@ -1323,7 +1369,12 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
       const size_t o = sizeof(Op) * (size_t)ch.r[i];
       const size_t bytes = sizeof(Op) * (size_t)(ch.r[i + 1] - ch.r[i]);
       hipStream_t cs = i % 2 ? d.cst2 : d.cst;
-      hipError_t x = bytes ? hipMemcpyAsync(dst + o, src + o, bytes, hipMemcpyHostToDevice, cs)
+      const char *from = src + o;
+      if (stage && bytes) {
+        std::memcpy(st_ops + o, from, bytes);
+        from = st_ops + o;
+      }
+      hipError_t x = bytes ? hipMemcpyAsync(dst + o, from, bytes, hipMemcpyHostToDevice, cs)
                            : hipSuccess;
       if (x == hipSuccess) x = hipEventRecord(d.cev[(size_t)i], cs);
       return x;
@@ -1365,7 +1416,7 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
     };
     d.last.h2d_bytes = (int64_t)(in_bytes + sizeof(int64_t) * (size_t)(nk + 1) +
                                  (k32 && key_base ? sizeof(int64_t) * (size_t)nk : 0));
-    d.last.pinned = is_pinned(c, ops + r0, in_bytes);
+    d.last.pinned = pinned;
     WitOut wo;
     wo.n_records = nrec;
     if (want_wit) {
@@ -1402,21 +1453,35 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
       rcs[di] = r;
       return;
     }
-    e = hipMemcpyAsync(out + a, d.d_out, sizeof(lc_key_result) * (size_t)nk,
-                       hipMemcpyDeviceToHost, d.stream);
-    if (e == hipSuccess && want_wit && nrec)
-      e = hipMemcpyAsync(aux->witness + r0, d.d_wit, sizeof(int32_t) * (size_t)nrec,
-                         hipMemcpyDeviceToHost, d.stream);
-    if (e == hipSuccess && want_wit)
-      e = hipMemcpyAsync(aux->witness_kind + a, d.d_kind, sizeof(int32_t) * (size_t)nk,
-                         hipMemcpyDeviceToHost, d.stream);
-    if (e == hipSuccess && want_cert)
-      e = hipMemcpyAsync(aux->certificate + 4 * a, d.d_cert, 4 * sizeof(int32_t) * (size_t)nk,
-                         hipMemcpyDeviceToHost, d.stream);
-    if (e == hipSuccess && want_cert && aux->certificate_set && nrec)
-      e = hipMemcpyAsync(aux->certificate_set + r0, d.d_cset, sizeof(int32_t) * (size_t)nrec,
-                         hipMemcpyDeviceToHost, d.stream);
+    // outputs: straight into the caller's buffers, or (staged) into the
+    // pinned buffer and copied out once the stream is done
+    struct OutCopy {
+      void *to;
+      const void *from;
+      size_t bytes;
+    };
+    OutCopy oc[5];
+    int n_oc = 0;
+    oc[n_oc++] = {out + a, d.d_out, sizeof(lc_key_result) * (size_t)nk};
+    if (want_wit && nrec) oc[n_oc++] = {aux->witness + r0, d.d_wit, sizeof(int32_t) * (size_t)nrec};
+    if (want_wit) oc[n_oc++] = {aux->witness_kind + a, d.d_kind, sizeof(int32_t) * (size_t)nk};
+    if (want_cert) oc[n_oc++] = {aux->certificate + 4 * a, d.d_cert, 4 * sizeof(int32_t) * (size_t)nk};
+    if (want_cert && aux->certificate_set && nrec)
+      oc[n_oc++] = {aux->certificate_set + r0, d.d_cset, sizeof(int32_t) * (size_t)nrec};
+    size_t so = 0;
+    for (int i = 0; i < n_oc && e == hipSuccess; i++) {
+      void *to = stage ? st_out + so : oc[i].to;
+      so += up(oc[i].bytes);
+      e = hipMemcpyAsync(to, oc[i].from, oc[i].bytes, hipMemcpyDeviceToHost, d.stream);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
+    if (e == hipSuccess && stage) {
+      so = 0;
+      for (int i = 0; i < n_oc; i++) {
+        std::memcpy(oc[i].to, st_out + so, oc[i].bytes);
+        so += up(oc[i].bytes);
+      }
+    }
     if (e != hipSuccess) {
       set_err(c, std::string("hipMemcpyAsync D2H: ") + hipGetErrorString(e));
       rcs[di] = -EIO;
@@ -1579,6 +1644,7 @@ void lc_close(lc_ctx *c) {
     if (d.h_status) (void)hipHostFree(d.h_status);
     if (d.h_handoff) (void)hipHostFree(d.h_handoff);
     if (d.h_done) (void)hipHostFree(d.h_done);
+    if (d.h_stage) (void)hipHostFree(d.h_stage);
     if (d.e0) (void)hipEventDestroy(d.e0);
     if (d.e1) (void)hipEventDestroy(d.e1);
     if (d.e2) (void)hipEventDestroy(d.e2);
