@@ -1487,8 +1487,14 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
       rcs[di] = -EIO;
       return;
     }
+    // eh1 follows the last copy on the copy stream, which the compute stream
+    // waited for by the chunk's own event: it may complete a moment after the
+    // stream synchronised above (several device threads on one GPU), and an
+    // elapsed time read before then fails (h2d_ms would read 0)
     float hms = 0;
-    if (hipEventElapsedTime(&hms, d.eh0, d.eh1) == hipSuccess) d.last.h2d_ms = hms;
+    if (hipEventSynchronize(d.eh1) == hipSuccess &&
+        hipEventElapsedTime(&hms, d.eh0, d.eh1) == hipSuccess)
+      d.last.h2d_ms = hms;
     d.last.kernel_ms = d.kernel_ms;
     d.last.total_ms = std::chrono::duration<double, std::milli>(
                           std::chrono::steady_clock::now() - tw).count();
