@@ -307,6 +307,23 @@ constexpr int kMaxChunks = 48;
 // microseconds per copy, which small calls (C1, C4, C5) pay in full.
 // LC_STAGE=0 (A/B): the pageable copies.
 constexpr size_t kStageMax = size_t(8) << 20;
+bool stage_off() {
+  const char *e = getenv("LC_STAGE");
+  return e && e[0] == '0';
+}
+// The device's staging buffer (kStageMax bytes, allocated on first use), or
+// null with the context's error set.
+char *stage_buf(lc_ctx *c, Dev &d) {
+  if (!d.h_stage) {
+    if (hipHostMalloc(reinterpret_cast<void **>(&d.h_stage), kStageMax, 0) != hipSuccess) {
+      d.h_stage = nullptr;
+      set_err(c, "hipHostMalloc (staging) failed");
+      return nullptr;
+    }
+    d.stage_cap = kStageMax;
+  }
+  return d.h_stage;
+}
 
 // Device-side lc_aux outputs of one run_device call (null: not wanted).
 struct WitOut {
@@ -1271,21 +1288,12 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
         (want_wit ? up(sizeof(int32_t) * (size_t)nrec) + up(sizeof(int32_t) * (size_t)nk) : 0) +
         (want_cert ? up(4 * sizeof(int32_t) * (size_t)nk) + up(sizeof(int32_t) * (size_t)nrec) : 0);
     const size_t stage_need = up(off_bytes) + up(base_bytes) + up(in_bytes) + out_bytes;
-    const char *stage_env = getenv("LC_STAGE");
     // (not with lc_aux outputs: the drop-in's C5 call with witnesses and
     // certificates measured 0.05-0.1 ms slower staged)
-    const bool stage = !pinned && !want_wit && !want_cert && stage_need <= kStageMax &&
-                       !(stage_env && stage_env[0] == '0');
-    if (stage && d.stage_cap < stage_need) {
-      if (d.h_stage) (void)hipHostFree(d.h_stage);
-      d.h_stage = nullptr;
-      d.stage_cap = 0;
-      if (hipHostMalloc(reinterpret_cast<void **>(&d.h_stage), kStageMax, 0) != hipSuccess) {
-        set_err(c, "hipHostMalloc (staging) failed");
-        rcs[di] = -ENOMEM;
-        return;
-      }
-      d.stage_cap = kStageMax;
+    const bool stage = !pinned && !want_wit && !want_cert && stage_need <= kStageMax && !stage_off();
+    if (stage && !stage_buf(c, d)) {
+      rcs[di] = -ENOMEM;
+      return;
     }
     char *st_off = stage ? d.h_stage : nullptr;
     char *st_base = stage ? st_off + up(off_bytes) : nullptr;
@@ -2057,10 +2065,24 @@ int lc_check_frontiers(lc_ctx *c, const lc_op *ops, const int64_t *key_off, int6
   lc_fx_config *d_cfg = reinterpret_cast<lc_fx_config *>(d.d_gws);
   const lc_op *d_ops = static_cast<const lc_op *>(d.d_ops);
   hipStream_t st = d.stream;
-  HIP_TRY(c, hipMemcpyAsync(d.d_ops, ops + r0, sizeof(lc_op) * (size_t)nrec, hipMemcpyHostToDevice, st));
-  HIP_TRY(c, hipMemcpyAsync(d.d_off, key_off, sizeof(int64_t) * (size_t)(n_keys + 1),
-                            hipMemcpyHostToDevice, st));
-  HIP_TRY(c, hipMemcpyAsync(d_stop, stop_op, sizeof(int64_t) * (size_t)n_keys, hipMemcpyHostToDevice, st));
+  // the inputs: through the staging buffer when pageable and small (as lc_check's)
+  const void *src_ops = ops + r0, *src_off = key_off, *src_stop = stop_op;
+  const size_t ops_b = sizeof(lc_op) * (size_t)nrec, off_b = sizeof(int64_t) * (size_t)(n_keys + 1),
+               stop_b = sizeof(int64_t) * (size_t)n_keys;
+  if (ops_b + off_b + stop_b + 512 <= kStageMax && !stage_off() && !is_pinned(c, ops + r0, ops_b)) {
+    char *sb = stage_buf(c, d);
+    if (!sb) return -ENOMEM;
+    char *so = sb, *sf = so + ((ops_b + 255) & ~size_t(255)), *ss = sf + ((off_b + 255) & ~size_t(255));
+    std::memcpy(so, src_ops, ops_b);
+    std::memcpy(sf, src_off, off_b);
+    std::memcpy(ss, src_stop, stop_b);
+    src_ops = so;
+    src_off = sf;
+    src_stop = ss;
+  }
+  HIP_TRY(c, hipMemcpyAsync(d.d_ops, src_ops, ops_b, hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemcpyAsync(d.d_off, src_off, off_b, hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemcpyAsync(d_stop, src_stop, stop_b, hipMemcpyHostToDevice, st));
   HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
   d.status_dirty = true;
   HIP_TRY(c, lcdev::launch_frontier_dump(d_ops, d.d_off, d_stop, n_keys, p, d_cfg, max_per_key, d.d_jit,

@@ -2,7 +2,7 @@
 # small calls with and without it (LC_STAGE=0), interleaved
 set -o pipefail
 mkdir -p gpurun_out/stage
-[ "$1" = notests ] || { timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/stage/t.log 2>&1 || { tail -30 gpurun_out/stage/t.log; exit 1; }; }
+[ "$1" = notests ] || { timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/stage/t.log 2>&1 || { tail -30 gpurun_out/stage/t.log; exit 1; }; }
 [ "$1" = notests ] || tail -2 gpurun_out/stage/t.log
 for i in 1 2 3 4; do
   for s in 0 1; do
