@@ -304,9 +304,11 @@ constexpr int kMaxChunks = 48;
 // A call whose pageable inputs and outputs fit in kStageMax bytes copies them
 // through the device's pinned staging buffer (a memcpy on the host, then a
 // DMA from pinned memory): the runtime's pageable path costs tens of
-// microseconds per copy, which small calls (C1, C4, C5) pay in full.
+// microseconds per copy, which small calls (C1, C4) pay in full.  At a few
+// MB the runtime's path is the faster one again (a 4.8 MB input staged:
+// 0.07-0.15 ms slower, profiles/r05/stage_ab.txt).
 // LC_STAGE=0 (A/B): the pageable copies.
-constexpr size_t kStageMax = size_t(8) << 20;
+constexpr size_t kStageMax = size_t(2) << 20;
 bool stage_off() {
   const char *e = getenv("LC_STAGE");
   return e && e[0] == '0';
