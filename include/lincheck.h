@@ -224,13 +224,16 @@ typedef struct lc_aux {
  *   LC_CERT_PROOF    (ABI 4) c tokens in certificate_set[0 .. c): a case
  *                    analysis over who holds the open positions (needed, no
  *                    required holder), for infeasibility only the gap
- *                    matching's branching finds.  token = kind << 30 | a << 15
- *                    | b: FORCE (1) — position a has exactly one op able to
- *                    hold it under the choices so far, op b, which then holds
- *                    it; BRANCH (2) — position a has exactly b such ops, and b
- *                    sub-proofs follow, one per op in record order, each
- *                    assuming that op holds a; EMPTY (3) — no op can hold
- *                    position a.  A proof is FORCE* then BRANCH or EMPTY.
+ *                    matching's branching finds.  certificate_set holds only
+ *                    BRANCH tokens, in preorder: token = 2 << 30 | a << 15
+ *                    | b — position a has exactly b ops able to hold it under
+ *                    the choices so far, and b sub-proofs follow, one per op
+ *                    in record order, each assuming that op holds a.  Forced
+ *                    choices (a position with exactly one able op, which then
+ *                    holds it) and closing positions (no able op) are NOT
+ *                    written: a checker re-derives them by propagation before
+ *                    each token, as oracle/cert.c proof_ok does, and rejects
+ *                    a token whose position is forced or closed there.
  *                    "Able" is HALL's list of conditions, plus: an op chosen
  *                    at a+1 that is a CAS fixes the value a's holder writes,
  *                    one chosen at a-1 the value a CAS at a expects, and a

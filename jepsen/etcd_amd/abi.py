@@ -349,6 +349,9 @@ class Context:
         as pack32 makes them) and their key bases; returns as check()."""
         ops32 = as_ops32(ops32)
         base = None if key_base is None else np.ascontiguousarray(key_base, dtype=np.int64)
+        if base is not None and len(base) != len(key_off) - 1:
+            # lc_check32 reads n_keys bases: a short array would be read past its end
+            raise ValueError(f"key_base has {len(base)} entries for {len(key_off) - 1} keys")
         return self._check_host(lib().lc_check32, ops32, key_off, (_ptr(base),), opts,
                                 raise_on_error, witness, certificate)
 
@@ -363,7 +366,8 @@ class Context:
         key_off = np.ascontiguousarray(key_off, dtype=np.int64)
         n_keys = len(key_off) - 1
         stop = np.ascontiguousarray(stop_ops, dtype=np.int64)
-        assert len(stop) == n_keys
+        if len(stop) != n_keys:
+            raise ValueError(f"stop_ops has {len(stop)} entries for {n_keys} keys")
         buf = (LcFxConfig * max(1, n_keys * max_per_key))()
         n_out = np.zeros(max(n_keys, 1), dtype=np.int32)
         o = opts if opts is not None else default_opts()

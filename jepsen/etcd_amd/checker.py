@@ -219,7 +219,10 @@ class RegisterChecker:
                 if err is not None:
                     out["configs-error"] = err
             elif v == UNKNOWN:
-                out["cause"] = abi.REASONS.get(int(r["reason"]), "?")
+                # the Clojure shim's keys (mi355x.clj): :cause and :error
+                cause = abi.REASONS.get(int(r["reason"]), int(r["reason"]))
+                out["cause"] = cause
+                out["error"] = ["lincheck-reason", cause]
             results[k] = out
         if not self.independent:
             return results[None]
@@ -247,8 +250,13 @@ class RegisterChecker:
         parts = [ops[key_off[i]:key_off[i + 1]] for i in inv]
         sub_off = np.zeros(len(inv) + 1, dtype=np.int64)
         sub_off[1:] = np.cumsum([len(x) for x in parts])
-        got = self._context().check_frontiers(np.concatenate(parts), sub_off,
-                                              res["fail_op"][inv], D.MAX_ENTRIES, opts)
+        try:
+            got = self._context().check_frontiers(np.concatenate(parts), sub_off,
+                                                  res["fail_op"][inv], D.MAX_ENTRIES, opts)
+        except Exception:  # noqa: BLE001 — diagnostics only; the verdicts stand
+            # (as mi355x.clj batched-configs): every key falls back to the
+            # one-key re-search or its witness
+            return {}
         return {int(i): c for i, c in zip(inv, got) if c is not None}
 
     def _composed(self, k, linear, subs):

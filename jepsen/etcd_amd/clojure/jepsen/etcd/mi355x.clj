@@ -474,10 +474,13 @@
                                    (= 2 (.getInt kind (* 4 ki))))  ; LC_WITNESS_PREFIX
                     witness (when witnessed (vec (.getIntArray wit (* 4 k0) (count d))))]
                 [(nth keys ki)
+                 ;; the same keys as checker.py's map for the same history
                  (cond-> {:valid?   v
                           :analyzer :mi355x
-                          :configs-explored (.getLong out (+ b 24))}
+                          :configs-explored (.getLong out (+ b 24))
+                          :max-frontier (.getLong out (+ b 32))}
                    (false? v)     (merge {:op (op-map (nth d fail-op))
+                                          :fail-prefix-end fail-at
                                           :previous-ok (previous-ok d fail-at)
                                           ;; why the prefix at the failing return has no
                                           ;; linearization (include/lincheck.h LC_CERT_*)
@@ -521,7 +524,8 @@
                                                  (cond-> fa (:last-op wa) (assoc :last-op (:last-op wa)))
                                                  wa (merge wa (select-keys fa [:configs-error]))
                                                  :else fa)))
-                   (= v :unknown) (assoc :error [:lincheck-reason (reasons reason reason)]))]))))))
+                   (= v :unknown) (assoc :cause (reasons reason reason)
+                                         :error [:lincheck-reason (reasons reason reason)]))]))))))
 
 (defn linearizable
   "(checker/linearizable {:model m}) over the whole history, for the knossos
