@@ -133,6 +133,10 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         steps[i % TIME_EVERY != 0]()
+    # a batch of at most one key per resident workgroup (a C3 shard) is
+    # served by the resident version-order grid (lc_quiesce, lincheck.h):
+    # stopping it is part of the job, inside the timed region
+    ctx.quiesce()
     torch.cuda.synchronize()
     # this rank's own K steps; the job time is the MAX of these over ranks
     # (reduce_run).  The trailing barrier closes the timed region on every
@@ -301,7 +305,9 @@ def bind_steps(ctx, abi, d_ops, d_off, n_keys, d_out, stream):
 def c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream, steps=200, warmup=20):
     """A one-GPU predictor of BASELINE configs[2] (C3): the same C2 batch cut
     by lc_plan_partition into 1, 2, 4 and 8 shards, and each shard timed as
-    one lc_check_device step on this GPU.  A step at N GPUs takes as long as
+    one lc_check_device step on this GPU (a shard of at most one key per
+    resident workgroup — 8 shards of C2 — is served by the resident grid:
+    kernel_ms is then its device-clock time per request).  A step at N GPUs takes as long as
     its slowest shard (the ranks share nothing but the timing barrier), so
     max over shards is the implied N-GPU step and records / that the implied
     throughput.  A per-shard cost, not a scaling curve: the driver's 8-GPU
@@ -325,6 +331,7 @@ def c3_shards(ctx, abi, ops, key_off, d_ops, d_off, dev, stream, steps=200, warm
             t0 = time.perf_counter()
             for i in range(steps):
                 st2[i % TIME_EVERY != 0]()
+            ctx.quiesce()  # (the resident grid, as in the main loop)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3 / steps
             tot = ctx.totals(reset=True)

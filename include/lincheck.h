@@ -30,7 +30,8 @@ extern "C" {
 
 #define LC_ABI_VERSION 4  /* 3: lc_aux certificates, lc_device_stats, lc_host_register;
                              4: 24-byte lc_op32 records (lc_pack32, lc_check32,
-                             lc_check_device32), lc_last_call_profile */
+                             lc_check_device32), lc_last_call_profile, lc_quiesce
+                             (the resident version-order grid) */
 
 /* Op kinds: the three :f values of register.clj:98-100 (r / w / cas). */
 #define LC_F_READ  0
@@ -421,6 +422,16 @@ typedef struct lc_call_profile {
 } lc_call_profile;
 
 int lc_last_call_profile(lc_ctx *ctx, lc_call_profile *out);
+
+/* ABI 4: lc_check_device on a batch of at most one key per resident
+ * workgroup (1,536 on an MI355X) is served by a version-order grid that
+ * stays resident on the GPU between calls (no launch per call); it leaves on
+ * its own after LC_RESIDENT_IDLE_US microseconds (default 50) without a
+ * call, before any other work of the context runs on that GPU, and at
+ * lc_close.  lc_quiesce stops it now (a caller that is done calling, or
+ * wants the GPU to itself); the next call launches it again.  Returns 0, or
+ * -EIO.  LC_RESIDENT=0 in the environment disables the resident grid. */
+int lc_quiesce(lc_ctx *ctx);
 
 const char *lc_last_error(lc_ctx *ctx);
 void lc_close(lc_ctx *ctx);

@@ -170,6 +170,8 @@ def lib():
         L.lc_check_frontiers.restype = ctypes.c_int
         L.lc_last_totals.argtypes = [vp, ctypes.POINTER(LcTotals), i32]
         L.lc_last_totals.restype = ctypes.c_int
+        L.lc_quiesce.argtypes = [vp]
+        L.lc_quiesce.restype = ctypes.c_int
         L.lc_last_call_profile.argtypes = [vp, ctypes.POINTER(LcCallProfile)]
         L.lc_last_call_profile.restype = ctypes.c_int
         L.lc_key_cost.argtypes = [p, p, i64, p]
@@ -385,6 +387,13 @@ class Context:
             out.append([(int(c.version), int(c.value), tuple(int(c.pending[j]) for j in range(c.n_pending)))
                         for c in buf[k * max_per_key:k * max_per_key + n]])
         return out
+
+    def quiesce(self):
+        """lc_quiesce (ABI 4): stop the resident version-order grid now (it
+        otherwise leaves after LC_RESIDENT_IDLE_US without a call)."""
+        rc = lib().lc_quiesce(self._h)
+        if rc != 0:
+            raise LcError(rc, self.last_error())
 
     def totals(self, reset=False):
         """lc_last_totals (ABI 4): calls and device time summed since the last

@@ -1560,6 +1560,26 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
                    (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
 }
 
+// A key's result: a plain store, or (WT, the resident grid) write-through
+// eight-byte stores (sc1) that leave no line behind in this XCD's L2, so a
+// reader on any XCD sees them once the storing lane's stores have drained.
+typedef __attribute__((address_space(1))) uint64_t gu64_t;
+typedef __attribute__((address_space(1))) int64_t gi64_t;
+typedef __attribute__((address_space(1))) uint32_t gu32_t;
+template <bool WT>
+__device__ __forceinline__ void put_result(lc_key_result *o, const lc_key_result &r) {
+  if constexpr (WT) {
+    static_assert(sizeof(lc_key_result) == 40, "five words");
+    uint64_t w[5];
+    __builtin_memcpy(w, &r, sizeof(w));
+    gu64_t *g = (gu64_t *)o;
+#pragma unroll
+    for (int i = 0; i < 5; i++) __hip_atomic_store(g + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *o = r;
+  }
+}
+
 // Hand key over to the JIT tier (thread 0 only); tell the host there is work.
 // Hand key over (thread 0 only): a plain store of its flag (1: gap tier;
 // 2: jit-only — an :ok mutation without a version, a read [nil x],
@@ -2229,7 +2249,10 @@ __device__ __forceinline__ void fast_pass_on(int64_t key, const FastSinks &o, in
 // or at once for a key with nothing to decide — lets the persistent kernels
 // issue the next key's loads into them while this key is decided from LDS.
 // The crash-light pass (kModeLight) keeps the records for first_failure.
-template <int MODE, typename Next, class Op = lc_op, class Recs = FastRecs>
+// RES: the resident grid (below) — the key's first call comes through LDS
+// (thread 0 holds record 0) instead of a load that may be served from a
+// cache filled in an earlier request, and results are written through.
+template <int MODE, typename Next, class Op = lc_op, class Recs = FastRecs, bool RES = false>
 __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__restrict__ kops,
                                          int64_t kbase, const Recs &b, const KParams &p, FastLds &s,
                                          lc_key_result *__restrict__ out, const FastSinks &o,
@@ -2238,15 +2261,13 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
   // loop everything derived from it (LDS addresses, lane masks) would
   // otherwise be hoisted out and held in VGPRs across every key
   int tid = threadIdx.x;
-#if LC_PIPE
-  asm volatile("" : "+v"(tid));
-#endif
+  if constexpr (LC_PIPE || RES) asm volatile("" : "+v"(tid));
   const int lane = tid & (kWave - 1), w = __builtin_amdgcn_readfirstlane(tid / kWave);
   if (n64 <= 0 || n64 > kFastMax) {
     next();
     if (tid == 0) {
       if (n64 == 0)
-        out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 0};
+        put_result<RES>(out + key, lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 0});
       else
         fast_pass_on<MODE>(key, o, &s.raised);
     }
@@ -2276,18 +2297,19 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
     if (MODE != kModeFast || LC_PIPE)  // (claimed values start unclaimed)
       reinterpret_cast<int4 *>(s.Val)[tid] = make_int4(kAny, kAny, kAny, kAny);
   }
-#if LC_PIPE
-  if (tid == 0) {
-    s.A[kFastMax] = 0;
-    s.base = b.w[0].c.x;
+  int64_t base_idx;
+  if constexpr (LC_PIPE || RES) {
+    if (tid == 0) {
+      s.A[kFastMax] = 0;
+      s.base = rec_raw(b, 0, kbase).c.x;
+    }
+    __syncthreads();
+    base_idx = s.base;
+  } else {
+    if (tid == 0) s.A[kFastMax] = 0;
+    base_idx = first_call(kops, kbase);  // (a scalar load, beside the records')
+    __syncthreads();
   }
-  __syncthreads();
-  const int64_t base_idx = s.base;
-#else
-  if (tid == 0) s.A[kFastMax] = 0;
-  const int64_t base_idx = first_call(kops, kbase);  // (a scalar load, beside the records')
-  __syncthreads();
-#endif
   FGP_T(1);
   const int V0 = p.init_ver, init = p.init_val;
   int inel = 0, bad = 0, nmut = 0, jit_only = 0, giveup = 0, vbad = 0;
@@ -2513,7 +2535,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
   if (tid == 0) {
     const uint4 wb = *reinterpret_cast<const uint4 *>(s.wbad);
     if (!uni_bad && !(wb.x | wb.y | wb.z | wb.w))
-      out[key] = lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1};
+      put_result<RES>(out + key, lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1});
     else
       fast_pass_on<MODE>(key, o, &s.raised);
   }
@@ -2625,6 +2647,165 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier32_kernel(
   __shared__ FastLds s;
   const FastSinks o{flags, status, h_handoff, nullptr, nullptr, nullptr};
   if ((int64_t)blockIdx.x < n_keys) fast_one32<kModeFast>(ops, key_off, key_base, blockIdx.x, p, s, out, o);
+}
+
+// ---------------------------------------------------------------------------
+// Resident grid (kernels.h, launch_fast_resident).  A C3 shard's step (1,250
+// keys, ~12 us of kernel) paid ~10 us for its launch and the follower
+// kernel's completion signal; a grid that stays resident between calls pays
+// neither.  Memory protocol (MI355X_MICROARCH.md, inter-workgroup
+// visibility): the request is copied to device memory by write-through
+// stores, drained, then its number stored; every other workgroup polls that
+// one word with relaxed L1-bypassing loads and reads the request with such
+// loads; the records, offsets and first calls are also read L1-bypassing
+// (another kernel or a copy may have rewritten them since the last request,
+// while this CU's L1 still holds lines of them); results go out write-through
+// and each workgroup's storing lane drains its stores before it adds to the
+// arrival counter.
+
+// sc1 loads of this thread's records through a buffer descriptor whose range
+// check reads zeros past the key's end (the zero fill fast_issue does)
+__device__ __forceinline__ int64_t rfl64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t ld_wt(const int64_t *p) {
+  return __hip_atomic_load((gi64_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fast_issue_wt(const lc_op *kops, int n, int tid, FastRecs &b) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  void *base = reinterpret_cast<void *>(rfl64(reinterpret_cast<int64_t>(kops)));
+  const int bytes = __builtin_amdgcn_readfirstlane(n * (int)sizeof(lc_op));
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int off = (tid + u * kFastThreads) * (int)sizeof(lc_op);
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+    const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 16);
+    const u32x4 z = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 32, 0, 16);
+    __builtin_memcpy(&b.w[u].a, &x, 16);
+    __builtin_memcpy(&b.w[u].b, &y, 16);
+    __builtin_memcpy(&b.w[u].c, &z, 16);
+  }
+}
+
+// Key blockIdx.x of a request (rq: its words in LDS, read at use so nothing
+// of the request stays live across the request loop), as fast_one decides it
+__device__ __forceinline__ void fast_one_res(const uint64_t *rq, int64_t key, FastLds &s) {
+  auto w = [&](int i) { return rfl64((int64_t)res_val(rq[i])); };
+  const lc_op *ops = reinterpret_cast<const lc_op *>(w(0));
+  const int64_t *key_off = reinterpret_cast<const int64_t *>(w(1));
+  lc_key_result *out = reinterpret_cast<lc_key_result *>(w(3));
+  const FastSinks o{reinterpret_cast<int32_t *>(w(4)), reinterpret_cast<KStatus *>(w(5)),
+                    reinterpret_cast<int32_t *>(w(6)), nullptr, nullptr, nullptr};
+  KParams p;
+  p.init_ver = (int32_t)(uint32_t)w(7);
+  p.init_val = (int32_t)(uint32_t)w(8);
+  p.budget = 0;      // (the version-order tier reads neither)
+  p.time_ticks = 0;
+  const int64_t off0 = rfl64(ld_wt(key_off));
+  const int64_t beg = rfl64(ld_wt(key_off + key)), end = rfl64(ld_wt(key_off + key + 1));
+  const lc_op *kops = ops + (beg - off0);
+  const int64_t n = end - beg;
+  // (the thread index opaque, so the record offsets are not hoisted out of
+  // the request loop and held in VGPRs between requests)
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  FastRecs rr;
+  fast_issue_wt(kops, n > 0 && n <= kFastMax ? (int)n : 0, tid, rr);
+  if (tid == 0) s.raised = 0;
+  auto nop = [] {};
+  fast_key<kModeFast, decltype(nop) &, lc_op, FastRecs, true>(key, n, kops, 0, rr, p, s, out, o,
+                                                             nullptr, nop);
+}
+
+// every wait of the grid is bounded by a poll count too (a clock that did
+// not advance could not keep a wave alive) and the workgroups other than 0
+// by a wall-clock bound of their own
+constexpr uint32_t kResPollCap0 = 1u << 20;   // workgroup 0 (one PCIe read per poll)
+constexpr uint32_t kResPollCap = 1u << 22;    // the others (L2 reads)
+constexpr uint64_t kResStrayTicks = 20000000; // 200 ms of the 100 MHz clock
+
+// (6 waves per SIMD: at most 80 VGPRs and 104 SGPRs, six workgroups per CU,
+// 1,536 on the chip; left alone the request loop takes 84 VGPRs, and 7 per
+// CU spills)
+__global__ __launch_bounds__(kFastThreads, 6) void fast_resident_kernel(ResHost *h, ResDev *dv,
+                                                                        uint64_t idle_ticks) {
+  __shared__ FastLds s;
+  __shared__ uint64_t rq[kResWords];
+  const int tid = threadIdx.x;
+  const uint32_t G = gridDim.x;
+  const uint32_t nshard = min((uint32_t)kResShards, G), shard = blockIdx.x % nshard;
+  const uint32_t per = G / nshard + (shard < G % nshard ? 1u : 0u);
+  const bool first = blockIdx.x == 0;
+  gu64_t *const src = first ? (gu64_t *)h->req : (gu64_t *)dv->req;
+  uint32_t seq = 0;
+  uint64_t idle_from = wall_clock64();
+  for (;;) {
+    if (tid < kWave) {
+      // wave 0 takes request seq + 1: every word tagged with its number
+      // (workgroup 0 from host memory, the others from its copy)
+      const uint32_t want = (seq + 1) & 0xFFFFu;
+      const uint64_t t0 = wall_clock64();
+      uint64_t w = 0;
+      bool leave = false;
+      for (uint32_t polls = 0;; polls++) {
+        if (tid < kResWords)
+          w = first ? __hip_atomic_load(src + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                    : __hip_atomic_load(src + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all(tid >= kResWords || (uint32_t)(w >> 48) == want)) break;
+        const uint64_t now = wall_clock64();
+        if (first ? (now - idle_from > idle_ticks || polls >= kResPollCap0)
+                  : (now - t0 > kResStrayTicks || polls >= kResPollCap)) {
+          leave = true;
+          break;
+        }
+        if (first) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(4);
+      }
+      if (leave) {
+        // workgroup 0 on its idle bound: says so, and hands the others an
+        // exit request; the others on their stray bound just go
+        if (first && tid == 0)
+          __hip_atomic_store((gu32_t *)&h->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w = res_word(tid == 2 ? (uint64_t)kResExitKeys : 0u, want);
+      } else if (first && tid == 0) {
+        __hip_atomic_store((gu64_t *)&h->t0, (uint64_t)wall_clock64(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (tid < kResWords) {
+        if (first)
+          __hip_atomic_store((gu64_t *)dv->req + tid, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        rq[tid] = w;
+      }
+    }
+    __syncthreads();
+    seq++;
+    const int64_t n_keys = rfl64((int64_t)res_val(rq[2]));
+    if (n_keys == kResExitKeys) return;
+    // one key per workgroup (the host launches at least n_keys workgroups)
+    if ((int64_t)blockIdx.x < n_keys) fast_one_res(rq, blockIdx.x, s);
+    // (every key's LDS reads done before the next request's; rq rewritten
+    // only after this barrier)
+    __syncthreads();
+    if (tid == 0) {
+      // thread 0 made every global store of this workgroup (results,
+      // handoff flags and words, workgroup 0's detection time): drained
+      // before it arrives
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t v = __hip_atomic_fetch_add((gu32_t *)&dv->ticket[shard * 32], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT) + 1;
+      if (v % per == 0) {  // this shard's last arrival of this request
+        const uint32_t t = __hip_atomic_fetch_add((gu32_t *)&dv->top, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) + 1;
+        if (t % nshard == 0)  // the request's last arrival
+          __hip_atomic_store((gu64_t *)&h->done, (uint64_t)seq << 32 | (uint32_t)wall_clock64(),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    idle_from = wall_clock64();
+  }
 }
 
 // Crash-light pass over the keys the version-order tier handed to the gap
@@ -3036,6 +3217,14 @@ hipError_t launch_widen32(const lc_op32 *d_in, const int64_t *d_key_off, const i
   return hipGetLastError();
 }
 
+hipError_t launch_fast_resident(ResHost *h_res, ResDev *d_res, int64_t grid, uint64_t idle_ticks,
+                                hipStream_t stream) {
+  if (grid <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fast_resident_kernel, dim3((unsigned)grid), dim3(kFastThreads), 0, stream, h_res,
+                     d_res, idle_ticks);
+  return hipGetLastError();
+}
+
 hipError_t launch_done_signal(uint32_t *h_done, uint32_t seq, hipStream_t stream) {
   hipLaunchKernelGGL(done_signal_kernel, dim3(1), dim3(64), 0, stream, h_done, seq);
   return hipGetLastError();
@@ -3072,7 +3261,7 @@ hipError_t launch_witness_init(const lc_op *d_ops, const int64_t *d_key_off, int
 // grid): occupancy per CU x CUs, cached per device and kernel.
 template <typename K>
 static int64_t resident_wgs(K kernel, int which, size_t dyn_lds) {
-  static std::atomic<int> cache[64][2];
+  static std::atomic<int> cache[64][3];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   int c = cache[dev][which].load(std::memory_order_relaxed);
@@ -3088,6 +3277,16 @@ static int64_t resident_wgs(K kernel, int which, size_t dyn_lds) {
     cache[dev][which].store(c, std::memory_order_relaxed);
   }
   return c;
+}
+
+// (at most 6 per CU whatever the occupancy query says: the SGPR count admits
+// no more, and a workgroup that cannot become resident would never run)
+int64_t fast_resident_capacity() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    return 0;
+  return std::min<int64_t>(resident_wgs(fast_resident_kernel, 2, 0), 6 * (int64_t)cus);
 }
 
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,

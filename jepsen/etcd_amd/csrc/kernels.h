@@ -83,6 +83,52 @@ constexpr int kLdsCap = 128;     // configurations per LDS region (3 regions/wav
 // around the launch and waiting on the second: an empty 1,250-workgroup
 // launch took 10.1 us per step this way against 15.0 (tools/doorbell_probe.hip).
 hipError_t launch_done_signal(uint32_t *h_done, uint32_t seq, hipStream_t stream);
+
+// Resident version-order grid (check_kernel.hip, "Resident grid"): for
+// lc_check_device calls on batches of at most one key per resident
+// workgroup, a grid launched once stays on the GPU and serves request after
+// request, so back-to-back calls (a C3 shard's step) pay no launch and no
+// follower kernel.  A request is kResWords eight-byte words, each carrying
+// the request's number (mod 2^16) in its top 16 bits — the data is its own
+// flag: the host writes them to ResHost::req; wave 0 of workgroup 0 polls
+// that line (one PCIe read per poll) until every word carries the next
+// number, copies the words to ResDev::req with write-through stores, and
+// wave 0 of every other workgroup polls those until every word carries it.
+// Each workgroup then decides key blockIdx.x exactly as fast_tier_kernel
+// does (records, offsets and first calls read with L1-bypassing loads,
+// results written through) and, its stores drained, adds to a sharded
+// arrival counter; the last arrival stores (number << 32 | wall clock) to
+// ResHost::done.  A key the tier hands over is flagged as in
+// fast_tier_kernel (the host then stops the grid, whose exit publishes the
+// flags, before the later tiers run).  A request with n_keys == kResExitKeys
+// ends the grid; workgroup 0 also leaves after idle_ticks of the 100 MHz
+// wall clock without a request (ResHost::exited = 1; the others follow its
+// exit request), and every wait is bounded by a poll count too, so the grid
+// always drains.
+constexpr int kResWords = 9;   // ops, key_off, n_keys, out, flags, status, h_handoff, init_ver, init_val
+constexpr int kResShards = 16;
+constexpr int64_t kResExitKeys = (int64_t(1) << 47) - 1;
+__host__ __device__ inline uint64_t res_word(uint64_t v, uint32_t seq) {
+  return (v & ((uint64_t(1) << 48) - 1)) | (uint64_t)(seq & 0xFFFFu) << 48;
+}
+__host__ __device__ inline uint64_t res_val(uint64_t w) { return w & ((uint64_t(1) << 48) - 1); }
+struct alignas(128) ResHost {  // hipHostMalloc(Mapped | Coherent)
+  uint64_t req[16];            // host: the request words (kResWords used)
+  uint64_t done;               // device: (number << 32) | low 32 bits of the wall clock at completion
+  uint64_t t0;                 // device: wall clock (low 32 bits) when workgroup 0 saw the request
+  uint32_t exited;             // device: 1 once workgroup 0 left on its idle bound
+  uint32_t pad[27];
+};
+struct alignas(128) ResDev {   // hipMalloc, zeroed before each grid launch
+  uint64_t req[16];
+  uint32_t ticket[kResShards * 32];
+  uint32_t top;
+  uint32_t pad1[31];
+};
+hipError_t launch_fast_resident(ResHost *h_res, ResDev *d_res, int64_t grid, uint64_t idle_ticks,
+                                hipStream_t stream);
+// resident 256-thread workgroups of fast_resident_kernel on this device
+int64_t fast_resident_capacity();
 hipError_t launch_fast_tier(const lc_op *d_ops, const int64_t *d_key_off,
                             int64_t n_keys, const KParams &p,
                             lc_key_result *d_out, int32_t *d_flags,

@@ -185,6 +185,21 @@ struct Dev {
   uint32_t *h_done = nullptr, *h_done_dev = nullptr;
   uint32_t seq = 0;
   bool timing_pending = false;
+  // the resident version-order grid (kernels.h launch_fast_resident), on its
+  // own stream; res_grid: workgroups of the live grid (0: none)
+  lcdev::ResHost *res_h = nullptr, *res_h_dev = nullptr;
+  lcdev::ResDev *res_d = nullptr;
+  hipStream_t rst = nullptr;
+  int64_t res_grid = 0;
+  uint32_t res_seq = 0;
+  int res_khz = 0;          // the device's wall-clock rate
+  int64_t res_idle_us = 50; // LC_RESIDENT_IDLE_US (read at each grid launch)
+  int64_t res_cap = -1;     // lcdev::fast_resident_capacity() (once)
+  bool res_broken = false;  // a request the grid did not complete: launches only from then on
+  // this device's share of lc_last_totals: written only by the device's own
+  // thread during a call (check_host runs one per device), summed by
+  // lc_last_totals after the threads are joined
+  lc_totals tot{};
   // lc_check's small calls from pageable memory: inputs and outputs pass
   // through this pinned buffer (kStageMax)
   char *h_stage = nullptr;
@@ -207,7 +222,6 @@ struct lc_ctx {
   std::vector<std::pair<const char *, uint64_t>> pinned;
   std::mutex pin_mu;
   lc_call_profile prof{};  // lc_last_call_profile
-  lc_totals totals{};      // lc_last_totals
 };
 
 namespace {
@@ -402,9 +416,9 @@ void settle_timing(lc_ctx *c, Dev &d) {
   if (hipEventSynchronize(d.ef) == hipSuccess && hipEventElapsedTime(&ms, d.e0, d.ef) == hipSuccess) {
     d.fast_ms = ms;
     d.kernel_ms = ms;
-    c->totals.timed_calls++;
-    c->totals.fast_kernel_ms += ms;
-    c->totals.kernel_ms += ms;
+    d.tot.timed_calls++;
+    d.tot.fast_kernel_ms += ms;
+    d.tot.kernel_ms += ms;
   }
 }
 
@@ -438,6 +452,120 @@ int wait_done(lc_ctx *c, Dev &d, uint32_t seq, hipStream_t st) {
   }
 }
 
+// ---- Resident version-order grid (kernels.h, launch_fast_resident) ----
+// lc_check_device on a batch of at most one key per resident workgroup
+// (C3's 1,250-key shard) is served by a grid that stays on the GPU between
+// calls: the call writes the request and rings, the grid decides it and
+// signals, and back-to-back calls pay neither a launch nor the follower
+// kernel.  The grid leaves after LC_RESIDENT_IDLE_US (default 50) without a
+// request, before any other work of this library runs on the device, and at
+// lc_close.  LC_RESIDENT=0 turns it off (every call launches).
+bool resident_off() {
+  const char *e = getenv("LC_RESIDENT");
+  return e && e[0] == '0';
+}
+
+// Write request number d.res_seq + 1 (every word tagged with it).
+void res_ring(Dev &d, const uint64_t (&v)[lcdev::kResWords]) {
+  const uint32_t seq = ++d.res_seq;
+  for (int i = 0; i < lcdev::kResWords; i++)
+    __atomic_store_n(&d.res_h->req[i], lcdev::res_word(v[i], seq), __ATOMIC_RELEASE);
+}
+
+// Stop the grid (if one is live) and wait for it to leave.
+int res_stop(lc_ctx *c, Dev &d) {
+  if (!d.res_grid) return 0;
+  uint64_t v[lcdev::kResWords] = {};
+  v[2] = (uint64_t)lcdev::kResExitKeys;
+  res_ring(d, v);
+  d.res_grid = 0;
+  HIP_TRY(c, hipStreamSynchronize(d.rst));
+  return 0;
+}
+
+// One request: returns 0 with every key decided or flagged for the later
+// tiers (d.h_handoff as after fast_tier_kernel), its device time in
+// *dev_ms; 1 when the grid could not serve it (the caller launches
+// instead); or a negative error.
+int res_request(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off, int64_t n_keys,
+                const lcdev::KParams &p, lc_key_result *d_out, hipStream_t st, double *dev_ms) {
+  if (!d.res_h) {
+    if (hipHostMalloc(reinterpret_cast<void **>(&d.res_h), sizeof(lcdev::ResHost),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&d.res_h_dev), d.res_h, 0) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&d.res_d), sizeof(lcdev::ResDev)) != hipSuccess ||
+        hipStreamCreateWithFlags(&d.rst, hipStreamNonBlocking) != hipSuccess ||
+        hipDeviceGetAttribute(&d.res_khz, hipDeviceAttributeWallClockRate, d.id) != hipSuccess ||
+        d.res_khz <= 0) {
+      d.res_broken = true;
+      return 1;
+    }
+    std::memset(static_cast<void *>(d.res_h), 0, sizeof(lcdev::ResHost));
+  }
+  // the inputs (and this call's memsets) are ready once the caller's stream is
+  if (hipStreamQuery(st) != hipSuccess) HIP_TRY(c, hipStreamSynchronize(st));
+  lcdev::ResHost *h = d.res_h;
+  const uint64_t v[lcdev::kResWords] = {
+      (uint64_t)d_ops, (uint64_t)d_off, (uint64_t)n_keys, (uint64_t)d_out, (uint64_t)d.d_flags,
+      (uint64_t)d.d_status, (uint64_t)d.h_handoff_dev, (uint64_t)(uint32_t)p.init_ver,
+      (uint64_t)(uint32_t)p.init_val};
+  for (int attempt = 0; attempt < 3; attempt++) {
+    // a grid that left on its idle bound has finished (its stream drained)
+    // before a new one starts; a grid too small for this batch is stopped
+    if (d.res_grid && (__atomic_load_n(&h->exited, __ATOMIC_ACQUIRE) || d.res_grid < n_keys))
+      if (int e = res_stop(c, d)) return e;
+    if (!d.res_grid) {
+      // a new grid: numbering from 0 (no word tagged 1 yet), counters zero
+      for (int i = 0; i < 16; i++) __atomic_store_n(&h->req[i], 0, __ATOMIC_RELAXED);
+      __atomic_store_n(&h->exited, 0u, __ATOMIC_RELAXED);
+      __atomic_store_n(&h->done, 0, __ATOMIC_RELEASE);
+      d.res_seq = 0;
+      const char *ie = getenv("LC_RESIDENT_IDLE_US");  // (read at each launch)
+      d.res_idle_us = ie ? std::max<int64_t>(1, atoll(ie)) : 50;
+      HIP_TRY(c, hipMemsetAsync(d.res_d, 0, sizeof(lcdev::ResDev), d.rst));
+      HIP_TRY(c, lcdev::launch_fast_resident(d.res_h_dev, d.res_d, n_keys,
+                                             (uint64_t)d.res_idle_us * (uint64_t)d.res_khz / 1000u,
+                                             d.rst));
+      d.res_grid = n_keys;
+    }
+    res_ring(d, v);
+    const uint32_t seq = d.res_seq;
+    // wait for the completion; every 1,024 rounds check that the grid has
+    // not left (idle bound before the request: serve it from a new grid)
+    // and bound the wait (a request is at most ~0.1 ms of device work)
+    const auto t0 = std::chrono::steady_clock::now();
+    bool left = false;
+    for (uint32_t i = 1;; i++) {
+      const uint64_t dn = __atomic_load_n(&h->done, __ATOMIC_ACQUIRE);
+      if ((uint32_t)(dn >> 32) == seq) {
+        const uint32_t a = (uint32_t)__atomic_load_n(&h->t0, __ATOMIC_RELAXED);
+        *dev_ms = (double)(uint32_t)((uint32_t)dn - a) / (double)d.res_khz;
+        return 0;
+      }
+      if ((i & 1023) == 0) {
+        if (__atomic_load_n(&h->exited, __ATOMIC_ACQUIRE)) {
+          left = true;
+          break;
+        }
+        const hipError_t q = hipStreamQuery(d.rst);
+        if (q != hipSuccess && q != hipErrorNotReady) {
+          set_err(c, std::string("resident grid: ") + hipGetErrorString(q));
+          d.res_grid = 0;
+          d.res_broken = true;
+          return -EIO;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) break;
+      }
+    }
+    if (int e = res_stop(c, d)) return e;
+    if (!left) break;  // not served in 500 ms: launches from now on
+    // (the grid left before it saw the request: the host was away longer
+    // than the idle bound) — again, from a new grid
+  }
+  d.res_broken = true;
+  return 1;
+}
+
 // Run the tiers for n_keys keys whose device arrays are in place.
 int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                int64_t n_keys, const lcdev::KParams &p,
@@ -445,7 +573,7 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                const WitOut &wo = WitOut()) {
   (void)settle_status(d);  // before use_fused or h_status is read
   settle_timing(c, d);     // before e0 / ef are recorded again
-  c->totals.calls++;
+  d.tot.calls++;
   d.kernel_ms = d.hbm_ms = d.fast_ms = d.jit_ms = d.gap_ms = 0;
   d.n_hbm = d.n_jit = d.n_gap = 0;
   d.malformed = 0;
@@ -571,7 +699,30 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   // signal (kernels.h launch_done_signal) instead of an event wait; with
   // LC_FLAG_NO_TIMING it records no events around the pass either.
   const bool signal = !wo.chunks && fast_on && n_keys > 0;
-  const bool timing = !signal || !(flags & LC_FLAG_NO_TIMING);
+  bool timing = !signal || !(flags & LC_FLAG_NO_TIMING);
+  // the resident grid serves lc_check_device's plain version-order pass on
+  // a batch of at most one key per resident workgroup (res_request); any
+  // other call on this device first stops a live grid
+  if (d.res_cap < 0) d.res_cap = lcdev::fast_resident_capacity();
+  const bool resident = signal && !fused && !want_wit && !wo.ops32 && !d.res_broken &&
+                        n_keys <= d.res_cap && !resident_off();
+  int res_rc = 1;  // 0: the grid decided the pass
+  double res_ms = 0;
+  if (resident) {
+    res_rc = res_request(c, d, d_ops, d_off, n_keys, p, d_out, st, &res_ms);
+    if (res_rc < 0) return res_rc;
+    if (res_rc == 1) {
+      // not served (the grid may have decided part of it): launch instead,
+      // from the state the pass starts from
+      HIP_TRY(c, hipMemsetAsync(d.d_status, 0, sizeof(lcdev::KStatus), st));
+      HIP_TRY(c, hipMemsetAsync(d.d_flags, 0, d.flags_cap, st));
+      __atomic_store_n(d.h_handoff, 0, __ATOMIC_RELEASE);
+    } else {
+      timing = true;  // (the grid's device clock: free)
+    }
+  } else if (d.res_grid) {
+    if (int e = res_stop(c, d)) return e;
+  }
   auto first_pass = [&](int64_t k0, int64_t nk, int64_t r0, int64_t nrec) -> int {
     const int64_t *off = d_off + k0;
     if (wo.ops32) {  // the native 24-byte pass (no lc_aux outputs)
@@ -598,8 +749,13 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
                                          d.h_handoff_dev, st));
     return 0;
   };
-  if (timing) HIP_TRY(c, hipEventRecord(d.e0, st));
-  if (const Chunks *ch = wo.chunks) {
+  if (res_rc == 0) {
+    // (decided by the resident grid)
+  } else if (timing) {
+    HIP_TRY(c, hipEventRecord(d.e0, st));
+  }
+  if (res_rc == 0) {
+  } else if (const Chunks *ch = wo.chunks) {
     // lc_check's pipeline: chunk i's copy is issued, the compute stream
     // waits for it, widens it (24-byte records) and decides its keys while
     // the copy engine moves chunk i + 1
@@ -619,8 +775,13 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     return e;
   }
   if (fast_on) {
-    if (timing) HIP_TRY(c, hipEventRecord(d.ef, st));
-    if (signal) {
+    if (res_rc == 0) {
+      // (completed already)
+    } else if (timing) {
+      HIP_TRY(c, hipEventRecord(d.ef, st));
+    }
+    if (res_rc == 0) {
+    } else if (signal) {
       HIP_TRY(c, lcdev::launch_done_signal(d.h_done_dev, ++d.seq, st));
       if (int e = wait_done(c, d, d.seq, st)) return e;
     } else {
@@ -629,7 +790,16 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
     n_jit = 0;
     jit_list = d.d_jit;
     const bool handed = __atomic_load_n(d.h_handoff, __ATOMIC_ACQUIRE) != 0;
-    if (signal && !handed) {
+    if (res_rc == 0) {
+      d.fast_ms = res_ms;
+      if (handed) {
+        // the grid's exit publishes the flags and the status words to the
+        // later tiers (and frees its CUs); their times are measured from here
+        if (int e = res_stop(c, d)) return e;
+        HIP_TRY(c, hipEventRecord(d.e0, st));
+        HIP_TRY(c, hipEventRecord(d.ef, st));
+      }
+    } else if (signal && !handed) {
       // every key decided: the pass's event time (if any) is read later
       d.timing_pending = timing;
     } else {
@@ -727,9 +897,9 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   if (n_jit == 0 && n_direct == 0) {
     d.kernel_ms = d.fast_ms + d.gap_ms;
     if (!d.timing_pending && timing) {
-      c->totals.timed_calls++;
-      c->totals.fast_kernel_ms += d.fast_ms;
-      c->totals.kernel_ms += d.kernel_ms;
+      d.tot.timed_calls++;
+      d.tot.fast_kernel_ms += d.fast_ms;
+      d.tot.kernel_ms += d.kernel_ms;
     }
     // after a handoff d_status is not zero: cleared behind this call's work
     // (the host has read it), not in front of the next call's
@@ -916,10 +1086,10 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
   HIP_TRY(c, hipStreamSynchronize(st));
   d.status_dirty = false;
   if (timing) {
-    c->totals.timed_calls++;
-    c->totals.fast_kernel_ms += d.fast_ms;
+    d.tot.timed_calls++;
+    d.tot.fast_kernel_ms += d.fast_ms;
   }
-  c->totals.kernel_ms += d.kernel_ms + d.hbm_ms;
+  d.tot.kernel_ms += d.kernel_ms + d.hbm_ms;
   return 0;
 }
 
@@ -1630,6 +1800,11 @@ int lc_open(uint32_t device_mask, lc_ctx **out) {
         lc_close(c);
         return -ENODEV;
       }
+      // pinned memory may be reused from a closed context: the completion
+      // word must not already hold this context's first sequence number
+      __atomic_store_n(d.h_done, 0u, __ATOMIC_RELEASE);
+      __atomic_store_n(d.h_handoff, 0, __ATOMIC_RELEASE);
+      __atomic_store_n(d.h_handoff + 1, 0, __ATOMIC_RELEASE);
       c->devs.push_back(d);
     }
     if (virt >= 2) break;
@@ -1649,6 +1824,10 @@ void lc_close(lc_ctx *c) {
   for (auto &pr : c->pinned) (void)hipHostUnregister(const_cast<char *>(pr.first));
   for (Dev &d : c->devs) {
     (void)hipSetDevice(d.id);
+    (void)res_stop(c, d);
+    if (d.rst) (void)hipStreamDestroy(d.rst);
+    if (d.res_d) (void)hipFree(d.res_d);
+    if (d.res_h) (void)hipHostFree(d.res_h);
     if (d.stream) (void)hipStreamSynchronize(d.stream);
     if (d.d_ops) (void)hipFree(d.d_ops);
     if (d.d_off) (void)hipFree(d.d_off);
@@ -1711,11 +1890,28 @@ int lc_last_stats(lc_ctx *c, lc_stats *out) {
   return 0;
 }
 
+int lc_quiesce(lc_ctx *c) {
+  if (!c) return -EINVAL;
+  for (Dev &d : c->devs) {
+    if (!d.res_grid) continue;
+    (void)hipSetDevice(d.id);
+    if (int e = res_stop(c, d)) return e;
+  }
+  return 0;
+}
+
 int lc_last_totals(lc_ctx *c, lc_totals *out, int32_t reset) {
   if (!c || !out) return -EINVAL;
-  for (Dev &d : c->devs) settle_timing(c, d);
-  *out = c->totals;
-  if (reset) c->totals = lc_totals{};
+  lc_totals t{};
+  for (Dev &d : c->devs) {
+    settle_timing(c, d);
+    t.calls += d.tot.calls;
+    t.timed_calls += d.tot.timed_calls;
+    t.fast_kernel_ms += d.tot.fast_kernel_ms;
+    t.kernel_ms += d.tot.kernel_ms;
+    if (reset) d.tot = lc_totals{};
+  }
+  *out = t;
   return 0;
 }
 

@@ -27,7 +27,7 @@ def untok(t):
     return t >> 30, (t >> 15) & 0x7FFF, t & 0x7FFF
 
 
-def find(recs, cut, v0=0, init=-1, proof=True):
+def find(recs, cut, v0=0, init=-1, proof=True, proof_budget=PROOF_NODES):
     n = len(recs)
     inp = [r[4] <= cut for r in recs]
     req = [inp[i] and recs[i][5] <= cut for i in range(n)]
@@ -155,7 +155,8 @@ def find(recs, cut, v0=0, init=-1, proof=True):
     # fixes the value or uses the op another one needs): a proof by forced
     # choices and case splits over the candidates (LC_CERT_PROOF), as the
     # device's finder searches for it (cert.hip, prove)
-    toks = prove(recs, gaps, held, claim, inp, req, mut, pin, pos, v0, init) if proof else None
+    toks = (prove(recs, gaps, held, claim, inp, req, mut, pin, pos, v0, init, proof_budget)
+            if proof else None)
     if toks is not None and len(toks) <= n and max(gaps) < 1 << 15 and n <= 1 << 15:
         return (PROOF, -1, -1, len(toks), toks)
     return (NONE, -1, -1, 0, [])

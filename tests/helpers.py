@@ -178,3 +178,34 @@ def dup_versions(keys, seed, frac=0.5):
             recs[b][3] = recs[a][3]
         out.append(recs)
     return out
+
+
+def proof_cap_key(k_free=10, conflict=3, pad=2100):
+    """An invalid version-pinned key whose refutation needs a case analysis
+    larger than the certificate finder's PROOF search budget (2,048 nodes,
+    cert.hip / tests/cert_ref.py) but whose proof would fit the key's
+    certificate set (one token per record): positions 0..k_free-1 each need
+    a distinct value (a read of version p+1 claims it) and have two crashed
+    writes of that value; the last `conflict` positions all need value 99
+    and only conflict-1 crashed writes of 99 exist.  The search splits every
+    free position before it reaches the conflict, so its tree has ~2^(k_free
+    + 2) nodes and 2^(k_free + 1) - 1 case splits.  Reads [nil nil] after the
+    failing return pad the key to `pad` records.  Fails at the read of
+    version k_free + conflict (record index 3 k_free + 2 conflict + 1)."""
+    recs, t = [], 0
+    vals = list(range(k_free)) + [99] * conflict
+    for p in range(k_free + conflict):
+        if p < k_free:
+            for _ in range(2):
+                recs.append([W, p, N, N, t, INF])
+                t += 1
+        elif p == k_free:
+            for _ in range(conflict - 1):
+                recs.append([W, 99, N, N, t, INF])
+                t += 1
+        recs.append([R, vals[p], N, p + 1, t, t + 1])
+        t += 2
+    while len(recs) < pad:
+        recs.append([R, N, N, N, t, t + 1])
+        t += 2
+    return recs

@@ -217,3 +217,25 @@ def test_tampered_proofs_are_rejected():
             assert st[0] == oracle.CERT_BAD, (i, toks, v)
             n_checked += 1
     assert n_checked > 100 and max(lens) >= 1, (n_checked, lens)
+
+
+def test_proof_search_budget_is_the_cap():
+    """helpers.proof_cap_key: invalid, and refutable only by a case analysis
+    of 2,047 splits.  At the finder's budget (2,048 nodes, the device's
+    cert.hip kNodes) the PROOF search gives up — no certificate, never a
+    wrong one — and with a larger budget the same finder's proof is accepted
+    by the checker: what stops it is the node cap, not the token room (one
+    token per record of the key)."""
+    from helpers import proof_cap_key
+    recs = proof_cap_key()
+    ops, off = pack_keys([recs])
+    _, j = oracle.check(ops, off, algo=oracle.JITC, n_threads=1, max_configs=1 << 22)
+    assert j["verdict"][0] == 0 and j["fail_op"][0] == 34
+    cut = int(j["fail_prefix_end"][0])
+    assert cert_ref.find([tuple(r) for r in recs], cut)[0] == cert_ref.NONE
+    kind, a, b, c, toks = cert_ref.find([tuple(r) for r in recs], cut, proof_budget=1 << 16)
+    assert kind == cert_ref.PROOF and c == len(toks) == 2047 <= len(recs)
+    cert = np.array([kind, a, b, c], dtype=np.int32)
+    cset = np.zeros(len(recs), dtype=np.int32)
+    cset[:c] = toks
+    assert oracle.check_certificate(ops, off, cert, cset, _res(np.array([cut])))[0] == oracle.CERT_OK

@@ -323,3 +323,23 @@ def test_gap_tier_early_launch_equal(ctx, monkeypatch, seed):
     assert (a == b).all() and (ka == kb).all() and (wa == wb).all()
     certify(ops, off, b, wb, kb)
     assert (b["verdict"][:6] == 0).any() and (b["verdict"] == 1).any()
+
+
+def test_proof_search_over_its_cap_leaves_no_certificate(ctx):
+    """helpers.proof_cap_key: the device's PROOF search (cert.hip, 2,048
+    nodes) runs out before it refutes the failing prefix.  The key stays
+    invalid with the oracle's fail op and a checked PREFIX witness, and
+    carries LC_CERT_NONE (certified on the witness side only) — next to a
+    branch-fixture key the same call proves, so the cap is per key."""
+    from helpers import proof_cap_key
+    z = np.load(os.path.join(GOLDEN, "branch.npz"))
+    k0 = [z["ops"][z["key_off"][0]:z["key_off"][1]].tolist()]
+    ops, off = pack_keys([proof_cap_key()] + k0)
+    _, r, wit, kind, cert, cset = ctx.check(ops, off, witness=True, certificate=True)
+    assert list(r["verdict"]) == [0, 0] and r["fail_op"][0] == 34
+    assert r["fail_op"][1] == z["fail_op"][0]
+    assert list(kind) == [abi.LC_WITNESS_PREFIX, abi.LC_WITNESS_PREFIX]
+    certify(ops, off, r, wit, kind)
+    assert cert[0, 0] == abi.LC_CERT_NONE and cert[1, 0] == abi.LC_CERT_PROOF
+    st = oracle.check_certificate(ops, off, cert.reshape(-1), cset, r)
+    assert st[1] == oracle.CERT_OK

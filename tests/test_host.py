@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     assert set(names) == {
         "lc_open", "lc_check", "lc_check_device", "lc_last_stats", "lc_last_error",
         "lc_pack32", "lc_check32", "lc_check_device32", "lc_last_call_profile",
-        "lc_check_frontiers", "lc_edn_ops32", "lc_edn_key_base", "lc_last_totals",
+        "lc_check_frontiers", "lc_edn_ops32", "lc_edn_key_base", "lc_last_totals", "lc_quiesce",
         "lc_last_device_stats", "lc_host_register", "lc_host_unregister",
         "lc_close", "lc_default_opts", "lc_plan_partition", "lc_abi_version",
         "lc_check_ex", "lc_check_device_ex", "lc_key_cost", "lc_build_id",

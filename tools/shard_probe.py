@@ -37,6 +37,7 @@ def main():
             t0 = time.perf_counter()
             for _ in range(steps):
                 call()
+            ctx.quiesce()
             torch.cuda.synchronize()
             us = (time.perf_counter() - t0) * 1e6 / steps
             res = np.frombuffer(out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)[:nk]
