@@ -56,6 +56,14 @@ __device__ unsigned int g_fgdone;
 #define FGP_ADD(i, a, b)
 #endif
 
+#ifdef LC_FAST_PROF  // dev only: per-phase clocks of fast_tier_kernel (thread 0), summed over keys
+__device__ unsigned long long g_fp[8];
+__device__ unsigned int g_fpdone;
+#define FP_T(i) const uint64_t fp_t##i = __builtin_amdgcn_s_memtime()
+#else
+#define FP_T(i)
+#endif
+
 #ifdef HBM_PROFILE
 // Dev only (tools/build_variants.sh NAME -DHBM_PROFILE): per cooperative
 // return, by log2 of its larger set: returns, device ticks (100 MHz), LDS-
@@ -1530,6 +1538,20 @@ __global__ __launch_bounds__(kWave *kWavesPerWG) void frontier_dump_kernel(
 #ifndef LC_PIPE
 #define LC_PIPE 0
 #endif
+// The resident grid's decision: the version-order tier's two record passes
+// (1), or value claims as LDS compare-and-swaps in the one pass (0, as the
+// fused pass)
+#ifndef LC_RES_TWO_PASS
+#define LC_RES_TWO_PASS 1
+#endif
+// The other workgroups' polls of workgroup 0's copy: s_sleep between polls,
+// and one word per poll (1) or every word (0)
+#ifndef LC_RES_SLEEP
+#define LC_RES_SLEEP 4
+#endif
+#ifndef LC_RES_POLL1
+#define LC_RES_POLL1 0
+#endif
 constexpr int kFastThreads = 256;
 constexpr int kFastWaves = kFastThreads / kWave;
 constexpr int kFastMax = kFastMaxRecords;
@@ -2275,6 +2297,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
   }
   const int n = (int)n64;
   FGP_T(0);
+  FP_T(0);
 #if LC_FAST_DEV == 2  // dev timing only: loads, no decision
   {
     int64_t x = 0;
@@ -2294,7 +2317,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
     reinterpret_cast<uint4 *>(s.A)[tid] = make_uint4(0, 0, 0, 0);  // nothing constrains t_k from below
     reinterpret_cast<uint4 *>(s.B)[tid] = make_uint4(kNever, kNever, kNever, kNever);
     reinterpret_cast<uint2 *>(s.Own)[tid] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-    if (MODE != kModeFast || LC_PIPE)  // (claimed values start unclaimed)
+    if (MODE != kModeFast || LC_PIPE || (RES && !LC_RES_TWO_PASS))  // (claimed values start unclaimed)
       reinterpret_cast<int4 *>(s.Val)[tid] = make_int4(kAny, kAny, kAny, kAny);
   }
   int64_t base_idx;
@@ -2311,6 +2334,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
     __syncthreads();
   }
   FGP_T(1);
+  FP_T(1);
   const int V0 = p.init_ver, init = p.init_val;
   int inel = 0, bad = 0, nmut = 0, jit_only = 0, giveup = 0, vbad = 0;
   int ext = 0;  // past the last placed position and the highest read version
@@ -2323,7 +2347,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
   // and checks the claims in a second pass over the registers (measured ~2 %
   // faster on C2 than the compare-and-swaps); the fused and light passes
   // claim in pass 1 and free the records.
-  constexpr bool kTwoPass = MODE == kModeFast && !LC_PIPE;
+  constexpr bool kTwoPass = MODE == kModeFast && !LC_PIPE && !(RES && !LC_RES_TWO_PASS);
   auto claim = [&](int k, int v) {  // value v required at version V0+k+1 (k >= 0)
     if constexpr (!kTwoPass) {
       const int old = atomicCAS(&s.Val[k], kAny, v);
@@ -2430,6 +2454,7 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
   }
   __syncthreads();
   FGP_T(2);
+  FP_T(2);
   uint32_t wor;
   int M;
   {
@@ -2526,10 +2551,12 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
       else if (k == n) hole |= (k > M) & (aa[j] != 0);
     }
   }
+  FP_T(3);
   if (timing_fails(s, M, tid)) hole = 1;
   const uint32_t wbad = __ballot(hole) ? 1u : 0u;
   if (lane == 0) s.wbad[w] = wbad;
   __syncthreads();
+  FP_T(4);
   // (the fused pass hands invalid keys over: the first-failure rule there
   // costs 5 VGPRs, 72 -> 77, and a wave per SIMD on crash-heavy batches)
   if (tid == 0) {
@@ -2538,6 +2565,15 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
       put_result<RES>(out + key, lc_key_result{LC_VALID, LC_REASON_NONE, -1, -1, 0, 1});
     else
       fast_pass_on<MODE>(key, o, &s.raised);
+#ifdef LC_FAST_PROF
+    if (MODE == kModeFast) {
+      atomicAdd(&g_fp[1], (unsigned long long)(fp_t1 - fp_t0));  // records landed + LDS init
+      atomicAdd(&g_fp[2], (unsigned long long)(fp_t2 - fp_t1));  // pass 1 (placement, bounds)
+      atomicAdd(&g_fp[3], (unsigned long long)(fp_t3 - fp_t2));  // order check, pass 2 (claims)
+      atomicAdd(&g_fp[4], (unsigned long long)(fp_t4 - fp_t3));  // timing scan + barrier
+      atomicAdd(&g_fp[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - fp_t4));  // result
+    }
+#endif
   }
 }
 
@@ -2590,8 +2626,16 @@ __device__ __forceinline__ void fast_one(const lc_op *__restrict__ ops,
                                          const int64_t *__restrict__ key_off, int64_t key,
                                          const KParams &p, FastLds &s,
                                          lc_key_result *__restrict__ out, const FastSinks &o) {
+#ifdef LC_FAST_PROF
+  const uint64_t fp_e = __builtin_amdgcn_s_memtime();
+#endif
   const int64_t beg = key_off[key], end = key_off[key + 1];
   const lc_op *kops = ops + (beg - key_off[0]);
+#ifdef LC_FAST_PROF
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (MODE == kModeFast && threadIdx.x == 0)
+    atomicAdd(&g_fp[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - fp_e));  // offsets
+#endif
   FastRecs r;
   if (end - beg > 0 && end - beg <= kFastMax) fast_issue(kops, (int)(end - beg), threadIdx.x, r);
   if (threadIdx.x == 0) s.raised = 0;
@@ -2633,6 +2677,14 @@ __global__ __launch_bounds__(kFastThreads) void fast_tier_kernel(
   fast_run<kModeFast>(ops, key_off, n_keys, p, s, out, o);
 #else
   fast_one<kModeFast>(ops, key_off, blockIdx.x, p, s, out, o);
+#endif
+#ifdef LC_FAST_PROF
+  if (threadIdx.x == 0 && atomicAdd(&g_fpdone, 1u) == gridDim.x - 1) {
+    printf("fastprof keys %u offsets %llu land+init %llu pass1 %llu order+pass2 %llu timing %llu result %llu\n",
+           gridDim.x, g_fp[0], g_fp[1], g_fp[2], g_fp[3], g_fp[4], g_fp[5]);
+    for (int i = 0; i < 8; i++) g_fp[i] = 0;
+    g_fpdone = 0;
+  }
 #endif
 }
 
@@ -2751,6 +2803,20 @@ __global__ __launch_bounds__(kFastThreads, 6) void fast_resident_kernel(ResHost 
       uint64_t w = 0;
       bool leave = false;
       for (uint32_t polls = 0;; polls++) {
+        if (!first && LC_RES_POLL1) {
+          // one word per poll (the others only once it carries the number):
+          // 1,249 pollers beside the record stream
+          const uint64_t w0 = __hip_atomic_load(src + kResWords - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((uint32_t)(__builtin_amdgcn_readfirstlane((int)(uint32_t)(w0 >> 32)) >> 16) != want) {
+            const uint64_t now = wall_clock64();
+            if (now - t0 > kResStrayTicks || polls >= kResPollCap) {
+              leave = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(LC_RES_SLEEP);
+            continue;
+          }
+        }
         if (tid < kResWords)
           w = first ? __hip_atomic_load(src + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                     : __hip_atomic_load(src + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2762,7 +2828,7 @@ __global__ __launch_bounds__(kFastThreads, 6) void fast_resident_kernel(ResHost 
           break;
         }
         if (first) __builtin_amdgcn_s_sleep(1);
-        else __builtin_amdgcn_s_sleep(4);
+        else __builtin_amdgcn_s_sleep(LC_RES_SLEEP);
       }
       if (leave) {
         // workgroup 0 on its idle bound: says so, and hands the others an
@@ -2784,7 +2850,9 @@ __global__ __launch_bounds__(kFastThreads, 6) void fast_resident_kernel(ResHost 
     seq++;
     const int64_t n_keys = rfl64((int64_t)res_val(rq[2]));
     if (n_keys == kResExitKeys) return;
-    // one key per workgroup (the host launches at least n_keys workgroups)
+    // one key per workgroup (the host launches at least n_keys workgroups;
+    // a loop over keys blockIdx.x, + G, ... needs 22 more SGPRs than the
+    // wave has and spills)
     if ((int64_t)blockIdx.x < n_keys) fast_one_res(rq, blockIdx.x, s);
     // (every key's LDS reads done before the next request's; rq rewritten
     // only after this barrier)

@@ -34,14 +34,18 @@ def main():
             for _ in range(20):
                 call()
             torch.cuda.synchronize()
+            ctx.totals(reset=True)
             t0 = time.perf_counter()
             for _ in range(steps):
                 call()
             ctx.quiesce()
             torch.cuda.synchronize()
             us = (time.perf_counter() - t0) * 1e6 / steps
+            tot = ctx.totals(reset=True)
+            dev_us = tot["fast_kernel_ms"] * 1e3 / max(1, tot["timed_calls"])
             res = np.frombuffer(out.cpu().numpy().tobytes(), dtype=abi.RESULT_DTYPE)[:nk]
             print(json.dumps({"keys": nk, "us_per_step": round(us, 2),
+                              "device_us": round(dev_us, 2), "timed": tot["timed_calls"],
                               "valid": int((res["verdict"] == 1).sum()),
                               "lib": os.environ.get("LINCHECK_LIB", "in-tree")}), flush=True)
 
