@@ -270,6 +270,7 @@ def main():
         line["c1_leg"] = c1_leg(ctx, abi)
         line["host_leg"] = host_leg(ctx, abi, ops, key_off, n_inv)
         line["host_leg32"] = host_leg32(ctx, abi, ops, key_off)
+        line["host_leg16"] = host_leg16(ctx, abi, ops, key_off)
         line["hot_key"] = hot_key(ctx, abi)
         line["search_leg"] = search_leg(ctx, abi, d_ops, d_off, d_out, my_keys, stream, n_ops)
         line["mixed_leg"] = mixed_leg(ctx, abi, dev, stream)
@@ -483,6 +484,51 @@ def host_leg32(ctx, abi, ops, key_off):
         finally:
             if mode == "registered":
                 ctx.host_unregister(o32)
+        i = 1 + int(np.argsort(times[1:])[1])
+        t = times[i]
+        d = devs[i][0]
+        out[mode] = {"call_ms": t * 1e3, "ops_per_s": int(key_off[-1]) / t,
+                     "h2d_ms": d["h2d_ms"],
+                     "h2d_gb_per_s": d["h2d_bytes"] / (d["h2d_ms"] * 1e-3) / 1e9
+                     if d["h2d_ms"] > 0 else None,
+                     "profile": profs[i], "valid": int((r["verdict"] == 1).sum()),
+                     "result_mismatches_vs_lc_check": int((r != want).sum())}
+    return out
+
+
+def host_leg16(ctx, abi, ops, key_off):
+    """The drop-in's rate on 16-byte lc_op16 records (round 6: 15-bit value
+    ids, which every key of C2 fits — the JVM shim and the EDN reader emit
+    them directly when a batch fits): lc_check16 from host memory, a third of
+    lc_check's PCIe bytes (two thirds of lc_check32's); chunked copies, each chunk
+    widened on the device and decided while the next crosses.  Pageable, then
+    page-locked.  Results compared with lc_check's field for field; lc_pack16
+    timed apart.  Never `value`; the median of calls 2-4."""
+    t0 = time.perf_counter()
+    got = abi.pack16(ops, key_off)
+    pack_ms = (time.perf_counter() - t0) * 1e3
+    if got is None:
+        return {"skipped": "an id above LC_ID15_MAX (the batch goes as lc_op32)"}
+    o16, base = got
+    _, want = ctx.check(ops, key_off)
+    out = {"workload": "C2 batch from host memory as 16-byte records (lc_check16)",
+           "pack16_ms": pack_ms, "bytes": int(o16.nbytes)}
+    for mode in ("pageable", "registered"):
+        if mode == "registered":
+            t0 = time.perf_counter()
+            ctx.host_register(o16)
+            out["register_ms"] = (time.perf_counter() - t0) * 1e3
+        try:
+            times, profs, devs = [], [], []
+            for _ in range(4):
+                t0 = time.perf_counter()
+                _, r = ctx.check16(o16, key_off, base)
+                times.append(time.perf_counter() - t0)
+                profs.append(ctx.call_profile())
+                devs.append(ctx.device_stats())
+        finally:
+            if mode == "registered":
+                ctx.host_unregister(o16)
         i = 1 + int(np.argsort(times[1:])[1])
         t = times[i]
         d = devs[i][0]

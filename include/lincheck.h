@@ -28,10 +28,12 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 4  /* 3: lc_aux certificates, lc_device_stats, lc_host_register;
+#define LC_ABI_VERSION 5  /* 3: lc_aux certificates, lc_device_stats, lc_host_register;
                              4: 24-byte lc_op32 records (lc_pack32, lc_check32,
-                             lc_check_device32), lc_last_call_profile, lc_quiesce
-                             (the resident version-order grid) */
+                             lc_check_device32), lc_last_call_profile;
+                             5: 16-byte lc_op16 records (lc_pack16, lc_check16,
+                             lc_edn_ops16), lc_quiesce (the resident
+                             version-order grid) */
 
 /* Op kinds: the three :f values of register.clj:98-100 (r / w / cas). */
 #define LC_F_READ  0
@@ -403,6 +405,46 @@ int lc_check_device32(lc_ctx *ctx, const lc_op32 *d_ops, const int64_t *d_key_of
                       const int64_t *d_key_base, int64_t n_keys, const lc_opts *opts,
                       lc_key_result *d_out, void *stream, const lc_aux *aux);
 
+/*
+ * ABI 5: the same op in 16 bytes, for batches whose value ids fit
+ * 15 bits — the drop-in's host-to-device copy is PCIe-bound, and every value
+ * a key's history holds is interned per key to a small dense id:
+ *
+ *  fve       f << 30 | (value + 1) << 15 | (expected + 1): 2 + 15 + 15 bits;
+ *            value / expected ids in [-1, LC_ID15_MAX] (nil = -1 -> 0); a
+ *            value field of 0x7FFF marks a record lc_pack32 would mark
+ *            malformed (value -2)
+ *  version   as in lc_op32 (int32)
+ *  call, ret as in lc_op32 (relative to key_base[k]; LC_INF32: no return)
+ *
+ * Record r of key k stands for the lc_op32
+ *   {fve >> 30, v - 1 (v = fve >> 15 & 0x7FFF; 0x7FFF: -2),
+ *    (fve & 0x7FFF) - 1 (0x7FFF: -2), version, call, ret}
+ * and lc_check16 returns exactly what lc_check32 returns for those records
+ * (and so what lc_check returns for the records lc_pack16 was given).
+ * lc_pack16 narrows lc_op records by lc_pack32's rules, or returns -ERANGE
+ * (nothing written that the caller may use) when a record that is not
+ * malformed holds a value or expected id above LC_ID15_MAX: such a batch
+ * goes as lc_op32.
+ */
+typedef struct lc_op16 {
+  uint32_t fve;
+  int32_t version;
+  uint32_t call;
+  uint32_t ret;
+} lc_op16;
+
+#define LC_ID15_MAX 0x7FFD
+
+int lc_pack16(const lc_op *ops, const int64_t *key_off, int64_t n_keys, lc_op16 *out,
+              int64_t *key_base);
+
+/* lc_check_ex on 16-byte records from host memory (as lc_check32: chunked
+ * copies on the copy streams; each chunk widened on the device and decided
+ * while the next one crosses PCIe). */
+int lc_check16(lc_ctx *ctx, const lc_op16 *ops, const int64_t *key_off, const int64_t *key_base,
+               int64_t n_keys, const lc_opts *opts, lc_key_result *out, const lc_aux *aux);
+
 /* Where the host wall time of the last lc_check / lc_check_ex / lc_check32
  * call went (ABI 4): the argument checks, the split over devices, the start
  * of the per-device threads, their ends, the frontier-exchange re-search
@@ -423,7 +465,7 @@ typedef struct lc_call_profile {
 
 int lc_last_call_profile(lc_ctx *ctx, lc_call_profile *out);
 
-/* ABI 4: lc_check_device on a batch of at most one key per resident
+/* ABI 5: lc_check_device on a batch of at most one key per resident
  * workgroup (1,536 on an MI355X) is served by a version-order grid that
  * stays resident on the GPU between calls (no launch per call); it leaves on
  * its own after LC_RESIDENT_IDLE_US microseconds (default 50) without a

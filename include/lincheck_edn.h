@@ -92,6 +92,12 @@ const int64_t *lc_edn_key_off(const lc_edn_history *h);
 const lc_op32 *lc_edn_ops32(lc_edn_history *h);
 const int64_t *lc_edn_key_base(lc_edn_history *h);
 
+/* The same records as 16-byte lc_op16 (n_ops; round 6), the inputs of
+ * lc_check16 with lc_edn_key_base's bases, packed by lc_pack16's rules on the
+ * first call; NULL when some value id does not fit 15 bits (use
+ * lc_edn_ops32) or on a null history.  Valid until lc_edn_free. */
+const lc_op16 *lc_edn_ops16(lc_edn_history *h);
+
 /* EDN text of key i as it first appeared (NUL-terminated). */
 const char *lc_edn_key(const lc_edn_history *h, int64_t key);
 

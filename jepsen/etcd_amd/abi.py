@@ -166,6 +166,11 @@ def lib():
         L.lc_check_device32.restype = ctypes.c_int
         L.lc_pack32.argtypes = [p, p, i64, p, p]
         L.lc_pack32.restype = ctypes.c_int
+        L.lc_pack16.argtypes = [p, p, i64, p, p]
+        L.lc_pack16.restype = ctypes.c_int
+        L.lc_check16.argtypes = [vp, p, p, p, i64, ctypes.POINTER(LcOpts), p,
+                                 ctypes.POINTER(LcAux)]
+        L.lc_check16.restype = ctypes.c_int
         L.lc_check_frontiers.argtypes = [vp, p, p, i64, p, ctypes.POINTER(LcOpts), vp, i32, p]
         L.lc_check_frontiers.restype = ctypes.c_int
         L.lc_last_totals.argtypes = [vp, ctypes.POINTER(LcTotals), i32]
@@ -244,6 +249,34 @@ def pack32(ops, key_off):
     rc = lib().lc_pack32(_ptr(ops), _ptr(key_off), len(key_off) - 1, _ptr(out), _ptr(base))
     if rc != 0:
         raise LcError(rc, "lc_pack32")
+    return out, base
+
+
+def as_ops16(ops16):
+    a = np.ascontiguousarray(ops16, dtype=np.uint32)
+    if a.ndim != 2 or a.shape[1] != 4:
+        a = a.reshape(-1, 4)
+    return a
+
+
+LC_ID15_MAX = 0x7FFD
+ERANGE = 34
+
+
+def pack16(ops, key_off):
+    """lc_pack16 (include/lincheck.h, round 6): (ops16 (n, 4) uint32 — fve,
+    version, call, ret — key_base int64 per key), or None when some record
+    that is not malformed holds a value or expected id above LC_ID15_MAX
+    (the batch then goes as lc_op32: pack32)."""
+    ops = as_ops(ops)
+    key_off = np.ascontiguousarray(key_off, dtype=np.int64)
+    out = np.zeros((len(ops), 4), dtype=np.uint32)
+    base = np.zeros(max(len(key_off) - 1, 0), dtype=np.int64)
+    rc = lib().lc_pack16(_ptr(ops), _ptr(key_off), len(key_off) - 1, _ptr(out), _ptr(base))
+    if rc == -ERANGE:
+        return None
+    if rc != 0:
+        raise LcError(rc, "lc_pack16")
     return out, base
 
 
@@ -357,6 +390,17 @@ class Context:
         return self._check_host(lib().lc_check32, ops32, key_off, (_ptr(base),), opts,
                                 raise_on_error, witness, certificate)
 
+    def check16(self, ops16, key_off, key_base=None, opts=None, raise_on_error=True,
+                witness=False, certificate=False):
+        """lc_check16 (round 6): 16-byte records from host memory ((n, 4)
+        uint32, as pack16 makes them) and their key bases; returns as check()."""
+        ops16 = as_ops16(ops16)
+        base = None if key_base is None else np.ascontiguousarray(key_base, dtype=np.int64)
+        if base is not None and len(base) != len(key_off) - 1:
+            raise ValueError(f"key_base has {len(base)} entries for {len(key_off) - 1} keys")
+        return self._check_host(lib().lc_check16, ops16, key_off, (_ptr(base),), opts,
+                                raise_on_error, witness, certificate)
+
     def check_frontiers(self, ops, key_off, stop_ops, max_per_key=10, opts=None):
         """lc_check_frontiers (include/lincheck_fx.h, ABI 4): for every key,
         up to max_per_key configurations of its JIT frontier just before the
@@ -389,7 +433,7 @@ class Context:
         return out
 
     def quiesce(self):
-        """lc_quiesce (ABI 4): stop the resident version-order grid now (it
+        """lc_quiesce (ABI 5): stop the resident version-order grid now (it
         otherwise leaves after LC_RESIDENT_IDLE_US without a call)."""
         rc = lib().lc_quiesce(self._h)
         if rc != 0:

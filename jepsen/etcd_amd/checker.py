@@ -148,12 +148,19 @@ class RegisterChecker:
         o = abi.default_opts(self.max_configs_per_key, m.version, init,
                              flags=abi.LC_FLAG_WHOLE_GPU if self.whole_gpu else 0,
                              time_budget_ms=self.time_budget_ms)
-        # the drop-in's call (ABI 4): 24-byte records, what crosses PCIe
-        # (the JVM shim packs them directly; here lc_pack32 narrows the
-        # 48-byte pack by the same rules)
-        ops32, key_base = abi.pack32(ops, key_off)
-        _, res, wit, kind, cert, cset = self._context().check32(
-            ops32, key_off, key_base, o, witness=True, certificate=True)
+        # the drop-in's call (ABI 5): 16-byte records when every value id
+        # fits 15 bits, else 24-byte ones — what crosses PCIe (the JVM shim
+        # packs them directly; here lc_pack16 / lc_pack32 narrow the 48-byte
+        # pack by the same rules)
+        p16 = abi.pack16(ops, key_off)
+        if p16 is not None:
+            ops16, key_base = p16
+            _, res, wit, kind, cert, cset = self._context().check16(
+                ops16, key_off, key_base, o, witness=True, certificate=True)
+        else:
+            ops32, key_base = abi.pack32(ops, key_off)
+            _, res, wit, kind, cert, cset = self._context().check32(
+                ops32, key_off, key_base, o, witness=True, certificate=True)
         cfgs_of = self._configs(ops, key_off, res, o)
         results = {}
         n_fallback = 0  # one-key frontier re-searches run for diagnostics in this call

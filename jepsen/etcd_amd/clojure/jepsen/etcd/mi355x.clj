@@ -12,9 +12,11 @@
   The JVM side does the host preprocessing (client ops only, the independent
   per-key split, knossos-style invoke/completion pairing with :fail pairs
   dropped and :info ops pending forever, per-key value interning by Clojure
-  =) and packs one 24-byte lc_op32 record per operation into off-heap memory
-  (ABI 4: the int32 fields the device reads, half the PCIe bytes of the
-  48-byte lc_op).  One lc_check32 call (JNA, liblincheck.so; C ABI in
+  =) and packs one 16-byte lc_op16 record per operation (24-byte lc_op32
+  when some value id does not fit 15 bits) into off-heap memory
+  (ABI 5: a third of the PCIe bytes of the 48-byte lc_op; the 24-byte form
+  holds the int32 fields the device reads).  One lc_check16 / lc_check32
+  call (JNA, liblincheck.so; C ABI in
   include/lincheck.h) then decides every key on the MI355X GPUs of the
   control node.  The result has
   jepsen.independent/checker's shape, and each key's entry has
@@ -55,6 +57,8 @@
 (def ^:const LC_INF Long/MAX_VALUE)
 (def ^:const op-bytes 48)      ; lc_op (the frontier searches)
 (def ^:const op32-bytes 24)    ; lc_op32 (lc_check32, ABI 4)
+(def ^:const op16-bytes 16)    ; lc_op16 (lc_check16, round 6): value ids within 15 bits
+(def ^:const id15-max 0x7FFD)  ; LC_ID15_MAX
 (def ^:const field-max 0x7FFFFFFE)
 (def ^:const never 0xFFFFFFFF)
 (def ^:const result-bytes 40)
@@ -65,7 +69,7 @@
 
 (defn- fun ^Function [name] (.getFunction ^NativeLibrary @lib name))
 
-(def ^:const abi-min 4)  ; lc_check32 / lc_check_frontiers (include/lincheck.h LC_ABI_VERSION)
+(def ^:const abi-min 5)  ; lc_check16 / lc_check32 / lc_check_frontiers (include/lincheck.h LC_ABI_VERSION)
 
 (defonce ^:private ctx
   (delay
@@ -207,11 +211,31 @@
         rs     (mapv #(record model intern %) d)]
     [rs (intern)]))
 
+(defn- fits16?
+  "Whether an lc_op32 record (six ints) fits an lc_op16 (include/lincheck.h,
+  round 6): a malformed one always (value -2), else value and expected ids
+  within [-1, LC_ID15_MAX]."
+  [^ints arr ^long b]
+  (let [v (aget arr (+ b 1)), e (aget arr (+ b 2))]
+    (or (= v -2) (and (<= -1 v id15-max) (<= -1 e id15-max)))))
+
+(defn- to16
+  "lc_pack16's record from lc_pack32's (six ints at b): f << 30 | (value + 1)
+  << 15 | (expected + 1), version, call, ret; a malformed record's value field
+  0x7FFF, its expected clamped."
+  [^ints arr ^long b]
+  (let [f (long (aget arr b)), v (long (aget arr (+ b 1))), e (long (aget arr (+ b 2)))
+        v15 (if (= v -2) 0x7FFF (inc v))
+        x15 (max 0 (min 0x7FFF (inc e)))]
+    [(unchecked-int (bit-or (bit-shift-left f 30) (bit-shift-left v15 15) x15))
+     (aget arr (+ b 3)) (aget arr (+ b 4)) (aget arr (+ b 5))]))
+
 (defn- pack
-  "Packs all keys as 24-byte lc_op32 records: returns [keys completed-per-key
-  ^Memory ops ^Memory key-off ^Memory key-base n-records values-per-key]
-  (values: each key's id -> value map).  Records are filled into one int[]
-  and written to the off-heap buffer in a single bulk copy."
+  "Packs all keys as 16-byte lc_op16 records when every value id fits 15
+  bits, else as 24-byte lc_op32 records: returns [keys completed-per-key
+  ^Memory ops ^Memory key-off ^Memory key-base n-records values-per-key
+  record-bytes] (values: each key's id -> value map).  Records are filled
+  into one int[] and written to the off-heap buffer in a single bulk copy."
   [model subs]
   (let [keys  (vec (keys subs))
         nk    (count keys)
@@ -234,13 +258,23 @@
           (aset bases ki base)
           (conj! vals vm)
           (recur (inc ki) i'))))
-    (let [ops (Memory. (max 1 (* op32-bytes n)))
+    (let [w16 (loop [i 0] (cond (>= i n) true
+                                (fits16? arr (* 6 i)) (recur (inc i))
+                                :else false))
+          rb  (if w16 op16-bytes op32-bytes)
+          ops (Memory. (max 1 (* rb n)))
           off (Memory. (* 8 (inc nk)))
           bm  (Memory. (* 8 (max 1 nk)))]
-      (.write ops 0 arr 0 (alength arr))
+      (if w16
+        (let [a16 (int-array (* 4 n))]
+          (dotimes [i n]
+            (let [q (to16 arr (* 6 i))]
+              (dotimes [j 4] (aset a16 (+ (* 4 i) j) (unchecked-int (nth q j))))))
+          (.write ops 0 a16 0 (alength a16)))
+        (.write ops 0 arr 0 (alength arr)))
       (.write off 0 offs 0 (alength offs))
       (.write bm 0 bases 0 (alength bases))
-      [keys done ops off bm n (persistent! vals)])))
+      [keys done ops off bm n (persistent! vals) rb])))
 
 (defn- pack48
   "The 48-byte lc_op records of some keys (the frontier searches take
@@ -434,7 +468,8 @@
   come back :unknown one by one; lc_check32 fails (and this throws, for
   check-safe) only on unusable arguments or a GPU error."
   [model max-configs-per-key time-budget-ms flags subs]
-  (let [[keys done ops off base n vals] (pack model subs)
+  (let [[keys done ops off base n vals rb] (pack model subs)
+        check-fn (if (= rb op16-bytes) "lc_check16" "lc_check32")
         n-fallback (atom 0)
         nk   (count keys)
         out  (Memory. (* result-bytes nk))
@@ -449,10 +484,10 @@
                (.setLong 16 max-configs-per-key)
                (.setLong 24 time-budget-ms) (.setLong 32 flags))
         rc   (locking ctx
-               (.invokeInt (fun "lc_check32")
+               (.invokeInt (fun check-fn)
                            (object-array [@ctx ops off base (long nk) o out aux])))]
     (when-not (zero? rc)
-      (throw (ex-info "lc_check32 failed"
+      (throw (ex-info (str check-fn " failed")
                       {:rc rc :error (.invoke (fun "lc_last_error")
                                               String (object-array [@ctx]))})))
     (let [inv (vec (for [ki (range nk)

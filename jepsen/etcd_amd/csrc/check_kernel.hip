@@ -3248,7 +3248,40 @@ __global__ __launch_bounds__(256) void widen32_kernel(const int2 *__restrict__ i
   }
 }
 
+// lc_op16 records (include/lincheck.h, round 6) into lc_op records: one
+// 16-byte load and three 16-byte stores per record
+__global__ __launch_bounds__(256) void widen16_kernel(const uint4 *__restrict__ in,
+                                                      const int64_t *__restrict__ key_off,
+                                                      const int64_t *__restrict__ key_base,
+                                                      longlong2 *__restrict__ out) {
+  const int64_t k = blockIdx.x;
+  const int64_t off0 = key_off[0];
+  const int64_t b = key_off[k] - off0, e = key_off[k + 1] - off0;
+  const int64_t base = key_base ? key_base[k] : 0;
+  const int64_t step = (int64_t)blockDim.x * gridDim.y;
+  for (int64_t r = b + (int64_t)blockIdx.y * blockDim.x + threadIdx.x; r < e; r += step) {
+    const uint4 q = in[r];
+    const uint32_t v = (q.x >> 15) & 0x7FFFu, x = q.x & 0x7FFFu;
+    const int64_t value = v == 0x7FFFu ? -2 : (int64_t)v - 1;
+    const int64_t expected = x == 0x7FFFu ? -2 : (int64_t)x - 1;
+    out[3 * r] = make_longlong2((int64_t)(q.x >> 30), value);
+    out[3 * r + 1] = make_longlong2(expected, (int64_t)(int32_t)q.y);
+    out[3 * r + 2] = make_longlong2(base + (int64_t)q.z, q.w == LC_INF32 ? kInf : base + (int64_t)q.w);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_widen16(const lc_op16 *d_in, const int64_t *d_key_off, const int64_t *d_key_base,
+                          int64_t n_keys, int64_t max_len, lc_op *d_out, hipStream_t stream) {
+  if (n_keys <= 0) return hipSuccess;
+  if (n_keys > INT32_MAX) return hipErrorInvalidValue;
+  const unsigned gy = (unsigned)std::min<int64_t>(64, std::max<int64_t>(1, (max_len + 1023) / 1024));
+  hipLaunchKernelGGL(widen16_kernel, dim3((unsigned)n_keys, gy), dim3(256), 0, stream,
+                     reinterpret_cast<const uint4 *>(d_in), d_key_off, d_key_base,
+                     reinterpret_cast<longlong2 *>(d_out));
+  return hipGetLastError();
+}
 
 hipError_t launch_frontier_dump(const lc_op *d_ops, const int64_t *d_key_off, const int64_t *d_stop,
                                 int64_t n_keys, const KParams &p, lc_fx_config *d_out, int max,

@@ -672,6 +672,10 @@ struct lc_edn_history {
   std::vector<lc_op32> ops32;
   std::vector<int64_t> key_base;
   bool packed32 = false;
+  // lc_op16 records (round 6), made on first request: 1 packed, -1 an id
+  // does not fit 15 bits
+  std::vector<lc_op16> ops16;
+  int packed16 = 0;
   std::vector<std::string> keys;                  // display text
   std::vector<std::vector<std::string>> values;   // per key: display text by id
   std::vector<std::pair<size_t, size_t>> inv, comp;  // per record: op spans (comp beg == end: none)
@@ -978,6 +982,19 @@ static int pack32(lc_edn_history *h) {
 const lc_op32 *lc_edn_ops32(lc_edn_history *h) { return h && !pack32(h) ? h->ops32.data() : nullptr; }
 const int64_t *lc_edn_key_base(lc_edn_history *h) {
   return h && !pack32(h) ? h->key_base.data() : nullptr;
+}
+
+// The 16-byte form lc_check16 takes, by lc_pack16's rules (its key bases are
+// lc_pack32's: lc_edn_key_base), or null when an id does not fit 15 bits.
+const lc_op16 *lc_edn_ops16(lc_edn_history *h) {
+  if (!h) return nullptr;
+  if (h->packed16 == 0) {
+    const int64_t nk = (int64_t)h->key_off.size() - 1;
+    h->ops16.resize(std::max<size_t>(1, h->ops.size()));
+    std::vector<int64_t> base((size_t)std::max<int64_t>(1, nk));
+    h->packed16 = lc_pack16(h->ops.data(), h->key_off.data(), nk, h->ops16.data(), base.data()) ? -1 : 1;
+  }
+  return h->packed16 > 0 ? h->ops16.data() : nullptr;
 }
 
 const char *lc_edn_key(const lc_edn_history *h, int64_t key) {

@@ -186,6 +186,10 @@ hipError_t launch_witness_init(const lc_op *d_ops, const int64_t *d_key_off, int
 // 16-byte).  max_len: the longest key's records (sizes the grid).
 hipError_t launch_widen32(const lc_op32 *d_in, const int64_t *d_key_off, const int64_t *d_key_base,
                           int64_t n_keys, int64_t max_len, lc_op *d_out, hipStream_t stream);
+// The same for lc_op16 records (d_in 16-byte aligned): the 15-bit ids
+// unpacked (0x7FFF -> -2) as include/lincheck.h defines them.
+hipError_t launch_widen16(const lc_op16 *d_in, const int64_t *d_key_off, const int64_t *d_key_base,
+                          int64_t n_keys, int64_t max_len, lc_op *d_out, hipStream_t stream);
 
 // lc_check_frontiers (include/lincheck_fx.h): the LDS tier's search per key
 // up to the :ok return of record d_stop[k], its frontier written to

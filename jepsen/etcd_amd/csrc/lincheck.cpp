@@ -304,6 +304,7 @@ struct Chunks {
   std::function<int(int)> issue;
   const hipEvent_t *ready = nullptr;
   const lc_op32 *d_ops32 = nullptr;  // staging records to widen into d_ops (null: 48-byte copies)
+  const lc_op16 *d_ops16 = nullptr;  // (lc_check16) the same for 16-byte records
   const int64_t *d_base = nullptr;   // key bases for the widening (null: 0)
   int64_t max_len = 0;               // longest key (records)
 };
@@ -767,6 +768,10 @@ int run_device(lc_ctx *c, Dev &d, const lc_op *d_ops, const int64_t *d_off,
       if (nk <= 0) continue;
       if (ch->d_ops32 && !wo.ops32)
         HIP_TRY(c, lcdev::launch_widen32(ch->d_ops32 + r0, d_off + k0,
+                                         ch->d_base ? ch->d_base + k0 : nullptr, nk, ch->max_len,
+                                         const_cast<lc_op *>(d_ops) + r0, st));
+      if (ch->d_ops16)
+        HIP_TRY(c, lcdev::launch_widen16(ch->d_ops16 + r0, d_off + k0,
                                          ch->d_base ? ch->d_base + k0 : nullptr, nk, ch->max_len,
                                          const_cast<lc_op *>(d_ops) + r0, st));
       if (int e = first_pass(k0, nk, r0, nrec)) return e;
@@ -1266,6 +1271,19 @@ inline void rec_kind(const lc_op &o, bool *crashed_mut, bool *unpinned) {
               (mut || (o.f == LC_F_READ && o.value != LC_NIL));
 }
 
+// An lc_op16 record as the lc_op32 it stands for (include/lincheck.h)
+inline lc_op32 as32(const lc_op16 &q) {
+  const uint32_t v = q.fve >> 15 & 0x7FFFu, x = q.fve & 0x7FFFu;
+  return lc_op32{(int32_t)(q.fve >> 30), v == 0x7FFFu ? -2 : (int32_t)v - 1,
+                 x == 0x7FFFu ? -2 : (int32_t)x - 1, q.version, q.call, q.ret};
+}
+inline bool rec_crashed(const lc_op16 &o) { return o.ret == LC_INF32; }
+inline int64_t rec_call(const lc_op16 &o) { return (int64_t)o.call; }
+inline int64_t rec_ret(const lc_op16 &o) { return o.ret == LC_INF32 ? LC_INF : (int64_t)o.ret; }
+inline void rec_kind(const lc_op16 &o, bool *crashed_mut, bool *unpinned) {
+  rec_kind(as32(o), crashed_mut, unpinned);
+}
+
 template <class Op>
 double key_cost(const Op *o, int64_t n) {
   int64_t crashed = 0, unpinned = 0;
@@ -1359,6 +1377,7 @@ inline lc_op widen_op(const lc_op32 &o, int64_t base) {
   return lc_op{o.f, o.value, o.expected, o.version, base + (int64_t)o.call,
                o.ret == LC_INF32 ? LC_INF : base + (int64_t)o.ret};
 }
+inline lc_op widen_op(const lc_op16 &o, int64_t base) { return widen_op(as32(o), base); }
 
 // lc_check_ex (48-byte lc_op) and lc_check32 (24-byte lc_op32, ABI 4) from
 // host memory: the keys split over the context's devices (plan_devices), one
@@ -1375,6 +1394,8 @@ template <class Op>
 int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *key_base,
                int64_t n_keys, const lc_opts *opts, lc_key_result *out, const lc_aux *aux) {
   constexpr bool k32 = sizeof(Op) == sizeof(lc_op32);
+  constexpr bool k16 = sizeof(Op) == sizeof(lc_op16);
+  constexpr bool narrow = k32 || k16;  // records widened on the device, key bases
   const auto t0 = std::chrono::steady_clock::now();
   auto since = [&t0]() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1410,7 +1431,7 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
   // the longest key (the widening's grid); C4's 5,000-op key takes more
   // workgroups than a C2 key
   int64_t max_len = 0;
-  if (k32)
+  if (narrow)
     for (int64_t k = 0; k < n_keys; k++) max_len = std::max(max_len, key_off[k + 1] - key_off[k]);
 
   std::vector<int> rcs(nd, 0);
@@ -1437,8 +1458,9 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
     const size_t ops_bytes = sizeof(lc_op) * (size_t)nrec;  // on the device: 48-byte records
     const size_t in_bytes = sizeof(Op) * (size_t)nrec;      // what crosses PCIe
     int r = ensure(c, reinterpret_cast<char **>(&d.d_ops), &d.ops_cap, ops_bytes);
-    if (!r && k32) r = ensure(c, reinterpret_cast<char **>(&d.d_ops32), &d.ops32_cap, in_bytes);
-    if (!r && k32 && key_base) r = ensure(c, &d.d_base, &d.base_cap, sizeof(int64_t) * (size_t)nk);
+    // (the narrow records' staging: d_ops32, whichever width)
+    if (!r && narrow) r = ensure(c, reinterpret_cast<char **>(&d.d_ops32), &d.ops32_cap, in_bytes);
+    if (!r && narrow && key_base) r = ensure(c, &d.d_base, &d.base_cap, sizeof(int64_t) * (size_t)nk);
     if (!r) r = ensure(c, &d.d_off, &d.off_cap, sizeof(int64_t) * (size_t)(nk + 1));
     if (!r) r = ensure(c, &d.d_out, &d.out_cap, sizeof(lc_key_result) * (size_t)nk);
     if (!r && want_wit) r = ensure(c, &d.d_wit, &d.wit_cap, sizeof(int32_t) * (size_t)nrec);
@@ -1454,7 +1476,7 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
     auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
     const bool pinned = is_pinned(c, ops + r0, in_bytes);
     const size_t off_bytes = sizeof(int64_t) * (size_t)(nk + 1);
-    const size_t base_bytes = k32 && key_base ? sizeof(int64_t) * (size_t)nk : 0;
+    const size_t base_bytes = narrow && key_base ? sizeof(int64_t) * (size_t)nk : 0;
     const size_t out_bytes =
         up(sizeof(lc_key_result) * (size_t)nk) +
         (want_wit ? up(sizeof(int32_t) * (size_t)nrec) + up(sizeof(int32_t) * (size_t)nk) : 0) +
@@ -1506,17 +1528,16 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
     }
     ch.ready = d.cev.data();
     ch.max_len = max_len;
-    if (k32) {
-      ch.d_ops32 = static_cast<const lc_op32 *>(d.d_ops32);
-      ch.d_base = key_base ? d.d_base : nullptr;
-    }
+    if (k32) ch.d_ops32 = static_cast<const lc_op32 *>(d.d_ops32);
+    if (k16) ch.d_ops16 = static_cast<const lc_op16 *>(d.d_ops32);
+    if (narrow) ch.d_base = key_base ? d.d_base : nullptr;
     nchunks[di] = ch.n;
-    char *dst = static_cast<char *>(k32 ? d.d_ops32 : d.d_ops);
+    char *dst = static_cast<char *>(narrow ? d.d_ops32 : d.d_ops);
     const char *src = reinterpret_cast<const char *>(ops + r0);
     // the key offsets (and bases) lead; the compute stream waits for the
     // first chunk's event, which follows them on the copy stream
     hipError_t e = hipEventRecord(d.eh0, d.cst);
-    const void *src_off = key_off + a, *src_base = k32 && key_base ? key_base + a : nullptr;
+    const void *src_off = key_off + a, *src_base = narrow && key_base ? key_base + a : nullptr;
     if (stage) {
       std::memcpy(st_off, src_off, off_bytes);
       if (base_bytes) std::memcpy(st_base, src_base, base_bytes);
@@ -1595,7 +1616,7 @@ int check_host(lc_ctx *c, const Op *ops, const int64_t *key_off, const int64_t *
       if (helper.joinable()) helper.join();
     };
     d.last.h2d_bytes = (int64_t)(in_bytes + sizeof(int64_t) * (size_t)(nk + 1) +
-                                 (k32 && key_base ? sizeof(int64_t) * (size_t)nk : 0));
+                                 (narrow && key_base ? sizeof(int64_t) * (size_t)nk : 0));
     d.last.pinned = pinned;
     WitOut wo;
     wo.n_records = nrec;
@@ -2026,6 +2047,16 @@ int lc_check32(lc_ctx *c, const lc_op32 *ops, const int64_t *key_off, const int6
   return check_host(c, ops, key_off, key_base, n_keys, opts, out, aux);
 }
 
+int lc_check16(lc_ctx *c, const lc_op16 *ops, const int64_t *key_off, const int64_t *key_base,
+               int64_t n_keys, const lc_opts *opts, lc_key_result *out, const lc_aux *aux) {
+  if (!c) return -EINVAL;
+  if (reinterpret_cast<uintptr_t>(ops) % 4) {
+    set_err(c, "lc_check16: ops must be 4-byte aligned");
+    return -EINVAL;
+  }
+  return check_host(c, ops, key_off, key_base, n_keys, opts, out, aux);
+}
+
 int lc_last_call_profile(lc_ctx *c, lc_call_profile *out) {
   if (!c || !out) return -EINVAL;
   *out = c->prof;
@@ -2352,6 +2383,56 @@ int lc_pack32(const lc_op *ops, const int64_t *key_off, int64_t n_keys, lc_op32 
     for (auto &x : th) x.join();
   }
   return 0;
+}
+
+int lc_pack16(const lc_op *ops, const int64_t *key_off, int64_t n_keys, lc_op16 *out,
+              int64_t *key_base) {
+  if (n_keys < 0 || (n_keys > 0 && (!ops || !key_off || !out || !key_base))) return -EINVAL;
+  if (n_keys == 0) return 0;
+  if (key_off[0] < 0) return -EINVAL;
+  for (int64_t k = 0; k < n_keys; k++)
+    if (key_off[k + 1] < key_off[k]) return -EINVAL;
+  constexpr int64_t kFieldMax = 0x7FFFFFFE, kNever = 0xFFFFFFFFll;
+  // lc_pack32's narrowing, then the ids into 15 bits (a record it marks
+  // malformed: value field 0x7FFF, its expected field clamped — the device
+  // reads nothing else of a malformed key's records)
+  std::atomic<bool> range{true};
+  auto pack = [&](int64_t k0, int64_t k1) {
+    for (int64_t k = k0; k < k1; k++) {
+      const int64_t b = key_off[k], e = key_off[k + 1];
+      const int64_t base = e > b ? ops[b].call : 0;
+      key_base[k] = base;
+      for (int64_t i = b; i < e; i++) {
+        const lc_op &o = ops[i];
+        const int64_t rc = o.call - base, rr = o.ret - base;
+        const bool bad = o.value < -1 || o.value > kFieldMax || o.expected < -1 ||
+                         o.expected > kFieldMax || o.call < 0 || o.ret <= o.call || rc < 0 ||
+                         rc >= kNever || (o.ret != LC_INF && rr >= kNever);
+        if (!bad && (o.value > LC_ID15_MAX || o.expected > LC_ID15_MAX)) {
+          range.store(false, std::memory_order_relaxed);
+          return;
+        }
+        const uint32_t f = o.f >= 0 && o.f <= LC_F_CAS ? (uint32_t)o.f : 3u;
+        const uint32_t v = bad ? 0x7FFFu : (uint32_t)(o.value + 1);
+        const uint32_t x = (uint32_t)std::min<int64_t>(0x7FFF, std::max<int64_t>(0, o.expected + 1));
+        lc_op16 &q = out[i];
+        q.fve = f << 30 | v << 15 | x;
+        q.version = o.version < -1 || o.version > kFieldMax ? (int32_t)kFieldMax : (int32_t)o.version;
+        q.call = (uint32_t)rc;
+        q.ret = o.ret == LC_INF ? LC_INF32 : (uint32_t)rr == LC_INF32 ? LC_INF32 - 1 : (uint32_t)rr;
+      }
+    }
+  };
+  const int64_t n_rec = key_off[n_keys] - key_off[0];
+  const int nth = (int)std::min<int64_t>(16, std::max<int64_t>(1, std::min<int64_t>(n_keys, n_rec >> 18)));
+  if (nth <= 1) {
+    pack(0, n_keys);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nth; t++) th.emplace_back(pack, n_keys * t / nth, n_keys * (t + 1) / nth);
+    for (auto &x : th) x.join();
+  }
+  return range.load() ? 0 : -ERANGE;
 }
 
 }  // extern "C"

@@ -51,6 +51,8 @@ def _lib():
         L.lc_edn_ops32.restype = vp
         L.lc_edn_key_base.argtypes = [vp]
         L.lc_edn_key_base.restype = vp
+        L.lc_edn_ops16.argtypes = [vp]
+        L.lc_edn_ops16.restype = vp
         L.lc_edn_key.argtypes = [vp, i64]
         L.lc_edn_key.restype = ctypes.c_char_p
         L.lc_edn_op_text.argtypes = [vp, i64, ctypes.c_int]
@@ -107,6 +109,19 @@ class EdnHistory:
                                      shape=(max(self.n_keys, 1),))[: self.n_keys].copy()
         return o32, base
 
+    def ops16(self):
+        """The records as lc_op16 ((n, 4) uint32) and the keys' bases: what
+        lc_check16 takes (include/lincheck_edn.h, lc_edn_ops16), or None when
+        a value id does not fit 15 bits (use ops32)."""
+        L = _lib()
+        n = len(self.ops)
+        p16 = L.lc_edn_ops16(self._h)
+        if not p16:
+            return None
+        o16 = np.ctypeslib.as_array(ctypes.cast(p16, ctypes.POINTER(ctypes.c_uint32)),
+                                    shape=(max(n, 1) * 4,))[: n * 4].reshape(n, 4).copy()
+        return o16, self.ops32()[1]
+
     def op_text(self, rec, which=0):
         """EDN text of record rec's :invoke (0) or completion (1)."""
         t = _lib().lc_edn_op_text(self._h, rec, which)
@@ -155,9 +170,14 @@ def check(src, device_mask=0, independent=True, ctx=None, opts=None, model="vers
     own = ctx is None
     ctx = ctx or abi.Context(device_mask)
     try:
-        # the drop-in's call: 24-byte records across PCIe (ABI 4)
-        o32, base = h.ops32()
-        rc, res = ctx.check32(o32, h.key_off, base, opts=opts, raise_on_error=False)
+        # the drop-in's call: 16-byte records across PCIe when every value id
+        # fits 15 bits (ABI 5), else 24-byte ones (ABI 4)
+        p16 = h.ops16()
+        if p16 is not None:
+            rc, res = ctx.check16(p16[0], h.key_off, p16[1], opts=opts, raise_on_error=False)
+        else:
+            o32, base = h.ops32()
+            rc, res = ctx.check32(o32, h.key_off, base, opts=opts, raise_on_error=False)
         if rc != 0:
             raise abi.LcError(rc, ctx.last_error())
     finally:

@@ -40,6 +40,16 @@ def test_ops32_are_lc_pack32_of_the_records():
     assert (o32 == want).all() and (base == wbase).all() and len(base) == h.n_keys
 
 
+def test_ops16_are_lc_pack16_of_the_records():
+    """lc_edn_ops16 (round 6): the 16-byte records lc_check16 takes are
+    lc_pack16's of the parsed 48-byte ones, with lc_edn_key_base's bases."""
+    hist, _ = synth.jepsen_history(30, 60, concurrency=6, p_info=0.05, p_anomaly=0.3, seed=17)
+    h = edn.read(edn.to_edn(hist))
+    o16, base = h.ops16()
+    want, wbase = abi.pack16(h.ops, h.key_off)
+    assert (o16 == want).all() and (base == wbase).all() and len(base) == h.n_keys
+
+
 def test_threads_do_not_change_the_result():
     hist, _ = synth.jepsen_history(60, 400, concurrency=20, p_info=0.02, seed=3)
     text = edn.to_edn(hist).encode()

@@ -25,6 +25,7 @@ def test_library_exports_every_declared_symbol():
         "lc_open", "lc_check", "lc_check_device", "lc_last_stats", "lc_last_error",
         "lc_pack32", "lc_check32", "lc_check_device32", "lc_last_call_profile",
         "lc_check_frontiers", "lc_edn_ops32", "lc_edn_key_base", "lc_last_totals", "lc_quiesce",
+        "lc_pack16", "lc_check16", "lc_edn_ops16",
         "lc_last_device_stats", "lc_host_register", "lc_host_unregister",
         "lc_close", "lc_default_opts", "lc_plan_partition", "lc_abi_version",
         "lc_check_ex", "lc_check_device_ex", "lc_key_cost", "lc_build_id",
@@ -35,7 +36,7 @@ def test_library_exports_every_declared_symbol():
         "lc_fx_open_rccl", "lc_fx_abort", "lc_fx_frontier"}
     for n in names:
         assert hasattr(lib, n), n
-    assert abi.lib().lc_abi_version() == 4
+    assert abi.lib().lc_abi_version() == 5
 
 
 def test_struct_sizes():
