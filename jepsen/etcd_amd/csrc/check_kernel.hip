@@ -1538,6 +1538,15 @@ __global__ __launch_bounds__(kWave *kWavesPerWG) void frontier_dump_kernel(
 #ifndef LC_PIPE
 #define LC_PIPE 0
 #endif
+// The version-order tier's pass 1: the case analysis the fused and
+// crash-light passes run (1), or a branch-free form (0, A/B: 952 -> 723
+// instructions and 52 -> 10 branches per wave, but 61 -> 76 VGPRs in
+// fast_tier_kernel and 17 spilled in the resident grid's 80: C2's kernel
+// unchanged, the resident 1,250-key request 15.1 -> 21.3 us;
+// profiles/r06/pass_ab.txt)
+#ifndef LC_FAST_P1_BRANCHY
+#define LC_FAST_P1_BRANCHY 1
+#endif
 // The resident grid's decision: the version-order tier's two record passes
 // (1), or value claims as LDS compare-and-swaps in the one pass (0, as the
 // fused pass)
@@ -2356,6 +2365,60 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
   };
   // pass 1: place mutations, fold read intervals into A / B, claim values,
   // stash crashed writes/CAS
+  if constexpr (MODE == kModeFast && kTwoPass && !LC_FAST_P1_BRANCHY) {
+    // The version-order tier's pass 1, branch-free (the same placements,
+    // bounds and flags as the case analysis below, which the fused and
+    // crash-light passes keep): every record issues its two LDS atomics and
+    // two stores, a record that places nothing aimed at a no-op — max with
+    // 0, min with kNever, stores into the arrays' spare slot kFastMax + 1 —
+    // so the wave runs one straight line per record instead of ~13 masked
+    // branches
+    constexpr int kSpare = kFastMax + 1;
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const int r = tid + u * kFastThreads;
+      auto &&bw = rec_raw(b, u, kbase);
+      const Rec d = decode(bw, base_idx);
+      const uint32_t prev = (uint32_t)wave_shr1((int)d.call, 0);
+      // (a chunk's first call is read only when its first record is live,
+      // its last call only when the next chunk's first is)
+      if (lane == 0) s.first_call[u][w] = d.call;
+      if (lane == kWave - 1) s.last_call[u][w] = d.call;
+      const bool live = r < n;
+      const bool brec = live & (d.bad | (d.f > LC_F_CAS) | ((lane > 0) & (prev >= d.call)));
+      const bool ok = live & !brec;
+      const bool is_read = d.f == LC_F_READ;
+      // reads: a returned read other than [nil nil] constrains; [nil x] is
+      // the JIT tier's; a version index outside [0, n] no state reaches
+      const bool rd = ok & is_read & (d.ret != kNever) & !((d.ver == -1) & (d.val == -1));
+      const bool rd_nil = rd & (d.ver == -1);
+      const int k = d.ver - V0;
+      const bool rd_v = rd & (d.ver != -1);
+      const bool rd_bad = rd_v & ((k < 0) | (k > n));
+      const bool rd_ok = rd_v & !rd_bad;
+      // mutations: crashed or version-less ones are not pinned
+      const bool mu = ok & !is_read;
+      const bool mu_crash = mu & (d.ret == kNever), mu_nover = mu & (d.ver == -1);
+      const int pos = d.ver - V0 - 1;
+      const bool mu_v = mu & !mu_crash & !mu_nover;
+      const bool mu_bad = mu_v & ((pos < 0) | (pos >= n));
+      const bool mu_ok = mu_v & !mu_bad;
+      atomicMax(&s.A[rd_ok ? k : mu_ok ? pos : kSpare], (rd_ok | mu_ok) ? d.call + 1 : 0u);
+      atomicMin(&s.B[rd_ok && k > 0 ? k - 1 : mu_ok ? pos : 0],
+                ((rd_ok & (k > 0)) | mu_ok) ? d.ret : kNever);
+      const int ps = mu_ok ? pos : kSpare;
+      s.Own[ps] = (uint16_t)r;
+      s.Val[ps] = d.val;
+      // the claims on the initial value (the others: pass 2)
+      vbad |= (int)((mu_ok & (d.f == LC_F_CAS) & (pos == 0) & (d.exp != init)) |
+                    (rd_ok & (k == 0) & (d.val != -1) & (d.val != init)));
+      inel |= (int)(brec | rd_nil | mu_crash | mu_nover);
+      jit_only |= (int)(brec | rd_nil | (mu_nover & !mu_crash));
+      giveup |= (int)(mu_crash & (d.ver != -1));
+      bad |= (int)(rd_bad | mu_bad);
+      nmut += __popcll(__ballot(mu_ok));
+    }
+  } else
 #pragma unroll
   for (int u = 0; u < kPer; u++) {
     const int r = tid + u * kFastThreads;
@@ -2515,28 +2578,39 @@ __device__ __forceinline__ void fast_key(int64_t key, int64_t n64, const Op *__r
   int hole = 0;
   if constexpr (kTwoPass) {
     // pass 2: positions, duplicates, CAS expectations and read claims
-    // against the placed values
+    // against the placed values.  Pass 1 raised no flag, so every record is
+    // well formed, every mutation versioned, returned and placed at a
+    // position in [0, n), every read's version index in [0, n].  Branch-free:
+    // all eight LDS reads of a thread's four records issue together (a
+    // branch per record made them eight dependent round trips, ~3,000 cycles
+    // of a lone key's decision), then the checks.
+    int own[kPer], before[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      auto &&bw = rec_raw(b, u, kbase);
+      const int f = (int)bw.a.x, ver = (int)bw.b.y;
+      // mutation: Own[pos], Val[pos - 1]; read: Val[k - 1]  (k = ver - V0)
+      const int i2 = (f == LC_F_READ ? ver - V0 : ver - V0 - 1) - 1;
+      const int i1 = min(max(ver - V0 - 1, 0), kFastMax - 1);
+      own[u] = s.Own[i1];
+      before[u] = s.Val[min(max(i2, 0), kFastMax - 1)];
+    }
 #pragma unroll
     for (int u = 0; u < kPer; u++) {
       const int r = tid + u * kFastThreads;
-      if (r >= n) continue;
       auto &&bw = rec_raw(b, u, kbase);
       const int f = (int)bw.a.x, val = (int)bw.a.y, exp = (int)bw.b.x;
       const int ver = (int)bw.b.y;
-      if (f != LC_F_READ) {
-        const int pos = ver - V0 - 1;
-        if (pos >= M || s.Own[pos] != r) {
-          hole = 1;  // a gap below the last version, or a version held twice
-        } else if (f == LC_F_CAS && exp != (pos == 0 ? init : s.Val[pos - 1])) {
-          hole = 1;
-        }
-      } else if (ver != -1 && bw.c.y != kInf) {
-        const int k = ver - V0;
-        if (k > M)
-          hole = 1;  // a version no mutation wrote
-        else if (val != -1 && val != (k == 0 ? init : s.Val[k - 1]))
-          hole = 1;
-      }
+      const bool live = r < n, is_read = f == LC_F_READ;
+      const int pos = ver - V0 - 1, k = ver - V0;
+      const int bv = (is_read ? k : pos) == 0 ? init : before[u];
+      // a gap below the last version, a version held twice, or a CAS whose
+      // expectation is not the value before it
+      const bool mbad = (pos >= M) | (own[u] != r) | ((f == LC_F_CAS) & (exp != bv));
+      // a version no mutation wrote, or a value that is not the one there
+      const bool rbad = (k > M) | ((val != -1) & (val != bv));
+      const bool rchk = is_read & (ver != -1) & (bw.c.y != kInf);
+      hole |= (int)(live & ((!is_read & mbad) | (rchk & rbad)));
     }
   } else if (4 * tid <= n) {
     const uint2 own2 = reinterpret_cast<const uint2 *>(s.Own)[tid];

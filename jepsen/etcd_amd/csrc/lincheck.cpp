@@ -1277,7 +1277,6 @@ inline lc_op32 as32(const lc_op16 &q) {
   return lc_op32{(int32_t)(q.fve >> 30), v == 0x7FFFu ? -2 : (int32_t)v - 1,
                  x == 0x7FFFu ? -2 : (int32_t)x - 1, q.version, q.call, q.ret};
 }
-inline bool rec_crashed(const lc_op16 &o) { return o.ret == LC_INF32; }
 inline int64_t rec_call(const lc_op16 &o) { return (int64_t)o.call; }
 inline int64_t rec_ret(const lc_op16 &o) { return o.ret == LC_INF32 ? LC_INF : (int64_t)o.ret; }
 inline void rec_kind(const lc_op16 &o, bool *crashed_mut, bool *unpinned) {

@@ -22,17 +22,32 @@ from jepsen.etcd_amd import abi  # noqa: E402
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 bad_total = 0
 t_start = time.time()
+# invalid version-pinned keys (PREFIX witness) and those the certificate
+# finder left without a certificate (its PROOF search over its node or work
+# cap, cert.hip; certified on the witness side only)
+cert_totals = {"invalid_witnessed": 0, "no_certificate": 0}
 
 
 def compare(tag, ops, off, opts=None, algo=oracle.JITC, budget=1 << 18):
     global bad_total
     with abi.Context(device_mask=1) as ctx:
         _, g = ctx.check(ops, off, opts)
-        # the same batch as 24-byte records (lc_check32's native pass): every
-        # result field equal to the 48-byte call's
+        # the same batch as 24-byte records (lc_check32's native pass) and as
+        # 16-byte records (lc_check16): every result field equal to the
+        # 48-byte call's
         o32, b32 = abi.pack32(ops, off)
         _, g32 = ctx.check32(o32, off, b32, opts)
-    n32 = int((g32 != g).sum())
+        p16 = abi.pack16(ops, off)
+        g16 = ctx.check16(p16[0], off, p16[1], opts)[1] if p16 is not None else g
+        # witnesses and certificates: every certificate the checker reads
+        # must hold (never CERT_BAD); count the invalid keys left without one
+        _, gc, _, kind, cert, cset = ctx.check(ops, off, opts, witness=True, certificate=True)
+    n32 = int((g32 != g).sum()) + int((g16 != g).sum()) + int((gc != g).sum())
+    st = oracle.check_certificate(ops, off, cert.reshape(-1), cset, gc, n_threads=16)
+    n32 += int((st == oracle.CERT_BAD).sum())
+    invw = (gc["verdict"] == 0) & (kind == abi.LC_WITNESS_PREFIX)
+    cert_totals["invalid_witnessed"] += int(invw.sum())
+    cert_totals["no_certificate"] += int((invw & (cert[:, 0] == abi.LC_CERT_NONE)).sum())
     _, o = oracle.check(ops, off, algo=algo, n_threads=16, max_configs=budget,
                         init_version=opts.init_version if opts is not None else 0,
                         init_value=opts.init_value if opts is not None else -1)
@@ -42,8 +57,10 @@ def compare(tag, ops, off, opts=None, algo=oracle.JITC, budget=1 << 18):
         diff |= g["fail_op"] != o["fail_op"]
     bad = np.nonzero(known & diff)[0]
     gpu_unknown = int(((g["verdict"] == -1) & (o["verdict"] != -1)).sum())
-    print("%-34s keys %5d decided %5d gpu-only-unknown %3d mismatches %d 32-bit %d (%.0fs)"
-          % (tag, len(off) - 1, int(known.sum()), gpu_unknown, len(bad), n32, time.time() - t_start),
+    print("%-34s keys %5d decided %5d gpu-only-unknown %3d mismatches %d 32/16-bit+cert %d "
+          "invalid-witnessed %d no-cert %d (%.0fs)"
+          % (tag, len(off) - 1, int(known.sum()), gpu_unknown, len(bad), n32, int(invw.sum()),
+             int((invw & (cert[:, 0] == abi.LC_CERT_NONE)).sum()), time.time() - t_start),
           flush=True)
     for k in bad[:5]:
         print("   key", int(k), "gpu", g[k].tolist(), "oracle", int(o["verdict"][k]), int(o["fail_op"][k]))
@@ -142,5 +159,7 @@ for rd in range(rounds):
         print("%-34s keys %5d decided %5d mismatches %d" % ("fx classes ranks %d r%d" % (ranks, rd),
                                                             len(keys), ndec, nbad), flush=True)
         bad_total += nbad
+print("certificates: %d invalid witnessed keys, %d left without a certificate (the PROOF search over "
+      "its cap)" % (cert_totals["invalid_witnessed"], cert_totals["no_certificate"]))
 print("TOTAL mismatches", bad_total)
 sys.exit(1 if bad_total else 0)
