@@ -796,7 +796,29 @@ def model_leg(ctx, abi):
     t = float(np.median(times[1:]))
     hbm_ms = float(np.median([x["hbm_kernel_ms"] for x in st[1:]]))
     explored = int(r["configs_explored"].sum())
+    # the roofline SURVEY §8(d) states for the search: one 128-B table probe
+    # per configuration explored, against the HBM peak; beside it the
+    # counters' own traffic of hbm_coop_kernel<4> (a PMC pass of this leg,
+    # tools/pmc_kernel.sh + pmc_summary.py: the probes mostly hit LDS tables
+    # and L2, so the search is bound by its probes' latency, not by HBM)
+    roof = {"bound": "probe latency (LDS/L2 tables)", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+            "bytes_per_probe": 128, "kernel": "hbm_coop_kernel<4>", "kernel_ms": hbm_ms}
+    if hbm_ms > 0:
+        roof["achieved"] = 128.0 * explored / (hbm_ms * 1e-3) / 1e9
+        roof["frac"] = roof["achieved"] / HBM_PEAK_GBS
+    pmc = os.path.join(ROOT, "profiles", "r06", "pmc_model_hbm_coop4.json")
+    if os.path.exists(pmc):
+        try:
+            dj = json.load(open(pmc))["derived"]
+            roof["traffic_source"] = os.path.relpath(pmc, ROOT)
+            for k in ("hbm_bytes", "hbm_gb_per_s", "l2_hit_rate", "wait_any_frac_of_wave_cycles",
+                      "active_inst_frac_of_wave_cycles", "lds_bank_conflict_cycles_per_lds_inst"):
+                if k in dj:
+                    roof[k] = dj[k]
+        except (ValueError, OSError, KeyError):
+            pass
     return {"workload": "cas-register model: 1000 keys x 1000 ops, concurrency 20 (host buffers)",
+            "roofline": roof,
             "call_ms": t, "ops_per_s": int(off[-1]) / (t * 1e-3),
             "jit_kernel_ms": float(np.median([x["jit_kernel_ms"] for x in st[1:]])),
             "hbm_kernel_ms": hbm_ms,
