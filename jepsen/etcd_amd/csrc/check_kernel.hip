@@ -64,6 +64,14 @@ __device__ unsigned int g_fpdone;
 #define FP_T(i)
 #endif
 
+#ifdef LC_COOP_PROF
+// Dev only (tools/build_variants.sh NAME -DLC_COOP_PROF): wave 0's shader
+// clocks per cooperative workgroup, by phase of its returns (see
+// CoopProf); launch_hbm_coop prints them after the launch
+constexpr int kCpN = 20;
+__device__ unsigned long long g_cp[4096][2][kCpN];  // waves 0 and 1
+#define CP_NOW() __builtin_amdgcn_s_memtime()
+#endif
 #ifdef HBM_PROFILE
 // Dev only (tools/build_variants.sh NAME -DHBM_PROFILE): per cooperative
 // return, by log2 of its larger set: returns, device ticks (100 MHz), LDS-
@@ -184,6 +192,7 @@ struct SlotLds {
 // batches of 64 are claimed with an LDS counter, appends are reserved with
 // LDS atomics, barriers between levels).
 enum { kCoopExpand = 0, kCoopExit = 1 };
+constexpr int kVTab = 16;  // (LDS: four 4-wave workgroups per CU leave ~170 bytes each)
 constexpr uint32_t kBusy = 0x80000000u;  // table tag: claimed, configuration being written
 struct CoopShared {
   int cmd;
@@ -203,6 +212,9 @@ struct CoopShared {
   unsigned long long explored;
   long long budget;
   SlotLds slots;
+  // the slots legal at value id v - 1 whatever the version, for v < kVTab
+  // (used when no pending slot constrains the version: version-less models)
+  uint64_t vlegal[kVTab];
 };
 
 struct HbmStore {
@@ -217,6 +229,17 @@ struct HbmStore {
   uint32_t tmask_full;  // the workspace's table size - 1 (2 * cap entries)
   int hint = 0;    // largest R / W set of this key's returns so far
   uint32_t epoch;
+#ifdef LC_COOP_PROF
+  // [0] start barrier [1] split [2] split barrier [3] queue [4] end barrier
+  // (LDS-mode returns), [5] LDS-mode returns, [6] all cooperative returns'
+  // clocks, [7] whole keys, [8] cooperative returns, [9] HBM-mode ones,
+  // [10] keys; LDS-mode queue phase: [11] batches [12] successor rounds
+  // [13] queue-empty sleeps [14] clocks claiming [15] clocks waiting for
+  // ready flags [16] clocks computing candidates [17] clocks in rounds;
+  // ts: this return's marks
+  uint64_t cp[20] = {0};
+  uint64_t ts[6];
+#endif
   // Table size of a return (adaptive, round 2).  The sets of one return are
   // usually far smaller than the workspace's capacity, and a table sized for
   // the capacity spreads them over 512 KB per role: every probe missed L2
@@ -688,6 +711,9 @@ __device__ __forceinline__ uint64_t legal_by_state(const int4 &spre, int ver, in
 template <int LT>
 __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
   const int nw = st.nwaves;
+#ifdef LC_COOP_PROF
+  st.ts[1] = CP_NOW();
+#endif
   st.epoch = C.epoch;
   st.tmask = C.tmask;
   CoopTab<LT> &T = coop_tab<LT>();
@@ -711,6 +737,15 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
   const int4 spre = L.pre[lane];
   const int sval = L.val[lane];
   const uint64_t spbit = L.pbit[lane];
+  // Legality by value when no pending slot constrains the version (every
+  // slot's version mask nvm is 0): one ballot per value id, the waves
+  // sharing the ids; read after the split's barrier
+  const bool vt = (__ballot(spre.y != 0) & (muts | reads)) == 0;
+  if (vt)
+    for (int v = wave; v < kVTab; v += nw) {
+      const uint64_t m = __ballot(((((v - 1) ^ spre.z) & spre.w) == 0));
+      if (lane == 0) C.vlegal[v] = m;
+    }
   // split F into R (x linearized, its bit dropped) and W
   for (int j0 = wave * kWave; j0 < nF; j0 += nw * kWave) {
     const int j = j0 + lane;
@@ -750,6 +785,9 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
     }
   }
   if (__ballot(ovf) && lane == 0) atomicMin(&C.status, -3);
+#ifdef LC_COOP_PROF
+  st.ts[2] = CP_NOW();
+#endif
   if (lds) {
     // LDS: W is a work queue.  The split's claims must all be in the tables
     // before any successor is deduplicated against them: one barrier.
@@ -767,6 +805,9 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
     }
     coop_barrier();
   }
+#ifdef LC_COOP_PROF
+  st.ts[3] = CP_NOW();
+#endif
   const uint32_t ep16 = eb >> 16;
   const int kw = lds ? C.kw : 0;  // (written in the split, before the barrier above)
   for (;;) {
@@ -778,6 +819,10 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
     }
     for (;;) {  // batches of up to 64 W configurations
       int b = 0, k = 0;
+#ifdef LC_COOP_PROF
+      const uint64_t qc0 = CP_NOW();
+      int qsp = 0;
+#endif
       if (lds) {
         // Queue claim: (head, active) packed in one word, so a wave that
         // finds the queue empty leaves only when no wave is expanding (a
@@ -807,11 +852,18 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
               k = -1;
               break;
             }
+#ifdef LC_COOP_PROF
+            qsp++;
+#endif
             __builtin_amdgcn_s_sleep(1);
           }
         }
         k = uni(k);
         b = uni(b);
+#ifdef LC_COOP_PROF
+        st.cp[13] += (uint64_t)uni(qsp);
+        st.cp[14] += CP_NOW() - qc0;
+#endif
         if (k < 0) break;
       } else {
         if (lane == 0) b = atomicAdd(&C.head, kWave);
@@ -841,6 +893,9 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
           }
           break;
         }
+#ifdef LC_COOP_PROF
+        st.cp[15] += CP_NOW() - qc0;
+#endif
         lds_acquire();
         const int jj = act ? j : b;
         c.mask = T.smask[ROLE_W][jj];
@@ -849,23 +904,41 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
         c = st.get(rW, act ? j : b);
       }
       const int cver = sv_ver(c.sv), cval = sv_val(c.sv);
-      uint64_t cand = legal_by_state(spre, cver, cval, act) & muts & ~c.mask;
+      uint64_t cand;
+      if (vt && !__ballot(act && (uint32_t)(cval + 1) >= (uint32_t)kVTab))
+        cand = act ? C.vlegal[cval + 1] & muts & ~c.mask : 0;  // by value (versions free)
+      else
+        cand = legal_by_state(spre, cver, cval, act) & muts & ~c.mask;
       // an op only if its class predecessors (deadline order) are linearized
       for (uint64_t m = muts & ordered; m; m &= m - 1) {
         const int t = __builtin_ctzll(m);
         if (rl64(spbit, t) & ~c.mask) cand &= ~(1ull << t);
       }
+#ifdef LC_COOP_PROF
+      const uint64_t qc2 = CP_NOW();
+      if (lds) {
+        st.cp[11]++;
+        st.cp[16] += qc2 - qc0;
+      }
+#endif
       unsigned long long exw = 0;  // this batch's successors (one atomic per batch)
       for (;;) {
         const bool has = cand != 0;
         const uint64_t hb = __ballot(has);
         if (!hb) break;
+#ifdef LC_COOP_PROF
+        if (lds) st.cp[12]++;
+#endif
         exw += __popcll(hb);
         const int t = has ? __builtin_ctzll(cand) : 0;
         cand &= cand - 1;
         const int nver = cver + 1, nval = __shfl(sval, t);
         uint64_t nm = c.mask | (1ull << t);
-        nm |= legal_by_state(spre, nver, nval, has) & reads;  // eager read closure
+        // eager read closure
+        if (vt && !__ballot(has && (uint32_t)(nval + 1) >= (uint32_t)kVTab))
+          nm |= has ? C.vlegal[nval + 1] & reads : 0;
+        else
+          nm |= legal_by_state(spre, nver, nval, has) & reads;
         const bool toR = (nm & bs) != 0;
         const Cfg nc{toR ? nm & ~bs : nm, pack_sv(nver, nval)};
         if (lds) {  // inserts, set indices and appends in one pass
@@ -895,6 +968,9 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
           break;
         }
       }
+#ifdef LC_COOP_PROF
+      if (lds) st.cp[17] += CP_NOW() - qc2;
+#endif
       if (lane == 0 && exw) {
         const unsigned long long ex = atomicAdd(&C.explored, exw) + exw;
         if ((long long)ex > C.budget && C.status == 0) atomicMin(&C.status, -2);
@@ -911,7 +987,13 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
     }
     coop_barrier();
   }
+#ifdef LC_COOP_PROF
+  st.ts[4] = CP_NOW();
+#endif
   if (lds) coop_barrier();  // the global R appends, for wave 0 and the next split
+#ifdef LC_COOP_PROF
+  st.ts[5] = CP_NOW();
+#endif
 }
 
 // Wave 0's side of a cooperative return: publish, expand with the others.
@@ -930,6 +1012,9 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
   if (!lds) st.tmask = st.pick_tmask(nF, floor);
 #ifdef HBM_PROFILE
   const uint64_t tr0 = wall_clock64();
+#endif
+#ifdef LC_COOP_PROF
+  const uint64_t cr0 = CP_NOW();
 #endif
   for (;;) {
     st.begin_return();  // a fresh epoch per attempt: the aborted one's entries are stale
@@ -963,8 +1048,17 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
       C.explored = (unsigned long long)o.explored;
       C.budget = (long long)p.budget;
     }
+#ifdef LC_COOP_PROF
+    st.ts[0] = CP_NOW();
+#endif
     coop_barrier();  // the workers' start barrier
     coop_expand<LT>(st, C, lane, 0);
+#ifdef LC_COOP_PROF
+    if (lds && C.status == 0) {
+      for (int q = 0; q < 5; q++) st.cp[q] += st.ts[q + 1] - st.ts[q];
+      st.cp[5]++;
+    }
+#endif
     if (C.status != -3) break;
     if (lds) {
       lds = false;
@@ -985,6 +1079,11 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
   if (lane == 0 && blockIdx.x < 4096) {
     g_hwg[blockIdx.x][lds ? 0 : 1] += wall_clock64() - tr0;
   }
+#endif
+#ifdef LC_COOP_PROF
+  st.cp[6] += CP_NOW() - cr0;
+  st.cp[8]++;
+  if (!lds) st.cp[9]++;
 #endif
   if (C.status < 0) return C.status;
   o.explored = (int64_t)C.explored;
@@ -3230,7 +3329,14 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
 #ifdef HBM_PROFILE
       const uint64_t tk0 = wall_clock64();
 #endif
+#ifdef LC_COOP_PROF
+      const uint64_t ck0 = CP_NOW();
+#endif
       check_key(ops + (beg - key_base), (int)(end - beg), p, st, o, lane);
+#ifdef LC_COOP_PROF
+      st.cp[7] += CP_NOW() - ck0;
+      st.cp[10]++;
+#endif
 #ifdef HBM_PROFILE
       if (lane == 0 && blockIdx.x < 4096) g_hwg[blockIdx.x][2] += wall_clock64() - tk0;
 #endif
@@ -3246,6 +3352,10 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
       }
     }
     if (lane == 0) C.cmd = kCoopExit;
+#ifdef LC_COOP_PROF
+    if (lane == 0 && blockIdx.x < 4096)
+      for (int q = 0; q < kCpN; q++) g_cp[blockIdx.x][0][q] = st.cp[q];
+#endif
 #ifdef HBM_PROFILE
     __threadfence();
     if (lane == 0 && atomicAdd(&g_hdone, 1u) == gridDim.x - 1)
@@ -3274,6 +3384,10 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
       if (C.cmd == kCoopExit) break;
       coop_expand<LT>(st, C, lane, wave);
     }
+#ifdef LC_COOP_PROF
+    if (wave == 1 && lane == 0 && blockIdx.x < 4096)
+      for (int q = 0; q < kCpN; q++) g_cp[blockIdx.x][1][q] = st.cp[q];
+#endif
   }
 }
 
@@ -3556,6 +3670,42 @@ hipError_t launch_hbm_coop(const lc_op *d_ops, const int64_t *d_key_off, const i
     hipLaunchKernelGGL(hbm_coop_kernel<4>, dim3((unsigned)n_wg), dim3(4 * kWave), 0, stream,
                        d_ops, d_key_off, d_keys, n_list, p, d_out, static_cast<char *>(d_ws), cap,
                        d_ovf_out, d_n_ovf_out, d_malformed, d_next, last_tier);
+#ifdef LC_COOP_PROF
+  {
+    static unsigned long long h[4096][2][kCpN];
+    const int nw = std::min(n_wg, 4096);
+    void *sym = nullptr;
+    if (hipStreamSynchronize(stream) == hipSuccess && hipGetSymbolAddress(&sym, HIP_SYMBOL(g_cp)) == hipSuccess &&
+        hipMemcpy(h, sym, sizeof(h[0]) * nw, hipMemcpyDeviceToHost) == hipSuccess) {
+      for (int wv = 0; wv < 2; wv++) {
+        double sum[kCpN] = {0};
+        int slow = 0;
+        for (int w = 0; w < nw; w++) {
+          for (int q = 0; q < kCpN; q++) sum[q] += (double)h[w][wv][q];
+          if (h[w][0][7] > h[slow][0][7]) slow = w;
+        }
+        auto line = [&](const char *who, const double *v, double div, double rets) {
+          const double r = std::max(1.0, rets), bt = std::max(1.0, v[11]);
+          fprintf(stderr,
+                  "coopprof wave %d %s: key clocks %.0f, coop returns %.0f (%.0f HBM-mode) taking %.0f; LDS-mode "
+                  "returns %.0f: start-barrier %.0f split %.0f split-barrier %.0f queue %.0f end-barrier %.0f "
+                  "(clocks each); per return: batches %.2f rounds %.2f sleeps %.1f; per batch clocks: claim %.0f "
+                  "ready %.0f cand %.0f rounds %.0f\n",
+                  wv, who, v[7] / div, v[8] / div, v[9] / div, v[6] / div, v[5] / div, v[0] / r, v[1] / r,
+                  v[2] / r, v[3] / r, v[4] / r, v[11] / r, v[12] / r, v[13] / r, v[14] / bt, v[15] / bt,
+                  v[16] / bt, v[17] / bt);
+        };
+        double rets = 0;
+        for (int w = 0; w < nw; w++) rets += (double)h[w][0][5];
+        line("mean per workgroup", sum, std::max(1, nw), rets);
+        double sl[kCpN];
+        for (int q = 0; q < kCpN; q++) sl[q] = (double)h[slow][wv][q];
+        line("slowest workgroup", sl, 1.0, (double)h[slow][0][5]);
+      }
+      (void)hipMemset(sym, 0, sizeof(h[0]) * nw);
+    }
+  }
+#endif
   return hipGetLastError();
 }
 
