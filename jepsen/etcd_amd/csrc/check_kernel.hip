@@ -68,7 +68,7 @@ __device__ unsigned int g_fpdone;
 // Dev only (tools/build_variants.sh NAME -DLC_COOP_PROF): wave 0's shader
 // clocks per cooperative workgroup, by phase of its returns (see
 // CoopProf); launch_hbm_coop prints them after the launch
-constexpr int kCpN = 20;
+constexpr int kCpN = 24;
 __device__ unsigned long long g_cp[4096][2][kCpN];  // waves 0 and 1
 #define CP_NOW() __builtin_amdgcn_s_memtime()
 #endif
@@ -211,10 +211,13 @@ struct CoopShared {
   int lclear;       // the LDS epoch wrapped: clear the tags first
   unsigned long long explored;
   long long budget;
+  uint64_t fclear, fclose;  // F's pending updates (CoopStore), applied by the split
+  unsigned long long rand;  // AND of R's masks (every wave ANDs in what it adds)
   SlotLds slots;
   // the slots legal at value id v - 1 whatever the version, for v < kVTab
   // (used when no pending slot constrains the version: version-less models)
   uint64_t vlegal[kVTab];
+  int vt;  // vlegal holds this return's slots (no pending slot constrains the version)
 };
 
 struct HbmStore {
@@ -236,8 +239,10 @@ struct HbmStore {
   // [10] keys; LDS-mode queue phase: [11] batches [12] successor rounds
   // [13] queue-empty sleeps [14] clocks claiming [15] clocks waiting for
   // ready flags [16] clocks computing candidates [17] clocks in rounds;
+  // event loop: [18] clocks in calls [19] in single-configuration returns
+  // [20] after cooperative returns [21] calls [22] single returns;
   // ts: this return's marks
-  uint64_t cp[20] = {0};
+  uint64_t cp[24] = {0};
   uint64_t ts[6];
 #endif
   // Table size of a return (adaptive, round 2).  The sets of one return are
@@ -438,8 +443,10 @@ constexpr uint32_t kIdxOvf = 0xFFFEu;   // claimed past kLim (the return is redo
 template <int LT>
 struct CoopTab {
   // configurations per set: 12 B each (below) plus a 2-byte flag, with the
-  // tables at <= 42 % load: 864 in 38 KB (4-wave), 1,728 in 76 KB (8-wave)
-  static constexpr int kLim = LT * 27 / 64;
+  // tables at <= 42 % load: 844 in 38 KB (4-wave: 20 fewer than the load
+  // allows, for scr), 1,728 in 78 KB (8- and 16-wave)
+  static constexpr int kLim = LT * 27 / 64 - (LT < 4096 ? 20 : 0);
+  static constexpr int kScrWaves = LT < 4096 ? 4 : 16;
   static_assert(kLim < (int)kIdxOvf, "set index must fit 16 bits");
   uint32_t tag[2][LT];      // (epoch << 16) | index, per role
   // R and W of this return as (linearized set, value): within one return and
@@ -448,6 +455,8 @@ struct CoopTab {
   uint64_t smask[2][kLim];
   int32_t sval[2][kLim];
   uint16_t wrdy[kLim];      // W entry written (its epoch): the work queue's readiness
+  // per wave, a round's successors: (source lane << 6) | slot (coop_expand)
+  uint16_t scr[kScrWaves][kWave];
 };
 template <int LT>
 __device__ __forceinline__ CoopTab<LT> &coop_tab() {
@@ -459,6 +468,21 @@ struct CoopStore : HbmStore {
   static constexpr int kLT = LT;
   int last = 0;           // the previous return's larger set
   uint32_t lepoch = 0;    // LDS table epoch (16 bits; 0 is never current)
+  // The frontier's masks in the global region are brought up to date by the
+  // next return's split, not by wave 0 as the events come (round 6): slots
+  // retired since the last return (cleared from every configuration, before)
+  // and reads called since (each linearized where legal); and the AND of
+  // the last return's R, kept by the waves as they fill it
+  uint64_t fclear = 0, fclose = 0, rand = ~0ull;
+};
+// (check_key: the cooperative stores defer their frontier updates)
+template <class S, class = void>
+struct DeferF {
+  static constexpr bool value = false;
+};
+template <class S>
+struct DeferF<S, std::void_t<decltype(S::kLT)>> {
+  static constexpr bool value = S::kLT > 0;
 };
 
 // LDS-only fences: the tables are workgroup-private, so publishing an entry
@@ -737,23 +761,34 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
   const int4 spre = L.pre[lane];
   const int sval = L.val[lane];
   const uint64_t spbit = L.pbit[lane];
-  // Legality by value when no pending slot constrains the version (every
-  // slot's version mask nvm is 0): one ballot per value id, the waves
-  // sharing the ids; read after the split's barrier
-  const bool vt = (__ballot(spre.y != 0) & (muts | reads)) == 0;
-  if (vt)
-    for (int v = wave; v < kVTab; v += nw) {
-      const uint64_t m = __ballot(((((v - 1) ^ spre.z) & spre.w) == 0));
-      if (lane == 0) C.vlegal[v] = m;
-    }
-  // split F into R (x linearized, its bit dropped) and W
+  const bool vt = C.vt;  // (coop_return: C.vlegal)
+  // split F into R (x linearized, its bit dropped) and W, after F's pending
+  // updates: retired slots cleared, then reads called since linearized where
+  // legal (a freed slot a new read took: both, in that order)
+  const uint64_t fclear = C.fclear, fclose = C.fclose;
+  uint64_t rand = ~0ull;  // AND of the masks this wave adds to R
+  auto flush_rand = [&]() {
+    const uint64_t r = wave_and_u64(rand);
+    if (r != ~0ull && lane == 0)
+      __hip_atomic_fetch_and(&C.rand, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    rand = ~0ull;
+  };
   for (int j0 = wave * kWave; j0 < nF; j0 += nw * kWave) {
     const int j = j0 + lane;
     const bool v = j < nF;
     Cfg c{0, 0};
     if (v) c = st.get(rF, j);
+    c.mask &= ~fclear;
+    if (fclose) {
+      const int fver = sv_ver(c.sv), fval = sv_val(c.sv);
+      if (vt && !__ballot(v && (uint32_t)(fval + 1) >= (uint32_t)kVTab))
+        c.mask |= v ? C.vlegal[fval + 1] & fclose : 0;
+      else
+        c.mask |= legal_by_state(spre, fver, fval, v) & fclose;
+    }
     if (lds && j == 0) C.kw = sv_ver(c.sv) - __popcll(c.mask & muts);  // (any F config gives it)
     const bool has = v && (c.mask & bs);
+    if (has) rand &= c.mask & ~bs;
     const bool lacks = v && !(c.mask & bs);
     const uint64_t mh = __ballot(has), ml = __ballot(lacks);
     int bR = 0, bW = 0;
@@ -785,6 +820,7 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
     }
   }
   if (__ballot(ovf) && lane == 0) atomicMin(&C.status, -3);
+  flush_rand();  // (before the split's barrier)
 #ifdef LC_COOP_PROF
   st.ts[2] = CP_NOW();
 #endif
@@ -921,19 +957,34 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
         st.cp[16] += qc2 - qc0;
       }
 #endif
-      unsigned long long exw = 0;  // this batch's successors (one atomic per batch)
-      for (;;) {
-        const bool has = cand != 0;
-        const uint64_t hb = __ballot(has);
-        if (!hb) break;
+      // The batch's successors, one per lane and round: lane j of a round
+      // takes the successor at position r0 + j of the batch's list (source
+      // lanes in order, each its candidates by slot), so a round is full
+      // unless it is the last, whatever the spread of candidates per lane
+      const int ncand = __popcll(cand);
+      const int incl = wave_prefix_sum(ncand, lane);
+      const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
+      const unsigned long long exw = (unsigned long long)total;  // (one atomic per batch)
+      uint16_t *scr = T.scr[wave];
+      for (int r0 = 0; r0 < total; r0 += kWave) {
 #ifdef LC_COOP_PROF
         if (lds) st.cp[12]++;
 #endif
-        exw += __popcll(hb);
-        const int t = has ? __builtin_ctzll(cand) : 0;
-        cand &= cand - 1;
-        const int nver = cver + 1, nval = __shfl(sval, t);
-        uint64_t nm = c.mask | (1ull << t);
+        {
+          uint64_t cc = cand;
+          for (int i = incl - ncand; cc && i < r0 + kWave; i++, cc &= cc - 1)
+            if (i >= r0) scr[i - r0] = (uint16_t)((lane << 6) | __builtin_ctzll(cc));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        const bool has = r0 + lane < total;
+        const int e = has ? (int)scr[lane] : 0;
+        const int src = has ? e >> 6 : lane, t = e & 63;
+        const uint64_t cm = ((uint64_t)(uint32_t)__shfl((int)(c.mask >> 32), src) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)c.mask, src);
+        const int nver = __shfl(cver, src) + 1, nval = __shfl(sval, t);
+        uint64_t nm = cm | (1ull << t);
         // eager read closure
         if (vt && !__ballot(has && (uint32_t)(nval + 1) >= (uint32_t)kVTab))
           nm |= has ? C.vlegal[nval + 1] & reads : 0;
@@ -942,7 +993,8 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
         const bool toR = (nm & bs) != 0;
         const Cfg nc{toR ? nm & ~bs : nm, pack_sv(nver, nval)};
         if (lds) {  // inserts, set indices and appends in one pass
-          lds_insert_lanes(T, C, st, rR, toR ? ROLE_R : ROLE_W, nc, has, eb, ovf, lane);
+          if (lds_insert_lanes(T, C, st, rR, toR ? ROLE_R : ROLE_W, nc, has, eb, ovf, lane) && toR)
+            rand &= nc.mask;
           if (__ballot(ovf)) {
             if (lane == 0) atomicMin(&C.status, -3);
             break;
@@ -959,7 +1011,10 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
         const int aR = uni((int)aRW), aW = uni((int)(aRW >> 32));
         const bool fullR = aR + __popcll(bR) > lim, fullW = aW + __popcll(bW) > lim;
         const bool full = fullR || fullW;
-        if (insR && !fullR) st.reg(rR)[aR + lanes_below(bR)] = nc;
+        if (insR && !fullR) {
+          st.reg(rR)[aR + lanes_below(bR)] = nc;
+          rand &= nc.mask;
+        }
         if (insW && !fullW) st.reg(rW)[aW + lanes_below(bW)] = nc;
         // -3: this return's tables are too small (redone larger / in HBM);
         // -1: the workspace is full (next tier)
@@ -978,6 +1033,7 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
       if (lds && lane == 0) atomicAdd(&C.qword, ~0ull << 32);  // active - 1, after the appends
     }
     if (lds) break;
+    flush_rand();
     coop_barrier();  // the level's appends are done
     if (wave == 0 && lane == 0) {
       C.lo = hi;
@@ -990,6 +1046,7 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
 #ifdef LC_COOP_PROF
   st.ts[4] = CP_NOW();
 #endif
+  if (lds) flush_rand();
   if (lds) coop_barrier();  // the global R appends, for wave 0 and the next split
 #ifdef LC_COOP_PROF
   st.ts[5] = CP_NOW();
@@ -1005,6 +1062,19 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
   C.slots.val[lane] = sl.val;
   C.slots.pbit[lane] = sl.pbit;
   const uint64_t ordered = __ballot(sl.pbit != 0);  // (a ballot: outside the lane-0 block)
+  // Legality by value id when no pending slot constrains the version (every
+  // occupied slot's version mask nvm is 0: version-less models): lane v
+  // keeps the slots legal at value id v - 1 (one ballot each)
+  const bool vt = (__ballot(sl.nvm != 0) & mk.occ) == 0;
+  if (vt) {
+    uint64_t mine = 0;
+#pragma unroll
+    for (int v = 0; v < kVTab; v++) {
+      const uint64_t m = __ballot((((v - 1) ^ sl.nl) & sl.nlm) == 0);
+      if (lane == v) mine = m;
+    }
+    if (lane < kVTab) C.vlegal[lane] = mine;
+  }
   // LDS tables first when this frontier and the previous return's sets fit
   constexpr int kLim = CoopTab<LT>::kLim;
   bool lds = nF <= kLim && st.last <= kLim;
@@ -1047,6 +1117,10 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
       C.status = 0;
       C.explored = (unsigned long long)o.explored;
       C.budget = (long long)p.budget;
+      C.fclear = st.fclear;
+      C.fclose = st.fclose;
+      C.rand = ~0ull;
+      C.vt = vt;
     }
 #ifdef LC_COOP_PROF
     st.ts[0] = CP_NOW();
@@ -1088,6 +1162,8 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
   if (C.status < 0) return C.status;
   o.explored = (int64_t)C.explored;
   st.last = max(C.nR, C.nW);
+  st.fclear = st.fclose = 0;  // applied by this return's split
+  st.rand = C.rand;
   if (!lds) st.hint = max(st.hint, st.last);
   return C.nR;
 }
@@ -1274,6 +1350,16 @@ __device__ void dump_frontier(const Store &st, const Slot &sl, const Masks &mk, 
   dr.n = m;
 }
 
+#ifdef LC_COOP_PROF
+#define EL_PROF(stmt)                                  \
+  do {                                                 \
+    if constexpr (DeferF<Store>::value) { stmt; }      \
+  } while (0)
+#else
+#define EL_PROF(stmt) \
+  do {                \
+  } while (0)
+#endif
 template <class Store, bool kDump = false>
 __device__ void check_key(const lc_op *__restrict__ kops, const int n,
                           const KParams &p, Store &st, KeyOut &o,
@@ -1305,7 +1391,11 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
   Raw nxt = load_raw(kops, kWave + lane, n);
   int base = 0, i = 0;
 
+#ifdef LC_COOP_PROF
+  uint64_t el0 = 0;
+#endif
   for (;;) {
+    EL_PROF(el0 = CP_NOW());
     const uint32_t ncall = (i < n) ? (uint32_t)rl32((int)cur.call, i - base) : kNever;
     // Returns due before the next call: one ballot; the DPP min only when
     // several are due at once.
@@ -1372,7 +1462,9 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
         mk.occ |= bs;
         if (f == LC_F_READ) {
           mk.rdm |= bs;
-          if (!single) {  // eager read closure at the call, per configuration
+          if constexpr (DeferF<Store>::value) {
+            if (!single) st.fclose |= bs;  // (by the next split)
+          } else if (!single) {  // eager read closure at the call, per configuration
             for (int j = lane; j < nF; j += kWave) {
               const Cfg c = st.get(rF, j);
               if (pre_ok(nv, nvm, nl, nlm, sv_ver(c.sv), sv_val(c.sv)))
@@ -1389,6 +1481,7 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
         cmk = chunk_masks(cur, fsv);
         nxt = load_raw(kops, base + kWave + lane, n);
       }
+      EL_PROF(st.cp[18] += CP_NOW() - el0; st.cp[21]++);
       continue;
     }
 
@@ -1415,6 +1508,9 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
       }
     }
     bool empty = false;
+#ifdef LC_COOP_PROF
+    const bool was_single = single;
+#endif
     if (single) {
       // x is pending (a linearized op would have been retired).  Chain walk:
       // while exactly one mutation can step the lone configuration, the JIT
@@ -1466,6 +1562,7 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
                         __ballot(pre_ok(cur.nv, cur.nvm, cur.nl, cur.nlm, sv_ver(fsv), sv_val(fsv)));
       }
     }
+    EL_PROF(if (was_single) { st.cp[19] += CP_NOW() - el0; st.cp[22]++; });
     if (!single) {
       // the time budget is checked where time goes: returns on the general
       // (multi-configuration) path
@@ -1484,6 +1581,9 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
         o.reason = r == -1 ? LC_REASON_FRONTIER_LDS : LC_REASON_CONFIG_BUDGET;
         return;
       }
+#ifdef LC_COOP_PROF
+      const uint64_t pr0 = CP_NOW();
+#endif
       const int t = rF;
       rF = rR;
       rR = t;
@@ -1492,21 +1592,32 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
       empty = nF == 0;
       if (!empty) {
         retire(sl, mk, bs, lane);  // x returned
-        uint64_t acc = ~0ull;
-        for (int j = lane; j < nF; j += kWave) acc &= st.get(rF, j).mask;
-        const uint64_t rb = mk.occ & wave_and_u64(acc);
-        if (rb) {
-          retire(sl, mk, rb, lane);
-          for (int j = lane; j < nF; j += kWave)
-            st.set_mask_lane(rF, j, st.get(rF, j).mask & ~rb);
+        uint64_t rb;
+        if constexpr (DeferF<Store>::value) {
+          rb = mk.occ & st.rand;  // (the AND the return's waves kept)
+          if (rb) {
+            retire(sl, mk, rb, lane);
+            st.fclear |= rb;  // (by the next split)
+          }
+        } else {
+          uint64_t acc = ~0ull;
+          for (int j = lane; j < nF; j += kWave) acc &= st.get(rF, j).mask;
+          rb = mk.occ & wave_and_u64(acc);
+          if (rb) {
+            retire(sl, mk, rb, lane);
+            for (int j = lane; j < nF; j += kWave)
+              st.set_mask_lane(rF, j, st.get(rF, j).mask & ~rb);
+          }
         }
         if (nF == 1) {  // back to the register-resident frontier (mask now empty)
           fsv = rfl64(st.get(rF, 0).sv);
+          if constexpr (DeferF<Store>::value) st.fclear = st.fclose = 0;
           single = true;
           cmk.legal_now = cmk.isread &
                           __ballot(pre_ok(cur.nv, cur.nvm, cur.nl, cur.nlm, sv_ver(fsv), sv_val(fsv)));
         }
       }
+      EL_PROF(st.cp[20] += CP_NOW() - pr0);
     }
     if (empty) {
       o.verdict = LC_INVALID;
@@ -3326,6 +3437,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
       KeyOut o;
       st.hint = 0;  // table-size hints: per key
       st.last = 0;
+      st.fclear = st.fclose = 0;
 #ifdef HBM_PROFILE
       const uint64_t tk0 = wall_clock64();
 #endif
@@ -3698,6 +3810,10 @@ hipError_t launch_hbm_coop(const lc_op *d_ops, const int64_t *d_key_off, const i
         double rets = 0;
         for (int w = 0; w < nw; w++) rets += (double)h[w][0][5];
         line("mean per workgroup", sum, std::max(1, nw), rets);
+        if (wv == 0)
+          fprintf(stderr, "coopprof event loop per workgroup: calls %.0f taking %.0f, single returns %.0f taking "
+                  "%.0f, after cooperative returns %.0f\n", sum[21] / nw, sum[18] / nw, sum[22] / nw,
+                  sum[19] / nw, sum[20] / nw);
         double sl[kCpN];
         for (int q = 0; q < kCpN; q++) sl[q] = (double)h[slow][wv][q];
         line("slowest workgroup", sl, 1.0, (double)h[slow][0][5]);
