@@ -68,7 +68,7 @@ __device__ unsigned int g_fpdone;
 // Dev only (tools/build_variants.sh NAME -DLC_COOP_PROF): wave 0's shader
 // clocks per cooperative workgroup, by phase of its returns (see
 // CoopProf); launch_hbm_coop prints them after the launch
-constexpr int kCpN = 24;
+constexpr int kCpN = 26;
 __device__ unsigned long long g_cp[4096][2][kCpN];  // waves 0 and 1
 #define CP_NOW() __builtin_amdgcn_s_memtime()
 #endif
@@ -242,7 +242,7 @@ struct HbmStore {
   // event loop: [18] clocks in calls [19] in single-configuration returns
   // [20] after cooperative returns [21] calls [22] single returns;
   // ts: this return's marks
-  uint64_t cp[24] = {0};
+  uint64_t cp[26] = {0};
   uint64_t ts[6];
 #endif
   // Table size of a return (adaptive, round 2).  The sets of one return are
@@ -485,6 +485,11 @@ struct DeferF<S, std::void_t<decltype(S::kLT)>> {
   static constexpr bool value = S::kLT > 0;
 };
 
+// Sleep of a wave whose work queue is empty while others expand, or whose
+// claimed entries are not yet written (s_sleep units of 64 clocks)
+#ifndef LC_COOP_SLEEP
+#define LC_COOP_SLEEP 1
+#endif
 // LDS-only fences: the tables are workgroup-private, so publishing an entry
 // waits for LDS (lgkmcnt) only, not for the wave's global R appends.
 __device__ __forceinline__ void lds_release() {
@@ -891,7 +896,7 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
 #ifdef LC_COOP_PROF
             qsp++;
 #endif
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(LC_COOP_SLEEP);
           }
         }
         k = uni(k);
@@ -920,7 +925,7 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
               ovf = true;
               break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(LC_COOP_SLEEP);
           }
         if (__ballot(ovf)) {
           if (lane == 0) {
@@ -1058,6 +1063,9 @@ template <int LT>
 __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, int s, int rF, int rR,
                            int rW, int nF, const KParams &p, KeyOut &o, int lane) {
   CoopShared &C = *st.coop;
+#ifdef LC_COOP_PROF
+  const uint64_t ce0 = CP_NOW();
+#endif
   C.slots.pre[lane] = make_int4(sl.nv, sl.nvm, sl.nl, sl.nlm);
   C.slots.val[lane] = sl.val;
   C.slots.pbit[lane] = sl.pbit;
@@ -1085,6 +1093,7 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
 #endif
 #ifdef LC_COOP_PROF
   const uint64_t cr0 = CP_NOW();
+  st.cp[23] += cr0 - ce0;
 #endif
   for (;;) {
     st.begin_return();  // a fresh epoch per attempt: the aborted one's entries are stale
@@ -1572,6 +1581,7 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
         return;
       }
       int r;
+      EL_PROF(st.cp[24] += CP_NOW() - el0);
       if constexpr (std::is_base_of<HbmStore, Store>::value)
         r = general_return_par(st, sl, mk, s, rF, rR, rW, nF, p, o, lane);
       else
@@ -3812,8 +3822,9 @@ hipError_t launch_hbm_coop(const lc_op *d_ops, const int64_t *d_key_off, const i
         line("mean per workgroup", sum, std::max(1, nw), rets);
         if (wv == 0)
           fprintf(stderr, "coopprof event loop per workgroup: calls %.0f taking %.0f, single returns %.0f taking "
-                  "%.0f, after cooperative returns %.0f\n", sum[21] / nw, sum[18] / nw, sum[22] / nw,
-                  sum[19] / nw, sum[20] / nw);
+                  "%.0f, after cooperative returns %.0f; before them: event loop %.0f, coop_return's "
+                  "publish %.0f\n", sum[21] / nw, sum[18] / nw, sum[22] / nw,
+                  sum[19] / nw, sum[20] / nw, sum[24] / nw, sum[23] / nw);
         double sl[kCpN];
         for (int q = 0; q < kCpN; q++) sl[q] = (double)h[slow][wv][q];
         line("slowest workgroup", sl, 1.0, (double)h[slow][0][5]);
