@@ -68,7 +68,7 @@ __device__ unsigned int g_fpdone;
 // Dev only (tools/build_variants.sh NAME -DLC_COOP_PROF): wave 0's shader
 // clocks per cooperative workgroup, by phase of its returns (see
 // CoopProf); launch_hbm_coop prints them after the launch
-constexpr int kCpN = 26;
+constexpr int kCpN = 30;
 __device__ unsigned long long g_cp[4096][2][kCpN];  // waves 0 and 1
 #define CP_NOW() __builtin_amdgcn_s_memtime()
 #endif
@@ -242,7 +242,7 @@ struct HbmStore {
   // event loop: [18] clocks in calls [19] in single-configuration returns
   // [20] after cooperative returns [21] calls [22] single returns;
   // ts: this return's marks
-  uint64_t cp[26] = {0};
+  uint64_t cp[30] = {0};
   uint64_t ts[6];
 #endif
   // Table size of a return (adaptive, round 2).  The sets of one return are
@@ -427,37 +427,51 @@ struct HbmStore {
 // dependent table round trips: in HBM (tag load, CAS, entry store, release)
 // one probe took ~1.4 us.  A return whose frontier fits runs its expansion
 // with both tables and both sets in LDS (R is also appended to the global
-// region the event loop reads); one whose sets outgrow kLim is redone with
+// region the event loop reads); one whose sets outgrow the pool is redone with
 // the HBM tables (status -3, as for the adaptive HBM size), so R, the
 // explored count and the verdict do not depend on it.
-// A table entry is 4 bytes, (epoch << 16) | index into the role's set; the
-// sets hold 12-byte configurations (CoopTab), so a 4-wave workgroup fits 864
-// per set in its 40 KB (four per CU) and an 8-wave one 1,728 in 80 KB.
+// Round 6: both roles share one table and one pool of set entries — R
+// takes pool slots from the bottom, W from the top — so a return fits while
+// nR + nW fits the pool, whatever its split (the returns that outgrew the
+// per-role sets had one set just past the limit and the other far below).
+// A table entry is 4 bytes, (epoch << 16) | (role << 15) | index into the
+// role's set; the pool holds 12-byte configurations plus a 1-byte ready flag
+// (CoopTab): 1,688 in a 4-wave workgroup's 40 KB (four per CU), 3,456 in an
+// 8- or 16-wave one's 80 KB.
 #ifndef LC_LEPOCH_MASK
-#define LC_LEPOCH_MASK 0xFFFFu  // tests build a variant with 0x3 to wrap every 3 returns
+#define LC_LEPOCH_MASK 0xFFu  // (8 bits: wrdy; a dev build with 0x3 wraps every 3 returns)
 #endif
 constexpr uint32_t kLepochMask = LC_LEPOCH_MASK;
 constexpr int kSpinMax = 1 << 22;       // queue waits (s_sleep 1 each) before giving up
 constexpr uint32_t kIdxBusy = 0xFFFFu;  // claimed, index not yet published
-constexpr uint32_t kIdxOvf = 0xFFFEu;   // claimed past kLim (the return is redone)
+constexpr uint32_t kIdxOvf = 0xFFFEu;   // claimed past the pool (the return is redone)
 template <int LT>
 struct CoopTab {
-  // configurations per set: 12 B each (below) plus a 2-byte flag, with the
-  // tables at <= 42 % load: 844 in 38 KB (4-wave: 20 fewer than the load
-  // allows, for scr), 1,728 in 78 KB (8- and 16-wave)
-  static constexpr int kLim = LT * 27 / 64 - (LT < 4096 ? 20 : 0);
+  // pool entries: 13 B each (below), the table (2 * LT entries) at <= 42 %
+  // load: 1,688 in 38 KB (4-wave: 40 fewer than the load allows, for scr),
+  // 3,456 in 78 KB (8- and 16-wave)
+  static constexpr int kPool = LT * 27 / 32 - (LT < 4096 ? 40 : 0);
   static constexpr int kScrWaves = LT < 4096 ? 4 : 16;
-  static_assert(kLim < (int)kIdxOvf, "set index must fit 16 bits");
-  uint32_t tag[2][LT];      // (epoch << 16) | index, per role
+  static_assert(kPool < 0x7FFE, "set index must fit 15 bits");
+  uint32_t tag[2 * LT];     // (epoch << 16) | (role << 15) | index
   // R and W of this return as (linearized set, value): within one return and
   // role the version follows from the set (every configuration has freed the
-  // same mutation slots), so it is not stored; W's is kw + popc(mask & muts)
-  uint64_t smask[2][kLim];
-  int32_t sval[2][kLim];
-  uint16_t wrdy[kLim];      // W entry written (its epoch): the work queue's readiness
+  // same mutation slots), so it is not stored; W's is kw + popc(mask & muts).
+  // R's index i is pool slot i, W's is kPool - 1 - i
+  uint64_t smask[kPool];
+  int32_t sval[kPool];
+  uint8_t wrdy[kPool];      // W entry i written (its epoch): the work queue's readiness
   // per wave, a round's successors: (source lane << 6) | slot (coop_expand)
   uint16_t scr[kScrWaves][kWave];
 };
+template <int LT>
+__device__ __forceinline__ int pool_slot(int role, int ix) {
+  return role == ROLE_R ? ix : CoopTab<LT>::kPool - 1 - ix;
+}
+// a configuration's table position: R and W probe apart
+__device__ __forceinline__ uint32_t pool_hash(const Cfg &c, int role) {
+  return HbmStore::hash(c.mask, c.sv ^ ((uint64_t)role << 63));
+}
 template <int LT>
 __device__ __forceinline__ CoopTab<LT> &coop_tab() {
   __shared__ CoopTab<LT> t;
@@ -467,7 +481,8 @@ template <int LT>
 struct CoopStore : HbmStore {
   static constexpr int kLT = LT;
   int last = 0;           // the previous return's larger set
-  uint32_t lepoch = 0;    // LDS table epoch (16 bits; 0 is never current)
+  int lsum = 0;           // and its nR + nW
+  uint32_t lepoch = 0;    // LDS table epoch (8 bits; 0 is never current)
   // The frontier's masks in the global region are brought up to date by the
   // next return's split, not by wave 0 as the events come (round 6): slots
   // retired since the last return (cleared from every configuration, before)
@@ -520,37 +535,41 @@ __device__ __forceinline__ void lds_tag_publish(uint32_t *p, uint32_t v) {
 // publish (epoch, index).  A busy entry is re-read next round; its owner
 // publishes within the round it claimed it, so no wave waits on another
 // wave's unfinished loop.  A lane that probed LT/4 entries, or whose index
-// is past kLim, sets ovf.  Returns 1 (inserted) or 0 (already there).
+// is past the pool, sets ovf.  Returns 1 (inserted) or 0 (already there).
 template <int LT>
 __device__ __forceinline__ int lds_insert_lanes(CoopTab<LT> &T, CoopShared &C, HbmStore &st,
                                                 int rR, int role, const Cfg &c, bool want,
                                                 uint32_t eb, bool &ovf, int lane) {
-  uint32_t h = HbmStore::hash(c.mask, c.sv) & (LT - 1);
+  constexpr int P = CoopTab<LT>::kPool;
+  constexpr uint32_t TM = 2 * LT - 1;
+  const uint32_t rbit = (uint32_t)role << 15;
+  uint32_t h = pool_hash(c, role) & TM;
   int res = 0, probes = 0;
   bool pend = want;
   while (__ballot(pend)) {
     bool won = false;
     if (pend) {
-      const uint32_t t = lds_tag_load(&T.tag[role][h]);
+      const uint32_t t = lds_tag_load(&T.tag[h]);
       if ((t & 0xFFFF0000u) == eb) {
-        const uint32_t ix = t & 0xFFFFu;
-        if (ix < kIdxOvf) {
+        const uint32_t lo = t & 0xFFFFu;
+        if (lo < kIdxOvf) {
           // (mask, value) decide: the version follows from the mask (CoopTab)
-          if (T.smask[role][ix] == c.mask && T.sval[role][ix] == sv_val(c.sv)) {
+          const int sl = pool_slot<LT>(role, (int)(lo & 0x7FFFu));
+          if ((lo & 0x8000u) == rbit && T.smask[sl] == c.mask && T.sval[sl] == sv_val(c.sv)) {
             pend = false;  // already there
           } else {
-            h = (h + 1) & (LT - 1);
-            if (++probes >= LT / 4) {
+            h = (h + 1) & TM;
+            if (++probes >= LT / 2) {
               ovf = true;
               pend = false;
             }
           }
-        } else if (ix == kIdxOvf) {
+        } else if (lo == kIdxOvf) {
           ovf = true;
           pend = false;
         }  // kIdxBusy: re-read next round
       } else {
-        won = atomicCAS(&T.tag[role][h], t, eb | kIdxBusy) == t;
+        won = atomicCAS(&T.tag[h], t, eb | kIdxBusy) == t;
       }
     }
     const uint64_t wR = __ballot(won && role == ROLE_R), wW = __ballot(won && role == ROLE_W);
@@ -559,21 +578,24 @@ __device__ __forceinline__ int lds_insert_lanes(CoopTab<LT> &T, CoopShared &C, H
       if (lane == 0)
         a = atomicAdd(&C.nRW, (unsigned long long)__popcll(wR) | ((unsigned long long)__popcll(wW) << 32));
       const int aR = uni((int)a), aW = uni((int)(a >> 32));
+      // R's slots [0, nR) and W's [P - nW, P) stay apart while nR + nW fits:
+      // every reservation checks the totals including all earlier ones
+      const bool fits = aR + __popcll(wR) + aW + __popcll(wW) <= P;
       if (won) {
         const int ix = role == ROLE_R ? aR + lanes_below(wR) : aW + lanes_below(wW);
         uint32_t pub = eb | kIdxOvf;
-        const bool fits = ix < CoopTab<LT>::kLim;
         if (fits) {
-          T.smask[role][ix] = c.mask;
-          T.sval[role][ix] = sv_val(c.sv);
+          const int sl = pool_slot<LT>(role, ix);
+          T.smask[sl] = c.mask;
+          T.sval[sl] = sv_val(c.sv);
           if (role == ROLE_R) st.reg(rR)[ix] = c;
-          pub = eb | (uint32_t)ix;
+          pub = eb | rbit | (uint32_t)ix;
         } else {
           ovf = true;
         }
-        lds_tag_publish(&T.tag[role][h], pub);
+        lds_tag_publish(&T.tag[h], pub);
         if (fits && role == ROLE_W)  // queue readiness, after the release above
-          __hip_atomic_store(&T.wrdy[ix], (uint16_t)(eb >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(&T.wrdy[ix], (uint8_t)(eb >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         res = 1;
         pend = false;
       }
@@ -586,15 +608,16 @@ __device__ __forceinline__ int lds_insert_lanes(CoopTab<LT> &T, CoopShared &C, H
 template <int LT>
 __device__ __forceinline__ void lds_claim_lane(CoopTab<LT> &T, int role, const Cfg &c, int ix,
                                                uint32_t eb, bool &ovf) {
-  uint32_t h = HbmStore::hash(c.mask, c.sv) & (LT - 1);
+  constexpr uint32_t TM = 2 * LT - 1;
+  uint32_t h = pool_hash(c, role) & TM;
   lds_release();  // the set entry before its tag
-  for (int probes = 0; probes < LT / 4;) {
-    const uint32_t t = lds_tag_load(&T.tag[role][h]);
+  for (int probes = 0; probes < LT / 2;) {
+    const uint32_t t = lds_tag_load(&T.tag[h]);
     if ((t & 0xFFFF0000u) != eb) {
-      if (atomicCAS(&T.tag[role][h], t, eb | (uint32_t)ix) == t) return;
+      if (atomicCAS(&T.tag[h], t, eb | ((uint32_t)role << 15) | (uint32_t)ix) == t) return;
       continue;  // lost the race for this entry: re-read it
     }
-    h = (h + 1) & (LT - 1);
+    h = (h + 1) & TM;
     probes++;
   }
   ovf = true;
@@ -747,13 +770,13 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
   st.tmask = C.tmask;
   CoopTab<LT> &T = coop_tab<LT>();
   const bool lds = C.lds;  // uniform over the workgroup
-  const int lim = lds ? CoopTab<LT>::kLim : st.lim(nw);
+  constexpr int P = CoopTab<LT>::kPool;
+  const int lim = lds ? P : st.lim(nw);
   const uint32_t eb = C.lepoch << 16;  // LDS tables' epoch
   bool ovf = false;
-  if (lds && C.lclear) {  // the 16-bit LDS epoch wrapped: clear the tags
-    uint32_t *tg = &T.tag[0][0];
-    for (int i = wave * kWave + lane; i < 2 * LT; i += nw * kWave) tg[i] = 0;
-    for (int i = wave * kWave + lane; i < CoopTab<LT>::kLim; i += nw * kWave) T.wrdy[i] = 0;
+  if (lds && C.lclear) {  // the 8-bit LDS epoch wrapped: clear the tags and flags
+    for (int i = wave * kWave + lane; i < 2 * LT; i += nw * kWave) T.tag[i] = 0;
+    for (int i = wave * kWave + lane; i < P; i += nw * kWave) T.wrdy[i] = 0;
     lds_barrier();
   }
   const uint64_t bs = C.bs, ordered = C.ordered;
@@ -803,21 +826,21 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
     }
     bR = __builtin_amdgcn_readfirstlane(bR);
     bW = __builtin_amdgcn_readfirstlane(bW);
-    if (lds) {  // nF <= kLim: both sets fit
+    if (lds) {  // nF <= the pool: nR + nW = nF fits
       if (has) {
         const Cfg rc{c.mask & ~bs, c.sv};
         const int ix = bR + lanes_below(mh);
         st.reg(rR)[ix] = rc;
-        T.smask[ROLE_R][ix] = rc.mask;
-        T.sval[ROLE_R][ix] = sv_val(rc.sv);
+        T.smask[ix] = rc.mask;
+        T.sval[ix] = sv_val(rc.sv);
         lds_claim_lane(T, ROLE_R, rc, ix, eb, ovf);
       }
       if (lacks) {
         const int ix = bW + lanes_below(ml);
-        T.smask[ROLE_W][ix] = c.mask;
-        T.sval[ROLE_W][ix] = sv_val(c.sv);
+        T.smask[P - 1 - ix] = c.mask;
+        T.sval[P - 1 - ix] = sv_val(c.sv);
         lds_claim_lane(T, ROLE_W, c, ix, eb, ovf);  // (releases the entry first)
-        __hip_atomic_store(&T.wrdy[ix], (uint16_t)(eb >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&T.wrdy[ix], (uint8_t)(eb >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     } else {
       if (has) st.claim_unique_lane(ROLE_R, rR, bR + lanes_below(mh), Cfg{c.mask & ~bs, c.sv});
@@ -878,8 +901,7 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
             const unsigned long long q =
                 __hip_atomic_load(&C.qword, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             const int h = (int)(uint32_t)q;
-            const int n = min(__hip_atomic_load(&C.nW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
-                              CoopTab<LT>::kLim);
+            const int n = min(__hip_atomic_load(&C.nW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), P);
             if (h < n) {
               const int kk = min(kWave, n - h);
               if (atomicCAS(&C.qword, q, q + (unsigned long long)kk + (1ull << 32)) == q) {
@@ -918,10 +940,13 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
       Cfg c;
       if (lds) {
         // entries reserved by a wave still in its round: wait for their flag
+        // (an entry reserved past the pool never gets one: its wave sets the
+        // status, and the return is redone)
         if (act)
           for (int spin = 0; __hip_atomic_load(&T.wrdy[j], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP) != ep16; spin++) {
-            if (spin == kSpinMax) {  // safety net (a writer is always mid-round): redone in HBM
+                                               __HIP_MEMORY_SCOPE_WORKGROUP) != (uint8_t)ep16; spin++) {
+            if (spin == kSpinMax ||  // (safety net: a writer is always mid-round)
+                __hip_atomic_load(&C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
               ovf = true;
               break;
             }
@@ -938,9 +963,9 @@ __device__ void coop_expand(HbmStore &st, CoopShared &C, int lane, int wave) {
         st.cp[15] += CP_NOW() - qc0;
 #endif
         lds_acquire();
-        const int jj = act ? j : b;
-        c.mask = T.smask[ROLE_W][jj];
-        c.sv = pack_sv(kw + __popcll(c.mask & muts), T.sval[ROLE_W][jj]);
+        const int jj = P - 1 - (act ? j : b);
+        c.mask = T.smask[jj];
+        c.sv = pack_sv(kw + __popcll(c.mask & muts), T.sval[jj]);
       } else {
         c = st.get(rW, act ? j : b);
       }
@@ -1083,9 +1108,10 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
     }
     if (lane < kVTab) C.vlegal[lane] = mine;
   }
-  // LDS tables first when this frontier and the previous return's sets fit
-  constexpr int kLim = CoopTab<LT>::kLim;
-  bool lds = nF <= kLim && st.last <= kLim;
+  // LDS tables first when this frontier fits the pool and the previous
+  // return's sets did not far outgrow it
+  constexpr int kPool = CoopTab<LT>::kPool;
+  bool lds = nF <= kPool && st.lsum <= 2 * kPool;
   const uint32_t floor = max(1024u, 256u * (uint32_t)st.nwaves);
   if (!lds) st.tmask = st.pick_tmask(nF, floor);
 #ifdef HBM_PROFILE
@@ -1141,11 +1167,17 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
       for (int q = 0; q < 5; q++) st.cp[q] += st.ts[q + 1] - st.ts[q];
       st.cp[5]++;
     }
+    if (lds && C.status == -3) st.cp[25] += CP_NOW() - st.ts[0];
+    if (!lds) {
+      st.cp[26]++;
+      st.cp[27] += CP_NOW() - st.ts[0];
+      st.cp[28] += (uint64_t)max(C.nR, C.nW);
+    }
 #endif
     if (C.status != -3) break;
     if (lds) {
       lds = false;
-      st.tmask = st.pick_tmask(max(nF, kLim), floor);
+      st.tmask = st.pick_tmask(max(nF, kPool / 2), floor);
     } else {
       st.tmask = st.grow_tmask();
     }
@@ -1171,6 +1203,7 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
   if (C.status < 0) return C.status;
   o.explored = (int64_t)C.explored;
   st.last = max(C.nR, C.nW);
+  st.lsum = C.nR + C.nW;
   st.fclear = st.fclose = 0;  // applied by this return's split
   st.rand = C.rand;
   if (!lds) st.hint = max(st.hint, st.last);
@@ -3419,9 +3452,8 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
   constexpr int LT = NW >= 8 ? 4096 : 2048;  // LDS table entries per role
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   {  // LDS tags and W flags start stale (epochs start at 1)
-    uint32_t *tg = &coop_tab<LT>().tag[0][0];
-    for (int i = threadIdx.x; i < 2 * LT; i += NW * kWave) tg[i] = 0;
-    for (int i = threadIdx.x; i < CoopTab<LT>::kLim; i += NW * kWave) coop_tab<LT>().wrdy[i] = 0;
+    for (int i = threadIdx.x; i < 2 * LT; i += NW * kWave) coop_tab<LT>().tag[i] = 0;
+    for (int i = threadIdx.x; i < CoopTab<LT>::kPool; i += NW * kWave) coop_tab<LT>().wrdy[i] = 0;
     __syncthreads();
   }
   char *w = ws + (size_t)blockIdx.x * hbm_wave_bytes(cap);
@@ -3446,7 +3478,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
       const int64_t beg = key_off[key], end = key_off[key + 1];
       KeyOut o;
       st.hint = 0;  // table-size hints: per key
-      st.last = 0;
+      st.last = st.lsum = 0;
       st.fclear = st.fclose = 0;
 #ifdef HBM_PROFILE
       const uint64_t tk0 = wall_clock64();
@@ -3825,6 +3857,11 @@ hipError_t launch_hbm_coop(const lc_op *d_ops, const int64_t *d_key_off, const i
                   "%.0f, after cooperative returns %.0f; before them: event loop %.0f, coop_return's "
                   "publish %.0f\n", sum[21] / nw, sum[18] / nw, sum[22] / nw,
                   sum[19] / nw, sum[20] / nw, sum[24] / nw, sum[23] / nw);
+        if (wv == 0)
+          fprintf(stderr, "coopprof HBM mode: failed LDS attempts' clocks %.0f per workgroup (slowest %.0f); HBM "
+                  "attempts %.2f (slowest %.0f) taking %.0f (slowest %.0f), mean larger set %.0f\n",
+                  sum[25] / nw, (double)h[slow][0][25], sum[26] / nw, (double)h[slow][0][26], sum[27] / nw,
+                  (double)h[slow][0][27], sum[28] / std::max(1.0, sum[26]));
         double sl[kCpN];
         for (int q = 0; q < kCpN; q++) sl[q] = (double)h[slow][wv][q];
         line("slowest workgroup", sl, 1.0, (double)h[slow][0][5]);
