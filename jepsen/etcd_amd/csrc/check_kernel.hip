@@ -489,6 +489,9 @@ struct CoopStore : HbmStore {
   // and reads called since (each linearized where legal); and the AND of
   // the last return's R, kept by the waves as they fill it
   uint64_t fclear = 0, fclose = 0, rand = ~0ull;
+  // lane v < kVTab: the slots legal at value id v - 1 whatever the version
+  // (kept as slots are taken, check_key; published as C.vlegal)
+  uint64_t vleg = 0;
 };
 // (check_key: the cooperative stores defer their frontier updates)
 template <class S, class = void>
@@ -1097,17 +1100,9 @@ __device__ int coop_return(CoopStore<LT> &st, const Slot &sl, const Masks &mk, i
   const uint64_t ordered = __ballot(sl.pbit != 0);  // (a ballot: outside the lane-0 block)
   // Legality by value id when no pending slot constrains the version (every
   // occupied slot's version mask nvm is 0: version-less models): lane v
-  // keeps the slots legal at value id v - 1 (one ballot each)
+  // kept the slots legal at value id v - 1 as they were taken (st.vleg)
   const bool vt = (__ballot(sl.nvm != 0) & mk.occ) == 0;
-  if (vt) {
-    uint64_t mine = 0;
-#pragma unroll
-    for (int v = 0; v < kVTab; v++) {
-      const uint64_t m = __ballot((((v - 1) ^ sl.nl) & sl.nlm) == 0);
-      if (lane == v) mine = m;
-    }
-    if (lane < kVTab) C.vlegal[lane] = mine;
-  }
+  if (vt && lane < kVTab) C.vlegal[lane] = st.vleg;
   // LDS tables first when this frontier fits the pool and the previous
   // return's sets did not far outgrow it
   constexpr int kPool = CoopTab<LT>::kPool;
@@ -1487,6 +1482,10 @@ __device__ void check_key(const lc_op *__restrict__ kops, const int n,
           pbit = cls & __ballot(sl.ret <= ret);  // before s (equal: both crashed, called first)
           if (((cls & ~pbit) >> lane) & 1) sl.pbit |= bs;  // the later ones wait for s
           if (ret == kNever) mk.crashed |= bs;
+        }
+        if constexpr (DeferF<Store>::value) {  // (coop_return's value table)
+          const bool ok = (((lane - 1) ^ nl) & nlm) == 0;
+          st.vleg = ok ? st.vleg | bs : st.vleg & ~bs;
         }
         if (lane == s) {
           sl.nv = nv;
@@ -3479,6 +3478,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
       KeyOut o;
       st.hint = 0;  // table-size hints: per key
       st.last = st.lsum = 0;
+      st.vleg = 0;
       st.fclear = st.fclose = 0;
 #ifdef HBM_PROFILE
       const uint64_t tk0 = wall_clock64();
