@@ -503,6 +503,14 @@ struct DeferF<S, std::void_t<decltype(S::kLT)>> {
   static constexpr bool value = S::kLT > 0;
 };
 
+// Wave priority of wave 0 (s_setprio): the event loop between returns is
+// each key's serial path, so it issues ahead of other workgroups' expansion
+// waves on its SIMD (model_leg 9.22 -> 8.88 ms; raising the expansion
+// waves' too, or dropping wave 0's during its share of the expansion,
+// measured slower: profiles/r06/model_prio_ab.txt)
+#ifndef LC_COOP_PRIO
+#define LC_COOP_PRIO 3
+#endif
 // Sleep of a wave whose work queue is empty while others expand, or whose
 // claimed entries are not yet written (s_sleep units of 64 clocks)
 #ifndef LC_COOP_SLEEP
@@ -3467,6 +3475,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
   hbm_zero_tags(st.tags, cap);
   st.epoch = 0;  // epochs start at 1
   if (wave == 0) {
+    if (LC_COOP_PRIO) __builtin_amdgcn_s_setprio(LC_COOP_PRIO);  // (LC_COOP_PRIO above)
     const int64_t key_base = key_off[0];
     for (;;) {  // list entries claimed one at a time (next: zero at launch)
       int li = 0;
