@@ -59,7 +59,7 @@ def parse():
                     help="timed region only (no CPU baseline, no hot-key leg): "
                          "for rocprofv3 runs whose per-kernel averages must "
                          "match the bench line")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05", "traffic_fast_tier.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r06", "traffic_fast_tier.json"))
     return ap.parse_args()
 
 
