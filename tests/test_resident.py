@@ -116,3 +116,25 @@ def test_resident_totals_count_every_call(ctx, monkeypatch):
     t = ctx.totals(reset=True)
     assert t["calls"] == 20 and t["timed_calls"] == 20
     assert 0 < t["fast_kernel_ms"] / 20 < 1.0
+
+
+@pytest.mark.parametrize("resident", ["0", "1"])
+def test_contexts_reopened_signal_path(monkeypatch, resident):
+    """Contexts opened and closed in turn, one signal-path call each (the
+    follower kernel's completion word, or the resident grid's), alternating a
+    clean batch with one whose invalid keys must be handed over: pinned words
+    reused from a closed context (h_done, h_handoff) must not let a
+    call return before its pass, nor hide a handoff."""
+    clean = abi.synth(300, 100, concurrency=8, seed=61)[:2]
+    bad = abi.synth(300, 100, concurrency=8, p_anomaly=0.4, seed=62)[:2]
+    with abi.Context(device_mask=1) as c0:
+        want = [c0.check(o, f)[1] for o, f in (clean, bad)]
+    assert (want[1]["verdict"] == 0).any() and (want[0]["verdict"] == 1).all()
+    devs = [(_dev(o), _dev(f)) for o, f in (clean, bad)]
+    monkeypatch.setenv("LC_RESIDENT", resident)
+    for i in range(12):
+        k = i % 2
+        with abi.Context(device_mask=1) as ctx:
+            got = _run(ctx, devs[k][0], devs[k][1], 300)
+        for f in ("verdict", "reason", "fail_op", "fail_prefix_end"):
+            assert (got[f] == want[k][f]).all(), (i, f)
