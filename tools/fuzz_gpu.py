@@ -98,6 +98,32 @@ for rd in range(rounds):
             print("   long key", k, "gpu", got, "restated", exp)
     print("%-34s keys %5d mismatches %d" % ("long crash-heavy r%d" % rd, 6, nbad), flush=True)
     bad_total += nbad
+    # the cooperative tier (LDS pool, value table, packed rounds, deferred
+    # frontier updates) against the one-wave tier (HBM tables, serial
+    # worklist) on version-less keys: every result field
+    for conc, opk, pan in ((10, 300, 0.0), (14, 400, 0.01), (18, 600, 0.0)):
+        ops, off, _, _ = abi.synth(96, opk, concurrency=conc, seed=base + 31 * conc)
+        ops = ops.copy()
+        ops[:, 3] = -1
+        if pan:
+            rr = np.random.default_rng(base + conc)
+            reads = np.nonzero((ops[:, 0] == abi.LC_F_READ) & (ops[:, 5] != abi.LC_INF))[0]
+            ops[rr.choice(reads, int(len(reads) * pan), replace=False), 1] = 12345
+        co = abi.default_opts(flags=abi.LC_FLAG_NO_GAP_TIER, time_budget_ms=5000)
+        res = {}
+        for mode in ("0", "1"):
+            os.environ["LC_HBM_COOP"] = mode
+            with abi.Context(device_mask=1) as ctx:
+                res[mode] = ctx.check(ops, off, co)[1]
+        del os.environ["LC_HBM_COOP"]
+        a, b = res["0"], res["1"]
+        done = (a["verdict"] != -1) & (b["verdict"] != -1)
+        nbad = 0
+        for f in ("verdict", "reason", "fail_op", "fail_prefix_end", "configs_explored", "max_frontier"):
+            nbad = max(nbad, int((a[f][done] != b[f][done]).sum()))
+        print("%-34s keys %5d decided %5d mismatches %d" % ("coop vs one-wave c%d n%d r%d" % (conc, opk, rd),
+                                                            len(off) - 1, int(done.sum()), nbad), flush=True)
+        bad_total += nbad
     rng = random.Random(base)
     keys = [random_mutex(rng, rng.randrange(1, 24)) for _ in range(1500)]
     ops, off = pack_keys(keys)
