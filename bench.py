@@ -796,6 +796,19 @@ def model_leg(ctx, abi):
     t = float(np.median(times[1:]))
     hbm_ms = float(np.median([x["hbm_kernel_ms"] for x in st[1:]]))
     explored = int(r["configs_explored"].sum())
+    # the same batch as the drop-ins send it (checker.py, mi355x.clj: 16-byte
+    # records when every id fits): a third of the PCIe bytes; beside call_ms
+    # (48-byte records), which stays the leg's figure
+    call16 = None
+    p16 = abi.pack16(ops, off)
+    if p16 is not None:
+        t16 = []
+        for _ in range(4):
+            t0 = time.perf_counter()
+            _, r16 = ctx.check16(p16[0], off, p16[1])
+            t16.append((time.perf_counter() - t0) * 1e3)
+        call16 = {"call_ms": float(np.median(t16[1:])),
+                  "result_mismatches_vs_48_byte": int((r16 != r).sum())}
     # the roofline SURVEY §8(d) states for the search: one 128-B table probe
     # per configuration explored, against the HBM peak; beside it the
     # counters' own traffic of hbm_coop_kernel<4> (a PMC pass of this leg,
@@ -826,9 +839,10 @@ def model_leg(ctx, abi):
             "configs_explored": explored,
             # probe throughput: every configuration explored is one dedup probe
             # (most in LDS tables since round 2; HBM bytes per probe from the
-            # PMC pass, profiles/r02/pmc_model_hbm_coop4.json)
+            # PMC pass, profiles/r06/pmc_model_hbm_coop4.json)
             "probes_per_s": explored / (hbm_ms * 1e-3) if hbm_ms > 0 else None,
             "max_frontier": int(r["max_frontier"].max()),
+            "records16": call16,
             "valid": int((r["verdict"] == 1).sum()), "unknown": int((r["verdict"] == -1).sum())}
 
 
