@@ -590,3 +590,30 @@ def test_register_checker_end_to_end(tmp_path):
     assert res["results"][0]["timeline"]["valid?"] is True
     assert C.check_safe(chk, {}, [{"type": "invoke", "process": 0, "value": None}]) == \
         {"valid?": True, "results": {}, "failures": []}
+
+
+def test_cooperative_pool_and_epoch_wrap_agree(ctx, monkeypatch):
+    """The model leg's own keys (version-less, 1,000 ops, concurrency 20):
+    hundreds of cooperative returns per key, so the 8-bit LDS epoch wraps
+    (tables cleared), and the keys with the largest frontiers have returns
+    past the LDS pool (nR + nW > 1,688: redone on HBM tables).  The six
+    largest-frontier keys through the cooperative tier against the one-wave
+    tier (HBM tables, serial worklist) — every result field."""
+    ops, off, _, _ = abi.synth(1000, 1000, concurrency=20, seed=7)
+    ops = ops.copy()
+    ops[:, 3] = abi.LC_NIL
+    _, full = ctx.check(ops, off)
+    pick = np.argsort(full["max_frontier"])[-6:]
+    keys = [ops[off[k]:off[k + 1]] for k in pick]
+    sub = np.concatenate(keys)
+    soff = np.concatenate([[0], np.cumsum([len(x) for x in keys])]).astype(np.int64)
+    o = abi.default_opts(flags=abi.LC_FLAG_NO_GAP_TIER, time_budget_ms=60000)
+    monkeypatch.setenv("LC_HBM_COOP", "0")
+    _, a = ctx.check(sub, soff, o)
+    monkeypatch.setenv("LC_HBM_COOP", "4")
+    _, b = ctx.check(sub, soff, o)
+    assert (a["verdict"] == 1).all() and (b["verdict"] == 1).all()
+    assert int(b["max_frontier"].max()) > 1688  # returns past the pool
+    for f in ("verdict", "reason", "fail_op", "fail_prefix_end", "configs_explored", "max_frontier"):
+        assert (a[f] == b[f]).all(), f
+        assert (b[f] == full[f][pick]).all(), f
