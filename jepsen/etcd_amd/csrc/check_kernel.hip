@@ -206,7 +206,7 @@ struct CoopShared {
   int head, lo, hi, go, status;
   unsigned long long qword;  // LDS work queue: claimed head (low), expanding waves (high)
   int lds;  // this attempt keeps its tables and sets in LDS (CoopTab)
-  uint32_t lepoch;  // its LDS epoch (16 bits)
+  uint32_t lepoch;  // its LDS epoch (8 bits)
   int kw;           // LDS mode: W's versions are kw + popc(mask & muts) (set by the split)
   int lclear;       // the LDS epoch wrapped: clear the tags first
   unsigned long long explored;
@@ -3456,7 +3456,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
     const int64_t cap, int32_t *__restrict__ ovf_out, int32_t *__restrict__ n_ovf_out,
     int32_t *__restrict__ n_malformed, int32_t *__restrict__ next, const int last_tier) {
   __shared__ CoopShared C;
-  constexpr int LT = NW >= 8 ? 4096 : 2048;  // LDS table entries per role
+  constexpr int LT = NW >= 8 ? 4096 : 2048;  // LDS table: 2 * LT entries (both roles)
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   {  // LDS tags and W flags start stale (epochs start at 1)
     for (int i = threadIdx.x; i < 2 * LT; i += NW * kWave) coop_tab<LT>().tag[i] = 0;
