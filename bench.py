@@ -783,12 +783,12 @@ def model_leg(ctx, abi):
     """knossos's cas-register model (no versions) on C2-shaped histories,
     1,000 keys x 1,000 ops, concurrency 20: without version pinning every key
     needs the frontier search and its HBM tier (§9 of DESIGN.md).  Not part
-    of `value`; median of 3 calls after one warm-up."""
+    of `value`; median of 5 calls after one warm-up."""
     ops, off, _, _ = abi.synth(1000, 1000, concurrency=20, seed=7)
     ops = ops.copy()
     ops[:, 3] = abi.LC_NIL  # cas-register: the same histories without versions
     times, st = [], []
-    for _ in range(4):
+    for _ in range(6):
         t0 = time.perf_counter()
         _, r = ctx.check(ops, off)
         times.append((time.perf_counter() - t0) * 1e3)
